@@ -1,0 +1,53 @@
+// Shared helpers for the gfx950 kernels of libvclip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "vclip.h"
+
+namespace vc {
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+// error state (thread-local, set by host entry points)
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+int check_launch(const char* what);
+
+// f32 -> bf16 round-to-nearest-even (hipcc lowers the scalar cast to v_cvt_pk_bf16_f32)
+__device__ __forceinline__ unsigned short f2bf(float x) {
+    __bf16 b = (__bf16)x;
+    return __builtin_bit_cast(unsigned short, b);
+}
+__device__ __forceinline__ unsigned int pack2bf(float lo, float hi) {
+    return (unsigned int)f2bf(lo) | ((unsigned int)f2bf(hi) << 16);
+}
+__device__ __forceinline__ float bf2f(unsigned short u) {
+    return __builtin_bit_cast(float, ((unsigned int)u) << 16);
+}
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+    // gelu_fast: 0.5x(1+tanh(0.7978845608 x (1 + 0.044715 x^2)))  (TF5/activations.py)
+    const float u = 0.7978845608f * x * (1.0f + 0.044715f * x * x);
+    return 0.5f * x * (1.0f + tanhf(u));
+}
+__device__ __forceinline__ float gelu_erf(float x) {
+    return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+}  // namespace vc

@@ -1,0 +1,301 @@
+// HBM-bound kernels of the path: frame gather/normalise, tubelet im2col, LayerNorm,
+// CLS init and the classifier head.  Plus the C-ABI error plumbing.
+#include "common.hpp"
+
+#include <cstdio>
+
+namespace vc {
+
+static thread_local std::string g_last_error;
+
+void set_error(const std::string& msg) { g_last_error = msg; }
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        g_last_error = std::string(what) + ": " + hipGetErrorString(e);
+        return (int)e;
+    }
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------
+// Frame gather.  One thread moves 16 B of a source frame row (u8 mode) or 4 pixels
+// (float modes: 12 source bytes -> 3 planes x 4 values).
+// frames [nclips][F][H][W][C] u8; idx [nclips][T]; clamp like dataset.py:252-253.
+// ---------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) gather_u8_kernel(const uint8_t* __restrict__ frames, int64_t F,
+                                                        int64_t frame_bytes, const int64_t* __restrict__ idx,
+                                                        int64_t T, uint8_t* __restrict__ out) {
+    const int64_t clip_t = blockIdx.y;  // clip * T + t
+    const int64_t clip = clip_t / T;
+    int64_t f = idx[clip_t];
+    f = f < 0 ? 0 : (f > F - 1 ? F - 1 : f);
+    const uint8_t* src = frames + (clip * F + f) * frame_bytes;
+    uint8_t* dst = out + clip_t * frame_bytes;
+    const int64_t n16 = frame_bytes >> 4;
+    for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += (int64_t)gridDim.x * 256)
+        reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+    // tail bytes (frame_bytes not a multiple of 16)
+    const int64_t tail0 = n16 << 4;
+    if (blockIdx.x == 0)
+        for (int64_t i = tail0 + threadIdx.x; i < frame_bytes; i += 256) dst[i] = src[i];
+}
+
+template <bool BF16>
+__global__ void __launch_bounds__(256) gather_norm_kernel(const uint8_t* __restrict__ frames, int64_t F,
+                                                          int64_t HW, const int64_t* __restrict__ idx, int64_t T,
+                                                          float scale, float shift, void* __restrict__ out) {
+    // C == 3 (RGB) specialisation: thread handles 4 consecutive pixels = 12 bytes.
+    const int64_t clip_t = blockIdx.y;
+    const int64_t clip = clip_t / T;
+    int64_t f = idx[clip_t];
+    f = f < 0 ? 0 : (f > F - 1 ? F - 1 : f);
+    const uint8_t* src = frames + (clip * F + f) * HW * 3;
+    const int64_t nq = HW >> 2;
+    for (int64_t q = blockIdx.x * 256 + threadIdx.x; q < nq; q += (int64_t)gridDim.x * 256) {
+        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src + q * 12);
+        uint32_t w0 = s32[0], w1 = s32[1], w2 = s32[2];
+        uint8_t b[12];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            b[i] = (w0 >> (8 * i)) & 0xff;
+            b[4 + i] = (w1 >> (8 * i)) & 0xff;
+            b[8 + i] = (w2 >> (8 * i)) & 0xff;
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            float v0 = (float)b[0 * 3 + c] * scale + shift;
+            float v1 = (float)b[1 * 3 + c] * scale + shift;
+            float v2 = (float)b[2 * 3 + c] * scale + shift;
+            float v3 = (float)b[3 * 3 + c] * scale + shift;
+            const int64_t o = (clip_t * 3 + c) * HW + q * 4;
+            if (BF16) {
+                uint2 p;
+                p.x = pack2bf(v0, v1);
+                p.y = pack2bf(v2, v3);
+                *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + o) = p;
+            } else {
+                *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + o) = make_float4(v0, v1, v2, v3);
+            }
+        }
+    }
+    // tail pixels (HW % 4)
+    if (blockIdx.x == 0) {
+        for (int64_t p = (nq << 2) + threadIdx.x; p < HW; p += 256)
+            for (int c = 0; c < 3; ++c) {
+                float v = (float)src[p * 3 + c] * scale + shift;
+                const int64_t o = (clip_t * 3 + c) * HW + p;
+                if (BF16)
+                    reinterpret_cast<uint16_t*>(out)[o] = f2bf(v);
+                else
+                    reinterpret_cast<float*>(out)[o] = v;
+            }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Tubelet im2col.  pixel [B][T][C][H][W] f32 -> A[(b,t',hp,wp)][(c,kt,kh,kw)] bf16.
+// One thread converts 8 consecutive pixels of one image row (coalesced 32-B reads).
+// ---------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) im2col_kernel(const float* __restrict__ pix, int64_t total8, int T, int C,
+                                                     int H, int W, int kt, int kh, int kw, uint16_t* __restrict__ A,
+                                                     int64_t lda) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= total8) return;
+    const int W8 = W >> 3;
+    int64_t r = i;
+    const int x8 = r % W8;
+    r /= W8;
+    const int y = r % H;
+    r /= H;
+    const int c = r % C;
+    r /= C;
+    const int t = r % T;
+    const int64_t b = r / T;
+    const float4* s = reinterpret_cast<const float4*>(pix + ((((b * T + t) * C + c) * H + y) * (int64_t)W) + x8 * 8);
+    const float4 u = s[0], v = s[1];
+    const int nt = T / kt, nh = H / kh, nw = W / kw;
+    const int tp = t / kt, it = t % kt, hp = y / kh, ih = y % kh;
+    const int x = x8 * 8, wp = x / kw, iw = x % kw;
+    const int64_t m = ((b * nt + tp) * nh + hp) * (int64_t)nw + wp;
+    const int64_t k = (((int64_t)c * kt + it) * kh + ih) * kw + iw;
+    uint4 o;
+    o.x = pack2bf(u.x, u.y);
+    o.y = pack2bf(u.z, u.w);
+    o.z = pack2bf(v.x, v.y);
+    o.w = pack2bf(v.z, v.w);
+    *reinterpret_cast<uint4*>(A + m * lda + k) = o;
+}
+
+// ---------------------------------------------------------------------------------
+// LayerNorm f32 -> bf16, one wave per row, D = 64*V*4 (V float4 per lane).
+// ---------------------------------------------------------------------------------
+template <int V>
+__global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict__ x, int64_t ldx, int64_t M,
+                                                        const float* __restrict__ g, const float* __restrict__ be,
+                                                        float eps, uint16_t* __restrict__ y, int64_t ldy) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    constexpr int D = V * 256;
+    const float4* xr = reinterpret_cast<const float4*>(x + row * ldx);
+    float4 v[V];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        v[i] = xr[i * 64 + lane];
+        s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    }
+    const float mean = wave_sum(s) * (1.0f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+        q += (a * a + b * b) + (c * c + d * d);
+    }
+    const float rstd = rsqrtf(wave_sum(q) * (1.0f / D) + eps);
+    const float4* g4 = reinterpret_cast<const float4*>(g);
+    const float4* b4 = reinterpret_cast<const float4*>(be);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const float4 gg = g4[i * 64 + lane], bb = b4[i * 64 + lane];
+        uint2 o;
+        o.x = pack2bf((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y);
+        o.y = pack2bf((v[i].z - mean) * rstd * gg.z + bb.z, (v[i].w - mean) * rstd * gg.w + bb.w);
+        *reinterpret_cast<uint2*>(y + row * ldy + (i * 64 + lane) * 4) = o;
+    }
+}
+
+__global__ void cls_init_kernel(const float* __restrict__ cls, const float* __restrict__ pos, float* __restrict__ x,
+                                int64_t ldx, int64_t S, int64_t D) {
+    const int64_t b = blockIdx.x;
+    for (int64_t n = threadIdx.x; n < D; n += blockDim.x) x[b * S * ldx + n] = cls[n] + pos[n];
+}
+
+// LN of each clip's CLS row then the tiny classifier GEMV, fp32 throughout.
+__global__ void __launch_bounds__(256) cls_head_kernel(const float* __restrict__ x, int64_t ldx, int64_t S, int64_t D,
+                                                       const float* __restrict__ g, const float* __restrict__ be,
+                                                       float eps, const float* __restrict__ Wc,
+                                                       const float* __restrict__ bc, int64_t nl,
+                                                       float* __restrict__ logits) {
+    __shared__ float red[8];
+    __shared__ float ybuf[4096];
+    const int64_t b = blockIdx.x;
+    const float* xr = x + b * S * ldx;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    float s = 0.f;
+    for (int64_t n = tid; n < D; n += 256) s += xr[n];
+    s = wave_sum(s);
+    if (lane == 0) red[w] = s;
+    __syncthreads();
+    const float mean = (red[0] + red[1] + red[2] + red[3]) / (float)D;
+    __syncthreads();
+    float q = 0.f;
+    for (int64_t n = tid; n < D; n += 256) {
+        float d = xr[n] - mean;
+        q += d * d;
+    }
+    q = wave_sum(q);
+    if (lane == 0) red[w] = q;
+    __syncthreads();
+    const float rstd = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)D + eps);
+    for (int64_t n = tid; n < D; n += 256) ybuf[n] = (xr[n] - mean) * rstd * g[n] + be[n];
+    __syncthreads();
+    for (int64_t c = w; c < nl; c += 4) {
+        float a = 0.f;
+        for (int64_t n = lane; n < D; n += 64) a += ybuf[n] * Wc[c * D + n];
+        a = wave_sum(a);
+        if (lane == 0) logits[b * nl + c] = a + bc[c];
+    }
+}
+
+}  // namespace vc
+
+using namespace vc;
+
+extern "C" {
+
+const char* vc_version(void) { return "vclip 0.1.0 gfx950"; }
+
+const char* vc_last_error(void) { return g_last_error.c_str(); }
+
+int vc_frame_gather(const uint8_t* frames, int64_t nclips, int64_t F, int64_t H, int64_t W, int64_t C,
+                    const int64_t* idx, int64_t T, int out_kind, float scale, float shift, void* out,
+                    hipStream_t stream) {
+    if (!frames || !idx || !out) return fail(VC_ERR_INVALID_ARG, "vc_frame_gather: null pointer");
+    if (nclips <= 0 || F <= 0 || H <= 0 || W <= 0 || C <= 0 || T <= 0)
+        return fail(VC_ERR_INVALID_ARG, "vc_frame_gather: non-positive size");
+    if (nclips * T > 65535) return fail(VC_ERR_INVALID_ARG, "vc_frame_gather: nclips*T > 65535");
+    const int64_t HW = H * W;
+    if (out_kind == VC_GATHER_U8_NHWC) {
+        const int64_t fb = HW * C;
+        if (((uintptr_t)frames | (uintptr_t)out) & 15 || fb & 15)
+            return fail(VC_ERR_INVALID_ARG, "vc_frame_gather(u8): frames/out need 16-B alignment and frame size % 16 == 0");
+        int64_t nb = (fb / 16 + 255) / 256;
+        dim3 grid((unsigned)(nb > 256 ? 256 : nb), (unsigned)(nclips * T));
+        gather_u8_kernel<<<grid, 256, 0, stream>>>(frames, F, fb, idx, T, (uint8_t*)out);
+        return check_launch("vc_frame_gather");
+    }
+    if (C != 3) return fail(VC_ERR_UNSUPPORTED, "vc_frame_gather: float modes need C == 3");
+    if (((uintptr_t)frames & 3) || ((uintptr_t)out & 15) || (HW & 3))
+        return fail(VC_ERR_INVALID_ARG, "vc_frame_gather: alignment (frames 4 B, out 16 B, H*W % 4 == 0)");
+    int64_t nb = (HW / 4 + 255) / 256;
+    dim3 grid((unsigned)(nb > 256 ? 256 : nb), (unsigned)(nclips * T));
+    if (out_kind == VC_GATHER_F32_NCHW)
+        gather_norm_kernel<false><<<grid, 256, 0, stream>>>(frames, F, HW, idx, T, scale, shift, out);
+    else if (out_kind == VC_GATHER_BF16_NCHW)
+        gather_norm_kernel<true><<<grid, 256, 0, stream>>>(frames, F, HW, idx, T, scale, shift, out);
+    else
+        return fail(VC_ERR_INVALID_ARG, "vc_frame_gather: bad out_kind");
+    return check_launch("vc_frame_gather");
+}
+
+int vc_tubelet_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C, int64_t H, int64_t W, int kt,
+                      int kh, int kw, uint16_t* A, int64_t lda, hipStream_t stream) {
+    if (!pixel_values || !A) return fail(VC_ERR_INVALID_ARG, "vc_tubelet_im2col: null pointer");
+    if (T % kt || H % kh || W % kw || kw % 8 || W % 8 || lda % 8 || lda < C * kt * kh * kw)
+        return fail(VC_ERR_INVALID_ARG, "vc_tubelet_im2col: shape not divisible by tubelet / 8-wide rows");
+    const int64_t total8 = B * T * C * H * (W / 8);
+    const int64_t nb = (total8 + 255) / 256;
+    im2col_kernel<<<(unsigned)nb, 256, 0, stream>>>(pixel_values, total8, (int)T, (int)C, (int)H, (int)W, kt, kh, kw,
+                                                   A, lda);
+    return check_launch("vc_tubelet_im2col");
+}
+
+int vc_layernorm_f32_bf16(const float* x, int64_t ldx, int64_t M, int64_t D, const float* gamma, const float* beta,
+                          float eps, uint16_t* y, int64_t ldy, hipStream_t stream) {
+    if (!x || !gamma || !beta || !y) return fail(VC_ERR_INVALID_ARG, "vc_layernorm: null pointer");
+    if (ldx % 4 || ldy % 4) return fail(VC_ERR_INVALID_ARG, "vc_layernorm: ld must be a multiple of 4");
+    const unsigned nb = (unsigned)((M + 3) / 4);
+    switch (D) {
+        case 256: layernorm_kernel<1><<<nb, 256, 0, stream>>>(x, ldx, M, gamma, beta, eps, y, ldy); break;
+        case 512: layernorm_kernel<2><<<nb, 256, 0, stream>>>(x, ldx, M, gamma, beta, eps, y, ldy); break;
+        case 768: layernorm_kernel<3><<<nb, 256, 0, stream>>>(x, ldx, M, gamma, beta, eps, y, ldy); break;
+        case 1024: layernorm_kernel<4><<<nb, 256, 0, stream>>>(x, ldx, M, gamma, beta, eps, y, ldy); break;
+        default: return fail(VC_ERR_UNSUPPORTED, "vc_layernorm: D must be 256/512/768/1024");
+    }
+    return check_launch("vc_layernorm_f32_bf16");
+}
+
+int vc_cls_init(const float* cls, const float* pos, float* x, int64_t ldx, int64_t B, int64_t S, int64_t D,
+                hipStream_t stream) {
+    if (!cls || !pos || !x) return fail(VC_ERR_INVALID_ARG, "vc_cls_init: null pointer");
+    cls_init_kernel<<<(unsigned)B, 256, 0, stream>>>(cls, pos, x, ldx, S, D);
+    return check_launch("vc_cls_init");
+}
+
+int vc_cls_head(const float* x, int64_t ldx, int64_t B, int64_t S, int64_t D, const float* gamma, const float* beta,
+                float eps, const float* Wc, const float* bc, int64_t num_labels, float* logits, hipStream_t stream) {
+    if (!x || !gamma || !beta || !Wc || !bc || !logits) return fail(VC_ERR_INVALID_ARG, "vc_cls_head: null pointer");
+    if (D > 4096) return fail(VC_ERR_UNSUPPORTED, "vc_cls_head: D > 4096");
+    cls_head_kernel<<<(unsigned)B, 256, 0, stream>>>(x, ldx, S, D, gamma, beta, eps, Wc, bc, num_labels, logits);
+    return check_launch("vc_cls_head");
+}
+
+}  // extern "C"

@@ -1,0 +1,144 @@
+"""torch-tensor front end of the libvclip.so kernels.
+
+Each function validates shapes/dtypes/devices on the host (a kernel is never launched
+on operands whose shape it does not support), then calls the C-ABI with raw device
+pointers and torch's current HIP stream, so the work orders correctly with torch ops
+and is captured by torch.cuda graphs.  No CPU fallback exists: CPU tensors raise.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+EPI = {"bias": 0, "bias_gelu_tanh": 1, "bias_gelu_erf": 2, "bias_resid_f32": 3, "embed_f32": 4}
+GATHER_KIND = {"u8": 0, "f32": 1, "bf16": 2}
+
+
+def _dev(*ts):
+    for t in ts:
+        if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+            raise _lib.VclipError("vclip ops need CUDA(HIP) tensors; there is no CPU path")
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _p(t):
+    return t.data_ptr()
+
+
+def _need(cond, msg):
+    if not cond:
+        raise _lib.VclipError(msg)
+
+
+def frame_gather(frames: torch.Tensor, idx: torch.Tensor, kind: str = "f32", scale: float = 1.0 / 63.75,
+                 shift: float = -3.0, out: torch.Tensor | None = None) -> torch.Tensor:
+    """frames u8 [N,F,H,W,C], idx int64 [N,T] -> u8 [N,T,H,W,C] or f32/bf16 [N,T,C,H,W]."""
+    _dev(frames, idx)
+    _need(frames.dtype == torch.uint8 and frames.dim() == 5 and frames.is_contiguous(), "frames: u8 [N,F,H,W,C]")
+    _need(idx.dtype == torch.int64 and idx.dim() == 2 and idx.is_contiguous() and idx.shape[0] == frames.shape[0],
+          "idx: int64 [N,T]")
+    N, F, H, W, C = frames.shape
+    T = idx.shape[1]
+    if kind == "u8":
+        shape, dt = (N, T, H, W, C), torch.uint8
+    else:
+        shape, dt = (N, T, C, H, W), (torch.float32 if kind == "f32" else torch.bfloat16)
+    if out is None:
+        out = torch.empty(shape, dtype=dt, device=frames.device)
+    _need(tuple(out.shape) == shape and out.dtype == dt and out.is_contiguous(), "frame_gather: bad out")
+    _lib.call("vc_frame_gather", _p(frames), N, F, H, W, C, _p(idx), T, GATHER_KIND[kind], scale, shift, _p(out),
+              _stream(frames))
+    return out
+
+
+def tubelet_im2col(pix: torch.Tensor, tubelet, out: torch.Tensor) -> torch.Tensor:
+    """pix f32 [B,T,C,H,W] -> out bf16 [>= B*nt*nh*nw, C*kt*kh*kw] (rows beyond are untouched)."""
+    _dev(pix, out)
+    _need(pix.dtype == torch.float32 and pix.dim() == 5 and pix.is_contiguous(), "pixel_values: f32 [B,T,C,H,W]")
+    B, T, C, H, W = pix.shape
+    kt, kh, kw = tubelet
+    ntok = B * (T // kt) * (H // kh) * (W // kw)
+    _need(out.dtype == torch.bfloat16 and out.dim() == 2 and out.shape[0] >= ntok and out.shape[1] == C * kt * kh * kw
+          and out.is_contiguous(), "im2col out: bf16 [rows, C*kt*kh*kw]")
+    _lib.call("vc_tubelet_im2col", _p(pix), B, T, C, H, W, kt, kh, kw, _p(out), out.stride(0), _stream(pix))
+    return out
+
+
+def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: str, out: torch.Tensor,
+         aux: torch.Tensor | None = None, group: int = 0, group_stride: int = 0, group_offset: int = 0,
+         m: int | None = None) -> torch.Tensor:
+    """out (+)= epilogue(a[:m] @ w.T + bias).  a bf16 [M,K], w bf16 [N,K], bias f32 [N]."""
+    _dev(a, w, bias, out)
+    M = a.shape[0] if m is None else m
+    K = a.shape[1]
+    N = w.shape[0]
+    _need(a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and bias.dtype == torch.float32, "gemm dtypes")
+    _need(a.stride(1) == 1 and w.stride(1) == 1 and out.stride(-1) == 1 and w.shape[1] == K, "gemm layout")
+    _need(bias.numel() == N and bias.is_contiguous(), "gemm bias")
+    e = EPI[epilogue]
+    if e in (0, 1, 2):
+        _need(out.dtype == torch.bfloat16, "gemm out must be bf16 for this epilogue")
+    else:
+        _need(out.dtype == torch.float32, "gemm out must be f32 for this epilogue")
+    if e == 4:
+        _need(aux is not None and aux.dtype == torch.float32 and aux.stride(1) == 1 and group > 0, "embed aux")
+        _need((M - 1) // group * group_stride + group_offset + (M - 1) % group < out.shape[0], "embed out rows")
+    else:
+        _need(out.shape[0] >= M, "gemm out rows")
+    _need(a.shape[0] >= M, "gemm a rows")
+    aux_p = _p(aux) if aux is not None else None
+    ldaux = aux.stride(0) if aux is not None else 0
+    _lib.call("vc_gemm_bf16", _p(a), a.stride(0), _p(w), w.stride(0), M, N, K, _p(bias), e, _p(out), out.stride(0),
+              aux_p, ldaux, group, group_stride, group_offset, _stream(a))
+    return out
+
+
+def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, out: torch.Tensor,
+              m: int | None = None) -> torch.Tensor:
+    _dev(x, gamma, beta, out)
+    M = x.shape[0] if m is None else m
+    D = x.shape[1]
+    _need(x.dtype == torch.float32 and out.dtype == torch.bfloat16 and x.stride(1) == 1 and out.stride(1) == 1,
+          "layernorm: x f32, out bf16, unit column stride")
+    _need(gamma.numel() == D and beta.numel() == D and out.shape[1] >= D and out.shape[0] >= M, "layernorm shapes")
+    _lib.call("vc_layernorm_f32_bf16", _p(x), x.stride(0), M, D, _p(gamma), _p(beta), eps, _p(out), out.stride(0),
+              _stream(x))
+    return out
+
+
+def attention(qkv: torch.Tensor, B: int, S: int, H: int, scale: float, out: torch.Tensor) -> torch.Tensor:
+    """qkv bf16 [rows, 3*H*64] (q|k|v per token row b*S+s) -> out bf16 [rows, H*64]."""
+    _dev(qkv, out)
+    _need(qkv.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and qkv.stride(1) == 1 and out.stride(1) == 1,
+          "attention dtypes/layout")
+    _need(qkv.shape[1] >= 3 * H * 64 and out.shape[1] >= H * 64, "attention columns")
+    # the kernel reads K/V rows up to (B-1)*S + roundup(S,64) - 1
+    _need(qkv.shape[0] >= (B - 1) * S + (S + 63) // 64 * 64, "attention: qkv needs row padding to a 64-key tile")
+    _need(out.shape[0] >= B * S, "attention out rows")
+    _lib.call("vc_attention_fwd", _p(qkv), qkv.stride(0), B, S, H, 64, scale, _p(out), out.stride(0), _stream(qkv))
+    return out
+
+
+def cls_init(cls: torch.Tensor, pos: torch.Tensor, x: torch.Tensor, B: int, S: int) -> torch.Tensor:
+    _dev(cls, pos, x)
+    D = cls.numel()
+    _need(x.dtype == torch.float32 and x.shape[0] >= B * S and x.shape[1] >= D, "cls_init x")
+    _lib.call("vc_cls_init", _p(cls), _p(pos), _p(x), x.stride(0), B, S, D, _stream(x))
+    return x
+
+
+def cls_head(x: torch.Tensor, B: int, S: int, gamma, beta, eps: float, wc: torch.Tensor, bc: torch.Tensor,
+             out: torch.Tensor | None = None) -> torch.Tensor:
+    _dev(x, gamma, beta, wc, bc)
+    D = gamma.numel()
+    nl = wc.shape[0]
+    _need(wc.dtype == torch.float32 and wc.is_contiguous() and wc.shape[1] == D, "cls_head weight f32 [nl, D]")
+    if out is None:
+        out = torch.empty((B, nl), dtype=torch.float32, device=x.device)
+    _lib.call("vc_cls_head", _p(x), x.stride(0), B, S, D, _p(gamma), _p(beta), eps, _p(wc), _p(bc), nl, _p(out),
+              _stream(x))
+    return out

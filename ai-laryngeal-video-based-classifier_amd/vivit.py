@@ -1,0 +1,267 @@
+"""ViViT-B/16x2 video classifier on the libvclip.so kernels — drop-in for the reference's
+`create_model` (vivit_transformer/vivit_classifier/models/vivit_model.py:4-52), which
+returns an HF `VivitForVideoClassification` called as `model(pixel_values=...)` and
+read through `.logits` (vivit_transformer/vivit_classifier/trainers/trainer.py:141-142,
+vivit_transformer/inference.py:192-193).
+
+Device data layout (one forward of B clips, S = 1 + (T/2)(H/16)(W/16) tokens):
+  rows r = b*S + s, padded to Mpad = roundup(B*S + 128, 256) so every GEMM runs on
+  whole 128-row tiles and attention can read a full 64-key tile past each clip's end;
+  residual stream X   f32  [Mpad, D]          (fp32 residual adds, as the fp32 reference)
+  LN output Y         bf16 [Mpad, D]
+  fused q|k|v         bf16 [Mpad, 3D]
+  attention out O     bf16 [Mpad, D]
+  MLP hidden          bf16 [Mpad, 4D]
+Weights are packed once per device: bf16 [N, K] (nn.Linear layout), q|k|v concatenated,
+fp32 biases / LayerNorm / position table / classifier.
+"""
+from __future__ import annotations
+
+import json
+import math
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import ops
+from .weights import vivit_param_shapes
+
+
+class VivitConfig:
+    """Minimal stand-in for transformers.VivitConfig (fields the path and the reference's
+    checkpoint dict use: trainer.py:281-299 saves config.to_dict(), id2label, label2id)."""
+
+    defaults = dict(image_size=224, num_frames=32, tubelet_size=[2, 16, 16], num_channels=3, hidden_size=768,
+                    num_hidden_layers=12, num_attention_heads=12, intermediate_size=3072, hidden_act="gelu_fast",
+                    hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0, initializer_range=0.02,
+                    layer_norm_eps=1e-6, qkv_bias=True, model_type="vivit")
+
+    def __init__(self, **kw):
+        d = dict(self.defaults)
+        d.update(kw)
+        id2label = d.pop("id2label", None) or {0: "LABEL_0", 1: "LABEL_1"}
+        self.id2label = {int(k): v for k, v in id2label.items()}
+        self.label2id = d.pop("label2id", None) or {v: k for k, v in self.id2label.items()}
+        d.pop("num_labels", None)
+        for k, v in d.items():
+            setattr(self, k, v)
+        self.tubelet_size = list(self.tubelet_size)
+
+    @property
+    def num_labels(self):
+        return len(self.id2label)
+
+    def to_dict(self):
+        d = {k: getattr(self, k) for k in self.defaults}
+        d["id2label"] = {str(k): v for k, v in self.id2label.items()}
+        d["label2id"] = dict(self.label2id)
+        return d
+
+    @classmethod
+    def from_dict(cls, d):
+        return cls(**d)
+
+    def as_shape_cfg(self):
+        return dict(hidden_size=self.hidden_size, intermediate_size=self.intermediate_size,
+                    tubelet_size=self.tubelet_size, num_channels=self.num_channels, num_frames=self.num_frames,
+                    image_size=self.image_size, num_hidden_layers=self.num_hidden_layers,
+                    num_labels=self.num_labels)
+
+    def __repr__(self):
+        return f"VivitConfig({json.dumps(self.to_dict())})"
+
+
+class ClassifierOutput:
+    """Mimics the `.logits` / `.loss` access of transformers' ImageClassifierOutput."""
+
+    def __init__(self, logits, loss=None):
+        self.logits = logits
+        self.loss = loss
+
+    def __getitem__(self, i):
+        return (self.loss, self.logits)[i] if self.loss is not None else (self.logits,)[i]
+
+
+def _round_up(x, m):
+    return (x + m - 1) // m * m
+
+
+class VivitForVideoClassification(torch.nn.Module):
+    """fp32 master parameters in HF naming (state_dict compatible with transformers-5
+    `VivitForVideoClassification`), bf16/fp32 packed device copies for the kernels."""
+
+    def __init__(self, config: VivitConfig):
+        super().__init__()
+        self.config = config
+        c = config
+        if c.hidden_size // c.num_attention_heads != 64:
+            raise ValueError("libvclip attention supports head_dim 64 only")
+        self.params = torch.nn.ParameterDict()
+        self._names = list(vivit_param_shapes(c.as_shape_cfg()).keys())
+        for name, shape in vivit_param_shapes(c.as_shape_cfg()).items():
+            self.params[name.replace(".", "__")] = torch.nn.Parameter(torch.zeros(shape), requires_grad=False)
+        self._packed = None
+        self._ws = {}
+        self.kernel_events = None
+
+    # ---- state dict in HF naming ---------------------------------------------------
+    def hf_state_dict(self):
+        return OrderedDict((n, self.params[n.replace(".", "__")]) for n in self._names)
+
+    def state_dict(self, *a, **k):  # noqa: D401 - HF key names, like the reference's model
+        return OrderedDict((n, p.detach()) for n, p in self.hf_state_dict().items())
+
+    def load_state_dict(self, sd, strict: bool = True):
+        from .checkpoint import convert_state_dict
+        sd = convert_state_dict(sd)
+        missing = [n for n in self._names if n not in sd]
+        unexpected = [k for k in sd if k not in self._names]
+        if strict and (missing or unexpected):
+            raise KeyError(f"load_state_dict: missing={missing[:5]} unexpected={unexpected[:5]}")
+        with torch.no_grad():
+            for n in self._names:
+                if n in sd:
+                    v = sd[n]
+                    v = torch.as_tensor(np.asarray(v)) if not isinstance(v, torch.Tensor) else v
+                    self.params[n.replace(".", "__")].copy_(v.reshape(self.params[n.replace(".", "__")].shape))
+        self._packed = None
+        return missing, unexpected
+
+    def P(self, name):
+        return self.params[name.replace(".", "__")]
+
+    # ---- device packing ----------------------------------------------------------
+    def _pack(self, device):
+        if self._packed is not None and self._packed["device"] == device:
+            return self._packed
+        c = self.config
+        bf = torch.bfloat16
+        f32 = torch.float32
+        P = lambda n: self.P(n).detach().to(device)  # noqa: E731
+        D = c.hidden_size
+        kt, kh, kw = c.tubelet_size
+        pk = {"device": device}
+        pk["w_emb"] = P("vivit.embeddings.patch_embeddings.projection.weight").reshape(D, -1).to(bf).contiguous()
+        pk["b_emb"] = P("vivit.embeddings.patch_embeddings.projection.bias").to(f32).contiguous()
+        pk["pos"] = P("vivit.embeddings.position_embeddings").reshape(-1, D).to(f32).contiguous()
+        pk["cls"] = P("vivit.embeddings.cls_token").reshape(D).to(f32).contiguous()
+        layers = []
+        for i in range(c.num_hidden_layers):
+            p = f"vivit.layers.{i}."
+            L = {}
+            L["ln1_g"] = P(p + "layernorm_before.weight").contiguous()
+            L["ln1_b"] = P(p + "layernorm_before.bias").contiguous()
+            L["ln2_g"] = P(p + "layernorm_after.weight").contiguous()
+            L["ln2_b"] = P(p + "layernorm_after.bias").contiguous()
+            L["w_qkv"] = torch.cat([P(p + f"attention.{n}.weight") for n in ("q_proj", "k_proj", "v_proj")]).to(bf).contiguous()
+            L["b_qkv"] = torch.cat([P(p + f"attention.{n}.bias") for n in ("q_proj", "k_proj", "v_proj")]).contiguous()
+            L["w_o"] = P(p + "attention.o_proj.weight").to(bf).contiguous()
+            L["b_o"] = P(p + "attention.o_proj.bias").contiguous()
+            L["w_1"] = P(p + "mlp.fc1.weight").to(bf).contiguous()
+            L["b_1"] = P(p + "mlp.fc1.bias").contiguous()
+            L["w_2"] = P(p + "mlp.fc2.weight").to(bf).contiguous()
+            L["b_2"] = P(p + "mlp.fc2.bias").contiguous()
+            layers.append(L)
+        pk["layers"] = layers
+        pk["lnf_g"] = P("vivit.layernorm.weight").contiguous()
+        pk["lnf_b"] = P("vivit.layernorm.bias").contiguous()
+        pk["w_cls"] = P("classifier.weight").to(f32).contiguous()
+        pk["b_cls"] = P("classifier.bias").to(f32).contiguous()
+        self._packed = pk
+        return pk
+
+    def geometry(self, B):
+        c = self.config
+        kt, kh, kw = c.tubelet_size
+        npatch = (c.num_frames // kt) * (c.image_size // kh) * (c.image_size // kw)
+        S = npatch + 1
+        Mpad = _round_up(B * S + 128, 256)
+        Memb = _round_up(B * npatch, 128)
+        return npatch, S, Mpad, Memb
+
+    def _workspace(self, B, device):
+        key = (B, str(device))
+        if key in self._ws:
+            return self._ws[key]
+        c = self.config
+        D, I = c.hidden_size, c.intermediate_size
+        kt, kh, kw = c.tubelet_size
+        npatch, S, Mpad, Memb = self.geometry(B)
+        bf = torch.bfloat16
+        z = lambda *s, dt=bf: torch.zeros(s, dtype=dt, device=device)  # noqa: E731
+        ws = dict(A_emb=z(Memb, c.num_channels * kt * kh * kw), X=z(Mpad, D, dt=torch.float32), Y=z(Mpad, D),
+                  QKV=z(Mpad, 3 * D), O=z(Mpad, D), Hd=z(Mpad, I), logits=z(B, c.num_labels, dt=torch.float32))
+        self._ws = {key: ws}  # keep one shape resident
+        return ws
+
+    # ---- forward -----------------------------------------------------------------
+    @torch.no_grad()
+    def forward(self, pixel_values: torch.Tensor = None, labels: torch.Tensor = None, **kw):
+        if pixel_values is None:
+            raise ValueError("pixel_values required")
+        if pixel_values.device.type != "cuda":
+            raise RuntimeError("VivitForVideoClassification (vclip_amd) runs on the GPU only: move pixel_values "
+                               "to cuda (the reference's `.to(device)`, trainer.py:92)")
+        x = pixel_values.contiguous().float() if pixel_values.dtype != torch.float32 else pixel_values.contiguous()
+        logits = self.forward_logits(x)
+        loss = None
+        if labels is not None:
+            loss = torch.nn.functional.cross_entropy(logits, labels.to(logits.device))
+        return ClassifierOutput(logits, loss)
+
+    def forward_logits(self, pix: torch.Tensor) -> torch.Tensor:
+        c = self.config
+        B, T, C, H, W = pix.shape
+        if T != c.num_frames or H != c.image_size or W != c.image_size or C != c.num_channels:
+            raise ValueError(f"pixel_values {tuple(pix.shape)} do not match config "
+                             f"(T={c.num_frames}, C={c.num_channels}, {c.image_size}^2)")
+        pk = self._pack(pix.device)
+        ws = self._workspace(B, pix.device)
+        D = c.hidden_size
+        npatch, S, Mpad, Memb = self.geometry(B)
+        eps = c.layer_norm_eps
+        X, Y, QKV, O, Hd = ws["X"], ws["Y"], ws["QKV"], ws["O"], ws["Hd"]
+        ops.tubelet_im2col(pix, c.tubelet_size, ws["A_emb"])
+        ops.gemm(ws["A_emb"], pk["w_emb"], pk["b_emb"], "embed_f32", X, aux=pk["pos"][1:], group=npatch,
+                 group_stride=S, group_offset=1, m=Memb)
+        ops.cls_init(pk["cls"], pk["pos"], X, B, S)
+        act = "bias_gelu_tanh" if c.hidden_act in ("gelu_fast", "gelu_pytorch_tanh", "gelu_new") else "bias_gelu_erf"
+        scale = 1.0 / math.sqrt(D // c.num_attention_heads)
+        ev = self.kernel_events  # optional per-launch HIP-event timing of the attention kernel (bench.py)
+        for L in pk["layers"]:
+            ops.layernorm(X, L["ln1_g"], L["ln1_b"], eps, Y)
+            ops.gemm(Y, L["w_qkv"], L["b_qkv"], "bias", QKV)
+            if ev is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+            ops.attention(QKV, B, S, c.num_attention_heads, scale, O)
+            if ev is not None:
+                e1.record()
+                ev.append((e0, e1))
+            ops.gemm(O, L["w_o"], L["b_o"], "bias_resid_f32", X)
+            ops.layernorm(X, L["ln2_g"], L["ln2_b"], eps, Y)
+            ops.gemm(Y, L["w_1"], L["b_1"], act, Hd)
+            ops.gemm(Hd, L["w_2"], L["b_2"], "bias_resid_f32", X)
+        return ops.cls_head(X, B, S, pk["lnf_g"], pk["lnf_b"], eps, pk["w_cls"], pk["b_cls"], out=ws["logits"])
+
+
+def create_model(model_name="google/vivit-b-16x2-kinetics400", num_classes=2, class_labels=None, num_frames=32,
+                 device="cuda", logger=None, weights_seed: int = 0):
+    """Drop-in for vivit_transformer/vivit_classifier/models/vivit_model.py:4-52.
+
+    The reference pulls `VivitConfig.from_pretrained(model_name)` and pretrained weights
+    from the HF hub; this image has no network, so the architecture of the named
+    checkpoint (ViViT-B/16x2) is built with seeded synthetic weights (vclip_amd.weights)
+    unless a checkpoint is loaded afterwards with `load_state_dict`.  As in the
+    reference, `num_labels` follows `class_labels` (id2label) and `num_frames` is set.
+    """
+    class_labels = class_labels or ["non-referral", "referral"]
+    id2label = {i: l for i, l in enumerate(class_labels)}
+    cfg = VivitConfig(num_frames=num_frames, id2label=id2label, label2id={l: i for i, l in id2label.items()})
+    if logger:
+        logger.info(f"Creating ViViT model {model_name} (num_frames={num_frames}, labels={class_labels}) on {device}")
+    model = VivitForVideoClassification(cfg)
+    from .weights import make_vivit_weights
+    model.load_state_dict(make_vivit_weights(cfg.as_shape_cfg(), seed=weights_seed))
+    return model.to(device) if device else model

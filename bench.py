@@ -1,0 +1,165 @@
+"""Headline benchmark: clips/sec of the ViViT-B/16x2 forward, 32x224^2 clips, batch 8
+per GPU, bf16 MFMA compute (BASELINE.json `metric`, configs[1]), plus the logit
+max-abs-error vs the fp32 CPU reference and a roofline line for the dominant kernel.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline]
+
+One process per GPU (torch.distributed.run for N > 1, backend nccl = RCCL).  Clips
+shard as independent data-parallel units: each rank runs its own batch and no
+collective touches the hot path; a barrier + device sync bracket the
+timed region and the MAX elapsed over ranks is used.  Inputs (synthetic, seeded, per
+rank) are resident in HBM before timing starts.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+ATTN_GFLOP_PER_CLIP_LAYER = 4.0 * 3137 * 3137 * 64 * 12 / 1e9  # QK^T + PV, 30.23 GF
+VIVIT_GFLOP_PER_CLIP = 903.05   # measured with torch.utils.flop_counter on the HF model
+ATTN_GFLOP_PER_CLIP = 362.77
+PEAK_BF16_TFLOPS = 2500.0       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+
+
+def _dist():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        lr = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(lr)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", lr))
+        return dist, dist.get_rank(), ws, lr
+    return None, 0, 1, 0
+
+
+def cpu_baseline(model_cfg, n_clips, gpu_logits_fn):
+    """The fp32 CPU oracle (oracle/vivit_ref.py, a 'port' of the reference's HF ViViT
+    forward) on the host cores: a bounded sample of `n_clips` clips, one at a time
+    (B=1, as the reference's inference CLI runs).  Also returns the logit error of the
+    GPU path on the same clips."""
+    from oracle.vivit_ref import vivit_forward
+    from vclip_amd.weights import make_synthetic_clips, make_vivit_weights
+
+    sd = {k: torch.from_numpy(v) for k, v in make_vivit_weights(model_cfg, seed=0).items()}
+    pix = make_synthetic_clips(n_clips, model_cfg["num_frames"], model_cfg["image_size"], seed=1)
+    cores = torch.get_num_threads()
+    with torch.no_grad():
+        vivit_forward(sd, model_cfg, torch.from_numpy(pix[:1]))  # warm-up
+        t0 = time.perf_counter()
+        ref = [vivit_forward(sd, model_cfg, torch.from_numpy(pix[i:i + 1])) for i in range(n_clips)]
+        dt = time.perf_counter() - t0
+    ref = torch.cat(ref).numpy()
+    got = gpu_logits_fn(pix)
+    err = float(np.abs(got - ref).max())
+    return {"value": n_clips / dt, "unit": "clips/s", "cores": cores, "kind": "port",
+            "sample": f"{n_clips} clips ViViT-B/16x2 32x224^2 fp32 forward, B=1 each, oracle/vivit_ref.py "
+                      f"(eager attention), torch CPU {cores} threads"}, err
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8, help="clips per GPU per step")
+    ap.add_argument("--cpu-clips", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    a = ap.parse_args()
+
+    dist, rank, world, local = _dist()
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from vclip_amd.vivit import create_model
+    from vclip_amd.weights import make_synthetic_clips
+
+    model = create_model(num_frames=32, device=dev)
+    cfg = model.config
+    pix = torch.from_numpy(make_synthetic_clips(a.batch, 32, 224, seed=1 + rank)).to(dev)
+
+    for _ in range(a.warmup):
+        model.forward_logits(pix)
+    torch.cuda.synchronize()
+
+    model.kernel_events = []
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        model.forward_logits(pix)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    evs = model.kernel_events
+    model.kernel_events = None
+    attn_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+
+    if dist:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    clips = a.batch * a.steps * world
+    value = clips / dt
+    ms_per_step = dt / a.steps * 1e3
+    attn_tflops = ATTN_GFLOP_PER_CLIP_LAYER * a.batch / (attn_ms * 1e-3) / 1e3
+    model_tflops = VIVIT_GFLOP_PER_CLIP * a.batch / (ms_per_step * 1e-3) / 1e3
+
+    out = None
+    if rank == 0:
+        cpu = None
+        logit_err = None
+        if world == 1 and not a.no_cpu_baseline:
+            shape_cfg = dict(cfg.as_shape_cfg(), num_attention_heads=cfg.num_attention_heads,
+                             layer_norm_eps=cfg.layer_norm_eps)
+
+            def gpu_logits(p):
+                return model.forward_logits(torch.from_numpy(p).to(dev)).cpu().numpy().copy()
+
+            cpu, logit_err = cpu_baseline(shape_cfg, a.cpu_clips, gpu_logits)
+        out = {
+            "metric": "clips/sec fwd ViViT-B 32x224^2 bf16",
+            "value": round(value, 2),
+            "unit": "clips/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (uint8 frames RandomState(1+rank) -> ViViT processor affine; weights RandomState(0))",
+            "config": {"workload": "ViViT-B/16x2 forward, 32x224x224 clips, batch 8 per GPU (BASELINE configs[1])",
+                       "model": "ViViT-B/16x2 (joint space-time, 12L, d768, 12H, 3137 tokens)",
+                       "global_batch": a.batch * world, "seq_len": 3137, "parallelism": f"dp{world}"},
+            "logit_max_abs_err": logit_err,
+            "roofline": {"bound": "mfma", "kernel": "attn_fwd_d64_kernel", "achieved": round(attn_tflops, 1),
+                         "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4),
+                         "traffic": None, "avg_launch_ms": round(attn_ms, 4),
+                         "flop_per_launch": f"{ATTN_GFLOP_PER_CLIP_LAYER:.2f} GF/clip x {a.batch} clips"},
+            "model_tflops": round(model_tflops, 1),
+            "model_frac_of_peak": round(model_tflops / PEAK_BF16_TFLOPS, 4),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+    return out
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,122 @@
+/*
+ * vclip.h — C-ABI of libvclip.so, the MI355X (gfx950) kernels of the video-clip
+ * classification hot path.  Plain pointers, sizes and a hipStream_t; no torch types.
+ *
+ * The reference has no FFI: its arithmetic runs inside torch modules built by its model
+ * factories.  Each entry point below replaces one piece of that arithmetic; the
+ * reference interface it stands in for is cited per function.
+ *
+ * Conventions (SURVEY.md §8b "C-ABI"):
+ *   - every pointer is a DEVICE pointer owned by the caller (the library never frees
+ *     caller memory and never allocates in a launch: graph-capture safe);
+ *   - work is enqueued asynchronously on `stream` (pass the caller's current stream);
+ *   - return 0 on success, otherwise a hipError_t or VC_ERR_* code; the message is
+ *     available from vc_last_error() (thread-local);  no exception crosses the ABI;
+ *   - bf16 tensors are passed as uint16_t* (raw bfloat16 bits);
+ *   - single host thread per process, one process per GPU; re-entrant, no global
+ *     mutable device state.
+ */
+#ifndef VCLIP_H_
+#define VCLIP_H_
+
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VC_ERR_INVALID_ARG (-1)
+#define VC_ERR_UNSUPPORTED (-2)
+
+/* Library identity: returns a static string "vclip <version> gfx950". */
+const char* vc_version(void);
+
+/* Thread-local message of the last failing call ("" if none). */
+const char* vc_last_error(void);
+
+/* Output element types of vc_frame_gather. */
+#define VC_GATHER_U8_NHWC   0  /* out u8  [nclips][T][H][W][C]: exact copy of the sampled frames      */
+#define VC_GATHER_F32_NCHW  1  /* out f32 [nclips][T][C][H][W] = x*scale + shift                       */
+#define VC_GATHER_BF16_NCHW 2  /* out bf16[nclips][T][C][H][W] = bf16(x*scale + shift)                 */
+
+/*
+ * Frame-index gather (+ normalise + layout permute).
+ * Replaces: the per-clip frame gather `frames[idx - start_idx]` of
+ *   vivit_transformer/vivit_classifier/data_config/dataset.py:248-265 (u8 mode), and the
+ *   processor affine x/63.75-3 with the [T,H,W,C]->[T,C,H,W] stack of
+ *   vivit_transformer/vivit_classifier/trainers/trainer.py:62-95 (float modes).
+ * frames: u8 [nclips][F][H][W][C] (decoded frames of each clip, F per clip);
+ * idx:    int64 [nclips][T] frame indices, clamped to [0, F-1] like dataset.py:252-253.
+ */
+int vc_frame_gather(const uint8_t* frames, int64_t nclips, int64_t F, int64_t H, int64_t W, int64_t C,
+                    const int64_t* idx, int64_t T, int out_kind, float scale, float shift,
+                    void* out, hipStream_t stream);
+
+/*
+ * Tubelet im2col: pixel_values f32 [B][T][C][H][W] -> A bf16 [B*nt*nh*nw][C*kt*kh*kw]
+ * (row = token in t,h,w order; column = (c,kt,kh,kw) = Conv3d weight order).
+ * Replaces the input side of VivitTubeletEmbeddings (TF5/models/vivit/modeling_vivit.py:64-67).
+ */
+int vc_tubelet_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C, int64_t H, int64_t W,
+                      int kt, int kh, int kw, uint16_t* A, int64_t lda, hipStream_t stream);
+
+/* GEMM epilogues for vc_gemm_bf16. */
+#define VC_EPI_BIAS_BF16        0  /* out bf16[m][n]  = acc + bias[n]                               */
+#define VC_EPI_BIAS_GELU_TANH   1  /* out bf16[m][n]  = gelu_fast(acc + bias[n])  (ViViT MLP fc1)    */
+#define VC_EPI_BIAS_GELU_ERF    2  /* out bf16[m][n]  = gelu_erf(acc + bias[n])   (TimeSformer/Swin) */
+#define VC_EPI_BIAS_RESID_F32   3  /* out f32 [m][n] += acc + bias[n]             (o_proj, fc2)       */
+#define VC_EPI_EMBED_F32        4  /* out f32 [r(m)][n] = acc + bias[n] + aux[m % G][n],
+                                       r(m) = (m / G) * group_stride + group_offset (tubelet -> tokens) */
+
+/*
+ * C[M][N] = A[M][K] . W[N][K]^T  (bf16 inputs, fp32 accumulate on MFMA), fused epilogue.
+ * Replaces torch nn.Linear (cuBLAS addmm) of every q/k/v/o/fc1/fc2 projection
+ * (TF5/models/vivit/modeling_vivit.py:186-189, 229-237) and, with VC_EPI_EMBED_F32, the
+ * Conv3d GEMM + CLS/position add of TF5/.../modeling_vivit.py:64-67,126-146.
+ * Requirements: M % 128 == 0 (callers pad rows), N % 128 == 0, K % 64 == 0,
+ * lda/ldw multiples of 8 elements, 16-byte aligned pointers.
+ */
+int vc_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
+                 int64_t M, int64_t N, int64_t K, const float* bias, int epilogue,
+                 void* out, int64_t ldo, const float* aux, int64_t ldaux,
+                 int64_t G, int64_t group_stride, int64_t group_offset, hipStream_t stream);
+
+/*
+ * Row LayerNorm: y bf16[m][:] = (x[m]-mean)/sqrt(var+eps)*gamma + beta, x f32, stats f32.
+ * Replaces nn.LayerNorm layernorm_before/after (TF5/.../modeling_vivit.py:245-246, 258, 266).
+ */
+int vc_layernorm_f32_bf16(const float* x, int64_t ldx, int64_t M, int64_t D,
+                          const float* gamma, const float* beta, float eps,
+                          uint16_t* y, int64_t ldy, hipStream_t stream);
+
+/*
+ * Fused joint (non-causal) attention forward, head_dim 64, flash-style online softmax
+ * in fp32, MFMA bf16 for Q.K^T and P.V.
+ * qkv: bf16 rows of `ld` elements, row (b*S + s); head h's q at column h*64,
+ *      k at H*64 + h*64, v at 2*H*64 + h*64 (the fused q|k|v projection output).
+ * out: bf16 rows of `ldo` elements, head h at column h*64 (the o_proj input layout).
+ * softmax(scale * q.k) with `scale` = head_dim^-0.5 in ViViT.
+ * Rows of qkv must be readable up to (B-1)*S + roundup(S, 64) - 1 (callers pad).
+ * Replaces eager_attention_forward / SDPA (TF5/.../modeling_vivit.py:149-174, 177-223).
+ */
+int vc_attention_fwd(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, int64_t head_dim,
+                     float scale, uint16_t* out, int64_t ldo, hipStream_t stream);
+
+/* CLS rows: x[b*S][:] = cls[:] + pos[0][:]   (TF5/.../modeling_vivit.py:131-142). */
+int vc_cls_init(const float* cls, const float* pos, float* x, int64_t ldx, int64_t B, int64_t S, int64_t D,
+                hipStream_t stream);
+
+/*
+ * Classifier head on the CLS rows: logits[b][c] = LN(x[b*S])[:] . Wc[c][:] + bc[c] (fp32).
+ * Replaces the final LayerNorm + classifier of TF5/.../modeling_vivit.py:427, 556
+ * (only the CLS row feeds the logits, so only it is normalised).
+ */
+int vc_cls_head(const float* x, int64_t ldx, int64_t B, int64_t S, int64_t D,
+                const float* gamma, const float* beta, float eps,
+                const float* Wc, const float* bc, int64_t num_labels, float* logits, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VCLIP_H_ */

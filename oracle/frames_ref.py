@@ -1,0 +1,35 @@
+"""ORACLE — test infrastructure only.  numpy restatements of the byte/layout work:
+
+* frame gather: `frames[clip][clamp(idx)]` exactly as the reference dataset picks the
+  sampled frames out of a decoded clip (vivit_transformer/vivit_classifier/data_config/
+  dataset.py:248-255, positions clamped to the decoded range), optionally followed by the
+  ViViT processor affine x*(1/63.75) - 3 and the [T,H,W,C] -> [T,C,H,W] stack
+  (trainer.py:62-95; VivitImageProcessor rescale(1/127.5, offset) + normalize(0.5, 0.5));
+* tubelet im2col: the Conv3d k=s=(2,16,16) patch extraction of
+  TF5/models/vivit/modeling_vivit.py:64-67 (token order t,h,w; column order c,kt,kh,kw).
+"""
+import numpy as np
+
+
+def gather_u8(frames, idx):
+    """frames u8 [N,F,H,W,C], idx int [N,T] -> u8 [N,T,H,W,C]."""
+    N, F = frames.shape[:2]
+    idx = np.clip(np.asarray(idx, dtype=np.int64), 0, F - 1)
+    return np.stack([frames[n][idx[n]] for n in range(N)])
+
+
+def gather_norm(frames, idx, scale=np.float32(1.0 / 63.75), shift=np.float32(-3.0)):
+    """-> f32 [N,T,C,H,W] = x*scale + shift computed in fp32 (single rounding per op)."""
+    g = gather_u8(frames, idx).astype(np.float32)
+    y = g * np.float32(scale) + np.float32(shift)
+    return np.ascontiguousarray(y.transpose(0, 1, 4, 2, 3))
+
+
+def tubelet_im2col(pix, tubelet=(2, 16, 16)):
+    """pix f32 [B,T,C,H,W] -> [B*nt*nh*nw, C*kt*kh*kw] (same dtype)."""
+    B, T, C, H, W = pix.shape
+    kt, kh, kw = tubelet
+    x = pix.reshape(B, T // kt, kt, C, H // kh, kh, W // kw, kw)
+    # -> B, nt, nh, nw, C, kt, kh, kw
+    x = x.transpose(0, 1, 4, 6, 3, 2, 5, 7)
+    return np.ascontiguousarray(x.reshape(B * (T // kt) * (H // kh) * (W // kw), C * kt * kh * kw))

@@ -1,0 +1,201 @@
+"""GPU parity tests: each libvclip.so kernel (through the C-ABI via vclip_amd.ops)
+against the CPU oracle on the same seeded inputs.
+
+Tolerances: integer/byte work bit-exact; bf16-output kernels vs an fp32 reference of
+the same bf16-rounded inputs within bf16 rounding (stated per test).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.frames_ref import gather_norm, gather_u8, tubelet_im2col
+from oracle.vivit_ref import attention_ref, gelu_fast
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vclip_amd import _lib as L
+    L.load()
+
+
+def ops():
+    from vclip_amd import ops as O
+    return O
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+# ------------------------------------------------------------------------- frame gather
+@pytest.mark.parametrize("N,F,T,H,W", [(1, 300, 32, 224, 224), (3, 7, 32, 224, 224), (2, 1, 8, 16, 20), (1, 33, 1, 8, 8)])
+def test_frame_gather_u8_bit_exact(N, F, T, H, W):
+    rng = np.random.RandomState(N * 1000 + F)
+    fr = rng.randint(0, 256, size=(N, F, H, W, 3)).astype(np.uint8)
+    idx = rng.randint(-2, F + 3, size=(N, T)).astype(np.int64)  # includes out-of-range -> clamped
+    if (H * W * 3) % 16:
+        pytest.skip("u8 mode needs 16-B frames")
+    out = ops().frame_gather(torch.from_numpy(fr).to(DEV), torch.from_numpy(idx).to(DEV), kind="u8")
+    np.testing.assert_array_equal(out.cpu().numpy(), gather_u8(fr, idx))
+
+
+@pytest.mark.parametrize("N,F,T,H,W", [(2, 40, 32, 224, 224), (1, 5, 8, 16, 20), (1, 3, 4, 6, 6)])
+def test_frame_gather_norm(N, F, T, H, W):
+    rng = np.random.RandomState(7 + F)
+    fr = rng.randint(0, 256, size=(N, F, H, W, 3)).astype(np.uint8)
+    idx = rng.randint(0, F, size=(N, T)).astype(np.int64)
+    ft, it = torch.from_numpy(fr).to(DEV), torch.from_numpy(idx).to(DEV)
+    ref = gather_norm(fr, idx)
+    out = ops().frame_gather(ft, it, kind="f32").cpu().numpy()
+    np.testing.assert_allclose(out, ref, rtol=0, atol=2.5e-7)  # fma vs mul+add: <= 1 ulp at |x|<=3
+    outb = ops().frame_gather(ft, it, kind="bf16").float().cpu().numpy()
+    np.testing.assert_allclose(outb, torch.from_numpy(ref).bfloat16().float().numpy(), rtol=0, atol=1.6e-2)
+
+
+# ------------------------------------------------------------------------- im2col
+@pytest.mark.parametrize("B,T,H", [(1, 4, 32), (2, 32, 224)])
+def test_im2col_bit_exact(B, T, H):
+    rng = np.random.RandomState(B + T)
+    pix = rng.standard_normal((B, T, 3, H, H)).astype(np.float32)
+    n = B * (T // 2) * (H // 16) ** 2
+    out = torch.zeros((n + 64, 1536), dtype=torch.bfloat16, device=DEV)
+    ops().tubelet_im2col(torch.from_numpy(pix).to(DEV), (2, 16, 16), out)
+    ref = torch.from_numpy(tubelet_im2col(pix)).bfloat16()
+    assert torch.equal(out[:n].cpu(), ref)
+    assert out[n:].abs().sum().item() == 0
+
+
+# ------------------------------------------------------------------------- layernorm
+@pytest.mark.parametrize("M,D", [(7, 768), (25344, 768), (3, 256), (130, 1024)])
+def test_layernorm(M, D):
+    g = torch.Generator().manual_seed(M)
+    x = torch.randn(M, D, generator=g) * 3 + 1
+    gam = 1 + 0.1 * torch.randn(D, generator=g)
+    bet = 0.1 * torch.randn(D, generator=g)
+    y = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
+    ops().layernorm(x.to(DEV), gam.to(DEV), bet.to(DEV), 1e-6, y)
+    ref = torch.nn.functional.layer_norm(x, (D,), gam, bet, 1e-6)
+    err = (y.float().cpu() - ref).abs().max().item()
+    assert err <= 2e-2 * max(1.0, ref.abs().max().item()) * 0.5, err  # one bf16 rounding of |y|<~5
+
+
+# ------------------------------------------------------------------------- GEMM
+def _gemm_case(M, N, K, seed):
+    g = torch.Generator().manual_seed(seed)
+    a = bf(torch.randn(M, K, generator=g))
+    w = bf(torch.randn(N, K, generator=g) * 0.05)
+    bias = torch.randn(N, generator=g) * 0.1
+    ref = a.float() @ w.float().T + bias
+    return a, w, bias, ref
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 2304, 768), (384, 768, 3072), (25344, 768, 768)])
+def test_gemm_bias_bf16(M, N, K):
+    a, w, bias, ref = _gemm_case(M, N, K, M + N + K)
+    out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    ops().gemm(a.to(DEV), w.to(DEV), bias.to(DEV), "bias", out)
+    o = out.float().cpu()
+    err = ((o - ref).abs() / (ref.abs() + 1.0)).max().item()
+    assert err < 8e-3, err
+
+
+def test_gemm_orientation_asymmetric():
+    """A = I with an asymmetric W catches a transposed C write (cdna_hip_programming.md §3)."""
+    M = N = K = 128
+    a = torch.eye(M, K, dtype=torch.bfloat16)
+    w = bf(torch.arange(N * K, dtype=torch.float32).reshape(N, K) % 97 - 48)
+    bias = torch.zeros(N)
+    out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    ops().gemm(a.to(DEV), w.to(DEV), bias.to(DEV), "bias", out)
+    assert torch.equal(out.cpu().float(), w.float().T)
+
+
+@pytest.mark.parametrize("act", ["bias_gelu_tanh", "bias_gelu_erf"])
+def test_gemm_gelu(act):
+    M, N, K = 256, 3072, 768
+    a, w, bias, ref = _gemm_case(M, N, K, 11)
+    out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    ops().gemm(a.to(DEV), w.to(DEV), bias.to(DEV), act, out)
+    r = gelu_fast(ref) if act == "bias_gelu_tanh" else torch.nn.functional.gelu(ref)
+    err = ((out.float().cpu() - r).abs() / (r.abs() + 1.0)).max().item()
+    assert err < 8e-3, err
+
+
+def test_gemm_resid_f32():
+    M, N, K = 512, 768, 3072
+    a, w, bias, ref = _gemm_case(M, N, K, 12)
+    x0 = torch.randn(M, N)
+    x = x0.clone().to(DEV)
+    ops().gemm(a.to(DEV), w.to(DEV), bias.to(DEV), "bias_resid_f32", x)
+    np.testing.assert_allclose(x.cpu().numpy(), (x0 + ref).numpy(), rtol=1e-4, atol=1e-4)
+
+
+def test_gemm_embed_remap():
+    """Tubelet GEMM epilogue: row m -> token (m//G)*S + 1 + m%G, + bias + pos[1 + m%G]."""
+    G, B, D, K = 196, 2, 768, 1536
+    S = G + 1
+    M = 512  # >= B*G, multiple of 128
+    a, w, bias, ref = _gemm_case(M, D, K, 13)
+    pos = torch.randn(S, D)
+    out = torch.full((B * S + 512, D), 7.0, device=DEV)
+    ops().gemm(a.to(DEV), w.to(DEV), bias.to(DEV), "embed_f32", out, aux=pos[1:].to(DEV), group=G, group_stride=S,
+               group_offset=1, m=M)
+    o = out.cpu()
+    for m in [0, 1, 195, 196, 200, 391]:
+        r = (m // G) * S + 1 + m % G
+        np.testing.assert_allclose(o[r].numpy(), (ref[m] + pos[1 + m % G]).numpy(), rtol=1e-4, atol=1e-4)
+    assert (o[0] == 7.0).all() and (o[S] == 7.0).all()  # CLS rows untouched
+
+
+# ------------------------------------------------------------------------- attention
+@pytest.mark.parametrize("B,S,H", [(1, 8, 1), (2, 33, 2), (1, 64, 1), (1, 65, 3), (2, 197, 2), (1, 3137, 2),
+                                   (3, 1000, 1)])
+def test_attention(B, S, H):
+    g = torch.Generator().manual_seed(B * 100000 + S * 10 + H)
+    rows = (B - 1) * S + (S + 63) // 64 * 64 + 64
+    qkv = bf(torch.randn(rows, 3 * H * 64, generator=g) * 1.5)
+    out = torch.zeros(rows, H * 64, dtype=torch.bfloat16, device=DEV)
+    scale = 1 / 8.0
+    ops().attention(qkv.to(DEV), B, S, H, scale, out)
+    o = out.float().cpu()
+    q = qkv[: B * S].float().view(B, S, 3, H, 64)
+    ref = attention_ref(q[:, :, 0].transpose(1, 2), q[:, :, 1].transpose(1, 2), q[:, :, 2].transpose(1, 2), scale)
+    ref = ref.transpose(1, 2).reshape(B * S, H * 64)
+    err = (o[: B * S] - ref).abs().max().item()
+    assert err < 2.5e-2, err  # P rounded to bf16 before P.V, output rounded to bf16
+    assert o[B * S:].abs().sum().item() == 0  # nothing written past the last token
+
+
+def test_attention_spike_max_jump():
+    """Force the running max to jump at a late KV tile (online-softmax rescale path)."""
+    B, S, H = 1, 700, 1
+    rows = S + 128
+    qkv = torch.randn(rows, 192) * 0.2
+    qkv[:, 0:64] = 1.0  # all queries identical direction
+    qkv[650, 64:128] = 6.0  # one key, in the 11th tile, dominates
+    qkv = bf(qkv)
+    out = torch.zeros(rows, 64, dtype=torch.bfloat16, device=DEV)
+    ops().attention(qkv.to(DEV), B, S, H, 0.125, out)
+    q = qkv[:S].float().view(1, S, 3, 1, 64)
+    ref = attention_ref(q[:, :, 0].transpose(1, 2), q[:, :, 1].transpose(1, 2), q[:, :, 2].transpose(1, 2), 0.125)
+    err = (out[:S].float().cpu() - ref.transpose(1, 2).reshape(S, 64)).abs().max().item()
+    assert err < 2e-2, err
+
+
+# ------------------------------------------------------------------------- CLS head
+def test_cls_head():
+    B, S, D = 3, 17, 768
+    x = torch.randn(B * S + 5, D)
+    g, b = 1 + 0.1 * torch.randn(D), 0.1 * torch.randn(D)
+    wc, bc = torch.randn(2, D) * 0.02, torch.randn(2) * 0.02
+    out = ops().cls_head(x.to(DEV), B, S, g.to(DEV), b.to(DEV), 1e-6, wc.to(DEV), bc.to(DEV))
+    y = torch.nn.functional.layer_norm(x[::S][:B], (D,), g, b, 1e-6)
+    np.testing.assert_allclose(out.cpu().numpy(), (y @ wc.T + bc).numpy(), rtol=1e-4, atol=1e-5)

@@ -1,0 +1,46 @@
+"""CPU-side checks of the boundary: the C-ABI library builds, loads and exports every
+function include/vclip.h declares (no compute calls without a GPU); the product path
+refuses CPU tensors instead of falling back."""
+import ctypes
+
+import pytest
+import torch
+
+import vclip_amd._lib as L
+from vclip_amd import ops
+from vclip_amd.build import LIB_PATH, build
+
+
+@pytest.fixture(scope="module")
+def lib():
+    build()
+    return L.load()
+
+
+def test_header_symbols_exported(lib):
+    names = L.header_functions()
+    assert len(names) >= 9
+    raw = ctypes.CDLL(LIB_PATH)
+    for n in names:
+        assert hasattr(raw, n), f"{n} declared in vclip.h but not exported"
+        assert n in L.SIGNATURES, f"{n} has no ctypes signature"
+
+
+def test_version_and_error_string(lib):
+    assert lib.vc_version().decode().startswith("vclip")
+    assert lib.vc_last_error() is not None
+
+
+def test_invalid_args_fail_loudly_without_gpu(lib):
+    # shape validation happens before any HIP call: a bad shape returns an error code + message
+    rc = lib.vc_gemm_bf16(None, 0, None, 0, 100, 128, 64, None, 0, None, 0, None, 0, 0, 0, 0, None)
+    assert rc != 0
+    assert "null" in lib.vc_last_error().decode()
+    rc = lib.vc_attention_fwd(ctypes.c_void_p(16), 2304, 1, 10, 12, 128, 0.1, ctypes.c_void_p(16), 768, None)
+    assert rc != 0 and "head_dim" in lib.vc_last_error().decode()
+
+
+def test_ops_reject_cpu_tensors():
+    x = torch.zeros(256, 768)
+    with pytest.raises(L.VclipError):
+        ops.layernorm(x, torch.ones(768), torch.zeros(768), 1e-6, torch.zeros(256, 768, dtype=torch.bfloat16))
