@@ -172,6 +172,27 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
     }
 }
 
+// Generic-width LayerNorm (any D): one wave per row, three passes over the row (L1/L2-resident).
+__global__ void __launch_bounds__(256) layernorm_any_kernel(const float* __restrict__ x, int64_t ldx, int64_t M,
+                                                            int D, const float* __restrict__ g,
+                                                            const float* __restrict__ be, float eps,
+                                                            uint16_t* __restrict__ y, int64_t ldy) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const float* xr = x + row * ldx;
+    float s = 0.f;
+    for (int n = lane; n < D; n += 64) s += xr[n];
+    const float mean = wave_sum(s) / (float)D;
+    float q = 0.f;
+    for (int n = lane; n < D; n += 64) {
+        const float d = xr[n] - mean;
+        q += d * d;
+    }
+    const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
+    for (int n = lane; n < D; n += 64) y[row * ldy + n] = f2bf((xr[n] - mean) * rstd * g[n] + be[n]);
+}
+
 __global__ void cls_init_kernel(const float* __restrict__ cls, const float* __restrict__ pos, float* __restrict__ x,
                                 int64_t ldx, int64_t S, int64_t D) {
     const int64_t b = blockIdx.x;
@@ -278,7 +299,9 @@ int vc_layernorm_f32_bf16(const float* x, int64_t ldx, int64_t M, int64_t D, con
         case 512: layernorm_kernel<2><<<nb, 256, 0, stream>>>(x, ldx, M, gamma, beta, eps, y, ldy); break;
         case 768: layernorm_kernel<3><<<nb, 256, 0, stream>>>(x, ldx, M, gamma, beta, eps, y, ldy); break;
         case 1024: layernorm_kernel<4><<<nb, 256, 0, stream>>>(x, ldx, M, gamma, beta, eps, y, ldy); break;
-        default: return fail(VC_ERR_UNSUPPORTED, "vc_layernorm: D must be 256/512/768/1024");
+        default:
+            if (D <= 0 || D > 65536) return fail(VC_ERR_INVALID_ARG, "vc_layernorm: bad D");
+            layernorm_any_kernel<<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, gamma, beta, eps, y, ldy);
     }
     return check_launch("vc_layernorm_f32_bf16");
 }

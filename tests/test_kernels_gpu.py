@@ -74,7 +74,7 @@ def test_im2col_bit_exact(B, T, H):
 
 
 # ------------------------------------------------------------------------- layernorm
-@pytest.mark.parametrize("M,D", [(7, 768), (25344, 768), (3, 256), (130, 1024)])
+@pytest.mark.parametrize("M,D", [(7, 768), (25344, 768), (3, 256), (130, 1024), (5, 128), (9, 96), (33, 384)])
 def test_layernorm(M, D):
     g = torch.Generator().manual_seed(M)
     x = torch.randn(M, D, generator=g) * 3 + 1
