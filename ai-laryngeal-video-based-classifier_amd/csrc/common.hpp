@@ -36,9 +36,12 @@ __device__ __forceinline__ float bf2f(unsigned short u) {
 }
 
 __device__ __forceinline__ float gelu_tanh(float x) {
-    // gelu_fast: 0.5x(1+tanh(0.7978845608 x (1 + 0.044715 x^2)))  (TF5/activations.py)
+    // gelu_fast: 0.5x(1+tanh(u)), u = 0.7978845608 x (1 + 0.044715 x^2)  (TF5/activations.py)
+    // evaluated as x * sigmoid(2u) = x / (1 + 2^(-2u log2 e)): one v_exp_f32 + one v_rcp_f32
+    // instead of libm tanhf (rel. error ~1e-7, far below the bf16 rounding of the output).
     const float u = 0.7978845608f * x * (1.0f + 0.044715f * x * x);
-    return 0.5f * x * (1.0f + tanhf(u));
+    const float e = __builtin_amdgcn_exp2f(-2.8853900817779268f * u);  // 2*log2(e)
+    return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
 __device__ __forceinline__ float gelu_erf(float x) {
     return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));

@@ -1,41 +1,49 @@
 // bf16 MFMA GEMM with fused epilogues: C[M][N] = A[M][K] . W[N][K]^T (+ epilogue).
 //
 // gfx950 design (cdna_hip_programming.md §5):
-//   * 128x128x64 block tile, 4 waves (2x2), 64x64 per wave = 2x2 v_mfma_f32_32x32x16_bf16;
+//   * 512-thread workgroups (8 waves), block tile BM x BN x 64, wave tile (BM/WM) x (BN/WN)
+//     built from v_mfma_f32_32x32x16_bf16;
 //   * A and W tiles staged HBM->LDS by global_load_lds_dwordx4 (16 B/lane, 1 KiB per
-//     wave-instruction), double-buffered; XOR swizzle of the 16-B chunk applied on the
-//     SOURCE address (LDS image stays lane-linear, §5.4 rule 21) and on the ds_read_b128;
+//     wave-instruction) into a 3-slot LDS ring: tile t+2 is issued while tile t is
+//     computed, and the end-of-tile wait is a COUNTED `s_waitcnt vmcnt(N)` that retires
+//     only tile t+1, followed by a raw s_barrier (no __syncthreads: it would drain the
+//     ring with vmcnt(0)) — §5 "Pipelining across barriers";
+//   * the 16-B chunk XOR swizzle is applied on the SOURCE address (lane-linear LDS image,
+//     §5.4 rule 21) and on every ds_read_b128, so each 16-lane read group hits 16
+//     distinct bank slots;
+//   * fragment registers double-buffered across the four 16-deep k-steps of a tile so
+//     LDS latency overlaps the MFMAs of the previous k-step;
 //   * operands swapped (MFMA A = W rows, B = activation rows) so each lane's accumulator
 //     holds 4 consecutive output columns -> 8/16-byte epilogue stores;
-//   * bijective XCD remap of the block id so one XCD walks a contiguous band of row tiles
-//     (A rows stay in that XCD's L2 across the N tiles).
+//   * bijective XCD remap of the block id: one XCD walks a contiguous band of row tiles,
+//     keeping its A panel in that XCD's L2 across the N tiles (§5.5 T1).
 #include "common.hpp"
+
+#include <cmath>
 
 namespace vc {
 
-constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int TILE_BYTES = BM * BK * 2;  // 16 KiB per operand tile
+constexpr int GBK = 64;
 
-// physical 16-B chunk of logical chunk c in tile row r (128-B rows): spreads the 16 rows a
-// ds_read_b128 lane group touches over all 16 slots of the 256-B bank row.
+// physical 16-B chunk of logical chunk c in LDS row r (128-B rows): the 16 rows one
+// ds_read_b128 lane group touches land on all 16 slots of the 256-B bank row.
 __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
 
-__device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
-                                     (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+// LDS-DMA of 16 B per lane (1 KiB per wave-instruction) to LDS byte address `lds_addr`
+// (wave-uniform, M0).  Issued from inline asm so hipcc's wait-count scoreboard does not
+// see it: with a compiler-visible global_load_lds in the loop hipcc falls back to
+// lgkmcnt(0) before every MFMA; here its ds_read waits stay counted, and the DMA is
+// retired by our own vmcnt(N) (cdna_hip_programming.md §5.7 item 1, glds16_asm recipe).
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_addr) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_addr)
+                 : "memory");
 }
 
-// Stage a 128-row x 64-col bf16 tile (rows r0.., cols k0..) of a row-major matrix into LDS.
-// Wave w fills rows [32w, 32w+32): 4 wave-instructions of 8 rows each.
-__device__ __forceinline__ void stage_tile(const uint16_t* __restrict__ g, int64_t ld, int64_t r0, int64_t k0,
-                                           char* lds_tile, int wave, int lane) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int row = wave * 32 + i * 8 + (lane >> 3);
-        const int c = swz(row, lane & 7);
-        const uint16_t* src = g + (r0 + row) * ld + k0 + c * 8;
-        glds16(src, lds_tile + (wave * 32 + i * 8) * 128);
-    }
+__device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
 __device__ __forceinline__ v8bf lds_frag(const char* tile, int row, int chunk) {
@@ -43,74 +51,36 @@ __device__ __forceinline__ v8bf lds_frag(const char* tile, int row, int chunk) {
     return __builtin_bit_cast(v8bf, v);
 }
 
-template <int EPI>
-__global__ void __launch_bounds__(256, 2)
-gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
-                 int nbm, int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
-                 const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride, int64_t goff) {
-    __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];
+// s_waitcnt through the builtin (not inline asm) so the compiler's own wait-count
+// scoreboard sees it: simm16 = vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14].
+template <int NW>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(NW >= 0 && NW < 64, "vmcnt immediate");
+    __builtin_amdgcn_s_waitcnt((NW & 15) | ((NW >> 4) << 14) | 0x0F70);  // vmcnt(NW) only
+}
 
-    // XCD-aware bijective remap (blocks b and b+8 share an XCD under round-robin dispatch)
-    const int nwg = nbm * nbn;
-    const int bid = blockIdx.x;
-    const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
-    const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
-    const int tm = wgid / nbn, tn = wgid % nbn;
-    const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+__device__ __forceinline__ void block_sync_lds() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");  // compiler fence: LDS was written by DMA behind its back
+    __builtin_amdgcn_sched_barrier(0);
+}
 
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
-    const int r = lane & 31, h = lane >> 5;
-
-    v16f acc[2][2];
+// Epilogue shared by the GEMM kernels.  acc[i][j] holds D[n][m] of a 32x32 block:
+// lane -> m = mb + 32i + r; reg 4g+e -> n = nb + 32j + 8g + 4h + e (4 consecutive columns).
+template <int EPI, int MI, int NI>
+__device__ __forceinline__ void store_tile(const v16f (&acc)[MI][NI], int64_t mb, int64_t nb, int r, int h,
+                                           const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
+                                           const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride,
+                                           int64_t goff) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MI; ++i) {
+        const int64_t m = mb + i * 32 + r;
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-    const int nk = K / BK;
-    stage_tile(A, lda, m0, 0, smem, wave, lane);
-    stage_tile(W, ldw, n0, 0, smem + TILE_BYTES, wave, lane);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        char* At = smem + cur * 2 * TILE_BYTES;
-        char* Wt = At + TILE_BYTES;
-        if (kt + 1 < nk) {
-            char* An = smem + (cur ^ 1) * 2 * TILE_BYTES;
-            stage_tile(A, lda, m0, (int64_t)(kt + 1) * BK, An, wave, lane);
-            stage_tile(W, ldw, n0, (int64_t)(kt + 1) * BK, An + TILE_BYTES, wave, lane);
-        }
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            const int ch = kk * 2 + h;
-            v8bf wf0 = lds_frag(Wt, wn * 64 + r, ch);
-            v8bf wf1 = lds_frag(Wt, wn * 64 + 32 + r, ch);
-            v8bf af0 = lds_frag(At, wm * 64 + r, ch);
-            v8bf af1 = lds_frag(At, wm * 64 + 32 + r, ch);
-            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf0, af0, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf1, af0, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf0, af1, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf1, af1, acc[1][1], 0, 0, 0);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-
-    // Epilogue.  acc[i][j] holds D[n][m]: lane -> m = ..+ i*32 + r; reg 4g+e -> n = ..+ j*32 + 8g + 4h + e.
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int64_t m = m0 + wm * 64 + i * 32 + r;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < NI; ++j) {
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                const int64_t n = n0 + wn * 64 + j * 32 + g * 8 + h * 4;
+                const int64_t n = nb + j * 32 + g * 8 + h * 4;
                 const float4 bb = *reinterpret_cast<const float4*>(bias + n);
                 float v0 = acc[i][j][4 * g + 0] + bb.x;
                 float v1 = acc[i][j][4 * g + 1] + bb.y;
@@ -143,16 +113,613 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
     }
 }
 
+template <int BM, int BN, int WM, int WN, int EPI>
+__global__ void __launch_bounds__(512, 1)
+gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
+                 int nbm, int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
+                 const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride, int64_t goff) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int ST = 3;                       // LDS ring depth (tiles)
+    constexpr int SLOT = (BM + BN) * 128;       // bytes per ring slot (A then W, 128-B rows)
+    constexpr int TM = BM / WM, TN = BN / WN;   // wave tile
+    constexpr int MI = TM / 32, NI = TN / 32;
+    constexpr int AL = BM / 64, BL = BN / 64;   // glds per thread per tile (8 rows per wave-instr, 8 waves)
+    constexpr int LPT = AL + BL;
+    static_assert(WM * WN == 8 && TM % 32 == 0 && TN % 32 == 0, "8 waves, 32-multiple wave tiles");
+
+    const int nwg = nbm * nbn;
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+    const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+    const int tm = wgid / nbn, tn = wgid % nbn;
+    const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WN, wn = wave % WN;
+    const int r = lane & 31, h = lane >> 5;
+
+    // per-lane staging sources (k offset added per tile)
+    const uint16_t* asrc[AL];
+    const uint16_t* bsrc[BL];
+#pragma unroll
+    for (int i = 0; i < AL; ++i) {
+        const int row = wave * (BM / 8) + i * 8 + (lane >> 3);
+        asrc[i] = A + (m0 + row) * lda + swz(row, lane & 7) * 8;
+    }
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+        const int row = wave * (BN / 8) + i * 8 + (lane >> 3);
+        bsrc[i] = W + (n0 + row) * ldw + swz(row, lane & 7) * 8;
+    }
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
+    auto stage = [&](int t, int slot) {
+        const uint32_t s = lds0 + slot * SLOT;
+        const int64_t k0 = (int64_t)t * GBK;
+#pragma unroll
+        for (int i = 0; i < AL; ++i)
+            glds16(asrc[i] + k0, __builtin_amdgcn_readfirstlane(s + (wave * (BM / 8) + i * 8) * 128));
+#pragma unroll
+        for (int i = 0; i < BL; ++i)
+            glds16(bsrc[i] + k0, __builtin_amdgcn_readfirstlane(s + BM * 128 + (wave * (BN / 8) + i * 8) * 128));
+    };
+
+    v16f acc[MI][NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    const int nk = K / GBK;
+    stage(0, 0);
+    if (nk > 1) {
+        stage(1, 1);
+        wait_vm<LPT>();
+    } else {
+        wait_vm<0>();
+    }
+    block_sync_lds();
+
+    for (int t = 0; t < nk; ++t) {
+        const int slot = t % ST;
+        if (t + 2 < nk) stage(t + 2, (t + 2) % ST);
+        const char* At = smem + slot * SLOT;
+        const char* Wt = At + BM * 128;
+
+        v8bf af[2][MI], wf[2][NI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) af[0][i] = lds_frag(At, wm * TM + i * 32 + r, h);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) wf[0][j] = lds_frag(Wt, wn * TN + j * 32 + r, h);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const int cb = kk & 1, nb = cb ^ 1;
+            if (kk < 3) {
+                const int ch = (kk + 1) * 2 + h;
+#pragma unroll
+                for (int i = 0; i < MI; ++i) af[nb][i] = lds_frag(At, wm * TM + i * 32 + r, ch);
+#pragma unroll
+                for (int j = 0; j < NI; ++j) wf[nb][j] = lds_frag(Wt, wn * TN + j * 32 + r, ch);
+            }
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+                for (int j = 0; j < NI; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[cb][j], af[cb][i], acc[i][j], 0, 0, 0);
+        }
+        // retire tile t+1 (tile t+2 may stay in flight), then all waves pass the barrier
+        if (t + 2 < nk) wait_vm<LPT>();
+        else wait_vm<0>();
+        block_sync_lds();
+    }
+
+    store_tile<EPI, MI, NI>(acc, m0 + wm * TM, n0 + wn * TN, r, h, bias, out, ldo, aux, ldaux, G, gstride, goff);
+}
+
+// ---------------------------------------------------------------------------------
+// 256x256 block tile, BK = 32 half-tiles in a 4-slot LDS ring (4 x 32 KiB).  Eight waves
+// as 2 (rows) x 4 (cols), wave tile 128 x 64 = 4 x 2 blocks of 32x32x16 MFMAs.  Half-tile
+// t+3 is issued while t is computed; the end-of-step wait retires only t+1
+// (vmcnt(8): t+2 and t+3 stay in flight across the barrier).  64-B LDS rows; the chunk
+// swizzle c ^ ((row >> 2) & 3) makes every ds_read_b128 lane group conflict-free.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ int swz64(int r, int c) { return c ^ ((r >> 2) & 3); }
+
+__device__ __forceinline__ v8bf lds_frag64(const char* tile, int row, int chunk) {
+    const v8s v = *reinterpret_cast<const v8s*>(tile + row * 64 + swz64(row, chunk) * 16);
+    return __builtin_bit_cast(v8bf, v);
+}
+
+template <int EPI, int ABL = 0>  // ABL: ablation bits for timing studies (1: no loop loads, 2: no MFMA)
+__global__ void __launch_bounds__(512, 1)
+gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
+                     int nbm, int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
+                     const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride, int64_t goff) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int BM = 256, BN = 256, BKH = 32, NS = 4;
+    constexpr int SLOT = (BM + BN) * 64;   // 32 KiB
+    constexpr int TM = 128, TN = 64, MI = 4, NI = 2;
+
+    const int nwg = nbm * nbn;
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
+    const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+    const int tm = wgid / nbn, tn = wgid % nbn;
+    const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int r = lane & 31, h = lane >> 5;
+
+    // staging: wave w fills A rows [32w, 32w+32) and W rows [32w, 32w+32), 16 rows per glds
+    const uint16_t* asrc[2];
+    const uint16_t* bsrc[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int row = wave * 32 + i * 16 + (lane >> 2);
+        const int c = swz64(row, lane & 3);
+        asrc[i] = A + (m0 + row) * lda + c * 8;
+        bsrc[i] = W + (n0 + row) * ldw + c * 8;
+    }
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
+    auto stage = [&](int t) {
+        const uint32_t s = lds0 + (t % NS) * SLOT;
+        const int64_t k0 = (int64_t)t * BKH;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) glds16(asrc[i] + k0, __builtin_amdgcn_readfirstlane(s + (wave * 32 + i * 16) * 64));
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            glds16(bsrc[i] + k0, __builtin_amdgcn_readfirstlane(s + BM * 64 + (wave * 32 + i * 16) * 64));
+    };
+
+    v16f acc[MI][NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    const int nk = K / BKH;
+    // fragments of one 16-deep k-step (kk) of half-tile t
+    auto read_frags = [&](int t, int kk, v8bf (&fa)[MI], v8bf (&fw)[NI]) {
+        if constexpr (ABL & 8) {  // timing ablation: no LDS fragment reads
+#pragma unroll
+            for (int i = 0; i < MI; ++i) {
+                v8s z = {(short)t, (short)kk, 0, 0, 0, 0, 0, (short)i};
+                fa[i] = __builtin_bit_cast(v8bf, z);
+            }
+#pragma unroll
+            for (int j = 0; j < NI; ++j) {
+                v8s z = {(short)kk, (short)t, 0, 0, 0, 0, 0, (short)j};
+                fw[j] = __builtin_bit_cast(v8bf, z);
+            }
+            return;
+        }
+        const char* At = smem + (t % NS) * SLOT;
+        const char* Wt = At + BM * 64;
+        const int ch = kk * 2 + h;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) fa[i] = lds_frag64(At, wm * TM + i * 32 + r, ch);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) fw[j] = lds_frag64(Wt, wn * TN + j * 32 + r, ch);
+    };
+    auto mfmas = [&](const v8bf (&fa)[MI], const v8bf (&fw)[NI]) {
+        if constexpr (ABL & 2) {
+#pragma unroll
+            for (int i = 0; i < MI; ++i) asm volatile("" ::"v"(fa[i]));
+#pragma unroll
+            for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(fw[j]));
+            return;
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[j], fa[i], acc[i][j], 0, 0, 0);
+    };
+    // 6 fragment reads ride between 8 MFMAs
+    auto interleave = [&]() {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    };
+
+    // prologue: half-tiles 0..2 in flight; wait for 0, read its first k-step
+    v8bf fa0[MI], fw0[NI], fa1[MI], fw1[NI];
+    stage(0);
+    if (nk > 1) stage(1);
+    if (nk > 2) stage(2);
+    if (nk > 2) wait_vm<8>();
+    else if (nk > 1) wait_vm<4>();
+    else wait_vm<0>();
+    block_sync_lds();
+    read_frags(0, 0, fa0, fw0);
+
+    // software pipeline: k-step 0 MFMAs overlap the k-step-1 reads of the same half-tile;
+    // k-step 1 MFMAs overlap the k-step-0 reads of the next half-tile, which is
+    // published by the one barrier per half-tile (vmcnt retires only tile t+1).
+    // (the last half-tile is peeled so the loop body has no join in front of its MFMAs:
+    // a join makes hipcc's wait-count merge fall back to lgkmcnt(0))
+    for (int t = 0; t < nk - 1; ++t) {
+        if (!(ABL & 1) && t + 3 < nk) stage(t + 3);
+        read_frags(t, 1, fa1, fw1);
+        mfmas(fa0, fw0);
+        interleave();
+        if (t + 3 < nk) wait_vm<8>();
+        else if (t + 2 < nk) wait_vm<4>();
+        else wait_vm<0>();
+        block_sync_lds();
+        read_frags(t + 1, 0, fa0, fw0);
+        mfmas(fa1, fw1);
+        interleave();
+    }
+    read_frags(nk - 1, 1, fa1, fw1);
+    mfmas(fa0, fw0);
+    mfmas(fa1, fw1);
+    if constexpr (ABL & 4) {  // timing ablation: no epilogue
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(acc[i][j]));
+        return;
+    }
+    store_tile<EPI, MI, NI>(acc, m0 + wm * TM, n0 + wn * TN, r, h, bias, out, ldo, aux, ldaux, G, gstride, goff);
+}
+
+// ---------------------------------------------------------------------------------
+// Persistent variant of the 256x256 kernel for the bf16-output epilogues (q|k|v, fc1):
+// one workgroup per CU walks its tiles; the next tile's first three half-tiles are put in
+// flight BEFORE the current tile's epilogue, so the epilogue stores (and the prologue
+// latency) hide behind the next tile's loads.  The bias lives in LDS (no VMEM in the
+// epilogue, so the counted vmcnt stays exact), and each lane's 4+4 columns are merged
+// with v_permlane32_swap into 16-byte stores (cdna_hip_programming.md T21).
+// ---------------------------------------------------------------------------------
+template <int EPI, int ABL = 0>  // ABL: timing ablations (1 no loop loads, 2 no MFMA, 4 no stores, 8 no LDS reads)
+__global__ void __launch_bounds__(512, 1)
+gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
+                         int nbm, int nbn, int K, int N, const float* __restrict__ bias, uint16_t* __restrict__ out,
+                         int64_t ldo) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int BM = 256, BN = 256, BKH = 32, NS = 4;
+    constexpr int SLOT = (BM + BN) * 64;   // 32 KiB
+    constexpr int TM = 128, TN = 64, MI = 4, NI = 2;
+    constexpr int NST = MI * NI * 2;       // 16-B stores per wave per tile epilogue
+    float* bias_lds = reinterpret_cast<float*>(smem + NS * SLOT);
+
+    const int ntiles = nbm * nbn;
+    const int G = gridDim.x;               // multiple of 8 (host guarantees)
+    const int b = blockIdx.x;
+    const int lane_slot = (b & 7) * (G >> 3) + (b >> 3);  // XCD-contiguous slot of this WG in a round
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int r = lane & 31, h = lane >> 5;
+
+    // bias -> LDS once
+    for (int n = tid * 4; n < N; n += 512 * 4)
+        *reinterpret_cast<float4*>(bias_lds + n) = *reinterpret_cast<const float4*>(bias + n);
+    __syncthreads();
+
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
+    const int nk = K / BKH;
+    const int arow = wave * 32 + (lane >> 2);           // staging row (+16 for the second piece)
+    const int acol0 = swz64(arow, lane & 3) * 8;
+    const int acol1 = swz64(arow + 16, lane & 3) * 8;
+
+    auto stage = [&](int64_t m0, int64_t n0, int t, int slotidx) {
+        if constexpr (ABL & 1) {
+            if (t >= 3) return;
+        }
+        const uint32_t s = lds0 + (slotidx % NS) * SLOT;
+        const int64_t k0 = (int64_t)t * BKH;
+        glds16(A + (m0 + arow) * lda + k0 + acol0, __builtin_amdgcn_readfirstlane(s + (wave * 32) * 64));
+        glds16(A + (m0 + arow + 16) * lda + k0 + acol1, __builtin_amdgcn_readfirstlane(s + (wave * 32 + 16) * 64));
+        glds16(W + (n0 + arow) * ldw + k0 + acol0, __builtin_amdgcn_readfirstlane(s + BM * 64 + (wave * 32) * 64));
+        glds16(W + (n0 + arow + 16) * ldw + k0 + acol1,
+               __builtin_amdgcn_readfirstlane(s + BM * 64 + (wave * 32 + 16) * 64));
+    };
+    auto read_frags = [&](int slotidx, int kk, v8bf (&fa)[MI], v8bf (&fw)[NI]) {
+        if constexpr (ABL & 8) {
+#pragma unroll
+            for (int i = 0; i < MI; ++i) {
+                v8s z = {(short)slotidx, (short)kk, 0, 0, 0, 0, 0, (short)i};
+                fa[i] = __builtin_bit_cast(v8bf, z);
+            }
+#pragma unroll
+            for (int j = 0; j < NI; ++j) {
+                v8s z = {(short)kk, (short)slotidx, 0, 0, 0, 0, 0, (short)j};
+                fw[j] = __builtin_bit_cast(v8bf, z);
+            }
+            return;
+        }
+        const char* At = smem + (slotidx % NS) * SLOT;
+        const char* Wt = At + BM * 64;
+        const int ch = kk * 2 + h;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) fa[i] = lds_frag64(At, wm * TM + i * 32 + r, ch);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) fw[j] = lds_frag64(Wt, wn * TN + j * 32 + r, ch);
+    };
+    v16f acc[MI][NI];
+    auto mfmas = [&](const v8bf (&fa)[MI], const v8bf (&fw)[NI]) {
+        if constexpr (ABL & 2) {
+#pragma unroll
+            for (int i = 0; i < MI; ++i) asm volatile("" ::"v"(fa[i]));
+#pragma unroll
+            for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(fw[j]));
+            return;
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[j], fa[i], acc[i][j], 0, 0, 0);
+    };
+    auto interleave = [&]() {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    };
+    auto tile_origin = [&](int it, int64_t& m0, int64_t& n0) {
+        const int tile = it * G + lane_slot;
+        const int tm = tile / nbn, tn = tile - (tile / nbn) * nbn;
+        m0 = (int64_t)tm * BM;
+        n0 = (int64_t)tn * BN;
+    };
+
+    int it = 0;
+    if (it * G + lane_slot >= ntiles) return;
+    int64_t m0, n0;
+    tile_origin(0, m0, n0);
+    int sbase = 0;  // ring slot of this tile's half-tile 0
+    stage(m0, n0, 0, sbase + 0);
+    stage(m0, n0, 1, sbase + 1);
+    stage(m0, n0, 2, sbase + 2);
+    wait_vm<8>();
+    block_sync_lds();
+    v8bf fa0[MI], fw0[NI], fa1[MI], fw1[NI];
+    read_frags(sbase, 0, fa0, fw0);
+    bool first = true;
+
+    while (true) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+        // half-tiles 0 and 1: the previous epilogue's NST stores are younger than t+1
+        for (int t = 0; t < 2; ++t) {
+            stage(m0, n0, t + 3, sbase + t + 3);
+            read_frags(sbase + t, 1, fa1, fw1);
+            mfmas(fa0, fw0);
+            interleave();
+            if (first) wait_vm<8>();
+            else wait_vm<8 + NST>();
+            block_sync_lds();
+            read_frags(sbase + t + 1, 0, fa0, fw0);
+            mfmas(fa1, fw1);
+            interleave();
+        }
+        for (int t = 2; t < nk - 1; ++t) {
+            if (t + 3 < nk) stage(m0, n0, t + 3, sbase + t + 3);
+            read_frags(sbase + t, 1, fa1, fw1);
+            mfmas(fa0, fw0);
+            interleave();
+            if (t + 3 < nk) wait_vm<8>();
+            else if (t + 2 < nk) wait_vm<4>();
+            else wait_vm<0>();
+            block_sync_lds();
+            read_frags(sbase + t + 1, 0, fa0, fw0);
+            mfmas(fa1, fw1);
+            interleave();
+        }
+        read_frags(sbase + nk - 1, 1, fa1, fw1);
+        mfmas(fa0, fw0);
+        mfmas(fa1, fw1);
+
+        // next tile's first three half-tiles go in flight before this tile's epilogue
+        ++it;
+        const bool more = it * G + lane_slot < ntiles;
+        int64_t nm0 = 0, nn0 = 0;
+        const int nbase = sbase + nk;
+        if (more) {
+            tile_origin(it, nm0, nn0);
+            stage(nm0, nn0, 0, nbase + 0);
+            stage(nm0, nn0, 1, nbase + 1);
+            stage(nm0, nn0, 2, nbase + 2);
+        }
+
+        // epilogue: + bias (LDS), activation, bf16, lane-pair swap -> 16-B row stores
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            const int64_t m = m0 + wm * TM + i * 32 + r;
+            uint16_t* orow = out + m * ldo;
+#pragma unroll
+            for (int j = 0; j < NI; ++j) {
+                unsigned pk[4][2];
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int nl = (int)n0 + wn * TN + j * 32 + g * 8 + h * 4;
+                    const float4 bb = *reinterpret_cast<const float4*>(bias_lds + nl);
+                    float v0 = acc[i][j][4 * g + 0] + bb.x;
+                    float v1 = acc[i][j][4 * g + 1] + bb.y;
+                    float v2 = acc[i][j][4 * g + 2] + bb.z;
+                    float v3 = acc[i][j][4 * g + 3] + bb.w;
+                    if (EPI == VC_EPI_BIAS_GELU_TANH) {
+                        v0 = gelu_tanh(v0); v1 = gelu_tanh(v1); v2 = gelu_tanh(v2); v3 = gelu_tanh(v3);
+                    } else if (EPI == VC_EPI_BIAS_GELU_ERF) {
+                        v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+                    }
+                    pk[g][0] = pack2bf(v0, v1);
+                    pk[g][1] = pack2bf(v2, v3);
+                }
+#pragma unroll
+                for (int g = 0; g < 4; g += 2) {
+                    // lower half: cols 8g..8g+7 (own g | upper's g); upper half: 8g+8..8g+15
+                    auto s0 = __builtin_amdgcn_permlane32_swap(pk[g][0], pk[g + 1][0], false, false);
+                    auto s1 = __builtin_amdgcn_permlane32_swap(pk[g][1], pk[g + 1][1], false, false);
+                    const int64_t col = n0 + wn * TN + j * 32 + g * 8 + h * 8;
+                    uint4 v;
+                    v.x = s0[0]; v.y = s1[0]; v.z = s0[1]; v.w = s1[1];
+                    if constexpr (ABL & 4) asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w), "v"(orow + col));
+                    else *reinterpret_cast<uint4*>(orow + col) = v;
+                }
+            }
+        }
+        if (!more) break;
+        first = false;
+        m0 = nm0;
+        n0 = nn0;
+        sbase = nbase;
+        // half-tile 0 of the new tile (older than its half-tiles 1, 2 and the NST stores)
+        wait_vm<8 + NST>();
+        block_sync_lds();
+        read_frags(sbase, 0, fa0, fw0);
+    }
+}
+
+// Tile configurations (BM, BN, WM, WN).
+struct GemmCfg {
+    int bm, bn;
+};
+static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}};
+constexpr int kNumCfgs = 5;
+
+template <int BM, int BN, int WM, int WN, int E>
+static int launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
+                      const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
+                      int64_t gs, int64_t go, hipStream_t stream) {
+    constexpr int lds = 3 * (BM + BN) * 128;
+    static bool attr_set = false;  // per instantiation; benign race (idempotent)
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, WM, WN, E>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
+        attr_set = true;
+    }
+    gemm_bf16_kernel<BM, BN, WM, WN, E><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(
+        A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go);
+    return check_launch("vc_gemm_bf16");
+}
+
+template <int E, int ABL = 0>
+static int launch_big(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
+                      const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
+                      int64_t gs, int64_t go, hipStream_t stream) {
+    constexpr int lds = 4 * 512 * 64;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_big_kernel<E, ABL>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
+        attr_set = true;
+    }
+    gemm_bf16_big_kernel<E, ABL><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo,
+                                                                          aux, ldaux, G, gs, go);
+    return check_launch("vc_gemm_bf16");
+}
+
+static int num_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, dev) == hipSuccess) n = p.multiProcessorCount;
+        if (n <= 0) n = 256;
+    }
+    return n;
+}
+
+template <int E, int ABL = 0>
+static int launch_persist(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
+                          int N, const float* bias, void* out, int64_t ldo, hipStream_t stream) {
+    const int lds = 4 * 512 * 64 + N * 4;
+    static int attr_set = 0;
+    if (attr_set < lds) {
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_persist_kernel<E, ABL>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
+        attr_set = 160 * 1024;
+    }
+    const int ntiles = nbm * nbn;
+    int grid = num_cus() / 8 * 8;
+    if (grid > (ntiles + 7) / 8 * 8) grid = (ntiles + 7) / 8 * 8;
+    gemm_bf16_persist_kernel<E, ABL><<<(unsigned)grid, 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, N, bias,
+                                                                      (uint16_t*)out, ldo);
+    return check_launch("vc_gemm_bf16");
+}
+
+template <int E>
+static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int64_t M, int64_t N,
+                      int K, const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
+                      int64_t gs, int64_t go, hipStream_t s) {
+    const int bm = kCfgs[cfg >= 10 ? 3 : cfg].bm, bn = kCfgs[cfg >= 10 ? 3 : cfg].bn;  // x3/x4 ablations: 256x256
+    const int nbm = (int)(M / bm), nbn = (int)(N / bn);
+    switch (cfg) {
+        case 0: return launch_cfg<256, 128, 4, 2, E>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 1: return launch_cfg<128, 128, 2, 4, E>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 2: return launch_cfg<128, 256, 2, 4, E>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 3: return launch_big<E>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 4:
+            if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF)
+                return launch_persist<E>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
+            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 4 supports bf16-output epilogues only");
+        case 14: return launch_persist<E, 1>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
+        case 24: return launch_persist<E, 2>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
+        case 44: return launch_persist<E, 4>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
+        case 84: return launch_persist<E, 8>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
+        case 64: return launch_persist<E, 6>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
+        case 74: return launch_persist<E, 7>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
+        case 154: return launch_persist<E, 15>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
+        case 13: return launch_big<E, 1>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 23: return launch_big<E, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 33: return launch_big<E, 3>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 43: return launch_big<E, 4>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 73: return launch_big<E, 7>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 83: return launch_big<E, 8>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 153: return launch_big<E, 15>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+    }
+    return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad config");
+}
+
+// Default tile choice (measured on MI355X at the ViViT-B/16x2 B=8 projection shapes,
+// tools/tune_gemm.py): the persistent 256x256 kernel whenever the epilogue is a bf16 store
+// and the grid is at least two rounds of 256 tiles; otherwise 128x256 (fc2-like, N = 768,
+// long K) or 128x128.
+static int pick_cfg(int64_t M, int64_t N, int64_t K, int epi) {
+    const bool bf16_out = epi == VC_EPI_BIAS_BF16 || epi == VC_EPI_BIAS_GELU_TANH || epi == VC_EPI_BIAS_GELU_ERF;
+    if (bf16_out && M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && K >= 192 && N <= 8192 &&
+        (M / 256) * (N / 256) >= 512)
+        return 4;
+    if (M % 128 == 0 && N % 256 == 0 && K >= 1536) return 2;
+    if (M % 256 == 0 && N % 128 == 0 && (M / 256) * (N / 128) >= 1024) return 0;
+    return 1;
+}
+
 }  // namespace vc
 
 using namespace vc;
 
-extern "C" int vc_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int64_t M, int64_t N,
-                            int64_t K, const float* bias, int epilogue, void* out, int64_t ldo, const float* aux,
-                            int64_t ldaux, int64_t G, int64_t group_stride, int64_t group_offset,
-                            hipStream_t stream) {
+extern "C" int vc_gemm_bf16_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int64_t M, int64_t N,
+                                int64_t K, const float* bias, int epilogue, void* out, int64_t ldo, const float* aux,
+                                int64_t ldaux, int64_t G, int64_t group_stride, int64_t group_offset, int cfg,
+                                hipStream_t stream) {
     if (!A || !W || !bias || !out) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: null pointer");
-    if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % BK)
+    if (M <= 0 || N <= 0 || K <= 0 || M % 128 || N % 128 || K % GBK)
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: need M%128==0, N%128==0, K%64==0 (got M=" +
                                             std::to_string(M) + " N=" + std::to_string(N) + " K=" + std::to_string(K) + ")");
     if (lda % 8 || ldw % 8 || ldo % 4 || lda < K || ldw < K || ldo < N)
@@ -161,20 +728,38 @@ extern "C" int vc_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, i
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: pointers must be 16-byte aligned");
     if (epilogue == VC_EPI_EMBED_F32 && (!aux || G <= 0 || ldaux % 4))
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: EMBED epilogue needs aux, G > 0");
-    const int nbm = (int)(M / BM), nbn = (int)(N / BN);
-    const int64_t nwg = (int64_t)nbm * nbn;
-    if (nwg > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: grid too large");
-#define VC_LAUNCH(E)                                                                                              \
-    gemm_bf16_kernel<E><<<(unsigned)nwg, 256, 0, stream>>>(A, lda, W, ldw, nbm, nbn, (int)K, bias, out, ldo, aux, \
-                                                          ldaux, G, group_stride, group_offset)
-    switch (epilogue) {
-        case VC_EPI_BIAS_BF16: VC_LAUNCH(VC_EPI_BIAS_BF16); break;
-        case VC_EPI_BIAS_GELU_TANH: VC_LAUNCH(VC_EPI_BIAS_GELU_TANH); break;
-        case VC_EPI_BIAS_GELU_ERF: VC_LAUNCH(VC_EPI_BIAS_GELU_ERF); break;
-        case VC_EPI_BIAS_RESID_F32: VC_LAUNCH(VC_EPI_BIAS_RESID_F32); break;
-        case VC_EPI_EMBED_F32: VC_LAUNCH(VC_EPI_EMBED_F32); break;
-        default: return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad epilogue");
+    if (cfg < 0) cfg = pick_cfg(M, N, K, epilogue);
+    const int ablation = cfg >= 10 ? cfg : -1;  // x3 / x4: timing-only ablations of cfg 3 / 4 (wrong results)
+    if (ablation > 0) cfg = (ablation % 10 == 4) ? 4 : 3;
+    if (cfg < 0 || cfg >= kNumCfgs || M % kCfgs[cfg].bm || N % kCfgs[cfg].bn)
+        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: no tile config divides M x N");
+    if ((M / kCfgs[cfg].bm) * (N / kCfgs[cfg].bn) > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: grid too large");
+    const int k = (int)K;
+    if (cfg == 4 && (K % 32 || K / 32 < 6 || N > 8192 || epilogue > VC_EPI_BIAS_GELU_ERF))
+        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 4 needs K%32==0, K>=192, N<=8192, bf16 epilogue");
+    if (ablation > 0) {
+        if (epilogue != VC_EPI_BIAS_BF16) return fail(VC_ERR_INVALID_ARG, "ablation: bias epilogue only");
+        return launch_epi<VC_EPI_BIAS_BF16>(ablation, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
     }
-#undef VC_LAUNCH
-    return check_launch("vc_gemm_bf16");
+    switch (epilogue) {
+        case VC_EPI_BIAS_BF16:
+            return launch_epi<VC_EPI_BIAS_BF16>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
+        case VC_EPI_BIAS_GELU_TANH:
+            return launch_epi<VC_EPI_BIAS_GELU_TANH>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
+        case VC_EPI_BIAS_GELU_ERF:
+            return launch_epi<VC_EPI_BIAS_GELU_ERF>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
+        case VC_EPI_BIAS_RESID_F32:
+            return launch_epi<VC_EPI_BIAS_RESID_F32>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
+        case VC_EPI_EMBED_F32:
+            return launch_epi<VC_EPI_EMBED_F32>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
+    }
+    return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad epilogue");
+}
+
+extern "C" int vc_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int64_t M, int64_t N,
+                            int64_t K, const float* bias, int epilogue, void* out, int64_t ldo, const float* aux,
+                            int64_t ldaux, int64_t G, int64_t group_stride, int64_t group_offset,
+                            hipStream_t stream) {
+    return vc_gemm_bf16_cfg(A, lda, W, ldw, M, N, K, bias, epilogue, out, ldo, aux, ldaux, G, group_stride,
+                            group_offset, -1, stream);
 }

@@ -70,7 +70,7 @@ def tubelet_im2col(pix: torch.Tensor, tubelet, out: torch.Tensor) -> torch.Tenso
 
 def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: str, out: torch.Tensor,
          aux: torch.Tensor | None = None, group: int = 0, group_stride: int = 0, group_offset: int = 0,
-         m: int | None = None) -> torch.Tensor:
+         m: int | None = None, cfg: int = -1) -> torch.Tensor:
     """out (+)= epilogue(a[:m] @ w.T + bias).  a bf16 [M,K], w bf16 [N,K], bias f32 [N]."""
     _dev(a, w, bias, out)
     M = a.shape[0] if m is None else m
@@ -92,8 +92,8 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: str, ou
     _need(a.shape[0] >= M, "gemm a rows")
     aux_p = _p(aux) if aux is not None else None
     ldaux = aux.stride(0) if aux is not None else 0
-    _lib.call("vc_gemm_bf16", _p(a), a.stride(0), _p(w), w.stride(0), M, N, K, _p(bias), e, _p(out), out.stride(0),
-              aux_p, ldaux, group, group_stride, group_offset, _stream(a))
+    _lib.call("vc_gemm_bf16_cfg", _p(a), a.stride(0), _p(w), w.stride(0), M, N, K, _p(bias), e, _p(out),
+              out.stride(0), aux_p, ldaux, group, group_stride, group_offset, cfg, _stream(a))
     return out
 
 
@@ -110,8 +110,13 @@ def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: flo
     return out
 
 
-def attention(qkv: torch.Tensor, B: int, S: int, H: int, scale: float, out: torch.Tensor) -> torch.Tensor:
-    """qkv bf16 [rows, 3*H*64] (q|k|v per token row b*S+s) -> out bf16 [rows, H*64]."""
+LOG2E = 1.4426950408889634
+
+
+def attention(qkv: torch.Tensor, B: int, S: int, H: int, scale: float, out: torch.Tensor,
+              q_prescaled: bool = False) -> torch.Tensor:
+    """qkv bf16 [rows, 3*H*64] (q|k|v per token row b*S+s) -> out bf16 [rows, H*64].
+    q_prescaled: q already holds q * scale * log2(e) (folded into the projection)."""
     _dev(qkv, out)
     _need(qkv.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and qkv.stride(1) == 1 and out.stride(1) == 1,
           "attention dtypes/layout")
@@ -119,7 +124,8 @@ def attention(qkv: torch.Tensor, B: int, S: int, H: int, scale: float, out: torc
     # the kernel reads K/V rows up to (B-1)*S + roundup(S,64) - 1
     _need(qkv.shape[0] >= (B - 1) * S + (S + 63) // 64 * 64, "attention: qkv needs row padding to a 64-key tile")
     _need(out.shape[0] >= B * S, "attention out rows")
-    _lib.call("vc_attention_fwd", _p(qkv), qkv.stride(0), B, S, H, 64, scale, _p(out), out.stride(0), _stream(qkv))
+    _lib.call("vc_attention_fwd", _p(qkv), qkv.stride(0), B, S, H, 64, scale, int(bool(q_prescaled)), _p(out),
+              out.stride(0), _stream(qkv))
     return out
 
 

@@ -154,8 +154,13 @@ class VivitForVideoClassification(torch.nn.Module):
             L["ln1_b"] = P(p + "layernorm_before.bias").contiguous()
             L["ln2_g"] = P(p + "layernorm_after.weight").contiguous()
             L["ln2_b"] = P(p + "layernorm_after.bias").contiguous()
-            L["w_qkv"] = torch.cat([P(p + f"attention.{n}.weight") for n in ("q_proj", "k_proj", "v_proj")]).to(bf).contiguous()
-            L["b_qkv"] = torch.cat([P(p + f"attention.{n}.bias") for n in ("q_proj", "k_proj", "v_proj")]).contiguous()
+            # softmax scale * log2(e) folded into the q projection (fp32 master -> one bf16 rounding),
+            # so the attention kernel's exp2 argument comes straight out of the QK^T MFMA
+            qs = (D // c.num_attention_heads) ** -0.5 * ops.LOG2E
+            L["w_qkv"] = torch.cat([P(p + "attention.q_proj.weight") * qs, P(p + "attention.k_proj.weight"),
+                                    P(p + "attention.v_proj.weight")]).to(bf).contiguous()
+            L["b_qkv"] = torch.cat([P(p + "attention.q_proj.bias") * qs, P(p + "attention.k_proj.bias"),
+                                    P(p + "attention.v_proj.bias")]).contiguous()
             L["w_o"] = P(p + "attention.o_proj.weight").to(bf).contiguous()
             L["b_o"] = P(p + "attention.o_proj.bias").contiguous()
             L["w_1"] = P(p + "mlp.fc1.weight").to(bf).contiguous()
@@ -235,7 +240,7 @@ class VivitForVideoClassification(torch.nn.Module):
             if ev is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-            ops.attention(QKV, B, S, c.num_attention_heads, scale, O)
+            ops.attention(QKV, B, S, c.num_attention_heads, scale, O, q_prescaled=True)
             if ev is not None:
                 e1.record()
                 ev.append((e0, e1))

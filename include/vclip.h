@@ -83,6 +83,15 @@ int vc_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
                  int64_t G, int64_t group_stride, int64_t group_offset, hipStream_t stream);
 
 /*
+ * Same as vc_gemm_bf16 with an explicit block-tile configuration (tuning hook):
+ *   cfg 0: 256x128, cfg 1: 128x128, cfg 2: 128x256 (rows x cols of C); -1 = automatic.
+ */
+int vc_gemm_bf16_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
+                     int64_t M, int64_t N, int64_t K, const float* bias, int epilogue,
+                     void* out, int64_t ldo, const float* aux, int64_t ldaux,
+                     int64_t G, int64_t group_stride, int64_t group_offset, int cfg, hipStream_t stream);
+
+/*
  * Row LayerNorm: y bf16[m][:] = (x[m]-mean)/sqrt(var+eps)*gamma + beta, x f32, stats f32.
  * Replaces nn.LayerNorm layernorm_before/after (TF5/.../modeling_vivit.py:245-246, 258, 266).
  */
@@ -96,12 +105,15 @@ int vc_layernorm_f32_bf16(const float* x, int64_t ldx, int64_t M, int64_t D,
  * qkv: bf16 rows of `ld` elements, row (b*S + s); head h's q at column h*64,
  *      k at H*64 + h*64, v at 2*H*64 + h*64 (the fused q|k|v projection output).
  * out: bf16 rows of `ldo` elements, head h at column h*64 (the o_proj input layout).
- * softmax(scale * q.k) with `scale` = head_dim^-0.5 in ViViT.
+ * softmax(scale * q.k) with `scale` = head_dim^-0.5 in ViViT.  The kernel evaluates
+ * exp2(q'.k - running max) with q' = q * scale * log2(e): if q_prescaled != 0 the
+ * producer already stored q' (e.g. folded into the q projection weights and bias, one
+ * rounding), otherwise the kernel forms q' in fp32 and re-rounds it to bf16.
  * Rows of qkv must be readable up to (B-1)*S + roundup(S, 64) - 1 (callers pad).
  * Replaces eager_attention_forward / SDPA (TF5/.../modeling_vivit.py:149-174, 177-223).
  */
 int vc_attention_fwd(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, int64_t head_dim,
-                     float scale, uint16_t* out, int64_t ldo, hipStream_t stream);
+                     float scale, int q_prescaled, uint16_t* out, int64_t ldo, hipStream_t stream);
 
 /* CLS rows: x[b*S][:] = cls[:] + pos[0][:]   (TF5/.../modeling_vivit.py:131-142). */
 int vc_cls_init(const float* cls, const float* pos, float* x, int64_t ldx, int64_t B, int64_t S, int64_t D,

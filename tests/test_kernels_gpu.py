@@ -107,6 +107,21 @@ def test_gemm_bias_bf16(M, N, K):
     assert err < 8e-3, err
 
 
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("epi", ["bias", "bias_gelu_tanh"])
+def test_gemm_every_tile_config(cfg, epi):
+    """Every block-tile configuration on a shape with more tiles than CUs (the persistent
+    config 4 then walks several tiles per workgroup and carries its LDS ring across them)."""
+    M, N, K = 25344, 2304, 768
+    a, w, bias, ref = _gemm_case(M, N, K, 100 + cfg)
+    if epi == "bias_gelu_tanh":
+        ref = gelu_fast(ref)
+    out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    ops().gemm(a.to(DEV), w.to(DEV), bias.to(DEV), epi, out, cfg=cfg)
+    err = ((out.float().cpu() - ref).abs() / (ref.abs() + 1.0)).max().item()
+    assert err < 8e-3, err
+
+
 def test_gemm_orientation_asymmetric():
     """A = I with an asymmetric W catches a transposed C write (cdna_hip_programming.md §3)."""
     M = N = K = 128
@@ -188,6 +203,34 @@ def test_attention_spike_max_jump():
     ref = attention_ref(q[:, :, 0].transpose(1, 2), q[:, :, 1].transpose(1, 2), q[:, :, 2].transpose(1, 2), 0.125)
     err = (out[:S].float().cpu() - ref.transpose(1, 2).reshape(S, 64)).abs().max().item()
     assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("mag", [0.05, 4.0, 12.0])
+def test_attention_score_scales(mag):
+    """Tiny scores (no rescale after the first block) up to huge ones (re-basing the running
+    max on most blocks, scores far beyond 2^THR) must all match the fp32 reference."""
+    B, S, H = 2, 777, 2
+    g = torch.Generator().manual_seed(int(mag * 100))
+    rows = (B - 1) * S + (S + 63) // 64 * 64 + 64
+    qkv = torch.randn(rows, 3 * H * 64, generator=g)
+    qkv[:, : 2 * H * 64] *= mag
+    # increasing key norms along the sequence force the max to keep growing
+    ramp = torch.linspace(0.2, 1.8, S).repeat(B)
+    qkv[: B * S, H * 64: 2 * H * 64] *= ramp[:, None]
+    qkv = bf(qkv)
+    # q pre-multiplied by scale*log2(e) (as the model folds it into the q projection): the
+    # kernel then takes q' as is, and the reference uses exactly the same q'
+    c = 0.125 * 1.4426950408889634
+    qkv[:, : H * 64] = bf(qkv[:, : H * 64].float() * c)
+    out = torch.zeros(rows, H * 64, dtype=torch.bfloat16, device=DEV)
+    ops().attention(qkv.to(DEV), B, S, H, 0.125, out, q_prescaled=True)
+    q = qkv[: B * S].float().view(B, S, 3, H, 64)
+    ref = attention_ref(q[:, :, 0].transpose(1, 2) / c, q[:, :, 1].transpose(1, 2), q[:, :, 2].transpose(1, 2), 0.125)
+    ref = ref.transpose(1, 2).reshape(B * S, H * 64)
+    o = out[: B * S].float().cpu()
+    assert torch.isfinite(o).all()
+    err = (o - ref).abs().max().item()
+    assert err < 3e-2, err
 
 
 # ------------------------------------------------------------------------- CLS head

@@ -36,7 +36,7 @@ def test_invalid_args_fail_loudly_without_gpu(lib):
     rc = lib.vc_gemm_bf16(None, 0, None, 0, 100, 128, 64, None, 0, None, 0, None, 0, 0, 0, 0, None)
     assert rc != 0
     assert "null" in lib.vc_last_error().decode()
-    rc = lib.vc_attention_fwd(ctypes.c_void_p(16), 2304, 1, 10, 12, 128, 0.1, ctypes.c_void_p(16), 768, None)
+    rc = lib.vc_attention_fwd(ctypes.c_void_p(16), 2304, 1, 10, 12, 128, 0.1, 0, ctypes.c_void_p(16), 768, None)
     assert rc != 0 and "head_dim" in lib.vc_last_error().decode()
 
 
