@@ -42,6 +42,33 @@ def _dist():
     return None, 0, 1, 0
 
 
+def timed_loop(step, steps: int, warmup: int, dist=None, sync=None):
+    """W untimed warm-up steps, then exactly `steps` timed steps bracketed by a barrier and
+    a device sync on both sides; returns the MAX elapsed seconds over ranks (the job's
+    wall time).  `sync` is the device synchronisation (torch.cuda.synchronize on GPU)."""
+    sync = sync or (lambda: None)
+    for _ in range(warmup):
+        step()
+    sync()
+    if dist:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64)
+        if dist.get_backend() == "nccl":
+            t = t.cuda()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
+
+
 def cpu_baseline(model_cfg, n_clips, gpu_logits_fn):
     """The fp32 CPU oracle (oracle/vivit_ref.py, a 'port' of the reference's HF ViViT
     forward) on the host cores: a bounded sample of `n_clips` clips, one at a time
@@ -87,29 +114,19 @@ def main():
     cfg = model.config
     pix = torch.from_numpy(make_synthetic_clips(a.batch, 32, 224, seed=1 + rank)).to(dev)
 
-    for _ in range(a.warmup):
-        model.forward_logits(pix)
-    torch.cuda.synchronize()
+    evs = []
 
-    model.kernel_events = []
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
+    def step():
         model.forward_logits(pix)
+
+    # HIP events around every attention launch of the timed steps (kernel-level roofline)
+    for _ in range(a.warmup):
+        step()
     torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    evs = model.kernel_events
+    model.kernel_events = evs
+    dt = timed_loop(step, a.steps, 0, dist, torch.cuda.synchronize)
     model.kernel_events = None
     attn_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
-
-    if dist:
-        t = torch.tensor([dt], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
 
     clips = a.batch * a.steps * world
     value = clips / dt
