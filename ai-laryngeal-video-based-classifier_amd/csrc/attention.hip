@@ -5,30 +5,32 @@
 // without materialising the S x S scores (472 MB fp32 per clip per layer in the eager path).
 //
 // gfx950 structure (cdna_hip_programming.md Appendix B "Fused attention prefill"):
-//   * workgroup = 4 waves = 128 query rows of one (clip, head); wave = 32 rows;
+//   * workgroup = 4 waves; each wave owns QB blocks of 32 query rows of one (clip, head),
+//     so every K/V fragment read from LDS feeds QB MFMAs;
 //   * K/V tiles of 64 keys staged by LDS-DMA (global_load_lds, issued from inline asm so
 //     hipcc's LDS wait counts stay exact) into a 3-slot ring; a counted vmcnt retires only
 //     the next tile, one raw s_barrier per tile; K image XOR-swizzled for ds_read_b128,
 //     V image swizzled for the ds_read_b64_tr_b16 transpose read;
 //   * swapped QK^T (S^T = K . Q^T): a query's scores live in ONE lane column, so the row
-//     max needs one cross-half exchange and only on the rare rescale path;
+//     max needs one cross-half exchange and only on the rare re-base path;
 //   * the running row max enters the QK^T MFMA chain as its initial accumulator
-//     (S' = Q.K^T*c - m, with c = scale*log2 e folded into Q), so the common path per
-//     score is max3 + exp2 + add + cvt; the max is re-based only when a score exceeds
-//     it by more than THR (defer-max, cdna_hip_programming.md T13: P <= 2^THR);
+//     (S' = Q'.K^T - m, with scale*log2 e folded into Q'), so the common path per score is
+//     max + exp2 + add + cvt; the max is re-based only when a score exceeds it by more
+//     than THR (defer-max, cdna_hip_programming.md T13: P <= 2^THR);
 //   * S'^T accumulator registers feed P.V directly as the B operand of O^T = V^T . P^T
 //     (§3 "An accumulator tile as the next MFMA's operand"); P never touches LDS;
 //   * output rows widened to 16-byte stores with v_permlane32_swap (T21).
 #include "common.hpp"
 
+#include <type_traits>
+
 namespace vc {
 
-constexpr int AQ = 128;  // query rows per workgroup
-constexpr int AK = 64;   // keys per tile
+constexpr int AK = 64;                      // keys per tile
 constexpr int KV_TILE_BYTES = AK * 64 * 2;  // 8 KiB (one of K or V)
 constexpr int KV_SLOT = 2 * KV_TILE_BYTES;  // K then V
 constexpr int NSLOT = 3;
-constexpr float THR = 8.0f;  // log2-domain headroom before the running max is re-based (2^THR = 256)
+constexpr float THR = 8.0f;  // log2-domain headroom before the running max is re-based
 
 __device__ __forceinline__ int kswz(int r, int c) { return c ^ ((r >> 1) & 7); }
 __device__ __forceinline__ int vswz(int r, int c) { return c ^ (((r >> 1) & 1) << 2); }
@@ -39,6 +41,23 @@ __device__ __forceinline__ void adma16(const void* gsrc, uint32_t lds_addr) {
                  : "=&s"(keep)
                  : "v"(gsrc), "s"(lds_addr)
                  : "memory");
+}
+
+// Same, saddr form: 64-bit wave-uniform base in SGPRs + 32-bit per-lane offset, so the
+// per-tile address advance is scalar arithmetic (no VALU).
+__device__ __forceinline__ void adma16s(const void* sbase, uint32_t voff, uint32_t lds_addr) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(sbase), "s"(lds_addr)
+                 : "memory");
+}
+
+// v_max3_f32 without the NaN-canonicalising v_max hipcc inserts in front of fmaxf
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
 }
 
 template <int N>
@@ -54,14 +73,24 @@ __device__ __forceinline__ void attn_sync() {
     __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int ABL>  // timing ablations: 1 no loop loads, 2 no exp, 4 no PV MFMA, 8 no QK MFMA
+// QB: 32-row query blocks per wave.  ABL: timing-only ablations (1 no loop loads, 2 no exp,
+// 4 no PV MFMA, 8 no QK MFMA) — results are wrong by design.
+template <int QB, int ABL>
 __global__ void __launch_bounds__(256, 2)
 attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, float c_log2,
                     uint16_t* __restrict__ out, int64_t ldo) {
+    constexpr int AQ = 4 * 32 * QB;  // query rows per workgroup
     __shared__ __attribute__((aligned(16))) char smem[NSLOT * KV_SLOT];
 
-    const int qblk = blockIdx.x;
-    const int bh = blockIdx.y;
+    // XCD-aware order: the workgroups of one (clip, head) share its K/V; give every XCD a
+    // contiguous range of linear ids so they meet in that XCD's L2 (blocks L and L+8 share
+    // an XCD under round-robin dispatch; bijective remap, §5 "XCD swizzle must be bijective")
+    const int nq = gridDim.x, nwg = gridDim.x * gridDim.y;
+    const int L = blockIdx.y * nq + blockIdx.x;
+    const int xq = nwg >> 3, xr = nwg & 7, xcd = L & 7;
+    const int wg = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (L >> 3);
+    const int qblk = wg % nq;
+    const int bh = wg / nq;
     const int b = bh / H, hh = bh % H;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -74,38 +103,42 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem);
 
-    // ---- Q^T fragments (B operand of S^T = K.Q^T): lane holds Q[q=r][d = 16kk + 8h + 0..7],
-    //      pre-scaled by c = scale*log2(e) so exp2 needs no multiply
-    const int q = qblk * AQ + wave * 32 + r;
-    const int qc = q < S ? q : S - 1;
-    v8bf qf[4];
-    {
+    // ---- Q'^T fragments (B operand of S^T = K.Q'^T): lane holds Q'[q][d = 16kk + 8h + 0..7]
+    int qrow_of[QB];
+    v8bf qf[QB][4];
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+        const int q = qblk * AQ + (wave * QB + qb) * 32 + r;
+        qrow_of[qb] = q;
+        const int qc = q < S ? q : S - 1;
         const uint16_t* qrow = qbase + (tok0 + qc) * ld + 8 * h;
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
             const v8s raw = *reinterpret_cast<const v8s*>(qrow + 16 * kk);
             if (c_log2 == 1.0f) {
-                qf[kk] = __builtin_bit_cast(v8bf, raw);  // producer folded the scale into q
+                qf[qb][kk] = __builtin_bit_cast(v8bf, raw);  // producer folded the scale into q
             } else {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) qf[kk][j] = (__bf16)(bf2f((unsigned short)raw[j]) * c_log2);
+                for (int j = 0; j < 8; ++j) qf[qb][kk][j] = (__bf16)(bf2f((unsigned short)raw[j]) * c_log2);
             }
         }
     }
 
-    // staging: 64 key rows of K and V (8 rows x 128 B per wave-instruction), wave w: rows 16w..16w+15
+    // staging: 64 key rows of K and V (8 rows x 128 B per wave-instruction), wave w: rows 16w..16w+15;
+    // per-lane byte offsets are loop-invariant, the tile advance goes into the scalar base
     const int srow = wave * 16 + (lane >> 3), spc = lane & 7;
-    const uint16_t* ksrc0 = kbase + (int64_t)srow * ld + kswz(srow, spc) * 8;
-    const uint16_t* ksrc1 = kbase + (int64_t)(srow + 8) * ld + kswz(srow + 8, spc) * 8;
-    const uint16_t* vsrc0 = vbase + (int64_t)srow * ld + vswz(srow, spc) * 8;
-    const uint16_t* vsrc1 = vbase + (int64_t)(srow + 8) * ld + vswz(srow + 8, spc) * 8;
+    const uint32_t ko0 = (uint32_t)(srow * ld + kswz(srow, spc) * 8) * 2;
+    const uint32_t ko1 = (uint32_t)((srow + 8) * ld + kswz(srow + 8, spc) * 8) * 2;
+    const uint32_t vo0 = (uint32_t)(srow * ld + vswz(srow, spc) * 8) * 2;
+    const uint32_t vo1 = (uint32_t)((srow + 8) * ld + vswz(srow + 8, spc) * 8) * 2;
     auto stage = [&](int t) {
         const uint32_t s = lds0 + (t % NSLOT) * KV_SLOT + wave * 16 * 128;
-        const int64_t off = (int64_t)t * AK * ld;
-        adma16(ksrc0 + off, __builtin_amdgcn_readfirstlane(s));
-        adma16(ksrc1 + off, __builtin_amdgcn_readfirstlane(s + 8 * 128));
-        adma16(vsrc0 + off, __builtin_amdgcn_readfirstlane(s + KV_TILE_BYTES));
-        adma16(vsrc1 + off, __builtin_amdgcn_readfirstlane(s + KV_TILE_BYTES + 8 * 128));
+        const uint16_t* kt = kbase + (int64_t)t * AK * ld;
+        const uint16_t* vt = vbase + (int64_t)t * AK * ld;
+        adma16s(kt, ko0, __builtin_amdgcn_readfirstlane(s));
+        adma16s(kt, ko1, __builtin_amdgcn_readfirstlane(s + 8 * 128));
+        adma16s(vt, vo0, __builtin_amdgcn_readfirstlane(s + KV_TILE_BYTES));
+        adma16s(vt, vo1, __builtin_amdgcn_readfirstlane(s + KV_TILE_BYTES + 8 * 128));
     };
 
     // per-lane constant LDS byte offsets (relative to a ring slot):
@@ -126,13 +159,15 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
         voff[db] = KV_TILE_BYTES + ra * 128 + vswz(ra, col >> 3) * 16 + (col & 7) * 2;
     }
 
-    v16f o0, o1;  // O^T[d][q]: d-block 0 and 1
+    v16f o[QB][2];     // O^T[d][q] per query block, d-blocks 0/1
+    v16f minit[QB];    // -running max of this lane's query, broadcast: initial accumulator of S'
+    float l_run[QB];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) { o0[e] = 0.f; o1[e] = 0.f; }
-    v16f minit;  // -running max of this lane's query, broadcast: initial accumulator of S'
+    for (int qb = 0; qb < QB; ++qb) {
 #pragma unroll
-    for (int e = 0; e < 16; ++e) minit[e] = 0.f;
-    float m_run = 0.f, l_run = 0.f;
+        for (int e = 0; e < 16; ++e) { o[qb][0][e] = 0.f; o[qb][1][e] = 0.f; minit[qb][e] = 0.f; }
+        l_run[qb] = 0.f;
+    }
 
     const int ntiles = (S + AK - 1) / AK;
     stage(0);
@@ -144,76 +179,108 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
     }
     attn_sync();
 
-    for (int t = 0; t < ntiles; ++t) {
+    // one K/V tile; the ring slot is a compile-time constant (loop unrolled by NSLOT), so
+    // every LDS address is a loop-invariant per-lane VGPR plus an immediate offset
+    auto tile = [&](auto slot_c, int t) {
+        constexpr int SLOTI = decltype(slot_c)::value;
         if (!(ABL & 1) && t + 2 < ntiles) stage(t + 2);
-        const char* slot = smem + (t % NSLOT) * KV_SLOT;
+        const char* slot = smem + SLOTI * KV_SLOT;
 
-        // ---- S'^T = K . Q'^T - m_run for the two 32-key blocks (-m_run enters as the C operand)
-        v16f s0, s1;
+        // ---- S'^T = K . Q'^T - m for QB query blocks x two 32-key blocks; each K fragment
+        //      feeds QB MFMAs (-m enters as the C operand of the first k-step)
+        v16f sc[QB][2];
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
             const v8bf k0 = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(slot + koff[kk]));
             const v8bf k1 = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(slot + koff[kk] + 4096));
-            if constexpr (ABL & 8) {
-                asm volatile("" ::"v"(k0), "v"(k1));
-                if (kk == 0) { s0 = minit; s1 = minit; }
-            } else {
-                s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[kk], kk == 0 ? minit : s0, 0, 0, 0);
-                s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[kk], kk == 0 ? minit : s1, 0, 0, 0);
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb) {
+                if constexpr (ABL & 8) {
+                    asm volatile("" ::"v"(k0), "v"(k1));
+                    if (kk == 0) { sc[qb][0] = minit[qb]; sc[qb][1] = minit[qb]; }
+                } else {
+                    sc[qb][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[qb][kk], kk == 0 ? minit[qb] : sc[qb][0], 0, 0, 0);
+                    sc[qb][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[qb][kk], kk == 0 ? minit[qb] : sc[qb][1], 0, 0, 0);
+                }
             }
         }
         // ---- mask keys beyond S (last tile only)
         const int kv0 = t * AK;
         if (kv0 + AK > S) {
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int key = (e & 3) + 8 * (e >> 2) + 4 * h;
-                if (kv0 + key >= S) s0[e] = -INFINITY;
-                if (kv0 + 32 + key >= S) s1[e] = -INFINITY;
-            }
+            for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int key = (e & 3) + 8 * (e >> 2) + 4 * h;
+                    if (kv0 + key >= S) sc[qb][0][e] = -INFINITY;
+                    if (kv0 + 32 + key >= S) sc[qb][1][e] = -INFINITY;
+                }
         }
 
-        // ---- online softmax: scores are already relative to m_run; re-base only when a row
-        //      grew by more than THR (tile 0 always establishes m_run)
-        float mx = fmaxf(fmaxf(s0[0], s0[1]), fmaxf(s1[0], s1[1]));
+        // ---- online softmax: scores are relative to m already; re-base only when a row grew
+        //      by more than THR (tile 0 always establishes m)
+        float mx[QB];
+        bool grow = false;
 #pragma unroll
-        for (int e = 2; e < 16; e += 2) mx = fmaxf(mx, fmaxf(fmaxf(s0[e], s0[e + 1]), fmaxf(s1[e], s1[e + 1])));
-        if (t == 0 || __any(mx > THR)) {
-            const float rowmax = fmaxf(mx, __shfl_xor(mx, 32, 64));
-            const float delta = (t == 0) ? rowmax : fmaxf(rowmax, 0.f);
-            const float alpha = (t == 0) ? 0.f : __builtin_amdgcn_exp2f(-delta);
-            m_run = (t == 0) ? rowmax : m_run + delta;
+        for (int qb = 0; qb < QB; ++qb) {
+            // four independent v_max3 chains, then combine (dependency depth 5)
+            const v16f& x = sc[qb][0];
+            const v16f& y = sc[qb][1];
+            float m0 = vmax3(x[0], x[1], x[2]), m1 = vmax3(x[8], x[9], x[10]);
+            float m2 = vmax3(y[0], y[1], y[2]), m3 = vmax3(y[8], y[9], y[10]);
+            m0 = vmax3(m0, x[3], x[4]); m1 = vmax3(m1, x[11], x[12]); m2 = vmax3(m2, y[3], y[4]); m3 = vmax3(m3, y[11], y[12]);
+            m0 = vmax3(m0, x[5], x[6]); m1 = vmax3(m1, x[13], x[14]); m2 = vmax3(m2, y[5], y[6]); m3 = vmax3(m3, y[13], y[14]);
+            m0 = vmax3(m0, x[7], m1); m2 = vmax3(m2, y[7], m3);
+            const float m = vmax3(m0, m2, vmax3(x[15], y[15], x[15]));
+            mx[qb] = m;
+            grow = grow || (m > THR);
+        }
+        if (t == 0 || __any(grow)) {
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb) {
+                const float rowmax = fmaxf(mx[qb], __shfl_xor(mx[qb], 32, 64));
+                const float delta = (t == 0) ? rowmax : fmaxf(rowmax, 0.f);
+                const float alpha = (t == 0) ? 0.f : __builtin_amdgcn_exp2f(-delta);
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    sc[qb][0][e] -= delta;
+                    sc[qb][1][e] -= delta;
+                    o[qb][0][e] *= alpha;
+                    o[qb][1][e] *= alpha;
+                    minit[qb][e] -= delta;
+                }
+                l_run[qb] *= alpha;
+            }
+        }
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
-                s0[e] -= delta;
-                s1[e] -= delta;
-                o0[e] *= alpha;
-                o1[e] *= alpha;
-                minit[e] = -m_run;
+                if constexpr (!(ABL & 2)) {
+                    sc[qb][0][e] = __builtin_amdgcn_exp2f(sc[qb][0][e]);
+                    sc[qb][1][e] = __builtin_amdgcn_exp2f(sc[qb][1][e]);
+                }
             }
-            l_run *= alpha;
+            const v16f& a = sc[qb][0];
+            const v16f& c = sc[qb][1];
+            const float a0 = (a[0] + a[1]) + (a[2] + a[3]), a1 = (a[4] + a[5]) + (a[6] + a[7]);
+            const float a2 = (a[8] + a[9]) + (a[10] + a[11]), a3 = (a[12] + a[13]) + (a[14] + a[15]);
+            const float c0 = (c[0] + c[1]) + (c[2] + c[3]), c1 = (c[4] + c[5]) + (c[6] + c[7]);
+            const float c2 = (c[8] + c[9]) + (c[10] + c[11]), c3 = (c[12] + c[13]) + (c[14] + c[15]);
+            l_run[qb] += ((a0 + a1) + (a2 + a3)) + ((c0 + c1) + (c2 + c3));
         }
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            if constexpr (!(ABL & 2)) {
-                s0[e] = __builtin_amdgcn_exp2f(s0[e]);
-                s1[e] = __builtin_amdgcn_exp2f(s1[e]);
-            }
-        }
-        float a0 = (s0[0] + s0[1]) + (s0[2] + s0[3]), a1 = (s0[4] + s0[5]) + (s0[6] + s0[7]);
-        float a2 = (s0[8] + s0[9]) + (s0[10] + s0[11]), a3 = (s0[12] + s0[13]) + (s0[14] + s0[15]);
-        float b0 = (s1[0] + s1[1]) + (s1[2] + s1[3]), b1 = (s1[4] + s1[5]) + (s1[6] + s1[7]);
-        float b2 = (s1[8] + s1[9]) + (s1[10] + s1[11]), b3 = (s1[12] + s1[13]) + (s1[14] + s1[15]);
-        l_run += ((a0 + a1) + (a2 + a3)) + ((b0 + b1) + (b2 + b3));
 
-        // ---- O^T += V^T . P^T: P fragment of (block kb, k-step s2) = regs 8s2..8s2+7 as bf16
+        // ---- O^T += V^T . P^T: P fragment of (key block kb, k-step s2) = regs 8s2..8s2+7;
+        //      every V^T fragment read from LDS feeds QB MFMAs
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
-                v8bf pf;
+                v8bf pf[QB];
 #pragma unroll
-                for (int jj = 0; jj < 8; ++jj) pf[jj] = (__bf16)(kb == 0 ? s0[8 * s2 + jj] : s1[8 * s2 + jj]);
+                for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+                    for (int jj = 0; jj < 8; ++jj) pf[qb][jj] = (__bf16)sc[qb][kb][8 * s2 + jj];
 #pragma unroll
                 for (int db = 0; db < 2; ++db) {
                     const char* pa = slot + voff[db] + (kb * 32 + 16 * s2) * 128;
@@ -223,12 +290,13 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
                     vv[0] = va[0]; vv[1] = va[1]; vv[2] = va[2]; vv[3] = va[3];
                     vv[4] = vb[0]; vv[5] = vb[1]; vv[6] = vb[2]; vv[7] = vb[3];
                     const v8bf vf = __builtin_bit_cast(v8bf, vv);
-                    if constexpr (ABL & 4) {
-                        asm volatile("" ::"v"(vf), "v"(pf));
-                    } else if (db == 0) {
-                        o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o0, 0, 0, 0);
-                    } else {
-                        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o1, 0, 0, 0);
+#pragma unroll
+                    for (int qb = 0; qb < QB; ++qb) {
+                        if constexpr (ABL & 4) {
+                            asm volatile("" ::"v"(vf), "v"(pf[qb]));
+                        } else {
+                            o[qb][db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[qb], o[qb][db], 0, 0, 0);
+                        }
                     }
                 }
             }
@@ -239,39 +307,61 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
             else attn_wait_vm<0>();
             attn_sync();
         }
+    };
+
+    int t = 0;
+    for (; t + NSLOT <= ntiles; t += NSLOT) {
+        tile(std::integral_constant<int, 0>{}, t);
+        tile(std::integral_constant<int, 1>{}, t + 1);
+        tile(std::integral_constant<int, 2>{}, t + 2);
     }
+    if (t < ntiles) tile(std::integral_constant<int, 0>{}, t);
+    if (t + 1 < ntiles) tile(std::integral_constant<int, 1>{}, t + 1);
 
     // ---- normalise and store O[q][d]: reg 4g+e of block db -> d = 32db + 8g + 4h + e;
     //      lane pairs (h=0/1) swap halves so each lane stores 16 contiguous bytes
-    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-    const float inv = 1.0f / l_tot;
-    unsigned pk[2][4][2];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-        pk[0][g][0] = pack2bf(o0[4 * g + 0] * inv, o0[4 * g + 1] * inv);
-        pk[0][g][1] = pack2bf(o0[4 * g + 2] * inv, o0[4 * g + 3] * inv);
-        pk[1][g][0] = pack2bf(o1[4 * g + 0] * inv, o1[4 * g + 1] * inv);
-        pk[1][g][1] = pack2bf(o1[4 * g + 2] * inv, o1[4 * g + 3] * inv);
+    for (int qb = 0; qb < QB; ++qb) {
+        const int q = qrow_of[qb];
+        const int qc = q < S ? q : S - 1;
+        const float l_tot = l_run[qb] + __shfl_xor(l_run[qb], 32, 64);
+        const float inv = 1.0f / l_tot;
+        unsigned pk[2][4][2];
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                pk[db][g][0] = pack2bf(o[qb][db][4 * g + 0] * inv, o[qb][db][4 * g + 1] * inv);
+                pk[db][g][1] = pack2bf(o[qb][db][4 * g + 2] * inv, o[qb][db][4 * g + 3] * inv);
+            }
+        uint16_t* orow = out + (tok0 + qc) * ldo + hh * 64;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int g = 0; g < 4; g += 2) {
+                auto x0 = __builtin_amdgcn_permlane32_swap(pk[db][g][0], pk[db][g + 1][0], false, false);
+                auto x1 = __builtin_amdgcn_permlane32_swap(pk[db][g][1], pk[db][g + 1][1], false, false);
+                uint4 v;
+                v.x = x0[0]; v.y = x1[0]; v.z = x0[1]; v.w = x1[1];
+                if (q < S) *reinterpret_cast<uint4*>(orow + db * 32 + g * 8 + h * 8) = v;
+            }
     }
-    uint16_t* orow = out + (tok0 + qc) * ldo + hh * 64;
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-        for (int g = 0; g < 4; g += 2) {
-            auto x0 = __builtin_amdgcn_permlane32_swap(pk[db][g][0], pk[db][g + 1][0], false, false);
-            auto x1 = __builtin_amdgcn_permlane32_swap(pk[db][g][1], pk[db][g + 1][1], false, false);
-            uint4 v;
-            v.x = x0[0]; v.y = x1[0]; v.z = x0[1]; v.w = x1[1];
-            if (q < S) *reinterpret_cast<uint4*>(orow + db * 32 + g * 8 + h * 8) = v;
-        }
+}
+
+template <int QB, int ABL>
+static void launch_attn(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, float c_log2, uint16_t* out,
+                        int64_t ldo, hipStream_t stream) {
+    constexpr int AQ = 4 * 32 * QB;
+    dim3 grid((unsigned)((S + AQ - 1) / AQ), (unsigned)(B * H));
+    attn_fwd_d64_kernel<QB, ABL><<<grid, 256, 0, stream>>>(qkv, ld, (int)S, (int)H, c_log2, out, ldo);
 }
 
 }  // namespace vc
 
 using namespace vc;
 
-extern "C" int vc_attention_fwd(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, int64_t head_dim,
-                                float scale, int q_prescaled, uint16_t* out, int64_t ldo, hipStream_t stream) {
+static int attn_checks(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, int64_t head_dim,
+                       const uint16_t* out, int64_t ldo) {
     if (!qkv || !out) return fail(VC_ERR_INVALID_ARG, "vc_attention_fwd: null pointer");
     if (head_dim != 64) return fail(VC_ERR_UNSUPPORTED, "vc_attention_fwd: head_dim must be 64");
     if (B <= 0 || S <= 0 || H <= 0 || ld < 3 * H * 64 || ldo < H * 64 || ld % 8 || ldo % 8)
@@ -279,20 +369,27 @@ extern "C" int vc_attention_fwd(const uint16_t* qkv, int64_t ld, int64_t B, int6
     if ((((uintptr_t)qkv) | ((uintptr_t)out)) & 15)
         return fail(VC_ERR_INVALID_ARG, "vc_attention_fwd: pointers must be 16-byte aligned");
     if (B * H > 65535 || S > (1 << 24)) return fail(VC_ERR_INVALID_ARG, "vc_attention_fwd: grid too large");
+    return 0;
+}
+
+extern "C" int vc_attention_fwd(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, int64_t head_dim,
+                                float scale, int q_prescaled, uint16_t* out, int64_t ldo, hipStream_t stream) {
+    if (int rc = attn_checks(qkv, ld, B, S, H, head_dim, out, ldo)) return rc;
     const float c_log2 = q_prescaled ? 1.0f : scale * 1.4426950408889634f;
-    dim3 grid((unsigned)((S + AQ - 1) / AQ), (unsigned)(B * H));
-    attn_fwd_d64_kernel<0><<<grid, 256, 0, stream>>>(qkv, ld, (int)S, (int)H, c_log2, out, ldo);
+    launch_attn<1, 0>(qkv, ld, B, S, H, c_log2, out, ldo, stream);
     return check_launch("vc_attention_fwd");
 }
 
-// Timing-only ablations of the attention kernel (results are wrong by design).
+// Timing-only ablations / variants of the attention kernel (tools/ablate_attn.py).
+// abl = 100*(QB-1) + ablation bits; ablation bits != 0 give wrong results by design.
 extern "C" int vc_attention_fwd_ablation(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H,
                                          float scale, uint16_t* out, int64_t ldo, int abl, hipStream_t stream) {
+    if (int rc = attn_checks(qkv, ld, B, S, H, 64, out, ldo)) return rc;
     const float c_log2 = scale * 1.4426950408889634f;
-    dim3 grid((unsigned)((S + AQ - 1) / AQ), (unsigned)(B * H));
-#define VC_ABL(N) case N: attn_fwd_d64_kernel<N><<<grid, 256, 0, stream>>>(qkv, ld, (int)S, (int)H, c_log2, out, ldo); break;
+#define VC_ABL(QB, N) case 100 * (QB - 1) + N: launch_attn<QB, N>(qkv, ld, B, S, H, c_log2, out, ldo, stream); break;
     switch (abl) {
-        VC_ABL(0) VC_ABL(1) VC_ABL(2) VC_ABL(4) VC_ABL(6) VC_ABL(8) VC_ABL(12) VC_ABL(14) VC_ABL(15)
+        VC_ABL(1, 0) VC_ABL(1, 1) VC_ABL(1, 2) VC_ABL(1, 4) VC_ABL(1, 6) VC_ABL(1, 8) VC_ABL(1, 12) VC_ABL(1, 14)
+        VC_ABL(1, 15) VC_ABL(2, 0) VC_ABL(2, 1) VC_ABL(2, 6) VC_ABL(2, 15)
         default: return fail(VC_ERR_INVALID_ARG, "bad ablation");
     }
 #undef VC_ABL
