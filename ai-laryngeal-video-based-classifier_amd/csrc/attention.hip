@@ -5,20 +5,24 @@
 // without materialising the S x S scores (472 MB fp32 per clip per layer in the eager path).
 //
 // gfx950 structure (cdna_hip_programming.md Appendix B "Fused attention prefill"):
-//   * workgroup = 4 waves; each wave owns QB blocks of 32 query rows of one (clip, head),
-//     so every K/V fragment read from LDS feeds QB MFMAs;
+//   * workgroup = 4 waves; each wave owns 32 query rows of one (clip, head); two
+//     workgroups per CU (two waves per SIMD);
 //   * K/V tiles of 64 keys staged by LDS-DMA (global_load_lds, issued from inline asm so
-//     hipcc's LDS wait counts stay exact) into a 3-slot ring; a counted vmcnt retires only
-//     the next tile, one raw s_barrier per tile; K image XOR-swizzled for ds_read_b128,
+//     hipcc's LDS wait counts stay exact) into a 4-slot ring; a counted vmcnt retires only
+//     the tile needed next, one raw s_barrier per tile; K image XOR-swizzled for ds_read_b128,
 //     V image swizzled for the ds_read_b64_tr_b16 transpose read;
 //   * swapped QK^T (S^T = K . Q^T): a query's scores live in ONE lane column, so the row
 //     max needs one cross-half exchange and only on the rare re-base path;
 //   * the running row max enters the QK^T MFMA chain as its initial accumulator
 //     (S' = Q'.K^T - m, with scale*log2 e folded into Q'), so the common path per score is
-//     max + exp2 + add + cvt; the max is re-based only when a score exceeds it by more
-//     than THR (defer-max, cdna_hip_programming.md T13: P <= 2^THR);
+//     exp2 + a packed add (row sum) + cvt: no per-tile max.  Since every P >= 0, a lane's
+//     partial row sum <= LIM = 2^8 bounds each P of the tile by 2^8 (an overflow shows as
+//     inf/NaN); only when that fails does the tile recompute S' and re-base m on its exact
+//     max (defer-max, cdna_hip_programming.md T13, with the sum as the detector);
 //   * S'^T accumulator registers feed P.V directly as the B operand of O^T = V^T . P^T
 //     (§3 "An accumulator tile as the next MFMA's operand"); P never touches LDS;
+//   * software pipeline inside each wave: the QK^T MFMAs of tile t+1 are issued before
+//     tile t's softmax, so the MFMA pipe runs them while the VALU does exp2/sum/cvt;
 //   * output rows widened to 16-byte stores with v_permlane32_swap (T21).
 #include "common.hpp"
 
@@ -29,8 +33,8 @@ namespace vc {
 constexpr int AK = 64;                      // keys per tile
 constexpr int KV_TILE_BYTES = AK * 64 * 2;  // 8 KiB (one of K or V)
 constexpr int KV_SLOT = 2 * KV_TILE_BYTES;  // K then V
-constexpr int NSLOT = 3;
-constexpr float THR = 8.0f;  // log2-domain headroom before the running max is re-based
+constexpr int NSLOT = 4;
+constexpr float LIM = 256.0f;  // partial row-sum bound (P <= 2^8) before the running max is re-based
 
 __device__ __forceinline__ int kswz(int r, int c) { return c ^ ((r >> 1) & 7); }
 __device__ __forceinline__ int vswz(int r, int c) { return c ^ (((r >> 1) & 1) << 2); }
@@ -53,13 +57,6 @@ __device__ __forceinline__ void adma16s(const void* sbase, uint32_t voff, uint32
                  : "memory");
 }
 
-// v_max3_f32 without the NaN-canonicalising v_max hipcc inserts in front of fmaxf
-__device__ __forceinline__ float vmax3(float a, float b, float c) {
-    float r;
-    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-
 template <int N>
 __device__ __forceinline__ void attn_wait_vm() {
     static_assert(N >= 0 && N < 16, "vmcnt");
@@ -73,13 +70,20 @@ __device__ __forceinline__ void attn_sync() {
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// QB: 32-row query blocks per wave.  ABL: timing-only ablations (1 no loop loads, 2 no exp,
-// 4 no PV MFMA, 8 no QK MFMA) — results are wrong by design.
+// QB: 32-row query blocks per wave.  Only QB = 1 is instantiated (two workgroups per CU, two
+// waves per SIMD, 256 VGPRs each).  QB = 2 (one wave per SIMD, every K/V fragment feeding
+// two MFMAs) needs S, S_next, O, Q' and the running max in ~330 registers: hipcc then
+// shuttles values through the accumulator file and it ran 1.3x slower.
+// ABL: timing-only ablations (1 no loop loads, 2 no exp, 4 no PV MFMA, 8 no QK MFMA) —
+// results are wrong by design; 16 re-bases on every tile (the LIM = 0 build of the
+// threshold sweep, cdna_hip_programming.md rule 26: must agree with the shipped build);
+// 32 drops the MFMA/VALU interleave directives (correct, timing comparison only).
 template <int QB, int ABL>
 __global__ void __launch_bounds__(256, 2)
 attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, float c_log2,
                     uint16_t* __restrict__ out, int64_t ldo) {
-    constexpr int AQ = 4 * 32 * QB;  // query rows per workgroup
+    static_assert(QB == 1, "see the QB note above");
+    constexpr int AQ = 128 * QB;  // query rows per workgroup (4 waves x QB x 32)
     __shared__ __attribute__((aligned(16))) char smem[NSLOT * KV_SLOT];
 
     // XCD-aware order: the workgroups of one (clip, head) share its K/V; give every XCD a
@@ -104,12 +108,10 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
         (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem);
 
     // ---- Q'^T fragments (B operand of S^T = K.Q'^T): lane holds Q'[q][d = 16kk + 8h + 0..7]
-    int qrow_of[QB];
     v8bf qf[QB][4];
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb) {
         const int q = qblk * AQ + (wave * QB + qb) * 32 + r;
-        qrow_of[qb] = q;
         const int qc = q < S ? q : S - 1;
         const uint16_t* qrow = qbase + (tok0 + qc) * ld + 8 * h;
 #pragma unroll
@@ -159,36 +161,19 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
         voff[db] = KV_TILE_BYTES + ra * 128 + vswz(ra, col >> 3) * 16 + (col & 7) * 2;
     }
 
-    v16f o[QB][2];     // O^T[d][q] per query block, d-blocks 0/1
-    v16f minit[QB];    // -running max of this lane's query, broadcast: initial accumulator of S'
-    float l_run[QB];
+    v16f o[QB][2];   // O^T[d][q] per query block, d-blocks 0/1
+    v16f minit[QB];  // -running max of this lane's query, broadcast: initial accumulator of S'
+    v2f l_run[QB];   // packed partial row sums
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) { o[qb][0][e] = 0.f; o[qb][1][e] = 0.f; minit[qb][e] = 0.f; }
-        l_run[qb] = 0.f;
+        l_run[qb] = v2f{0.f, 0.f};
     }
 
-    const int ntiles = (S + AK - 1) / AK;
-    stage(0);
-    if (ntiles > 1) {
-        stage(1);
-        attn_wait_vm<4>();
-    } else {
-        attn_wait_vm<0>();
-    }
-    attn_sync();
-
-    // one K/V tile; the ring slot is a compile-time constant (loop unrolled by NSLOT), so
-    // every LDS address is a loop-invariant per-lane VGPR plus an immediate offset
-    auto tile = [&](auto slot_c, int t) {
-        constexpr int SLOTI = decltype(slot_c)::value;
-        if (!(ABL & 1) && t + 2 < ntiles) stage(t + 2);
-        const char* slot = smem + SLOTI * KV_SLOT;
-
-        // ---- S'^T = K . Q'^T - m for QB query blocks x two 32-key blocks; each K fragment
-        //      feeds QB MFMAs (-m enters as the C operand of the first k-step)
-        v16f sc[QB][2];
+    // ---- S'^T = K . Q'^T - m for QB query blocks x two 32-key blocks of tile t; each K
+    //      fragment feeds QB MFMAs (-m enters as the C operand of the first k-step)
+    auto qk_mfma = [&](const char* slot, v16f (&sc)[QB][2]) {
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
             const v8bf k0 = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(slot + koff[kk]));
@@ -204,7 +189,10 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
                 }
             }
         }
-        // ---- mask keys beyond S (last tile only)
+    };
+    //      keys beyond S masked to -inf (last tile only)
+    auto qk = [&](const char* slot, int t, v16f (&sc)[QB][2]) {
+        qk_mfma(slot, sc);
         const int kv0 = t * AK;
         if (kv0 + AK > S) {
 #pragma unroll
@@ -216,42 +204,9 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
                     if (kv0 + 32 + key >= S) sc[qb][1][e] = -INFINITY;
                 }
         }
-
-        // ---- online softmax: scores are relative to m already; re-base only when a row grew
-        //      by more than THR (tile 0 always establishes m)
-        float mx[QB];
-        bool grow = false;
-#pragma unroll
-        for (int qb = 0; qb < QB; ++qb) {
-            // four independent v_max3 chains, then combine (dependency depth 5)
-            const v16f& x = sc[qb][0];
-            const v16f& y = sc[qb][1];
-            float m0 = vmax3(x[0], x[1], x[2]), m1 = vmax3(x[8], x[9], x[10]);
-            float m2 = vmax3(y[0], y[1], y[2]), m3 = vmax3(y[8], y[9], y[10]);
-            m0 = vmax3(m0, x[3], x[4]); m1 = vmax3(m1, x[11], x[12]); m2 = vmax3(m2, y[3], y[4]); m3 = vmax3(m3, y[11], y[12]);
-            m0 = vmax3(m0, x[5], x[6]); m1 = vmax3(m1, x[13], x[14]); m2 = vmax3(m2, y[5], y[6]); m3 = vmax3(m3, y[13], y[14]);
-            m0 = vmax3(m0, x[7], m1); m2 = vmax3(m2, y[7], m3);
-            const float m = vmax3(m0, m2, vmax3(x[15], y[15], x[15]));
-            mx[qb] = m;
-            grow = grow || (m > THR);
-        }
-        if (t == 0 || __any(grow)) {
-#pragma unroll
-            for (int qb = 0; qb < QB; ++qb) {
-                const float rowmax = fmaxf(mx[qb], __shfl_xor(mx[qb], 32, 64));
-                const float delta = (t == 0) ? rowmax : fmaxf(rowmax, 0.f);
-                const float alpha = (t == 0) ? 0.f : __builtin_amdgcn_exp2f(-delta);
-#pragma unroll
-                for (int e = 0; e < 16; ++e) {
-                    sc[qb][0][e] -= delta;
-                    sc[qb][1][e] -= delta;
-                    o[qb][0][e] *= alpha;
-                    o[qb][1][e] *= alpha;
-                    minit[qb][e] -= delta;
-                }
-                l_run[qb] *= alpha;
-            }
-        }
+    };
+    // P = exp2(S') in place; this lane's partial row sums (32 keys) as packed pairs
+    auto expsum = [&](v16f (&sc)[QB][2], v2f (&ps)[QB]) {
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb) {
 #pragma unroll
@@ -261,14 +216,102 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
                     sc[qb][1][e] = __builtin_amdgcn_exp2f(sc[qb][1][e]);
                 }
             }
-            const v16f& a = sc[qb][0];
-            const v16f& c = sc[qb][1];
-            const float a0 = (a[0] + a[1]) + (a[2] + a[3]), a1 = (a[4] + a[5]) + (a[6] + a[7]);
-            const float a2 = (a[8] + a[9]) + (a[10] + a[11]), a3 = (a[12] + a[13]) + (a[14] + a[15]);
-            const float c0 = (c[0] + c[1]) + (c[2] + c[3]), c1 = (c[4] + c[5]) + (c[6] + c[7]);
-            const float c2 = (c[8] + c[9]) + (c[10] + c[11]), c3 = (c[12] + c[13]) + (c[14] + c[15]);
-            l_run[qb] += ((a0 + a1) + (a2 + a3)) + ((c0 + c1) + (c2 + c3));
+            v2f u[8];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                u[j] = v2f{sc[qb][0][4 * j], sc[qb][0][4 * j + 1]} + v2f{sc[qb][0][4 * j + 2], sc[qb][0][4 * j + 3]};
+                u[4 + j] = v2f{sc[qb][1][4 * j], sc[qb][1][4 * j + 1]} + v2f{sc[qb][1][4 * j + 2], sc[qb][1][4 * j + 3]};
+            }
+            ps[qb] = ((u[0] + u[1]) + (u[2] + u[3])) + ((u[4] + u[5]) + (u[6] + u[7]));
         }
+    };
+    // exact row max of S (both lane halves); plain fmaxf, not inline-asm v_max3: the
+    // hazard recognizer must see these reads of fresh MFMA results to pad them
+    auto rowmax_of = [&](const v16f (&sc)[2]) {
+        float m0 = fmaxf(sc[0][0], sc[1][0]), m1 = fmaxf(sc[0][1], sc[1][1]);
+#pragma unroll
+        for (int e = 2; e < 16; e += 2) {
+            m0 = fmaxf(m0, fmaxf(sc[0][e], sc[1][e]));
+            m1 = fmaxf(m1, fmaxf(sc[0][e + 1], sc[1][e + 1]));
+        }
+        const float m = fmaxf(m0, m1);
+        return fmaxf(m, __shfl_xor(m, 32, 64));
+    };
+
+    const int ntiles = (S + AK - 1) / AK;
+    stage(0);
+    if (ntiles > 1) stage(1);
+    if (ntiles > 2) stage(2);
+    if (ntiles > 2) attn_wait_vm<4>();  // tiles 0 and 1 resident, 2 in flight
+    else attn_wait_vm<0>();
+    attn_sync();
+    // tile 0 establishes the running max m
+    v16f scur[QB][2];
+    qk(smem, 0, scur);
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+        const float m = rowmax_of(scur[qb]);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) { scur[qb][0][e] -= m; scur[qb][1][e] -= m; minit[qb][e] = -m; }
+    }
+
+    // one iteration: S' of tile t+1 is computed (MFMA) while tile t's softmax runs on the
+    // VALU, then O += P_t V_t.  Ring of NSLOT = 4: slot t (V_t), slot t+1 (K_{t+1}) are
+    // read, t+2 lands, t+3 is staged into the slot read one iteration ago.
+    // NEXT: 0 = tile t+1 is a full tile, 1 = tile t+1 may be partial (masked), 2 = t is last.
+    // In the unrolled main loop the slots are compile-time constants, so every LDS address is
+    // a loop-invariant per-lane VGPR plus an immediate offset.
+    auto iter = [&](auto next_c, const char* slot, const char* nslot, int t) {
+        constexpr int NEXT = decltype(next_c)::value;
+        if (!(ABL & 1) && t + 3 < ntiles) stage(t + 3);
+        v16f snext[QB][2];
+        if constexpr (NEXT == 0) qk_mfma(nslot, snext);
+        else if constexpr (NEXT == 1) qk(nslot, t + 1, snext);
+
+        // ---- online softmax with a deferred running max: scores are relative to m already.
+        //      Every P is >= 0, so a partial row sum <= LIM bounds every P of the tile by
+        //      LIM (an overflow shows up as inf); only when it fails is tile t recomputed
+        //      against an exact re-based max.
+        v2f ps[QB];
+        expsum(scur, ps);
+        if constexpr (NEXT == 0 && !(ABL & 32)) {
+            // full next tile: no mask branch, so its QK^T MFMAs share one scheduling region
+            // with this tile's exp2/sum; interleave them (VALU in every MFMA gap)
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+            for (int i = 0; i < 8 * QB; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);
+                if (i % QB == QB - 1 && i + 1 < 8 * QB) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            }
+        }
+        bool grow = false;
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) grow = grow || !(ps[qb][0] + ps[qb][1] <= ((ABL & 16) ? -1.0f : LIM));
+        if (__any(grow)) {
+            qk(slot, t, scur);
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb) {
+                const float delta = fmaxf(rowmax_of(scur[qb]), 0.f);
+                const float alpha = __builtin_amdgcn_exp2f(-delta);
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    scur[qb][0][e] -= delta;
+                    scur[qb][1][e] -= delta;
+                    o[qb][0][e] *= alpha;
+                    o[qb][1][e] *= alpha;
+                    minit[qb][e] -= delta;
+                }
+                if constexpr (NEXT != 2) {
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) { snext[qb][0][e] -= delta; snext[qb][1][e] -= delta; }
+                }
+                l_run[qb] *= alpha;
+            }
+            expsum(scur, ps);
+        }
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) l_run[qb] += ps[qb];
 
         // ---- O^T += V^T . P^T: P fragment of (key block kb, k-step s2) = regs 8s2..8s2+7;
         //      every V^T fragment read from LDS feeds QB MFMAs
@@ -280,7 +323,7 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
 #pragma unroll
                 for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
-                    for (int jj = 0; jj < 8; ++jj) pf[qb][jj] = (__bf16)sc[qb][kb][8 * s2 + jj];
+                    for (int jj = 0; jj < 8; ++jj) pf[qb][jj] = (__bf16)scur[qb][kb][8 * s2 + jj];
 #pragma unroll
                 for (int db = 0; db < 2; ++db) {
                     const char* pa = slot + voff[db] + (kb * 32 + 16 * s2) * 128;
@@ -301,30 +344,44 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
                 }
             }
 
-        // ---- retire tile t+1 (t+2 may stay in flight), then every wave passes the barrier
-        if (t + 1 < ntiles) {
-            if (t + 2 < ntiles) attn_wait_vm<4>();
+        // ---- tile t+2 must be resident for the next iteration's K read (t+3 may stay in
+        //      flight); the barrier also retires every wave's reads of slot t before the
+        //      next iteration stages t+4 into it
+        if (t + 2 < ntiles) {
+            if (t + 3 < ntiles) attn_wait_vm<4>();
             else attn_wait_vm<0>();
             attn_sync();
         }
+        if constexpr (NEXT != 2) {
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb) { scur[qb][0] = snext[qb][0]; scur[qb][1] = snext[qb][1]; }
+        }
     };
 
+    using full_c = std::integral_constant<int, 0>;
+    const int nfull = S / AK;  // full tiles
     int t = 0;
-    for (; t + NSLOT <= ntiles; t += NSLOT) {
-        tile(std::integral_constant<int, 0>{}, t);
-        tile(std::integral_constant<int, 1>{}, t + 1);
-        tile(std::integral_constant<int, 2>{}, t + 2);
+    for (; t + 5 <= nfull; t += NSLOT) {  // iterations t..t+3 all have a full next tile
+        iter(full_c{}, smem + 0 * KV_SLOT, smem + 1 * KV_SLOT, t);
+        iter(full_c{}, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, t + 1);
+        iter(full_c{}, smem + 2 * KV_SLOT, smem + 3 * KV_SLOT, t + 2);
+        iter(full_c{}, smem + 3 * KV_SLOT, smem + 0 * KV_SLOT, t + 3);
     }
-    if (t < ntiles) tile(std::integral_constant<int, 0>{}, t);
-    if (t + 1 < ntiles) tile(std::integral_constant<int, 1>{}, t + 1);
+    for (; t < ntiles; ++t) {  // at most 4 + 1 iterations: runtime slot, mask-checked next tile
+        const char* slot = smem + (t % NSLOT) * KV_SLOT;
+        const char* nslot = smem + ((t + 1) % NSLOT) * KV_SLOT;
+        if (t + 1 < ntiles) iter(std::integral_constant<int, 1>{}, slot, nslot, t);
+        else iter(std::integral_constant<int, 2>{}, slot, nslot, t);
+    }
 
     // ---- normalise and store O[q][d]: reg 4g+e of block db -> d = 32db + 8g + 4h + e;
     //      lane pairs (h=0/1) swap halves so each lane stores 16 contiguous bytes
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb) {
-        const int q = qrow_of[qb];
+        const int q = qblk * AQ + (wave * QB + qb) * 32 + r;
         const int qc = q < S ? q : S - 1;
-        const float l_tot = l_run[qb] + __shfl_xor(l_run[qb], 32, 64);
+        const float l_own = l_run[qb][0] + l_run[qb][1];
+        const float l_tot = l_own + __shfl_xor(l_own, 32, 64);
         const float inv = 1.0f / l_tot;
         unsigned pk[2][4][2];
 #pragma unroll
@@ -351,7 +408,7 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
 template <int QB, int ABL>
 static void launch_attn(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, float c_log2, uint16_t* out,
                         int64_t ldo, hipStream_t stream) {
-    constexpr int AQ = 4 * 32 * QB;
+    constexpr int AQ = 128 * QB;
     dim3 grid((unsigned)((S + AQ - 1) / AQ), (unsigned)(B * H));
     attn_fwd_d64_kernel<QB, ABL><<<grid, 256, 0, stream>>>(qkv, ld, (int)S, (int)H, c_log2, out, ldo);
 }
@@ -381,7 +438,7 @@ extern "C" int vc_attention_fwd(const uint16_t* qkv, int64_t ld, int64_t B, int6
 }
 
 // Timing-only ablations / variants of the attention kernel (tools/ablate_attn.py).
-// abl = 100*(QB-1) + ablation bits; ablation bits != 0 give wrong results by design.
+// abl = 100*(QB-1) + ablation bits (see attn_fwd_d64_kernel); bits 1..15 give wrong results by design.
 extern "C" int vc_attention_fwd_ablation(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H,
                                          float scale, uint16_t* out, int64_t ldo, int abl, hipStream_t stream) {
     if (int rc = attn_checks(qkv, ld, B, S, H, 64, out, ldo)) return rc;
@@ -389,7 +446,7 @@ extern "C" int vc_attention_fwd_ablation(const uint16_t* qkv, int64_t ld, int64_
 #define VC_ABL(QB, N) case 100 * (QB - 1) + N: launch_attn<QB, N>(qkv, ld, B, S, H, c_log2, out, ldo, stream); break;
     switch (abl) {
         VC_ABL(1, 0) VC_ABL(1, 1) VC_ABL(1, 2) VC_ABL(1, 4) VC_ABL(1, 6) VC_ABL(1, 8) VC_ABL(1, 12) VC_ABL(1, 14)
-        VC_ABL(1, 15) VC_ABL(2, 0) VC_ABL(2, 1) VC_ABL(2, 6) VC_ABL(2, 15)
+        VC_ABL(1, 15) VC_ABL(1, 16) VC_ABL(1, 32)
         default: return fail(VC_ERR_INVALID_ARG, "bad ablation");
     }
 #undef VC_ABL

@@ -100,12 +100,14 @@ __global__ void __launch_bounds__(256) gather_norm_kernel(const uint8_t* __restr
 }
 
 // ---------------------------------------------------------------------------------
-// Tubelet im2col.  pixel [B][T][C][H][W] f32 -> A[(b,t',hp,wp)][(c,kt,kh,kw)] bf16.
-// One thread converts 8 consecutive pixels of one image row (coalesced 32-B reads).
+// Tubelet im2col.  pixel [B][T][C][H][W] f32 -> A[token][(c,kt,kh,kw)] bf16, token in
+// (b,t',hp,wp) order (order 0, ViViT) or (b,hp,wp,t') order (order 1: patch-major,
+// time-minor, the TimeSformer token order).  One thread converts 8 consecutive pixels of
+// one image row (coalesced 32-B reads).
 // ---------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) im2col_kernel(const float* __restrict__ pix, int64_t total8, int T, int C,
-                                                     int H, int W, int kt, int kh, int kw, uint16_t* __restrict__ A,
-                                                     int64_t lda) {
+                                                     int H, int W, int kt, int kh, int kw, int order,
+                                                     uint16_t* __restrict__ A, int64_t lda) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= total8) return;
     const int W8 = W >> 3;
@@ -123,7 +125,7 @@ __global__ void __launch_bounds__(256) im2col_kernel(const float* __restrict__ p
     const int nt = T / kt, nh = H / kh, nw = W / kw;
     const int tp = t / kt, it = t % kt, hp = y / kh, ih = y % kh;
     const int x = x8 * 8, wp = x / kw, iw = x % kw;
-    const int64_t m = ((b * nt + tp) * nh + hp) * (int64_t)nw + wp;
+    const int64_t m = order ? ((b * nh + hp) * nw + wp) * (int64_t)nt + tp : ((b * nt + tp) * nh + hp) * (int64_t)nw + wp;
     const int64_t k = (((int64_t)c * kt + it) * kh + ih) * kw + iw;
     uint4 o;
     o.x = pack2bf(u.x, u.y);
@@ -277,16 +279,24 @@ int vc_frame_gather(const uint8_t* frames, int64_t nclips, int64_t F, int64_t H,
     return check_launch("vc_frame_gather");
 }
 
-int vc_tubelet_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C, int64_t H, int64_t W, int kt,
-                      int kh, int kw, uint16_t* A, int64_t lda, hipStream_t stream) {
-    if (!pixel_values || !A) return fail(VC_ERR_INVALID_ARG, "vc_tubelet_im2col: null pointer");
-    if (T % kt || H % kh || W % kw || kw % 8 || W % 8 || lda % 8 || lda < C * kt * kh * kw)
-        return fail(VC_ERR_INVALID_ARG, "vc_tubelet_im2col: shape not divisible by tubelet / 8-wide rows");
+int vc_patch_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C, int64_t H, int64_t W, int kt, int kh,
+                    int kw, int token_order, uint16_t* A, int64_t lda, hipStream_t stream) {
+    if (!pixel_values || !A) return fail(VC_ERR_INVALID_ARG, "vc_patch_im2col: null pointer");
+    if (kt <= 0 || kh <= 0 || kw <= 0 || T % kt || H % kh || W % kw || kw % 8 || W % 8 || lda % 8 ||
+        lda < C * kt * kh * kw)
+        return fail(VC_ERR_INVALID_ARG, "vc_patch_im2col: shape not divisible by tubelet / 8-wide rows");
+    if (token_order != VC_TOKENS_TIME_MAJOR && token_order != VC_TOKENS_PATCH_MAJOR)
+        return fail(VC_ERR_INVALID_ARG, "vc_patch_im2col: bad token_order");
     const int64_t total8 = B * T * C * H * (W / 8);
     const int64_t nb = (total8 + 255) / 256;
     im2col_kernel<<<(unsigned)nb, 256, 0, stream>>>(pixel_values, total8, (int)T, (int)C, (int)H, (int)W, kt, kh, kw,
-                                                   A, lda);
-    return check_launch("vc_tubelet_im2col");
+                                                   token_order, A, lda);
+    return check_launch("vc_patch_im2col");
+}
+
+int vc_tubelet_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C, int64_t H, int64_t W, int kt,
+                      int kh, int kw, uint16_t* A, int64_t lda, hipStream_t stream) {
+    return vc_patch_im2col(pixel_values, B, T, C, H, W, kt, kh, kw, VC_TOKENS_TIME_MAJOR, A, lda, stream);
 }
 
 int vc_layernorm_f32_bf16(const float* x, int64_t ldx, int64_t M, int64_t D, const float* gamma, const float* beta,

@@ -62,6 +62,57 @@ def make_vivit_weights(cfg: dict, seed: int = 0, std: float = 0.02) -> "OrderedD
     return out
 
 
+def timesformer_param_shapes(cfg: dict) -> "OrderedDict[str, tuple]":
+    """Parameter names and shapes of HF TimesformerForVideoClassification (divided space-time,
+    TF5/models/timesformer/modeling_timesformer.py:67-145, 148-398, 462-712), fixed order."""
+    D = cfg["hidden_size"]
+    I = cfg["intermediate_size"]
+    P = cfg["patch_size"]
+    C = cfg.get("num_channels", 3)
+    n_patch = (cfg["image_size"] // P) ** 2
+    L = cfg["num_hidden_layers"]
+    nl = cfg.get("num_labels", 2)
+    s = OrderedDict()
+    s["timesformer.embeddings.cls_token"] = (1, 1, D)
+    s["timesformer.embeddings.position_embeddings"] = (1, n_patch + 1, D)
+    s["timesformer.embeddings.time_embeddings"] = (1, cfg["num_frames"], D)
+    s["timesformer.embeddings.patch_embeddings.projection.weight"] = (D, C, P, P)
+    s["timesformer.embeddings.patch_embeddings.projection.bias"] = (D,)
+    for i in range(L):
+        p = f"timesformer.encoder.layer.{i}."
+        for att in ("attention", "temporal_attention"):
+            s[p + f"{att}.attention.qkv.weight"] = (3 * D, D)
+            s[p + f"{att}.attention.qkv.bias"] = (3 * D,)
+            s[p + f"{att}.output.dense.weight"] = (D, D)
+            s[p + f"{att}.output.dense.bias"] = (D,)
+        s[p + "intermediate.dense.weight"] = (I, D)
+        s[p + "intermediate.dense.bias"] = (I,)
+        s[p + "output.dense.weight"] = (D, I)
+        s[p + "output.dense.bias"] = (D,)
+        for ln in ("layernorm_before", "layernorm_after", "temporal_layernorm"):
+            s[p + f"{ln}.weight"] = (D,)
+            s[p + f"{ln}.bias"] = (D,)
+        s[p + "temporal_dense.weight"] = (D, D)
+        s[p + "temporal_dense.bias"] = (D,)
+    s["timesformer.layernorm.weight"] = (D,)
+    s["timesformer.layernorm.bias"] = (D,)
+    s["classifier.weight"] = (nl, D)
+    s["classifier.bias"] = (nl,)
+    return s
+
+
+def make_timesformer_weights(cfg: dict, seed: int = 0, std: float = 0.02) -> "OrderedDict[str, np.ndarray]":
+    rng = np.random.RandomState(seed)
+    out = OrderedDict()
+    for name, shape in timesformer_param_shapes(cfg).items():
+        w = rng.standard_normal(shape) * std
+        if name.endswith("norm_before.weight") or name.endswith("norm_after.weight") or \
+                name.endswith("temporal_layernorm.weight") or name == "timesformer.layernorm.weight":
+            w = w + 1.0
+        out[name] = np.ascontiguousarray(w.astype(np.float32))
+    return out
+
+
 def make_synthetic_frames(batch: int, num_frames: int, image_size: int, seed: int = 1) -> np.ndarray:
     """uint8 decoded frames [B, T, H, W, 3] (the layout the reference dataset returns,
     vivit_transformer/vivit_classifier/data_config/dataset.py:268-291)."""

@@ -27,7 +27,21 @@ sys.path.insert(0, ROOT)
 ATTN_GFLOP_PER_CLIP_LAYER = 4.0 * 3137 * 3137 * 64 * 12 / 1e9  # QK^T + PV, 30.23 GF
 VIVIT_GFLOP_PER_CLIP = 903.05   # measured with torch.utils.flop_counter on the HF model
 ATTN_GFLOP_PER_CLIP = 362.77
+ATTN_IO_BYTES_PER_CLIP = 3137 * 768 * 2 * 4  # q,k,v read + o written once, bf16
 PEAK_BF16_TFLOPS = 2500.0       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+
+
+def measured_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/rNN_*traffic.json, written by tools/traffic.sh: rocprofv3 FETCH_SIZE x2 +
+    WRITE_SIZE passes over this same bench command).  None when no summary exists."""
+    import glob
+    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
+    if not fs:
+        return None, None
+    with open(fs[-1]) as fh:
+        k = json.load(fh)["kernels"].get(kernel)
+    return (k["hbm_bytes_per_launch"] if k else None), os.path.relpath(fs[-1], ROOT)
 
 
 def _dist():
@@ -138,6 +152,7 @@ def main():
     if rank == 0:
         cpu = None
         logit_err = None
+        traffic, traffic_src = measured_traffic("attn_fwd_d64_kernel")
         if world == 1 and not a.no_cpu_baseline:
             shape_cfg = dict(cfg.as_shape_cfg(), num_attention_heads=cfg.num_attention_heads,
                              layer_norm_eps=cfg.layer_norm_eps)
@@ -165,7 +180,8 @@ def main():
             "logit_max_abs_err": logit_err,
             "roofline": {"bound": "mfma", "kernel": "attn_fwd_d64_kernel", "achieved": round(attn_tflops, 1),
                          "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4),
-                         "traffic": None, "avg_launch_ms": round(attn_ms, 4),
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "algorithmic_bytes": ATTN_IO_BYTES_PER_CLIP * a.batch, "avg_launch_ms": round(attn_ms, 4),
                          "flop_per_launch": f"{ATTN_GFLOP_PER_CLIP_LAYER:.2f} GF/clip x {a.batch} clips"},
             "model_tflops": round(model_tflops, 1),
             "model_frac_of_peak": round(model_tflops / PEAK_BF16_TFLOPS, 4),

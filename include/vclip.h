@@ -61,6 +61,19 @@ int vc_frame_gather(const uint8_t* frames, int64_t nclips, int64_t F, int64_t H,
 int vc_tubelet_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C, int64_t H, int64_t W,
                       int kt, int kh, int kw, uint16_t* A, int64_t lda, hipStream_t stream);
 
+/* Token orders of vc_patch_im2col. */
+#define VC_TOKENS_TIME_MAJOR  0  /* row = ((b*nt + t')*nh + hp)*nw + wp   (ViViT, modeling_vivit.py:64-67)          */
+#define VC_TOKENS_PATCH_MAJOR 1  /* row = ((b*nh + hp)*nw + wp)*nt + t'   (TimeSformer, modeling_timesformer.py:121-143) */
+
+/*
+ * vc_tubelet_im2col with an explicit token order.  With kt = 1 and VC_TOKENS_PATCH_MAJOR it is
+ * the input side of TimeSformer's per-frame Conv2d patch embedding re-ordered patch-major /
+ * time-minor (TimesformerPatchEmbeddings + the permute of TimesformerEmbeddings,
+ * TF5/models/timesformer/modeling_timesformer.py:45-60, 121-143).
+ */
+int vc_patch_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C, int64_t H, int64_t W,
+                    int kt, int kh, int kw, int token_order, uint16_t* A, int64_t lda, hipStream_t stream);
+
 /* GEMM epilogues for vc_gemm_bf16. */
 #define VC_EPI_BIAS_BF16        0  /* out bf16[m][n]  = acc + bias[n]                               */
 #define VC_EPI_BIAS_GELU_TANH   1  /* out bf16[m][n]  = gelu_fast(acc + bias[n])  (ViViT MLP fc1)    */
@@ -127,6 +140,38 @@ int vc_cls_init(const float* cls, const float* pos, float* x, int64_t ldx, int64
 int vc_cls_head(const float* x, int64_t ldx, int64_t B, int64_t S, int64_t D,
                 const float* gamma, const float* beta, float eps,
                 const float* Wc, const float* bc, int64_t num_labels, float* logits, hipStream_t stream);
+
+/* ---- TimeSformer divided space-time attention ------------------------
+ * Clip layout: rows b*S + r, S = 1 + P*T, r = 0 (CLS) or 1 + p*T + t (patch-major, time-minor).
+ * Frame layout: rows (b*T + t)*(1 + P) + j, j = 0 (CLS copy) or 1 + p (the spatial sequences). */
+
+/*
+ * Temporal attention: for each clip b, patch p and head, softmax(scale * q.k) v over the T
+ * rows 1 + p*T + t of the clip layout (one head_dim-64 slice per head of the fused q|k|v
+ * rows, as vc_attention_fwd).  out gets the same rows; CLS rows are not written.
+ * q_prescaled: q already carries scale*log2(e) (then exp2 is used), else q is scaled in fp32.
+ * Replaces TimesformerLayer's temporal branch attention (TF5/models/timesformer/
+ * modeling_timesformer.py:337-347 with TimesformerSelfAttention :148-180).  T <= 32.
+ */
+int vc_temporal_attention(const uint16_t* qkv, int64_t ld, int64_t B, int64_t P, int64_t T, int64_t H,
+                          int64_t head_dim, float scale, int q_prescaled, uint16_t* out, int64_t ldo,
+                          hipStream_t stream);
+
+#define VC_DIVIDED_TEMPORAL_TO_SPATIAL 0
+#define VC_DIVIDED_SPATIAL_TO_MLP      1
+/*
+ * Residual add + LayerNorm across the two layouts, fp32 residual x (clip layout), bf16 y, h.
+ *  mode 0: x[patch rows] += y[same rows] (y clip layout, the temporal_dense output) ->
+ *          h (frame layout) = LN(x) with each clip's CLS row LN-ed and copied to its T frames
+ *          (modeling_timesformer.py:349-366: temporal residual, CLS repeat, layernorm_before);
+ *  mode 1: x[patch row] += y[its frame-layout row]; x[CLS] += mean over t of y[(b*T+t)*(1+P)]
+ *          -> h (clip layout) = LN(x)   (modeling_timesformer.py:371-391: CLS mean, residual,
+ *          layernorm_after).
+ * D % 4 == 0, D <= 1024.
+ */
+int vc_divided_add_layernorm(float* x, int64_t ldx, const uint16_t* y, int64_t ldy, int64_t B, int64_t P, int64_t T,
+                             int64_t D, const float* gamma, const float* beta, float eps, int mode, uint16_t* h,
+                             int64_t ldh, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -11,6 +11,7 @@ Outputs (all data, no reference source):
   tests/golden/sampling.json     sampled frame indices for every sampler variant
   tests/golden/vivit_tiny.npz    tiny ViViT: inputs, weights seed, logits + hidden states
   tests/golden/vivit_full.json   ViViT-B/16x2 32f logits (B=2) + sha256 of weights/inputs
+  tests/golden/timesformer_tiny.npz / timesformer_full.json   the same for TimeSformer (8f)
   tests/golden/timesformer_tiny.npz  tiny TimeSformer logits (for the next §8 row)
 
 Usage:  PYTHONDONTWRITEBYTECODE=1 PYTHONHASHSEED=0 python tools/make_goldens.py [--skip-full]
@@ -288,16 +289,72 @@ def gen_vivit(skip_full):
     print("vivit_full logits", r["logits"])
 
 
+def _timesformer_golden(cfg_kwargs, batch, wseed, xseed, full):
+    import numpy as np
+    import torch
+    from transformers import TimesformerConfig, TimesformerForVideoClassification
+
+    sys.path.insert(0, ROOT)
+    from vclip_amd.weights import make_timesformer_weights, make_synthetic_clips, sha256_state
+
+    cfg = TimesformerConfig(**cfg_kwargs, id2label={0: "non-referral", 1: "referral"},
+                            label2id={"non-referral": 0, "referral": 1})
+    model = TimesformerForVideoClassification(cfg).eval()
+    sd = make_timesformer_weights(cfg_kwargs, seed=wseed)
+    missing, unexpected = model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=False)
+    assert not unexpected, unexpected
+    assert not missing, missing
+    pix = make_synthetic_clips(batch, cfg_kwargs["num_frames"], cfg_kwargs["image_size"], seed=xseed)
+    with torch.no_grad():
+        out = model(pixel_values=torch.from_numpy(pix), output_hidden_states=not full)
+    res = {"logits": out.logits.numpy()}
+    if not full:
+        res["hidden_states"] = np.stack([h.numpy() for h in out.hidden_states])
+        res["pixel_values"] = pix
+    res["weights_sha256"] = sha256_state(sd)
+    res["pixel_sha256"] = hashlib.sha256(np.ascontiguousarray(pix).tobytes()).hexdigest()
+    return res
+
+
+TSF_TINY = dict(image_size=64, patch_size=16, num_frames=4, num_channels=3, hidden_size=128, num_hidden_layers=2,
+                num_attention_heads=2, intermediate_size=256, hidden_act="gelu", layer_norm_eps=1e-6, qkv_bias=True,
+                attention_type="divided_space_time")
+TSF_B = dict(image_size=224, patch_size=16, num_frames=8, num_channels=3, hidden_size=768, num_hidden_layers=12,
+             num_attention_heads=12, intermediate_size=3072, hidden_act="gelu", layer_norm_eps=1e-6, qkv_bias=True,
+             attention_type="divided_space_time")
+
+
+def gen_timesformer(skip_full):
+    import numpy as np
+
+    r = _timesformer_golden(TSF_TINY, batch=3, wseed=0, xseed=1, full=False)
+    np.savez_compressed(os.path.join(GOLDEN, "timesformer_tiny.npz"), logits=r["logits"],
+                        hidden_states=r["hidden_states"], pixel_values=r["pixel_values"],
+                        config=json.dumps(TSF_TINY), weights_sha256=r["weights_sha256"])
+    print("timesformer_tiny logits", r["logits"])
+    if skip_full:
+        return
+    r = _timesformer_golden(TSF_B, batch=2, wseed=0, xseed=1, full=True)
+    with open(os.path.join(GOLDEN, "timesformer_full.json"), "w") as f:
+        json.dump({"config": TSF_B, "batch": 2, "weights_seed": 0, "input_seed": 1,
+                   "logits": r["logits"].tolist(), "weights_sha256": r["weights_sha256"],
+                   "pixel_sha256": r["pixel_sha256"],
+                   "oracle": "transformers TimesformerForVideoClassification, fp32 CPU"}, f, indent=1)
+    print("timesformer_full logits", r["logits"])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-full", action="store_true")
-    ap.add_argument("--only", choices=["sampling", "vivit"], default=None)
+    ap.add_argument("--only", choices=["sampling", "vivit", "timesformer"], default=None)
     a = ap.parse_args()
     os.makedirs(GOLDEN, exist_ok=True)
     if a.only in (None, "sampling"):
         gen_sampling()
     if a.only in (None, "vivit"):
         gen_vivit(a.skip_full)
+    if a.only in (None, "timesformer"):
+        gen_timesformer(a.skip_full)
 
 
 if __name__ == "__main__":
