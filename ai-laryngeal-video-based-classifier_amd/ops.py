@@ -55,8 +55,12 @@ def frame_gather(frames: torch.Tensor, idx: torch.Tensor, kind: str = "f32", sca
     return out
 
 
-def tubelet_im2col(pix: torch.Tensor, tubelet, out: torch.Tensor) -> torch.Tensor:
-    """pix f32 [B,T,C,H,W] -> out bf16 [>= B*nt*nh*nw, C*kt*kh*kw] (rows beyond are untouched)."""
+TOKEN_ORDER = {"time_major": 0, "patch_major": 1}
+
+
+def tubelet_im2col(pix: torch.Tensor, tubelet, out: torch.Tensor, order: str = "time_major") -> torch.Tensor:
+    """pix f32 [B,T,C,H,W] -> out bf16 [>= B*nt*nh*nw, C*kt*kh*kw] (rows beyond are untouched).
+    order "time_major": token (t', hp, wp) (ViViT); "patch_major": token (hp, wp, t') (TimeSformer)."""
     _dev(pix, out)
     _need(pix.dtype == torch.float32 and pix.dim() == 5 and pix.is_contiguous(), "pixel_values: f32 [B,T,C,H,W]")
     B, T, C, H, W = pix.shape
@@ -64,7 +68,9 @@ def tubelet_im2col(pix: torch.Tensor, tubelet, out: torch.Tensor) -> torch.Tenso
     ntok = B * (T // kt) * (H // kh) * (W // kw)
     _need(out.dtype == torch.bfloat16 and out.dim() == 2 and out.shape[0] >= ntok and out.shape[1] == C * kt * kh * kw
           and out.is_contiguous(), "im2col out: bf16 [rows, C*kt*kh*kw]")
-    _lib.call("vc_tubelet_im2col", _p(pix), B, T, C, H, W, kt, kh, kw, _p(out), out.stride(0), _stream(pix))
+    _need(H % kh == 0 and W % kw == 0 and T % kt == 0 and kw % 8 == 0, "im2col: shape not divisible by the patch")
+    _lib.call("vc_patch_im2col", _p(pix), B, T, C, H, W, kt, kh, kw, TOKEN_ORDER[order], _p(out), out.stride(0),
+              _stream(pix))
     return out
 
 
@@ -148,3 +154,39 @@ def cls_head(x: torch.Tensor, B: int, S: int, gamma, beta, eps: float, wc: torch
     _lib.call("vc_cls_head", _p(x), x.stride(0), B, S, D, _p(gamma), _p(beta), eps, _p(wc), _p(bc), nl, _p(out),
               _stream(x))
     return out
+
+
+def temporal_attention(qkv: torch.Tensor, B: int, P: int, T: int, H: int, scale: float, out: torch.Tensor,
+                       q_prescaled: bool = False) -> torch.Tensor:
+    """TimeSformer temporal attention on the clip layout (rows b*(1+P*T) + 1 + p*T + t):
+    qkv bf16 [rows, 3*H*64] -> out bf16 [rows, H*64] (CLS rows untouched)."""
+    _dev(qkv, out)
+    _need(qkv.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and qkv.stride(1) == 1 and out.stride(1) == 1,
+          "temporal_attention dtypes/layout")
+    _need(qkv.shape[1] >= 3 * H * 64 and out.shape[1] >= H * 64, "temporal_attention columns")
+    _need(qkv.shape[0] >= B * (1 + P * T) and out.shape[0] >= B * (1 + P * T), "temporal_attention rows")
+    _need(T <= 32, "temporal_attention: T <= 32")
+    _lib.call("vc_temporal_attention", _p(qkv), qkv.stride(0), B, P, T, H, 64, scale, int(bool(q_prescaled)), _p(out),
+              out.stride(0), _stream(qkv))
+    return out
+
+
+DIVIDED_MODE = {"temporal_to_spatial": 0, "spatial_to_mlp": 1}
+
+
+def divided_add_layernorm(x: torch.Tensor, y: torch.Tensor, B: int, P: int, T: int, gamma, beta, eps: float,
+                          mode: str, h: torch.Tensor) -> torch.Tensor:
+    """Residual add + LayerNorm across the TimeSformer clip / frame layouts (see include/vclip.h)."""
+    _dev(x, y, gamma, beta, h)
+    D = gamma.numel()
+    _need(x.dtype == torch.float32 and y.dtype == torch.bfloat16 and h.dtype == torch.bfloat16, "divided_add_ln dtypes")
+    _need(x.stride(1) == 1 and y.stride(1) == 1 and h.stride(1) == 1 and D % 4 == 0 and D <= 1024, "divided_add_ln")
+    rows_c, rows_f = B * (1 + P * T), B * T * (1 + P)
+    _need(x.shape[0] >= rows_c and x.shape[1] >= D and y.shape[1] >= D and h.shape[1] >= D, "divided_add_ln shapes")
+    if mode == "temporal_to_spatial":
+        _need(y.shape[0] >= rows_c and h.shape[0] >= rows_f, "divided_add_ln rows")
+    else:
+        _need(y.shape[0] >= rows_f and h.shape[0] >= rows_c, "divided_add_ln rows")
+    _lib.call("vc_divided_add_layernorm", _p(x), x.stride(0), _p(y), y.stride(0), B, P, T, D, _p(gamma), _p(beta), eps,
+              DIVIDED_MODE[mode], _p(h), h.stride(0), _stream(x))
+    return h

@@ -1,0 +1,273 @@
+"""TimeSformer-B (divided space-time attention) video classifier on the libvclip.so
+kernels — drop-in for the reference's `create_model`
+(timesformer/timesformer_classifier/models/timesformer_model.py:4-53), which returns an
+HF `TimesformerForVideoClassification` called as `model(pixel_values=...)` and read
+through `.logits` (timesformer/timesformer_classifier/trainers/trainer.py, inference.py).
+
+Device data layout (B clips, T frames, P = (image/16)^2 patches, S = 1 + P*T tokens):
+  clip layout   rows b*S + r, r = 0 (CLS) or 1 + p*T + t (patch-major, time-minor, the HF
+                residual-stream order, TF5/models/timesformer/modeling_timesformer.py:121-143)
+  frame layout  rows (b*T + t)*(1 + P) + j, j = 0 (CLS copy) or 1 + p: one spatial
+                sequence per frame (:355-364), fed to the joint flash kernel with
+                B' = B*T, S' = 1 + P
+  both padded to Mpad = roundup(max(B*S, B*T*(1+P)) + 128, 256) rows;
+  residual X f32 [Mpad, D] (clip), LN outputs bf16 (clip / frame), q|k|v bf16 [Mpad, 3D],
+  attention out bf16 [Mpad, D], branch GEMM out bf16 [Mpad, D], MLP hidden bf16 [Mpad, 4D].
+Per layer (TF5/.../modeling_timesformer.py:332-398):
+  LN_t -> qkv_t GEMM -> temporal attention (VALU, T keys) -> one GEMM for
+  temporal_attention.output.dense followed by temporal_dense (folded: W = Wtd.Wto,
+  b = Wtd.bto + btd, in fp32 before the bf16 cast) -> [x += ., LN_before, permute to
+  frame layout, CLS copied per frame] -> qkv_s GEMM -> flash attention -> output.dense
+  GEMM -> [x += ., CLS += frame mean, LN_after] -> fc1 + exact GELU -> fc2 + residual.
+"""
+from __future__ import annotations
+
+import json
+import math
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import ops
+from .vivit import ClassifierOutput, _round_up
+from .weights import timesformer_param_shapes
+
+
+class TimesformerConfig:
+    """Minimal stand-in for transformers.TimesformerConfig (the fields the path and the
+    reference's checkpoint dict use; the factory sets num_classes / video_size too,
+    timesformer_model.py:27-31)."""
+
+    defaults = dict(image_size=224, patch_size=16, num_channels=3, num_frames=8, hidden_size=768,
+                    num_hidden_layers=12, num_attention_heads=12, intermediate_size=3072, hidden_act="gelu",
+                    hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0, initializer_range=0.02,
+                    layer_norm_eps=1e-6, qkv_bias=True, attention_type="divided_space_time", drop_path_rate=0.0,
+                    model_type="timesformer")
+
+    def __init__(self, **kw):
+        d = dict(self.defaults)
+        d.update(kw)
+        id2label = d.pop("id2label", None) or {0: "LABEL_0", 1: "LABEL_1"}
+        self.id2label = {int(k): v for k, v in id2label.items()}
+        self.label2id = d.pop("label2id", None) or {v: k for k, v in self.id2label.items()}
+        d.pop("num_labels", None)
+        self.num_classes = d.pop("num_classes", len(self.id2label))
+        self.video_size = d.pop("video_size", [d["num_frames"], d["image_size"], d["image_size"]])
+        for k, v in d.items():
+            setattr(self, k, v)
+
+    @property
+    def num_labels(self):
+        return len(self.id2label)
+
+    def to_dict(self):
+        d = {k: getattr(self, k) for k in self.defaults}
+        d["id2label"] = {str(k): v for k, v in self.id2label.items()}
+        d["label2id"] = dict(self.label2id)
+        d["num_classes"] = self.num_classes
+        d["video_size"] = list(self.video_size)
+        return d
+
+    @classmethod
+    def from_dict(cls, d):
+        return cls(**d)
+
+    def as_shape_cfg(self):
+        return dict(hidden_size=self.hidden_size, intermediate_size=self.intermediate_size, patch_size=self.patch_size,
+                    num_channels=self.num_channels, num_frames=self.num_frames, image_size=self.image_size,
+                    num_hidden_layers=self.num_hidden_layers, num_labels=self.num_labels)
+
+    def __repr__(self):
+        return f"TimesformerConfig({json.dumps(self.to_dict())})"
+
+
+class TimesformerForVideoClassification(torch.nn.Module):
+    """fp32 master parameters in HF naming (state_dict compatible with transformers'
+    `TimesformerForVideoClassification`), bf16/fp32 packed device copies for the kernels."""
+
+    def __init__(self, config: TimesformerConfig):
+        super().__init__()
+        self.config = config
+        c = config
+        if c.hidden_size // c.num_attention_heads != 64:
+            raise ValueError("libvclip attention supports head_dim 64 only")
+        if c.attention_type != "divided_space_time":
+            raise ValueError("only attention_type='divided_space_time' (the reference's K400 checkpoint) is built")
+        self.params = torch.nn.ParameterDict()
+        shapes = timesformer_param_shapes(c.as_shape_cfg())
+        self._names = list(shapes.keys())
+        for name, shape in shapes.items():
+            self.params[name.replace(".", "__")] = torch.nn.Parameter(torch.zeros(shape), requires_grad=False)
+        self._packed = None
+        self._ws = {}
+
+    def state_dict(self, *a, **k):
+        return OrderedDict((n, self.params[n.replace(".", "__")].detach()) for n in self._names)
+
+    def load_state_dict(self, sd, strict: bool = True):
+        sd = {k[len("module."):] if k.startswith("module.") else k: v for k, v in sd.items()}
+        missing = [n for n in self._names if n not in sd]
+        unexpected = [k for k in sd if k not in self._names]
+        if strict and (missing or unexpected):
+            raise KeyError(f"load_state_dict: missing={missing[:5]} unexpected={unexpected[:5]}")
+        with torch.no_grad():
+            for n in self._names:
+                if n in sd:
+                    v = sd[n]
+                    v = torch.as_tensor(np.asarray(v)) if not isinstance(v, torch.Tensor) else v
+                    dst = self.params[n.replace(".", "__")]
+                    dst.copy_(v.reshape(dst.shape))
+        self._packed = None
+        return missing, unexpected
+
+    def P(self, name):
+        return self.params[name.replace(".", "__")]
+
+    def _pack(self, device):
+        if self._packed is not None and self._packed["device"] == device:
+            return self._packed
+        c = self.config
+        bf, f32 = torch.bfloat16, torch.float32
+        P = lambda n: self.P(n).detach().to(device=device, dtype=f32)  # noqa: E731
+        D, T = c.hidden_size, c.num_frames
+        e = "timesformer.embeddings."
+        pk = {"device": device}
+        pk["w_emb"] = P(e + "patch_embeddings.projection.weight").reshape(D, -1).to(bf).contiguous()
+        pk["b_emb"] = P(e + "patch_embeddings.projection.bias").contiguous()
+        pos = P(e + "position_embeddings").reshape(-1, D)
+        tim = P(e + "time_embeddings").reshape(-1, D)
+        # EMBED epilogue table: row p*T + t = pos[1 + p] + time[t] (patch-major, time-minor)
+        pk["pos_time"] = (pos[1:, None, :] + tim[None, :T, :]).reshape(-1, D).contiguous()
+        pk["pos"] = pos.contiguous()
+        pk["cls"] = P(e + "cls_token").reshape(D).contiguous()
+        qs = (D // c.num_attention_heads) ** -0.5 * ops.LOG2E  # softmax scale * log2(e) folded into q
+
+        def qkv(prefix):
+            w = P(prefix + "attention.qkv.weight").clone()
+            b = P(prefix + "attention.qkv.bias").clone()
+            w[:D] *= qs
+            b[:D] *= qs
+            return w.to(bf).contiguous(), b.contiguous()
+
+        layers = []
+        for i in range(c.num_hidden_layers):
+            p = f"timesformer.encoder.layer.{i}."
+            L = {}
+            for ln, key in (("temporal_layernorm", "lnt"), ("layernorm_before", "ln1"), ("layernorm_after", "ln2")):
+                L[key + "_g"] = P(p + ln + ".weight").contiguous()
+                L[key + "_b"] = P(p + ln + ".bias").contiguous()
+            L["w_qkv_t"], L["b_qkv_t"] = qkv(p + "temporal_attention.")
+            wto, bto = P(p + "temporal_attention.output.dense.weight"), P(p + "temporal_attention.output.dense.bias")
+            wtd, btd = P(p + "temporal_dense.weight"), P(p + "temporal_dense.bias")
+            L["w_t"] = (wtd.double() @ wto.double()).to(bf).contiguous()
+            L["b_t"] = (wtd.double() @ bto.double() + btd.double()).to(f32).contiguous()
+            L["w_qkv_s"], L["b_qkv_s"] = qkv(p + "attention.")
+            L["w_o"] = P(p + "attention.output.dense.weight").to(bf).contiguous()
+            L["b_o"] = P(p + "attention.output.dense.bias").contiguous()
+            L["w_1"] = P(p + "intermediate.dense.weight").to(bf).contiguous()
+            L["b_1"] = P(p + "intermediate.dense.bias").contiguous()
+            L["w_2"] = P(p + "output.dense.weight").to(bf).contiguous()
+            L["b_2"] = P(p + "output.dense.bias").contiguous()
+            layers.append(L)
+        pk["layers"] = layers
+        pk["lnf_g"] = P("timesformer.layernorm.weight").contiguous()
+        pk["lnf_b"] = P("timesformer.layernorm.bias").contiguous()
+        pk["w_cls"] = P("classifier.weight").contiguous()
+        pk["b_cls"] = P("classifier.bias").contiguous()
+        self._packed = pk
+        return pk
+
+    def geometry(self, B):
+        c = self.config
+        P = (c.image_size // c.patch_size) ** 2
+        T = c.num_frames
+        S = 1 + P * T
+        Mpad = _round_up(max(B * S, B * T * (1 + P)) + 128, 256)
+        Memb = _round_up(B * P * T, 128)
+        return P, T, S, Mpad, Memb
+
+    def _workspace(self, B, device):
+        key = (B, str(device))
+        if key in self._ws:
+            return self._ws[key]
+        c = self.config
+        D, I = c.hidden_size, c.intermediate_size
+        P, T, S, Mpad, Memb = self.geometry(B)
+        bf = torch.bfloat16
+        z = lambda *s, dt=bf: torch.zeros(s, dtype=dt, device=device)  # noqa: E731
+        ws = dict(A_emb=z(Memb, c.num_channels * c.patch_size * c.patch_size), X=z(Mpad, D, dt=torch.float32),
+                  Hc=z(Mpad, D), Hf=z(Mpad, D), QKV=z(Mpad, 3 * D), O=z(Mpad, D), Yb=z(Mpad, D), Hd=z(Mpad, I),
+                  logits=z(B, c.num_labels, dt=torch.float32))
+        self._ws = {key: ws}
+        return ws
+
+    @torch.no_grad()
+    def forward(self, pixel_values: torch.Tensor = None, labels: torch.Tensor = None, **kw):
+        if pixel_values is None:
+            raise ValueError("pixel_values required")
+        if pixel_values.device.type != "cuda":
+            raise RuntimeError("TimesformerForVideoClassification (vclip_amd) runs on the GPU only")
+        x = pixel_values.contiguous().float() if pixel_values.dtype != torch.float32 else pixel_values.contiguous()
+        logits = self.forward_logits(x)
+        loss = None
+        if labels is not None:
+            loss = torch.nn.functional.cross_entropy(logits, labels.to(logits.device))
+        return ClassifierOutput(logits, loss)
+
+    def forward_logits(self, pix: torch.Tensor) -> torch.Tensor:
+        c = self.config
+        B, T, C, H, W = pix.shape
+        if T != c.num_frames or H != c.image_size or W != c.image_size or C != c.num_channels:
+            raise ValueError(f"pixel_values {tuple(pix.shape)} do not match config "
+                             f"(T={c.num_frames}, C={c.num_channels}, {c.image_size}^2)")
+        pk = self._pack(pix.device)
+        ws = self._workspace(B, pix.device)
+        P, T, S, Mpad, Memb = self.geometry(B)
+        Hn = c.num_attention_heads
+        eps = c.layer_norm_eps
+        X, Hc, Hf, QKV, O, Yb, Hd = (ws[k] for k in ("X", "Hc", "Hf", "QKV", "O", "Yb", "Hd"))
+        pc = c.patch_size
+        ops.tubelet_im2col(pix, (1, pc, pc), ws["A_emb"], order="patch_major")
+        ops.gemm(ws["A_emb"], pk["w_emb"], pk["b_emb"], "embed_f32", X, aux=pk["pos_time"], group=P * T,
+                 group_stride=S, group_offset=1, m=Memb)
+        ops.cls_init(pk["cls"], pk["pos"], X, B, S)
+        act = "bias_gelu_erf" if c.hidden_act == "gelu" else "bias_gelu_tanh"
+        scale = 1.0 / math.sqrt(c.hidden_size // Hn)
+        for L in pk["layers"]:
+            # temporal branch (clip layout)
+            ops.layernorm(X, L["lnt_g"], L["lnt_b"], eps, Hc, m=B * S)
+            ops.gemm(Hc, L["w_qkv_t"], L["b_qkv_t"], "bias", QKV)
+            ops.temporal_attention(QKV, B, P, T, Hn, scale, O, q_prescaled=True)
+            ops.gemm(O, L["w_t"], L["b_t"], "bias", Yb)
+            # spatial branch (frame layout)
+            ops.divided_add_layernorm(X, Yb, B, P, T, L["ln1_g"], L["ln1_b"], eps, "temporal_to_spatial", Hf)
+            ops.gemm(Hf, L["w_qkv_s"], L["b_qkv_s"], "bias", QKV)
+            ops.attention(QKV, B * T, 1 + P, Hn, scale, O, q_prescaled=True)
+            ops.gemm(O, L["w_o"], L["b_o"], "bias", Yb)
+            # MLP (clip layout)
+            ops.divided_add_layernorm(X, Yb, B, P, T, L["ln2_g"], L["ln2_b"], eps, "spatial_to_mlp", Hc)
+            ops.gemm(Hc, L["w_1"], L["b_1"], act, Hd)
+            ops.gemm(Hd, L["w_2"], L["b_2"], "bias_resid_f32", X)
+        return ops.cls_head(X, B, S, pk["lnf_g"], pk["lnf_b"], eps, pk["w_cls"], pk["b_cls"], out=ws["logits"])
+
+
+def create_model(model_name="facebook/timesformer-base-finetuned-k400", num_classes=2, class_labels=None,
+                 num_frames=8, device="cuda", logger=None, weights_seed: int = 0):
+    """Drop-in for timesformer/timesformer_classifier/models/timesformer_model.py:4-53.
+
+    The reference loads `TimesformerConfig.from_pretrained(model_name)` + K400 weights
+    (`ignore_mismatched_sizes=True` re-initialises the head, and the time embeddings when
+    num_frames != 8).  No network here: the TimeSformer-B architecture is built with seeded
+    synthetic weights (vclip_amd.weights) unless a checkpoint is loaded afterwards.
+    """
+    class_labels = class_labels or ["non-referral", "referral"]
+    id2label = {i: l for i, l in enumerate(class_labels)}
+    cfg = TimesformerConfig(num_frames=num_frames, id2label=id2label, label2id={l: i for i, l in id2label.items()},
+                            num_classes=num_classes, video_size=[num_frames, 224, 224])
+    if logger:
+        logger.info(f"Creating TimeSformer model based on {model_name} (num_frames={num_frames}) on {device}")
+    model = TimesformerForVideoClassification(cfg)
+    from .weights import make_timesformer_weights
+    model.load_state_dict(make_timesformer_weights(cfg.as_shape_cfg(), seed=weights_seed))
+    return model.to(device) if device else model

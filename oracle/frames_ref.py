@@ -25,11 +25,13 @@ def gather_norm(frames, idx, scale=np.float32(1.0 / 63.75), shift=np.float32(-3.
     return np.ascontiguousarray(y.transpose(0, 1, 4, 2, 3))
 
 
-def tubelet_im2col(pix, tubelet=(2, 16, 16)):
-    """pix f32 [B,T,C,H,W] -> [B*nt*nh*nw, C*kt*kh*kw] (same dtype)."""
+def tubelet_im2col(pix, tubelet=(2, 16, 16), order="time_major"):
+    """pix f32 [B,T,C,H,W] -> [B*nt*nh*nw, C*kt*kh*kw] (same dtype).  Token rows in (t',hp,wp)
+    order (ViViT Conv3d flatten, modeling_vivit.py:64-67) or, order="patch_major", (hp,wp,t')
+    (TimeSformer per-frame Conv2d + patch-major re-order, modeling_timesformer.py:121-143)."""
     B, T, C, H, W = pix.shape
     kt, kh, kw = tubelet
     x = pix.reshape(B, T // kt, kt, C, H // kh, kh, W // kw, kw)
-    # -> B, nt, nh, nw, C, kt, kh, kw
-    x = x.transpose(0, 1, 4, 6, 3, 2, 5, 7)
+    # -> B, nt, nh, nw, C, kt, kh, kw   (or B, nh, nw, nt, ... for patch-major)
+    x = x.transpose(0, 1, 4, 6, 3, 2, 5, 7) if order == "time_major" else x.transpose(0, 4, 6, 1, 3, 2, 5, 7)
     return np.ascontiguousarray(x.reshape(B * (T // kt) * (H // kh) * (W // kw), C * kt * kh * kw))
