@@ -27,7 +27,9 @@ SIGNATURES = {
     "vc_last_error": ([], ctypes.c_char_p),
     "vc_frame_gather": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_int, c_f, c_f, c_p, c_p], c_int),
     "vc_tubelet_im2col": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_p, c_i64, c_p], c_int),
-    "vc_patch_im2col": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_int, c_p, c_i64, c_p], c_int),
+    "vc_patch_im2col": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_int, c_int, c_p, c_i64, c_p],
+                        c_int),
+    "vc_layernorm_f32": ([c_p, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_p, c_i64, c_p], c_int),
     "vc_gemm_bf16": ([c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_int, c_p, c_i64, c_p, c_i64,
                       c_i64, c_i64, c_i64, c_p], c_int),
     "vc_gemm_bf16_cfg": ([c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_int, c_p, c_i64, c_p, c_i64,
@@ -37,6 +39,10 @@ SIGNATURES = {
     "vc_cls_init": ([c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p], c_int),
     "vc_cls_head": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_p, c_p, c_i64, c_p, c_p], c_int),
     "vc_temporal_attention": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_int, c_p, c_i64, c_p], c_int),
+    "vc_window_attention3d": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_int, c_int,
+                               c_int, c_p, c_i64, c_p, c_i64, c_p], c_int),
+    "vc_patch_merge_layernorm": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_p, c_i64, c_p], c_int),
+    "vc_pool_head": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_p, c_p, c_i64, c_p, c_p], c_int),
     "vc_divided_add_layernorm": ([c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_int, c_p,
                                   c_i64, c_p], c_int),
 }

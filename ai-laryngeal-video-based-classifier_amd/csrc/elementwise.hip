@@ -100,39 +100,50 @@ __global__ void __launch_bounds__(256) gather_norm_kernel(const uint8_t* __restr
 }
 
 // ---------------------------------------------------------------------------------
-// Tubelet im2col.  pixel [B][T][C][H][W] f32 -> A[token][(c,kt,kh,kw)] bf16, token in
-// (b,t',hp,wp) order (order 0, ViViT) or (b,hp,wp,t') order (order 1: patch-major,
-// time-minor, the TimeSformer token order).  One thread converts 8 consecutive pixels of
-// one image row (coalesced 32-B reads).
+// Tubelet im2col.  pixel f32 [B][T][C][H][W] (layout 0, HF video models) or [B][C][T][H][W]
+// (layout 1, torchvision video models) -> A[token][(c,kt,kh,kw)] bf16, token in (b,t',hp,wp)
+// order (order 0, ViViT / Swin) or (b,hp,wp,t') order (order 1: patch-major, time-minor,
+// the TimeSformer token order).  One thread converts VEC consecutive pixels of one image
+// row (VEC = 8, or 4 for 4-wide patches such as Swin's 2x4x4).
 // ---------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) im2col_kernel(const float* __restrict__ pix, int64_t total8, int T, int C,
-                                                     int H, int W, int kt, int kh, int kw, int order,
+template <int VEC>
+__global__ void __launch_bounds__(256) im2col_kernel(const float* __restrict__ pix, int64_t totalv, int T, int C,
+                                                     int H, int W, int kt, int kh, int kw, int order, int layout,
                                                      uint16_t* __restrict__ A, int64_t lda) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= total8) return;
-    const int W8 = W >> 3;
+    if (i >= totalv) return;
+    const int WV = W / VEC;
     int64_t r = i;
-    const int x8 = r % W8;
-    r /= W8;
+    const int xv = r % WV;
+    r /= WV;
     const int y = r % H;
     r /= H;
     const int c = r % C;
     r /= C;
     const int t = r % T;
     const int64_t b = r / T;
-    const float4* s = reinterpret_cast<const float4*>(pix + ((((b * T + t) * C + c) * H + y) * (int64_t)W) + x8 * 8);
-    const float4 u = s[0], v = s[1];
+    const int64_t plane = layout ? ((b * C + c) * T + t) : ((b * T + t) * C + c);
+    const float4* s = reinterpret_cast<const float4*>(pix + (plane * H + y) * (int64_t)W + xv * VEC);
     const int nt = T / kt, nh = H / kh, nw = W / kw;
     const int tp = t / kt, it = t % kt, hp = y / kh, ih = y % kh;
-    const int x = x8 * 8, wp = x / kw, iw = x % kw;
+    const int x = xv * VEC, wp = x / kw, iw = x % kw;
     const int64_t m = order ? ((b * nh + hp) * nw + wp) * (int64_t)nt + tp : ((b * nt + tp) * nh + hp) * (int64_t)nw + wp;
     const int64_t k = (((int64_t)c * kt + it) * kh + ih) * kw + iw;
-    uint4 o;
-    o.x = pack2bf(u.x, u.y);
-    o.y = pack2bf(u.z, u.w);
-    o.z = pack2bf(v.x, v.y);
-    o.w = pack2bf(v.z, v.w);
-    *reinterpret_cast<uint4*>(A + m * lda + k) = o;
+    const float4 u = s[0];
+    if constexpr (VEC == 8) {
+        const float4 v = s[1];
+        uint4 o;
+        o.x = pack2bf(u.x, u.y);
+        o.y = pack2bf(u.z, u.w);
+        o.z = pack2bf(v.x, v.y);
+        o.w = pack2bf(v.z, v.w);
+        *reinterpret_cast<uint4*>(A + m * lda + k) = o;
+    } else {
+        uint2 o;
+        o.x = pack2bf(u.x, u.y);
+        o.y = pack2bf(u.z, u.w);
+        *reinterpret_cast<uint2*>(A + m * lda + k) = o;
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -175,10 +186,12 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
 }
 
 // Generic-width LayerNorm (any D): one wave per row, three passes over the row (L1/L2-resident).
+// OUTF32: the output is f32 (y is a float*), e.g. Swin's patch_embed.norm feeding the residual stream.
+template <bool OUTF32 = false>
 __global__ void __launch_bounds__(256) layernorm_any_kernel(const float* __restrict__ x, int64_t ldx, int64_t M,
                                                             int D, const float* __restrict__ g,
                                                             const float* __restrict__ be, float eps,
-                                                            uint16_t* __restrict__ y, int64_t ldy) {
+                                                            void* __restrict__ y, int64_t ldy) {
     const int lane = threadIdx.x & 63;
     const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= M) return;
@@ -192,7 +205,13 @@ __global__ void __launch_bounds__(256) layernorm_any_kernel(const float* __restr
         q += d * d;
     }
     const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
-    for (int n = lane; n < D; n += 64) y[row * ldy + n] = f2bf((xr[n] - mean) * rstd * g[n] + be[n]);
+    for (int n = lane; n < D; n += 64) {
+        const float v = (xr[n] - mean) * rstd * g[n] + be[n];
+        if constexpr (OUTF32)
+            reinterpret_cast<float*>(y)[row * ldy + n] = v;
+        else
+            reinterpret_cast<uint16_t*>(y)[row * ldy + n] = f2bf(v);
+    }
 }
 
 __global__ void cls_init_kernel(const float* __restrict__ cls, const float* __restrict__ pos, float* __restrict__ x,
@@ -280,23 +299,29 @@ int vc_frame_gather(const uint8_t* frames, int64_t nclips, int64_t F, int64_t H,
 }
 
 int vc_patch_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C, int64_t H, int64_t W, int kt, int kh,
-                    int kw, int token_order, uint16_t* A, int64_t lda, hipStream_t stream) {
+                    int kw, int token_order, int layout, uint16_t* A, int64_t lda, hipStream_t stream) {
     if (!pixel_values || !A) return fail(VC_ERR_INVALID_ARG, "vc_patch_im2col: null pointer");
-    if (kt <= 0 || kh <= 0 || kw <= 0 || T % kt || H % kh || W % kw || kw % 8 || W % 8 || lda % 8 ||
-        lda < C * kt * kh * kw)
-        return fail(VC_ERR_INVALID_ARG, "vc_patch_im2col: shape not divisible by tubelet / 8-wide rows");
+    if (kt <= 0 || kh <= 0 || kw <= 0 || T % kt || H % kh || W % kw || kw % 4 || W % 4 || lda % 4 ||
+        lda < C * kt * kh * kw || ((uintptr_t)pixel_values & 15) || ((uintptr_t)A & 7))
+        return fail(VC_ERR_INVALID_ARG, "vc_patch_im2col: shape not divisible by the patch / 4-wide rows / alignment");
     if (token_order != VC_TOKENS_TIME_MAJOR && token_order != VC_TOKENS_PATCH_MAJOR)
         return fail(VC_ERR_INVALID_ARG, "vc_patch_im2col: bad token_order");
-    const int64_t total8 = B * T * C * H * (W / 8);
-    const int64_t nb = (total8 + 255) / 256;
-    im2col_kernel<<<(unsigned)nb, 256, 0, stream>>>(pixel_values, total8, (int)T, (int)C, (int)H, (int)W, kt, kh, kw,
-                                                   token_order, A, lda);
+    if (layout != VC_VIDEO_BTCHW && layout != VC_VIDEO_BCTHW) return fail(VC_ERR_INVALID_ARG, "vc_patch_im2col: bad layout");
+    if (kw % 8 == 0 && lda % 8 == 0 && !((uintptr_t)A & 15)) {
+        const int64_t totalv = B * T * C * H * (W / 8);
+        im2col_kernel<8><<<(unsigned)((totalv + 255) / 256), 256, 0, stream>>>(
+            pixel_values, totalv, (int)T, (int)C, (int)H, (int)W, kt, kh, kw, token_order, layout, A, lda);
+    } else {
+        const int64_t totalv = B * T * C * H * (W / 4);
+        im2col_kernel<4><<<(unsigned)((totalv + 255) / 256), 256, 0, stream>>>(
+            pixel_values, totalv, (int)T, (int)C, (int)H, (int)W, kt, kh, kw, token_order, layout, A, lda);
+    }
     return check_launch("vc_patch_im2col");
 }
 
 int vc_tubelet_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C, int64_t H, int64_t W, int kt,
                       int kh, int kw, uint16_t* A, int64_t lda, hipStream_t stream) {
-    return vc_patch_im2col(pixel_values, B, T, C, H, W, kt, kh, kw, VC_TOKENS_TIME_MAJOR, A, lda, stream);
+    return vc_patch_im2col(pixel_values, B, T, C, H, W, kt, kh, kw, VC_TOKENS_TIME_MAJOR, VC_VIDEO_BTCHW, A, lda, stream);
 }
 
 int vc_layernorm_f32_bf16(const float* x, int64_t ldx, int64_t M, int64_t D, const float* gamma, const float* beta,
@@ -311,9 +336,17 @@ int vc_layernorm_f32_bf16(const float* x, int64_t ldx, int64_t M, int64_t D, con
         case 1024: layernorm_kernel<4><<<nb, 256, 0, stream>>>(x, ldx, M, gamma, beta, eps, y, ldy); break;
         default:
             if (D <= 0 || D > 65536) return fail(VC_ERR_INVALID_ARG, "vc_layernorm: bad D");
-            layernorm_any_kernel<<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, gamma, beta, eps, y, ldy);
+            layernorm_any_kernel<false><<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, gamma, beta, eps, y, ldy);
     }
     return check_launch("vc_layernorm_f32_bf16");
+}
+
+int vc_layernorm_f32(const float* x, int64_t ldx, int64_t M, int64_t D, const float* gamma, const float* beta,
+                     float eps, float* y, int64_t ldy, hipStream_t stream) {
+    if (!x || !gamma || !beta || !y) return fail(VC_ERR_INVALID_ARG, "vc_layernorm_f32: null pointer");
+    if (D <= 0 || D > 65536 || ldx < D || ldy < D) return fail(VC_ERR_INVALID_ARG, "vc_layernorm_f32: bad D / ld");
+    layernorm_any_kernel<true><<<(unsigned)((M + 3) / 4), 256, 0, stream>>>(x, ldx, M, (int)D, gamma, beta, eps, y, ldy);
+    return check_launch("vc_layernorm_f32");
 }
 
 int vc_cls_init(const float* cls, const float* pos, float* x, int64_t ldx, int64_t B, int64_t S, int64_t D,

@@ -101,6 +101,8 @@ __device__ __forceinline__ void store_tile(const v16f (&acc)[MI][NI], int64_t mb
                     float4 x = *o;
                     x.x += v0; x.y += v1; x.z += v2; x.w += v3;
                     *o = x;
+                } else if (EPI == VC_EPI_BIAS_F32) {
+                    *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + m * ldo + n) = make_float4(v0, v1, v2, v3);
                 } else {  // VC_EPI_EMBED_F32
                     const int64_t gi = m / G, gr = m - gi * G;
                     const float4 a = *reinterpret_cast<const float4*>(aux + gr * ldaux + n);
@@ -752,6 +754,8 @@ extern "C" int vc_gemm_bf16_cfg(const uint16_t* A, int64_t lda, const uint16_t* 
             return launch_epi<VC_EPI_BIAS_RESID_F32>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
         case VC_EPI_EMBED_F32:
             return launch_epi<VC_EPI_EMBED_F32>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
+        case VC_EPI_BIAS_F32:
+            return launch_epi<VC_EPI_BIAS_F32>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
     }
     return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad epilogue");
 }

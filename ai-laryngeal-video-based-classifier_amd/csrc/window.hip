@@ -1,0 +1,341 @@
+// Video Swin 3D shifted-window attention, head_dim 32, bf16 MFMA.
+//
+// Replaces torchvision's ShiftedWindowAttention3d core (shifted_window_attention_3d: roll,
+// window partition, q.k^T * d^-1/2 + relative-position bias (+ -100 between shift regions),
+// softmax, .v, window reverse, roll back — as called by the reference's swin3d_t,
+// videoswintransformer/swin_video_classifier/models/swin3d.py:24-26).
+//
+// No data moves for the roll / partition / reverse: the window token n of window
+// (wt_i, wh_i, ww_i) at rolled grid position (wt_i*Wt + i, ...) is the token at original
+// position ((wt_i*Wt + i + st) mod T, ...), so the kernel gathers its q|k|v rows by index
+// from the projection output (token layout [B][T][H][W]) and scatters the output rows back
+// to the same positions, where the proj GEMM + residual run per token.
+//
+// One workgroup = 4 waves = one (window, head).  The window's K and V (vol <= 448 tokens x
+// 32 dims, bf16) are staged once into LDS (57 KB, 2 workgroups per CU); each wave walks
+// 32-query blocks: S^T = K.Q'^T with the bias tile as the MFMA C operand (biasT[h][k][q],
+// pre-scaled by log2 e like Q', -inf on padded keys), the shift-region mask as -inf
+// (torchvision adds -100: exp(-100) ~ 4e-44 is below fp32 resolution of the row sum, so the
+// results agree), online softmax in exp2, O^T += V^T.P^T with V^T from ds_read_b64_tr_b16.
+#include "common.hpp"
+
+namespace vc {
+
+constexpr int WNP_MAX = 448;  // max padded window volume (8*7*7 = 392 -> 448)
+
+__device__ __forceinline__ int kchunk_swz(int r, int c) { return c ^ ((r >> 2) & 3); }
+
+struct WinGeom {
+    int T, H, W;      // token grid (multiples of the window)
+    int wt, wh, ww;   // window
+    int st, sh, sw;   // shift (0 where none)
+    int nwt, nwh, nww;
+};
+
+// Shift-region label of one dimension for a rolled coordinate c (torchvision's t/h/w
+// slices: 0 below P-w, 1 in [P-w, P-s), 2 from P-s; with s == 0 the slices are (0,-w),
+// (-w,0) = empty and (0,None) = all, so every position gets 2).  Inside ONE window a
+// dimension takes at most two of these values ({0} or {1,2} or {2}), so "label == 2" is
+// one bit and the 3-bit code (t,h,w) compares equal exactly when the labels do.
+__device__ __forceinline__ int region_bit(int c, int P, int w, int s) {
+    if (s == 0) return 1;
+    return c >= P - s ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(256, 2)
+window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, int heads, int vol, int NP,
+                       const float* __restrict__ biasT, int masked, uint16_t* __restrict__ out, int64_t ldo) {
+    __shared__ __attribute__((aligned(16))) char kv[2 * WNP_MAX * 64];
+    __shared__ unsigned lab4[WNP_MAX / 8];  // 4-bit region code per window token (15: padding)
+
+    const int head = blockIdx.y;
+    const int nwin = g.nwt * g.nwh * g.nww;
+    const int b = blockIdx.x / nwin;
+    int r = blockIdx.x - b * nwin;
+    const int wi_t = r / (g.nwh * g.nww);
+    r -= wi_t * g.nwh * g.nww;
+    const int wi_h = r / g.nww, wi_w = r - (r / g.nww) * g.nww;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int hw = g.wh * g.ww;
+    const int C = heads * 32;
+
+    auto token_row = [&](int n, int* label) -> int64_t {
+        const int i = n / hw, j = (n / g.ww) % g.wh, k = n % g.ww;
+        const int tr = wi_t * g.wt + i, hr = wi_h * g.wh + j, wr = wi_w * g.ww + k;
+        if (label)
+            *label = 4 * region_bit(tr, g.T, g.wt, g.st) + 2 * region_bit(hr, g.H, g.wh, g.sh) +
+                     region_bit(wr, g.W, g.ww, g.sw);
+        int t = tr + g.st, hh = hr + g.sh, w = wr + g.sw;
+        t -= t >= g.T ? g.T : 0;
+        hh -= hh >= g.H ? g.H : 0;
+        w -= w >= g.W ? g.W : 0;
+        return (((int64_t)b * g.T + t) * g.H + hh) * g.W + w;
+    };
+
+    // ---- stage K (swizzled 16-B chunks) and V (plain 64-B rows) of this window/head in LDS
+    char* Ks = kv;
+    char* Vs = kv + WNP_MAX * 64;
+    for (int c = tid; c < NP * 4; c += 256) {
+        const int n = c >> 2, ch = c & 3;
+        uint4 kval = make_uint4(0, 0, 0, 0), vval = make_uint4(0, 0, 0, 0);
+        if (n < vol) {
+            const int64_t row = token_row(n, nullptr);
+            const uint16_t* src = qkv + row * ld + head * 32 + ch * 8;
+            kval = *reinterpret_cast<const uint4*>(src + C);
+            vval = *reinterpret_cast<const uint4*>(src + 2 * C);
+        }
+        *reinterpret_cast<uint4*>(Ks + n * 64 + kchunk_swz(n, ch) * 16) = kval;
+        *reinterpret_cast<uint4*>(Vs + n * 64 + ch * 16) = vval;
+    }
+    if (masked) {
+        for (int w8 = tid; w8 < NP / 8; w8 += 256) {
+            unsigned v = 0;
+            for (int e = 0; e < 8; ++e) {
+                int lb = 15;
+                if (w8 * 8 + e < vol) token_row(w8 * 8 + e, &lb);
+                v |= (unsigned)lb << (4 * e);
+            }
+            lab4[w8] = v;
+        }
+    }
+    __syncthreads();
+
+    const int rr = lane & 31, h = lane >> 5;
+    // per-lane LDS offsets: K fragment (key rr of a 32-key block, 16-B chunk 2kk+h)
+    int koff[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) koff[kk] = rr * 64 + kchunk_swz(rr, 2 * kk + h) * 16;
+    // V^T transpose read: rows 4h + tq (+8), columns gcol..gcol+3
+    const int gi = lane & 15;
+    const int tq = gi >> 2, tp = gi & 3;
+    const int gcol = ((lane >> 4) & 1) * 16 + tp * 4;
+    const int voff = (4 * h + tq) * 64 + gcol * 2;
+    const float* bh = biasT + (int64_t)head * NP * NP;
+    const int nqb = (vol + 31) / 32;
+    const int ntile = NP / 64;
+
+    for (int qb = wave; qb < nqb; qb += 4) {
+        const int qn = qb * 32 + rr;  // this lane's query (window-local)
+        const int qc = qn < vol ? qn : vol - 1;
+        int qlab = 0;
+        const int64_t qrow = token_row(qc, masked ? &qlab : nullptr);
+        v8bf qf[2];
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+            qf[kk] = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(qkv + qrow * ld + head * 32 + 16 * kk + 8 * h));
+        v16f o = {};
+        float m_run = -1e30f, l_run = 0.f;
+        for (int t = 0; t < ntile; ++t) {
+            v16f sc[2];
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+                // C = bias tile biasT[k][q]: reg e <-> key row (e&3) + 8(e>>2) + 4h, query qn
+                const float* bp = bh + (int64_t)(t * 64 + kb * 32 + 4 * h) * NP + qb * 32 + rr;
+#pragma unroll
+                for (int e = 0; e < 16; ++e) sc[kb][e] = bp[(int64_t)((e & 3) + 8 * (e >> 2)) * NP];
+            }
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb) {
+                    const v8bf kf = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(Ks + (t * 64 + kb * 32) * 64 + koff[kk]));
+                    sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kk], sc[kb], 0, 0, 0);
+                }
+            }
+            if (masked) {
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+                    for (int g4 = 0; g4 < 4; ++g4) {
+                        // keys t*64 + kb*32 + 8*g4 + 4h + 0..3: one 16-bit run of the nibble table
+                        const int k0 = t * 64 + kb * 32 + 8 * g4 + 4 * h;
+                        const unsigned wv = lab4[k0 >> 3] >> (4 * (k0 & 7));
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if ((int)((wv >> (4 * e)) & 15) != qlab) sc[kb][4 * g4 + e] = -INFINITY;
+                    }
+                }
+            }
+            float mx = m_run;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) mx = fmaxf(mx, sc[kb][e]);
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            const float alpha = __builtin_amdgcn_exp2f(m_run - mx);
+            m_run = mx;
+            float ls = 0.f;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    sc[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e] - mx);
+                    ls += sc[kb][e];
+                }
+            l_run = l_run * alpha + ls;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) o[e] *= alpha;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    v8bf pf;
+#pragma unroll
+                    for (int jj = 0; jj < 8; ++jj) pf[jj] = (__bf16)sc[kb][8 * s2 + jj];
+                    const char* pa = Vs + (t * 64 + kb * 32 + 16 * s2) * 64 + voff;
+                    const v4s va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)pa);
+                    const v4s vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(pa + 8 * 64));
+                    v8s vv;
+                    vv[0] = va[0]; vv[1] = va[1]; vv[2] = va[2]; vv[3] = va[3];
+                    vv[4] = vb[0]; vv[5] = vb[1]; vv[6] = vb[2]; vv[7] = vb[3];
+                    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf, vv), pf, o, 0, 0, 0);
+                }
+        }
+        // ---- O^T[d][q]: reg 4g+e -> d = 8g + 4h + e; lane pairs swap halves -> 16-B stores
+        const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+        const float inv = 1.0f / l_tot;
+        unsigned pk[4][2];
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            pk[g4][0] = pack2bf(o[4 * g4 + 0] * inv, o[4 * g4 + 1] * inv);
+            pk[g4][1] = pack2bf(o[4 * g4 + 2] * inv, o[4 * g4 + 3] * inv);
+        }
+        uint16_t* orow = out + qrow * ldo + head * 32;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; g4 += 2) {
+            auto x0 = __builtin_amdgcn_permlane32_swap(pk[g4][0], pk[g4 + 1][0], false, false);
+            auto x1 = __builtin_amdgcn_permlane32_swap(pk[g4][1], pk[g4 + 1][1], false, false);
+            uint4 v;
+            v.x = x0[0]; v.y = x1[0]; v.z = x0[1]; v.w = x1[1];
+            if (qn < vol) *reinterpret_cast<uint4*>(orow + g4 * 8 + h * 8) = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// PatchMerging gather + LayerNorm(4C): out[(b,t,i,j)] = LN(cat(x[2i,2j], x[2i+1,2j],
+// x[2i,2j+1], x[2i+1,2j+1])) (zero rows past an odd H/W edge, torchvision _patch_merging_pad).
+// One wave per output token, 4C <= 4096.
+// ---------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) patch_merge_ln_kernel(const float* __restrict__ x, int64_t ldx, int64_t B,
+                                                             int T, int H, int W, int C,
+                                                             const float* __restrict__ g,
+                                                             const float* __restrict__ be, float eps,
+                                                             uint16_t* __restrict__ y, int64_t ldy) {
+    const int lane = threadIdx.x & 63;
+    const int H2 = (H + 1) / 2, W2 = (W + 1) / 2;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= B * T * H2 * W2) return;
+    const int j = (int)(row % W2);
+    const int i = (int)((row / W2) % H2);
+    const int64_t bt = row / ((int64_t)W2 * H2);
+    const int C4 = 4 * C;
+    float s = 0.f;
+    // pass 1: sum (values re-read from L1/L2 in passes 2-3)
+    auto val = [&](int n) -> float {
+        const int q = n / C, c = n - q * C;  // q: 0 (2i,2j) 1 (2i+1,2j) 2 (2i,2j+1) 3 (2i+1,2j+1)
+        const int hh = 2 * i + (q & 1), ww = 2 * j + (q >> 1);
+        if (hh >= H || ww >= W) return 0.f;
+        return x[((bt * H + hh) * W + ww) * ldx + c];
+    };
+    for (int n = lane; n < C4; n += 64) s += val(n);
+    const float mean = wave_sum(s) / (float)C4;
+    float q = 0.f;
+    for (int n = lane; n < C4; n += 64) {
+        const float d = val(n) - mean;
+        q += d * d;
+    }
+    const float rstd = rsqrtf(wave_sum(q) / (float)C4 + eps);
+    for (int n = lane; n < C4; n += 64) y[row * ldy + n] = f2bf((val(n) - mean) * rstd * g[n] + be[n]);
+}
+
+// ---------------------------------------------------------------------------------
+// Final LayerNorm over every token, mean over the clip's tokens, classifier GEMV (fp32):
+// logits[b] = W . mean_n LN(x[b, n]) + bias  (torchvision SwinTransformer3d.forward:
+// norm -> avgpool -> flatten -> head).  One workgroup per clip; D <= 4096.
+// ---------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) pool_head_kernel(const float* __restrict__ x, int64_t ldx, int64_t ntok, int D,
+                                                        const float* __restrict__ g, const float* __restrict__ be,
+                                                        float eps, const float* __restrict__ Wc,
+                                                        const float* __restrict__ bc, int nl,
+                                                        float* __restrict__ logits) {
+    __shared__ float acc[4][4096];
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int n = lane; n < D; n += 64) acc[w][n] = 0.f;
+    for (int64_t tk = w; tk < ntok; tk += 4) {
+        const float* xr = x + ((int64_t)b * ntok + tk) * ldx;
+        float s = 0.f;
+        for (int n = lane; n < D; n += 64) s += xr[n];
+        const float mean = wave_sum(s) / (float)D;
+        float q = 0.f;
+        for (int n = lane; n < D; n += 64) {
+            const float d = xr[n] - mean;
+            q += d * d;
+        }
+        const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
+        for (int n = lane; n < D; n += 64) acc[w][n] += (xr[n] - mean) * rstd * g[n] + be[n];
+    }
+    __syncthreads();
+    for (int n = threadIdx.x; n < D; n += 256) acc[0][n] = (acc[0][n] + acc[1][n] + acc[2][n] + acc[3][n]) / (float)ntok;
+    __syncthreads();
+    for (int c = w; c < nl; c += 4) {
+        float a = 0.f;
+        for (int n = lane; n < D; n += 64) a += acc[0][n] * Wc[(int64_t)c * D + n];
+        a = wave_sum(a);
+        if (lane == 0) logits[(int64_t)b * nl + c] = a + bc[c];
+    }
+}
+
+}  // namespace vc
+
+using namespace vc;
+
+extern "C" {
+
+int vc_window_attention3d(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T, int64_t H, int64_t W, int64_t heads,
+                          int64_t head_dim, int wt, int wh, int ww, int st, int sh, int sw, const float* biasT,
+                          int64_t np, uint16_t* out, int64_t ldo, hipStream_t stream) {
+    if (!qkv || !biasT || !out) return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d: null pointer");
+    if (head_dim != 32) return fail(VC_ERR_UNSUPPORTED, "vc_window_attention3d: head_dim must be 32");
+    if (wt <= 0 || wh <= 0 || ww <= 0 || T % wt || H % wh || W % ww)
+        return fail(VC_ERR_UNSUPPORTED, "vc_window_attention3d: the token grid must be whole windows (no padding)");
+    if (st < 0 || sh < 0 || sw < 0 || st >= wt || sh >= wh || sw >= ww)
+        return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d: shift must be in [0, window)");
+    const int vol = wt * wh * ww;
+    if (np != (vol + 63) / 64 * 64 || np > WNP_MAX)
+        return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d: np must be roundup(window volume, 64) <= 448");
+    if (ld < 3 * heads * 32 || ldo < heads * 32 || ld % 8 || ldo % 8 || ((uintptr_t)qkv | (uintptr_t)out) & 15)
+        return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d: bad leading dimension / alignment");
+    WinGeom g{(int)T, (int)H, (int)W, wt, wh, ww, st, sh, sw, (int)(T / wt), (int)(H / wh), (int)(W / ww)};
+    const int64_t nwin = B * g.nwt * g.nwh * g.nww;
+    if (nwin > 0x7fffffff || heads > 65535) return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d: grid too large");
+    dim3 grid((unsigned)nwin, (unsigned)heads);
+    window_attn_d32_kernel<<<grid, 256, 0, stream>>>(qkv, ld, g, (int)heads, vol, (int)np, biasT,
+                                                     (st | sh | sw) ? 1 : 0, out, ldo);
+    return check_launch("vc_window_attention3d");
+}
+
+int vc_patch_merge_layernorm(const float* x, int64_t ldx, int64_t B, int64_t T, int64_t H, int64_t W, int64_t C,
+                             const float* gamma, const float* beta, float eps, uint16_t* y, int64_t ldy,
+                             hipStream_t stream) {
+    if (!x || !gamma || !beta || !y) return fail(VC_ERR_INVALID_ARG, "vc_patch_merge_layernorm: null pointer");
+    if (C <= 0 || 4 * C > 4096 || ldx < C || ldy < 4 * C)
+        return fail(VC_ERR_INVALID_ARG, "vc_patch_merge_layernorm: bad C / leading dimension");
+    const int64_t rows = B * T * ((H + 1) / 2) * ((W + 1) / 2);
+    patch_merge_ln_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, stream>>>(x, ldx, B, (int)T, (int)H, (int)W, (int)C,
+                                                                        gamma, beta, eps, y, ldy);
+    return check_launch("vc_patch_merge_layernorm");
+}
+
+int vc_pool_head(const float* x, int64_t ldx, int64_t B, int64_t ntok, int64_t D, const float* gamma,
+                 const float* beta, float eps, const float* Wc, const float* bc, int64_t num_labels, float* logits,
+                 hipStream_t stream) {
+    if (!x || !gamma || !beta || !Wc || !bc || !logits) return fail(VC_ERR_INVALID_ARG, "vc_pool_head: null pointer");
+    if (D <= 0 || D > 4096 || ntok <= 0) return fail(VC_ERR_UNSUPPORTED, "vc_pool_head: D in (0, 4096], ntok > 0");
+    pool_head_kernel<<<(unsigned)B, 256, 0, stream>>>(x, ldx, ntok, (int)D, gamma, beta, eps, Wc, bc, (int)num_labels,
+                                                      logits);
+    return check_launch("vc_pool_head");
+}
+
+}  // extern "C"

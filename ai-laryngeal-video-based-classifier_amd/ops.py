@@ -11,7 +11,7 @@ import torch
 
 from . import _lib
 
-EPI = {"bias": 0, "bias_gelu_tanh": 1, "bias_gelu_erf": 2, "bias_resid_f32": 3, "embed_f32": 4}
+EPI = {"bias": 0, "bias_gelu_tanh": 1, "bias_gelu_erf": 2, "bias_resid_f32": 3, "embed_f32": 4, "bias_f32": 5}
 GATHER_KIND = {"u8": 0, "f32": 1, "bf16": 2}
 
 
@@ -56,21 +56,27 @@ def frame_gather(frames: torch.Tensor, idx: torch.Tensor, kind: str = "f32", sca
 
 
 TOKEN_ORDER = {"time_major": 0, "patch_major": 1}
+VIDEO_LAYOUT = {"btchw": 0, "bcthw": 1}
 
 
-def tubelet_im2col(pix: torch.Tensor, tubelet, out: torch.Tensor, order: str = "time_major") -> torch.Tensor:
-    """pix f32 [B,T,C,H,W] -> out bf16 [>= B*nt*nh*nw, C*kt*kh*kw] (rows beyond are untouched).
-    order "time_major": token (t', hp, wp) (ViViT); "patch_major": token (hp, wp, t') (TimeSformer)."""
+def tubelet_im2col(pix: torch.Tensor, tubelet, out: torch.Tensor, order: str = "time_major",
+                   layout: str = "btchw") -> torch.Tensor:
+    """pix f32 [B,T,C,H,W] (layout "btchw") or [B,C,T,H,W] ("bcthw") -> out bf16
+    [>= B*nt*nh*nw, >= C*kt*kh*kw] (rows / columns beyond are untouched).
+    order "time_major": token (t', hp, wp) (ViViT, Swin); "patch_major": token (hp, wp, t') (TimeSformer)."""
     _dev(pix, out)
-    _need(pix.dtype == torch.float32 and pix.dim() == 5 and pix.is_contiguous(), "pixel_values: f32 [B,T,C,H,W]")
-    B, T, C, H, W = pix.shape
+    _need(pix.dtype == torch.float32 and pix.dim() == 5 and pix.is_contiguous(), "pixel_values: f32 5-D contiguous")
+    if layout == "btchw":
+        B, T, C, H, W = pix.shape
+    else:
+        B, C, T, H, W = pix.shape
     kt, kh, kw = tubelet
     ntok = B * (T // kt) * (H // kh) * (W // kw)
-    _need(out.dtype == torch.bfloat16 and out.dim() == 2 and out.shape[0] >= ntok and out.shape[1] == C * kt * kh * kw
-          and out.is_contiguous(), "im2col out: bf16 [rows, C*kt*kh*kw]")
-    _need(H % kh == 0 and W % kw == 0 and T % kt == 0 and kw % 8 == 0, "im2col: shape not divisible by the patch")
-    _lib.call("vc_patch_im2col", _p(pix), B, T, C, H, W, kt, kh, kw, TOKEN_ORDER[order], _p(out), out.stride(0),
-              _stream(pix))
+    _need(out.dtype == torch.bfloat16 and out.dim() == 2 and out.shape[0] >= ntok and out.shape[1] >= C * kt * kh * kw
+          and out.stride(1) == 1, "im2col out: bf16 [rows, >= C*kt*kh*kw]")
+    _need(H % kh == 0 and W % kw == 0 and T % kt == 0 and kw % 4 == 0, "im2col: shape not divisible by the patch")
+    _lib.call("vc_patch_im2col", _p(pix), B, T, C, H, W, kt, kh, kw, TOKEN_ORDER[order], VIDEO_LAYOUT[layout], _p(out),
+              out.stride(0), _stream(pix))
     return out
 
 
@@ -105,14 +111,30 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: str, ou
 
 def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, out: torch.Tensor,
               m: int | None = None) -> torch.Tensor:
+    """LayerNorm of the first gamma.numel() columns of each row (x f32 -> out bf16)."""
     _dev(x, gamma, beta, out)
     M = x.shape[0] if m is None else m
-    D = x.shape[1]
+    D = gamma.numel()
     _need(x.dtype == torch.float32 and out.dtype == torch.bfloat16 and x.stride(1) == 1 and out.stride(1) == 1,
           "layernorm: x f32, out bf16, unit column stride")
-    _need(gamma.numel() == D and beta.numel() == D and out.shape[1] >= D and out.shape[0] >= M, "layernorm shapes")
+    _need(beta.numel() == D and x.shape[1] >= D and out.shape[1] >= D and out.shape[0] >= M and x.shape[0] >= M,
+          "layernorm shapes")
     _lib.call("vc_layernorm_f32_bf16", _p(x), x.stride(0), M, D, _p(gamma), _p(beta), eps, _p(out), out.stride(0),
               _stream(x))
+    return out
+
+
+def layernorm_f32(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, out: torch.Tensor,
+                  m: int | None = None) -> torch.Tensor:
+    """f32 -> f32 LayerNorm over the first gamma.numel() columns of each row."""
+    _dev(x, gamma, beta, out)
+    M = x.shape[0] if m is None else m
+    D = gamma.numel()
+    _need(x.dtype == torch.float32 and out.dtype == torch.float32 and x.stride(1) == 1 and out.stride(1) == 1,
+          "layernorm_f32 dtypes")
+    _need(beta.numel() == D and x.shape[1] >= D and out.shape[1] >= D and x.shape[0] >= M and out.shape[0] >= M,
+          "layernorm_f32 shapes")
+    _lib.call("vc_layernorm_f32", _p(x), x.stride(0), M, D, _p(gamma), _p(beta), eps, _p(out), out.stride(0), _stream(x))
     return out
 
 
@@ -190,3 +212,54 @@ def divided_add_layernorm(x: torch.Tensor, y: torch.Tensor, B: int, P: int, T: i
     _lib.call("vc_divided_add_layernorm", _p(x), x.stride(0), _p(y), y.stride(0), B, P, T, D, _p(gamma), _p(beta), eps,
               DIVIDED_MODE[mode], _p(h), h.stride(0), _stream(x))
     return h
+
+
+def window_attention3d(qkv: torch.Tensor, B: int, grid, heads: int, window, shift, biasT: torch.Tensor,
+                       out: torch.Tensor) -> torch.Tensor:
+    """Swin 3D shifted-window attention (head_dim 32) on the token layout [B][T][H][W]:
+    qkv bf16 [>= B*T*H*W, >= 3*heads*32] (q pre-scaled by d^-1/2 * log2 e), biasT f32
+    [heads, np, np] (see include/vclip.h) -> out bf16 [rows, >= heads*32]."""
+    _dev(qkv, biasT, out)
+    T, H, W = grid
+    wt, wh, ww = window
+    st, sh, sw = shift
+    vol = wt * wh * ww
+    np_ = (vol + 63) // 64 * 64
+    _need(qkv.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and qkv.stride(1) == 1 and out.stride(1) == 1,
+          "window_attention3d dtypes")
+    _need(biasT.dtype == torch.float32 and biasT.is_contiguous() and tuple(biasT.shape) == (heads, np_, np_),
+          "window_attention3d biasT [heads, np, np] f32")
+    _need(qkv.shape[0] >= B * T * H * W and out.shape[0] >= B * T * H * W, "window_attention3d rows")
+    _need(qkv.shape[1] >= 3 * heads * 32 and out.shape[1] >= heads * 32, "window_attention3d columns")
+    _need(T % wt == 0 and H % wh == 0 and W % ww == 0, "window_attention3d: grid must be whole windows")
+    _lib.call("vc_window_attention3d", _p(qkv), qkv.stride(0), B, T, H, W, heads, 32, wt, wh, ww, st, sh, sw, _p(biasT),
+              np_, _p(out), out.stride(0), _stream(qkv))
+    return out
+
+
+def patch_merge_layernorm(x: torch.Tensor, B: int, grid, C: int, gamma, beta, eps: float,
+                          out: torch.Tensor) -> torch.Tensor:
+    """x f32 [>= B*T*H*W, >= C] -> out bf16 [>= B*T*ceil(H/2)*ceil(W/2), >= 4C]."""
+    _dev(x, gamma, beta, out)
+    T, H, W = grid
+    _need(x.dtype == torch.float32 and out.dtype == torch.bfloat16 and x.stride(1) == 1 and out.stride(1) == 1,
+          "patch_merge dtypes")
+    _need(gamma.numel() == 4 * C and out.shape[1] >= 4 * C and x.shape[1] >= C, "patch_merge columns")
+    _need(x.shape[0] >= B * T * H * W and out.shape[0] >= B * T * ((H + 1) // 2) * ((W + 1) // 2), "patch_merge rows")
+    _lib.call("vc_patch_merge_layernorm", _p(x), x.stride(0), B, T, H, W, C, _p(gamma), _p(beta), eps, _p(out),
+              out.stride(0), _stream(x))
+    return out
+
+
+def pool_head(x: torch.Tensor, B: int, ntok: int, gamma, beta, eps: float, wc: torch.Tensor, bc: torch.Tensor,
+              out: torch.Tensor | None = None) -> torch.Tensor:
+    _dev(x, gamma, beta, wc, bc)
+    D = gamma.numel()
+    nl = wc.shape[0]
+    _need(wc.dtype == torch.float32 and wc.is_contiguous() and wc.shape[1] == D and x.shape[0] >= B * ntok,
+          "pool_head shapes")
+    if out is None:
+        out = torch.empty((B, nl), dtype=torch.float32, device=x.device)
+    _lib.call("vc_pool_head", _p(x), x.stride(0), B, ntok, D, _p(gamma), _p(beta), eps, _p(wc), _p(bc), nl, _p(out),
+              _stream(x))
+    return out

@@ -1,0 +1,300 @@
+"""Video Swin Transformer (torchvision `swin3d_t/s/b` as the reference builds it) on the
+libvclip.so kernels — drop-in for `create_model(logger, model_size, pretrained, num_classes)`
+of videoswintransformer/swin_video_classifier/models/swin3d.py:7-53, which returns the
+torchvision model with `head` replaced by `Linear(768, num_classes)` and is called as
+`model(f32[B, 3, T, H, W])` -> `f32[B, num_classes]` (trainer.py:116, inference.py).
+
+Device data layout per stage s (C_s = 96 * 2^s channels, heads_s = C_s / 32):
+  tokens in torchvision's channels-last order rows ((b*T + t)*H + h)*W + w, padded to a
+  multiple of 256 rows; feature columns padded to a multiple of 128 (Cp) with zero weights,
+  so padded columns stay exactly 0 through every GEMM (the GEMM tiles need N % 128, K % 64);
+  residual X f32 [M, Cp]; LN output / attention output bf16 [M, Cp]; fused q|k|v bf16;
+  MLP hidden bf16 [M, roundup(4C, 128)].
+Per block: LN1 -> qkv GEMM (q pre-scaled by d^-1/2 * log2 e) -> shifted-window attention
+(gather/scatter by index: no roll / partition copies; bias + shift mask inside) -> proj
+GEMM + residual -> LN2 -> fc1 + exact GELU -> fc2 + residual.  Between stages: fused
+PatchMerging gather + LN(4C), then the reduction GEMM into the next stage's residual.
+Relative-position bias tables are expanded once per (block, window) into
+biasT[h][k][q] (f32, log2 e scaled, -inf on padded keys).
+
+Parity unpinned against torchvision itself (not installed here): checked against
+oracle/swin3d_ref.py, the restatement of torchvision's algorithm.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import ops
+from .weights import swin3d_param_shapes
+
+LOG2E = ops.LOG2E
+
+SWIN3D_CONFIGS = {
+    "tiny": dict(patch_size=(2, 4, 4), embed_dim=96, depths=(2, 2, 6, 2), num_heads=(3, 6, 12, 24),
+                 window_size=(8, 7, 7), mlp_ratio=4.0, layer_norm_eps=1e-5),
+    "small": dict(patch_size=(2, 4, 4), embed_dim=96, depths=(2, 2, 18, 2), num_heads=(3, 6, 12, 24),
+                  window_size=(8, 7, 7), mlp_ratio=4.0, layer_norm_eps=1e-5),
+    "base": dict(patch_size=(2, 4, 4), embed_dim=128, depths=(2, 2, 18, 2), num_heads=(4, 8, 16, 32),
+                 window_size=(8, 7, 7), mlp_ratio=4.0, layer_norm_eps=1e-5),
+}
+SWIN3D_CONFIGS["base_in22k"] = SWIN3D_CONFIGS["base"]
+
+
+def _ru(x, m):
+    return (x + m - 1) // m * m
+
+
+def relative_position_index(window_size):
+    """torchvision ShiftedWindowAttention3d.define_relative_position_index."""
+    wt, wh, ww = window_size
+    coords = torch.stack(torch.meshgrid(torch.arange(wt), torch.arange(wh), torch.arange(ww), indexing="ij"))
+    cf = torch.flatten(coords, 1)
+    rel = (cf[:, :, None] - cf[:, None, :]).permute(1, 2, 0).contiguous()
+    rel[:, :, 0] += wt - 1
+    rel[:, :, 1] += wh - 1
+    rel[:, :, 2] += ww - 1
+    rel[:, :, 0] *= (2 * wh - 1) * (2 * ww - 1)
+    rel[:, :, 1] *= 2 * ww - 1
+    return rel.sum(-1)
+
+
+def window_and_shift(size_thw, window_size, shift_size):
+    """torchvision _get_window_and_shift_size: clamp the window to the feature size (shift 0 there)."""
+    w, s = list(window_size), list(shift_size)
+    for i in range(3):
+        if size_thw[i] <= w[i]:
+            w[i] = size_thw[i]
+            s[i] = 0
+    return w, s
+
+
+def expand_bias(table, full_window, window, device):
+    """biasT[h][k][q] = log2e * table[index_full[:vol,:vol]][q][k][h] (torchvision
+    _get_relative_position_bias, sliced index of the FULL window when it shrinks);
+    -inf for padded keys k >= vol, 0 for padded queries."""
+    vol = window[0] * window[1] * window[2]
+    npad = _ru(vol, 64)
+    idx = relative_position_index(full_window)[:vol, :vol].reshape(-1).to(device)
+    bias = table.to(device=device, dtype=torch.float32)[idx].view(vol, vol, -1).permute(2, 0, 1)  # [h, q, k]
+    bt = torch.full((bias.shape[0], npad, npad), float("-inf"), dtype=torch.float32, device=device)
+    bt[:, :, vol:] = 0.0
+    bt[:, :vol, :vol] = bias.transpose(1, 2) * LOG2E
+    return bt.contiguous()
+
+
+class Swin3d(torch.nn.Module):
+    """fp32 master parameters in torchvision naming; bf16 / fp32 packed device copies."""
+
+    def __init__(self, cfg: dict, num_classes: int = 2):
+        super().__init__()
+        self.cfg = dict(cfg, num_classes=num_classes)
+        self.num_classes = num_classes
+        for h, C in zip(cfg["num_heads"], (cfg["embed_dim"] * 2 ** s for s in range(len(cfg["depths"])))):
+            if C // h != 32:
+                raise ValueError("libvclip window attention supports head_dim 32 only")
+        shapes = swin3d_param_shapes(self.cfg)
+        self._names = list(shapes.keys())
+        self.params = torch.nn.ParameterDict()
+        for n, s in shapes.items():
+            self.params[n.replace(".", "__")] = torch.nn.Parameter(torch.zeros(s), requires_grad=False)
+        self._packed = None
+        self._bias_cache = {}
+        self._ws = {}
+
+    def state_dict(self, *a, **k):
+        return OrderedDict((n, self.params[n.replace(".", "__")].detach()) for n in self._names)
+
+    def load_state_dict(self, sd, strict: bool = True):
+        sd = {k[len("module."):] if k.startswith("module.") else k: v for k, v in sd.items()}
+        sd = {k: v for k, v in sd.items() if not k.endswith("relative_position_index")}  # buffers, rebuilt
+        missing = [n for n in self._names if n not in sd]
+        unexpected = [k for k in sd if k not in self._names]
+        if strict and (missing or unexpected):
+            raise KeyError(f"load_state_dict: missing={missing[:5]} unexpected={unexpected[:5]}")
+        with torch.no_grad():
+            for n in self._names:
+                if n in sd:
+                    v = sd[n]
+                    v = torch.as_tensor(np.asarray(v)) if not isinstance(v, torch.Tensor) else v
+                    dst = self.params[n.replace(".", "__")]
+                    dst.copy_(v.reshape(dst.shape))
+        self._packed = None
+        self._bias_cache = {}
+        return missing, unexpected
+
+    # ---- packing -------------------------------------------------------------------
+    def _pack(self, device):
+        if self._packed is not None and self._packed["device"] == device:
+            return self._packed
+        c = self.cfg
+        bf, f32 = torch.bfloat16, torch.float32
+        P = lambda n: self.params[n.replace(".", "__")].detach().to(device=device, dtype=f32)  # noqa: E731
+
+        def padw(w, n_p, k_p, dt=bf):
+            out = torch.zeros((n_p, k_p), dtype=f32, device=device)
+            out[:w.shape[0], :w.shape[1]] = w
+            return out.to(dt).contiguous()
+
+        def padb(b, n_p):
+            out = torch.zeros(n_p, dtype=f32, device=device)
+            if b is not None:
+                out[:b.numel()] = b
+            return out
+
+        pk = {"device": device}
+        C0 = c["embed_dim"]
+        pt, ph, pw = c["patch_size"]
+        K0 = 3 * pt * ph * pw
+        pk["K0p"] = _ru(K0, 64)
+        pk["w_emb"] = padw(P("patch_embed.proj.weight").reshape(C0, K0), _ru(C0, 128), pk["K0p"])
+        pk["b_emb"] = padb(P("patch_embed.proj.bias"), _ru(C0, 128))
+        pk["ln_emb"] = (P("patch_embed.norm.weight").contiguous(), P("patch_embed.norm.bias").contiguous())
+        stages = []
+        for s, depth in enumerate(c["depths"]):
+            C = C0 * 2 ** s
+            Cp, hid = _ru(C, 128), int(C * c["mlp_ratio"])
+            hp = _ru(hid, 128)
+            qs = 32 ** -0.5 * LOG2E
+            blocks = []
+            for i in range(depth):
+                p = f"features.{2 * s}.{i}."
+                wq = P(p + "attn.qkv.weight").clone()
+                bq = P(p + "attn.qkv.bias").clone()
+                wq[:C] *= qs
+                bq[:C] *= qs
+                blocks.append(dict(
+                    ln1=(P(p + "norm1.weight").contiguous(), P(p + "norm1.bias").contiguous()),
+                    ln2=(P(p + "norm2.weight").contiguous(), P(p + "norm2.bias").contiguous()),
+                    w_qkv=padw(wq, _ru(3 * C, 128), Cp), b_qkv=padb(bq, _ru(3 * C, 128)),
+                    w_proj=padw(P(p + "attn.proj.weight"), Cp, Cp), b_proj=padb(P(p + "attn.proj.bias"), Cp),
+                    w_1=padw(P(p + "mlp.0.weight"), hp, Cp), b_1=padb(P(p + "mlp.0.bias"), hp),
+                    w_2=padw(P(p + "mlp.3.weight"), Cp, hp), b_2=padb(P(p + "mlp.3.bias"), Cp),
+                    table=P(p + "attn.relative_position_bias_table").contiguous()))
+            st = dict(C=C, Cp=Cp, hid=hid, hp=hp, heads=c["num_heads"][s], blocks=blocks)
+            if s < len(c["depths"]) - 1:
+                p = f"features.{2 * s + 1}."
+                st["merge_ln"] = (P(p + "norm.weight").contiguous(), P(p + "norm.bias").contiguous())
+                st["w_red"] = padw(P(p + "reduction.weight"), _ru(2 * C, 128), 4 * C)
+                st["b_red"] = padb(None, _ru(2 * C, 128))
+            stages.append(st)
+        pk["stages"] = stages
+        pk["norm"] = (P("norm.weight").contiguous(), P("norm.bias").contiguous())
+        pk["w_head"] = P("head.weight").contiguous()
+        pk["b_head"] = P("head.bias").contiguous()
+        self._packed = pk
+        return pk
+
+    def _biasT(self, s, i, window, device):
+        key = (s, i, tuple(window), str(device))
+        if key not in self._bias_cache:
+            tab = self._packed["stages"][s]["blocks"][i]["table"]
+            self._bias_cache[key] = expand_bias(tab, self.cfg["window_size"], window, device)
+        return self._bias_cache[key]
+
+    def geometry(self, B, T, H, W):
+        c = self.cfg
+        pt, ph, pw = c["patch_size"]
+        if T % pt or H % ph or W % pw:
+            raise ValueError("input T/H/W must be multiples of the patch size (2, 4, 4)")
+        g = [(T // pt, H // ph, W // pw)]
+        for _ in range(len(c["depths"]) - 1):
+            t, h, w = g[-1]
+            g.append((t, (h + 1) // 2, (w + 1) // 2))
+        return g
+
+    def _workspace(self, B, grids, device):
+        key = (B, tuple(grids), str(device))
+        if key in self._ws:
+            return self._ws[key]
+        c = self.cfg
+        bf, f32 = torch.bfloat16, torch.float32
+        z = lambda r, cols, dt=bf: torch.zeros((r, cols), dtype=dt, device=device)  # noqa: E731
+        ws = {"stages": []}
+        t0, h0, w0 = grids[0]
+        M0 = _ru(B * t0 * h0 * w0, 256)
+        ws["A_emb"] = z(M0, _ru(3 * 2 * 4 * 4, 64))
+        ws["E"] = z(M0, _ru(c["embed_dim"], 128), f32)
+        for s, (t, h, w) in enumerate(grids):
+            C = c["embed_dim"] * 2 ** s
+            Cp, hp = _ru(C, 128), _ru(int(C * c["mlp_ratio"]), 128)
+            M = _ru(B * t * h * w, 256)
+            st = dict(M=M, X=z(M, Cp, f32), Y=z(M, Cp), QKV=z(M, _ru(3 * C, 128)), O=z(M, Cp), Hd=z(M, hp))
+            if s < len(grids) - 1:
+                t2, h2, w2 = grids[s + 1]
+                st["Mg"] = z(_ru(B * t2 * h2 * w2, 256), 4 * C)
+            ws["stages"].append(st)
+        ws["logits"] = torch.zeros((B, self.num_classes), dtype=f32, device=device)
+        self._ws = {key: ws}
+        return ws
+
+    # ---- forward -------------------------------------------------------------------
+    @torch.no_grad()
+    def forward(self, video: torch.Tensor) -> torch.Tensor:
+        if video.device.type != "cuda":
+            raise RuntimeError("Swin3d (vclip_amd) runs on the GPU only: move the clip batch to cuda")
+        x = video.contiguous().float() if video.dtype != torch.float32 else video.contiguous()
+        return self.forward_logits(x)
+
+    def forward_logits(self, video: torch.Tensor) -> torch.Tensor:
+        c = self.cfg
+        B, Cin, T, H, W = video.shape
+        if Cin != 3:
+            raise ValueError("video must be [B, 3, T, H, W]")
+        pk = self._pack(video.device)
+        grids = self.geometry(B, T, H, W)
+        ws = self._workspace(B, grids, video.device)
+        eps = c["layer_norm_eps"]
+        pt, ph, pw = c["patch_size"]
+        t0, h0, w0 = grids[0]
+        M0 = ws["stages"][0]["M"]
+        ops.tubelet_im2col(video, (pt, ph, pw), ws["A_emb"], layout="bcthw")
+        ops.gemm(ws["A_emb"], pk["w_emb"], pk["b_emb"], "bias_f32", ws["E"], m=M0)
+        X = ws["stages"][0]["X"]
+        ops.layernorm_f32(ws["E"], pk["ln_emb"][0], pk["ln_emb"][1], eps, X, m=B * t0 * h0 * w0)
+        for s, (st, sw) in enumerate(zip(pk["stages"], ws["stages"])):
+            t, h, w = grids[s]
+            ntok = B * t * h * w
+            X, Y, QKV, O, Hd = sw["X"], sw["Y"], sw["QKV"], sw["O"], sw["Hd"]
+            for i, blk in enumerate(st["blocks"]):
+                shift_full = [0 if i % 2 == 0 else k // 2 for k in c["window_size"]]
+                window, shift = window_and_shift((t, h, w), c["window_size"], shift_full)
+                biasT = self._biasT(s, i, window, video.device)
+                ops.layernorm(X, blk["ln1"][0], blk["ln1"][1], eps, Y, m=ntok)
+                ops.gemm(Y, blk["w_qkv"], blk["b_qkv"], "bias", QKV)
+                ops.window_attention3d(QKV, B, (t, h, w), st["heads"], window, shift, biasT, O)
+                ops.gemm(O, blk["w_proj"], blk["b_proj"], "bias_resid_f32", X)
+                ops.layernorm(X, blk["ln2"][0], blk["ln2"][1], eps, Y, m=ntok)
+                ops.gemm(Y, blk["w_1"], blk["b_1"], "bias_gelu_erf", Hd)
+                ops.gemm(Hd, blk["w_2"], blk["b_2"], "bias_resid_f32", X)
+            if s < len(grids) - 1:
+                ops.patch_merge_layernorm(X, B, (t, h, w), st["C"], st["merge_ln"][0], st["merge_ln"][1], eps, sw["Mg"])
+                nxt = ws["stages"][s + 1]
+                ops.gemm(sw["Mg"], st["w_red"], st["b_red"], "bias_f32", nxt["X"], m=nxt["M"])
+        t, h, w = grids[-1]
+        return ops.pool_head(ws["stages"][-1]["X"], B, t * h * w, pk["norm"][0], pk["norm"][1], eps, pk["w_head"],
+                             pk["b_head"], out=ws["logits"])
+
+
+def create_model(logger=None, model_size="tiny", pretrained=True, num_classes=2, device="cuda", weights_seed: int = 0):
+    """Drop-in for videoswintransformer/swin_video_classifier/models/swin3d.py:7-53.
+
+    The reference loads torchvision's Kinetics-400 weights (`Swin3D_*_Weights.DEFAULT`) and
+    replaces the head; this image has no network, so the architecture of `model_size` is
+    built with seeded synthetic weights (vclip_amd.weights) unless a checkpoint is loaded
+    afterwards with `load_state_dict` (torchvision key names, `module.` prefixes stripped).
+    """
+    if model_size not in SWIN3D_CONFIGS:
+        raise ValueError(f"Unknown model size: {model_size}")
+    if logger:
+        logger.info(f"Creating Video Swin Transformer ({model_size}) model...")
+    cfg = SWIN3D_CONFIGS[model_size]
+    model = Swin3d(cfg, num_classes=num_classes)
+    from .weights import make_swin3d_weights
+    model.load_state_dict(make_swin3d_weights(dict(cfg, num_classes=num_classes), seed=weights_seed))
+    if logger:
+        logger.info(f"Modified classification head to output {num_classes} classes")
+    return model.to(device) if device else model

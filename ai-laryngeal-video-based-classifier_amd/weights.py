@@ -113,6 +113,71 @@ def make_timesformer_weights(cfg: dict, seed: int = 0, std: float = 0.02) -> "Or
     return out
 
 
+def swin3d_param_shapes(cfg: dict) -> "OrderedDict[str, tuple]":
+    """Parameter names and shapes of torchvision `swin3d_t` with the reference's replaced head
+    (videoswintransformer/swin_video_classifier/models/swin3d.py:24-44), in a fixed order.
+    The relative_position_index buffers are not parameters (rebuilt from the window size)."""
+    C0 = cfg["embed_dim"]
+    pt, ph, pw = cfg["patch_size"]
+    wt, wh, ww = cfg["window_size"]
+    nbias = (2 * wt - 1) * (2 * wh - 1) * (2 * ww - 1)
+    s = OrderedDict()
+    s["patch_embed.proj.weight"] = (C0, 3, pt, ph, pw)
+    s["patch_embed.proj.bias"] = (C0,)
+    s["patch_embed.norm.weight"] = (C0,)
+    s["patch_embed.norm.bias"] = (C0,)
+    for st, depth in enumerate(cfg["depths"]):
+        C = C0 * 2 ** st
+        heads = cfg["num_heads"][st]
+        hid = int(C * cfg.get("mlp_ratio", 4.0))
+        for i in range(depth):
+            p = f"features.{2 * st}.{i}."
+            s[p + "norm1.weight"] = (C,)
+            s[p + "norm1.bias"] = (C,)
+            s[p + "attn.relative_position_bias_table"] = (nbias, heads)
+            s[p + "attn.qkv.weight"] = (3 * C, C)
+            s[p + "attn.qkv.bias"] = (3 * C,)
+            s[p + "attn.proj.weight"] = (C, C)
+            s[p + "attn.proj.bias"] = (C,)
+            s[p + "norm2.weight"] = (C,)
+            s[p + "norm2.bias"] = (C,)
+            s[p + "mlp.0.weight"] = (hid, C)
+            s[p + "mlp.0.bias"] = (hid,)
+            s[p + "mlp.3.weight"] = (C, hid)
+            s[p + "mlp.3.bias"] = (C,)
+        if st < len(cfg["depths"]) - 1:
+            p = f"features.{2 * st + 1}."
+            s[p + "reduction.weight"] = (2 * C, 4 * C)
+            s[p + "norm.weight"] = (4 * C,)
+            s[p + "norm.bias"] = (4 * C,)
+    Cf = C0 * 2 ** (len(cfg["depths"]) - 1)
+    s["norm.weight"] = (Cf,)
+    s["norm.bias"] = (Cf,)
+    s["head.weight"] = (cfg.get("num_classes", 2), Cf)
+    s["head.bias"] = (cfg.get("num_classes", 2),)
+    return s
+
+
+def make_swin3d_weights(cfg: dict, seed: int = 0, std: float = 0.02) -> "OrderedDict[str, np.ndarray]":
+    rng = np.random.RandomState(seed)
+    out = OrderedDict()
+    for name, shape in swin3d_param_shapes(cfg).items():
+        w = rng.standard_normal(shape) * std
+        if name.endswith("norm.weight") or name.endswith("norm1.weight") or name.endswith("norm2.weight"):
+            w = w + 1.0
+        out[name] = np.ascontiguousarray(w.astype(np.float32))
+    return out
+
+
+def make_synthetic_video(batch: int, num_frames: int, image_size: int, seed: int = 1) -> np.ndarray:
+    """[B, 3, T, H, W] f32 (the torchvision video-model input layout, swin trainer.py:116):
+    the uint8 frames of make_synthetic_frames through the Swin/ResNet3D transform's
+    Normalize(0.45, 0.225) on x/255 (resize/crop skipped: frames are 224^2)."""
+    f = make_synthetic_frames(batch, num_frames, image_size, seed).astype(np.float32)
+    x = (f / np.float32(255.0) - np.float32(0.45)) / np.float32(0.225)
+    return np.ascontiguousarray(x.transpose(0, 4, 1, 2, 3))
+
+
 def make_synthetic_frames(batch: int, num_frames: int, image_size: int, seed: int = 1) -> np.ndarray:
     """uint8 decoded frames [B, T, H, W, 3] (the layout the reference dataset returns,
     vivit_transformer/vivit_classifier/data_config/dataset.py:268-291)."""

@@ -65,14 +65,19 @@ int vc_tubelet_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C
 #define VC_TOKENS_TIME_MAJOR  0  /* row = ((b*nt + t')*nh + hp)*nw + wp   (ViViT, modeling_vivit.py:64-67)          */
 #define VC_TOKENS_PATCH_MAJOR 1  /* row = ((b*nh + hp)*nw + wp)*nt + t'   (TimeSformer, modeling_timesformer.py:121-143) */
 
+/* Input layouts of vc_patch_im2col. */
+#define VC_VIDEO_BTCHW 0  /* [B][T][C][H][W]: HF pixel_values (ViViT, TimeSformer)                   */
+#define VC_VIDEO_BCTHW 1  /* [B][C][T][H][W]: torchvision video models (Swin3D, ResNet3D; trainer.py:116) */
+
 /*
- * vc_tubelet_im2col with an explicit token order.  With kt = 1 and VC_TOKENS_PATCH_MAJOR it is
- * the input side of TimeSformer's per-frame Conv2d patch embedding re-ordered patch-major /
- * time-minor (TimesformerPatchEmbeddings + the permute of TimesformerEmbeddings,
- * TF5/models/timesformer/modeling_timesformer.py:45-60, 121-143).
+ * vc_tubelet_im2col with an explicit token order and input layout; kw % 4 == 0.
+ * kt = 1 + VC_TOKENS_PATCH_MAJOR: the input side of TimeSformer's per-frame Conv2d patch
+ * embedding re-ordered patch-major / time-minor (TF5/models/timesformer/modeling_timesformer.py:
+ * 45-60, 121-143).  (2,4,4) + VC_VIDEO_BCTHW: torchvision PatchEmbed3d's Conv3d (Swin3D-T).
  */
 int vc_patch_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C, int64_t H, int64_t W,
-                    int kt, int kh, int kw, int token_order, uint16_t* A, int64_t lda, hipStream_t stream);
+                    int kt, int kh, int kw, int token_order, int layout, uint16_t* A, int64_t lda,
+                    hipStream_t stream);
 
 /* GEMM epilogues for vc_gemm_bf16. */
 #define VC_EPI_BIAS_BF16        0  /* out bf16[m][n]  = acc + bias[n]                               */
@@ -81,6 +86,7 @@ int vc_patch_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C, 
 #define VC_EPI_BIAS_RESID_F32   3  /* out f32 [m][n] += acc + bias[n]             (o_proj, fc2)       */
 #define VC_EPI_EMBED_F32        4  /* out f32 [r(m)][n] = acc + bias[n] + aux[m % G][n],
                                        r(m) = (m / G) * group_stride + group_offset (tubelet -> tokens) */
+#define VC_EPI_BIAS_F32         5  /* out f32 [m][n]  = acc + bias[n]             (Swin embed / merge)  */
 
 /*
  * C[M][N] = A[M][K] . W[N][K]^T  (bf16 inputs, fp32 accumulate on MFMA), fused epilogue.
@@ -128,6 +134,11 @@ int vc_layernorm_f32_bf16(const float* x, int64_t ldx, int64_t M, int64_t D,
 int vc_attention_fwd(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, int64_t head_dim,
                      float scale, int q_prescaled, uint16_t* out, int64_t ldo, hipStream_t stream);
 
+/* LayerNorm f32 -> f32 (any D; y may alias nothing of x).  Swin's patch_embed.norm (torchvision
+ * PatchEmbed3d, eps 1e-5) whose output is the fp32 residual stream. */
+int vc_layernorm_f32(const float* x, int64_t ldx, int64_t M, int64_t D, const float* gamma, const float* beta,
+                     float eps, float* y, int64_t ldy, hipStream_t stream);
+
 /* CLS rows: x[b*S][:] = cls[:] + pos[0][:]   (TF5/.../modeling_vivit.py:131-142). */
 int vc_cls_init(const float* cls, const float* pos, float* x, int64_t ldx, int64_t B, int64_t S, int64_t D,
                 hipStream_t stream);
@@ -172,6 +183,41 @@ int vc_temporal_attention(const uint16_t* qkv, int64_t ld, int64_t B, int64_t P,
 int vc_divided_add_layernorm(float* x, int64_t ldx, const uint16_t* y, int64_t ldy, int64_t B, int64_t P, int64_t T,
                              int64_t D, const float* gamma, const float* beta, float eps, int mode, uint16_t* h,
                              int64_t ldh, hipStream_t stream);
+
+/* ---- Video Swin 3D (torchvision swin3d_t) -------------------------------
+ * Token layout: rows ((b*T + t)*H + h)*W + w (channels-last [B][T][H][W][C]). */
+
+/*
+ * Shifted-window attention core, head_dim 32: for every window of (wt,wh,ww) tokens of the grid
+ * rolled by -(st,sh,sw), softmax(q'.k + bias [+ shift mask]) v per head.  qkv: bf16 rows of the
+ * fused q|k|v projection (head h: q at h*32, k at C + h*32, v at 2C + h*32, C = heads*32), with
+ * q' = q * d^-1/2 * log2(e) (folded into the projection).  biasT: f32 [heads][np][np],
+ * biasT[h][k][q] = log2(e) * relative_position_bias[h][q][k] for q, k < vol and -inf for
+ * k >= vol, np = roundup(wt*wh*ww, 64) <= 448.  The shift mask (tokens of different shift
+ * regions, torchvision's -100) is applied as -inf.  out: bf16 rows (head h at h*32), every
+ * token written once.  T, H, W must be whole windows.  Replaces shifted_window_attention_3d
+ * (torchvision.models.video.swin_transformer) between its qkv and proj Linears.
+ */
+int vc_window_attention3d(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T, int64_t H, int64_t W, int64_t heads,
+                          int64_t head_dim, int wt, int wh, int ww, int st, int sh, int sw, const float* biasT,
+                          int64_t np, uint16_t* out, int64_t ldo, hipStream_t stream);
+
+/*
+ * PatchMerging gather + LayerNorm(4C): y[(b,t,i,j)] = LN(cat(x[2i,2j], x[2i+1,2j], x[2i,2j+1],
+ * x[2i+1,2j+1])) in bf16 (zero rows past an odd edge); the Linear(4C, 2C) follows as a GEMM.
+ * Replaces torchvision PatchMerging's _patch_merging_pad + norm.  4C <= 4096.
+ */
+int vc_patch_merge_layernorm(const float* x, int64_t ldx, int64_t B, int64_t T, int64_t H, int64_t W, int64_t C,
+                             const float* gamma, const float* beta, float eps, uint16_t* y, int64_t ldy,
+                             hipStream_t stream);
+
+/*
+ * logits[b] = Wc . mean_n LN(x[b*ntok + n]) + bc (fp32): final norm, AdaptiveAvgPool3d(1) and
+ * head of torchvision SwinTransformer3d.forward (head replaced by the reference, swin3d.py:43-44).
+ */
+int vc_pool_head(const float* x, int64_t ldx, int64_t B, int64_t ntok, int64_t D, const float* gamma,
+                 const float* beta, float eps, const float* Wc, const float* bc, int64_t num_labels, float* logits,
+                 hipStream_t stream);
 
 #ifdef __cplusplus
 }

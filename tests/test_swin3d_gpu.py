@@ -1,0 +1,101 @@
+"""Video Swin 3D on the GPU: the shifted-window attention kernel and the end-to-end path vs
+oracle/swin3d_ref.py (fp32 CPU restatement of torchvision's swin3d; torchvision itself is
+not installed, so parity with the library is UNPINNED — SURVEY.md §8c).  Tolerances:
+attention outputs 2e-2 abs (bf16 operands, bf16 P), logits 1e-2 (north_star bf16)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import swin3d_ref as ref
+from vclip_amd.weights import make_swin3d_weights, make_synthetic_video
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+TINY = dict(patch_size=(2, 4, 4), embed_dim=32, depths=(2, 2), num_heads=(1, 2), window_size=(2, 3, 3),
+            mlp_ratio=4.0, layer_norm_eps=1e-5, num_classes=2)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vclip_amd import _lib
+    _lib.load()
+
+
+def _window_case(B, grid, C, window, shift, seed):
+    """Oracle attention (qkv from x, identity proj) vs qkv GEMM-free kernel call."""
+    from vclip_amd import ops
+    g = torch.Generator().manual_seed(seed)
+    heads = C // 32
+    T, H, W = grid
+    x = torch.randn(B, T, H, W, C, generator=g)
+    wt, wh, ww = window
+    nb = (2 * wt - 1) * (2 * wh - 1) * (2 * ww - 1)
+    p = {"a.qkv.weight": torch.randn(3 * C, C, generator=g) * C ** -0.5, "a.qkv.bias": torch.randn(3 * C, generator=g) * 0.1,
+         "a.proj.weight": torch.eye(C), "a.proj.bias": torch.zeros(C),
+         "a.relative_position_bias_table": torch.randn(nb, heads, generator=g) * 0.5}
+    want = ref.window_attention_3d(x, p, "a.", heads, window, shift)
+    # device: q|k|v rows with q pre-scaled by d^-1/2 log2 e, rounded to bf16 once
+    qkv = x.reshape(-1, C) @ p["a.qkv.weight"].T + p["a.qkv.bias"]
+    qkv[:, :C] *= 32 ** -0.5 * ops.LOG2E
+    qkv_d = qkv.bfloat16().to(DEV)
+    from vclip_amd.swin3d import expand_bias
+    w_eff, s_eff = ref.window_and_shift(grid, window, shift)
+    biasT = expand_bias(p["a.relative_position_bias_table"], window, w_eff, torch.device(DEV))
+    out = torch.zeros(B * T * H * W + 8, C, dtype=torch.bfloat16, device=DEV)
+    ops.window_attention3d(qkv_d, B, grid, heads, w_eff, s_eff, biasT, out)
+    got = out[:B * T * H * W].float().cpu().reshape(B, T, H, W, C)
+    # fp32 reference on the same bf16-rounded q|k|v isolates the kernel's own error
+    return got, want
+
+
+@pytest.mark.parametrize("B,grid,C,window,shift", [
+    (2, (4, 6, 6), 32, (2, 3, 3), (0, 0, 0)),
+    (2, (4, 6, 6), 64, (2, 3, 3), (1, 1, 1)),
+    (1, (16, 14, 14), 96, (8, 7, 7), (4, 3, 3)),
+    (1, (16, 7, 7), 64, (8, 7, 7), (4, 3, 3)),   # window == feature size in h, w: shift dropped there
+    (1, (2, 6, 6), 32, (2, 3, 3), (1, 1, 1)),    # t == window: t shift dropped
+])
+def test_window_attention3d(B, grid, C, window, shift):
+    got, want = _window_case(B, grid, C, window, shift, seed=C + sum(shift))
+    err = (got - want).abs().max().item()
+    assert err < 2e-2, err
+
+
+def _model(cfg, seed=0):
+    from vclip_amd.swin3d import Swin3d
+    m = Swin3d({k: v for k, v in cfg.items() if k != "num_classes"}, num_classes=cfg["num_classes"])
+    m.load_state_dict(make_swin3d_weights(cfg, seed=seed))
+    return m.to(DEV)
+
+
+def _oracle(cfg, video, seed=0):
+    sd = {k: torch.from_numpy(v) for k, v in make_swin3d_weights(cfg, seed=seed).items()}
+    with torch.no_grad():
+        return ref.swin3d_forward(sd, cfg, torch.from_numpy(video)).numpy()
+
+
+@pytest.mark.parametrize("T,HW", [(8, 48), (4, 48)])
+def test_swin3d_tiny_logits(T, HW):
+    video = make_synthetic_video(2, T, HW, seed=3)
+    want = _oracle(TINY, video)
+    got = _model(TINY)(torch.from_numpy(video).to(DEV)).cpu().numpy()
+    assert np.abs(got - want).max() < 1e-2, (got, want)
+
+
+def test_swin3d_t_full_logits():
+    cfg = dict(ref.SWIN3D_T)
+    video = make_synthetic_video(1, 32, 224, seed=1)
+    want = _oracle(cfg, video)
+    got = _model(cfg)(torch.from_numpy(video).to(DEV)).cpu().numpy()
+    assert np.abs(got - want).max() < 1e-2, (got, want)
+
+
+def test_swin3d_batch_invariance():
+    video = torch.from_numpy(make_synthetic_video(3, 8, 48, seed=4)).to(DEV)
+    m = _model(TINY)
+    full = m(video).clone()
+    one = m(video[1:2].contiguous()).clone()
+    assert torch.equal(full[1:2], one)

@@ -1,5 +1,6 @@
 """Forward throughput of the non-headline model families at their BASELINE configs
-(SURVEY.md §8(d)): TimeSformer-B 8f B=16 (cfg3), plus ViViT-B for reference.
+(SURVEY.md §8(d)): TimeSformer-B 8f B=16 (cfg3), Video Swin-T 32f (cfg4: B=4 per GPU),
+plus ViViT-B for reference.
 
   python tools/bench_models.py [--model timesformer] [--batch 16] [--steps 20] [--warmup 3]
 
@@ -16,11 +17,17 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-GFLOP = {"vivit": 903.05, "timesformer": 391.66}
+GFLOP = {"vivit": 903.05, "timesformer": 391.66, "swin3d_t": 175.53}
 
 
 def build(name, batch, dev):
     from vclip_amd.weights import make_synthetic_clips
+    if name == "swin3d_t":
+        from vclip_amd.swin3d import create_model
+        from vclip_amd.weights import make_synthetic_video
+        m = create_model(model_size="tiny", device=dev)
+        m.forward_logits = m.forward
+        return m, torch.from_numpy(make_synthetic_video(batch, 32, 224, seed=1)).to(dev)
     if name == "vivit":
         from vclip_amd.vivit import create_model
         m = create_model(num_frames=32, device=dev)
