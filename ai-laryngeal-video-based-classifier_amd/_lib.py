@@ -42,7 +42,7 @@ SIGNATURES = {
     "vc_window_attention3d": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_int, c_int,
                                c_int, c_p, c_i64, c_p, c_i64, c_p], c_int),
     "vc_patch_merge_layernorm": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_p, c_i64, c_p], c_int),
-    "vc_pool_head": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_p, c_p, c_i64, c_p, c_p], c_int),
+    "vc_pool_head": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_p, c_p, c_i64, c_p, c_p, c_p], c_int),
     "vc_divided_add_layernorm": ([c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_int, c_p,
                                   c_i64, c_p], c_int),
 }

@@ -185,6 +185,53 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
     }
 }
 
+// LayerNorm for any D % 4 == 0, D <= 1024 (Swin's 96/192/384, TimeSformer-tiny 128 ...):
+// one wave per row held in registers (up to 4 float4 per lane, masked), single HBM pass.
+template <bool OUTF32>
+__global__ void __launch_bounds__(256) layernorm_reg_kernel(const float* __restrict__ x, int64_t ldx, int64_t M, int D,
+                                                            const float* __restrict__ g, const float* __restrict__ be,
+                                                            float eps, void* __restrict__ y, int64_t ldy) {
+    const int lane = threadIdx.x & 63;
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const float* xr = x + row * ldx;
+    float4 v[4];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int n = (i * 64 + lane) * 4;
+        v[i] = n < D ? *reinterpret_cast<const float4*>(xr + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+        s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    }
+    const float mean = wave_sum(s) / (float)D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if ((i * 64 + lane) * 4 < D) {
+            const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+            q += (a * a + b * b) + (c * c + d * d);
+        }
+    }
+    const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int n = (i * 64 + lane) * 4;
+        if (n < D) {
+            const float4 gg = *reinterpret_cast<const float4*>(g + n), bb = *reinterpret_cast<const float4*>(be + n);
+            const float o0 = (v[i].x - mean) * rstd * gg.x + bb.x, o1 = (v[i].y - mean) * rstd * gg.y + bb.y;
+            const float o2 = (v[i].z - mean) * rstd * gg.z + bb.z, o3 = (v[i].w - mean) * rstd * gg.w + bb.w;
+            if constexpr (OUTF32) {
+                *reinterpret_cast<float4*>(reinterpret_cast<float*>(y) + row * ldy + n) = make_float4(o0, o1, o2, o3);
+            } else {
+                uint2 o;
+                o.x = pack2bf(o0, o1);
+                o.y = pack2bf(o2, o3);
+                *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(y) + row * ldy + n) = o;
+            }
+        }
+    }
+}
+
 // Generic-width LayerNorm (any D): one wave per row, three passes over the row (L1/L2-resident).
 // OUTF32: the output is f32 (y is a float*), e.g. Swin's patch_embed.norm feeding the residual stream.
 template <bool OUTF32 = false>
@@ -336,7 +383,10 @@ int vc_layernorm_f32_bf16(const float* x, int64_t ldx, int64_t M, int64_t D, con
         case 1024: layernorm_kernel<4><<<nb, 256, 0, stream>>>(x, ldx, M, gamma, beta, eps, y, ldy); break;
         default:
             if (D <= 0 || D > 65536) return fail(VC_ERR_INVALID_ARG, "vc_layernorm: bad D");
-            layernorm_any_kernel<false><<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, gamma, beta, eps, y, ldy);
+            if (D <= 1024 && D % 4 == 0 && !(((uintptr_t)x | (uintptr_t)gamma | (uintptr_t)beta) & 15) && !((uintptr_t)y & 7))
+                layernorm_reg_kernel<false><<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, gamma, beta, eps, y, ldy);
+            else
+                layernorm_any_kernel<false><<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, gamma, beta, eps, y, ldy);
     }
     return check_launch("vc_layernorm_f32_bf16");
 }
@@ -345,7 +395,12 @@ int vc_layernorm_f32(const float* x, int64_t ldx, int64_t M, int64_t D, const fl
                      float eps, float* y, int64_t ldy, hipStream_t stream) {
     if (!x || !gamma || !beta || !y) return fail(VC_ERR_INVALID_ARG, "vc_layernorm_f32: null pointer");
     if (D <= 0 || D > 65536 || ldx < D || ldy < D) return fail(VC_ERR_INVALID_ARG, "vc_layernorm_f32: bad D / ld");
-    layernorm_any_kernel<true><<<(unsigned)((M + 3) / 4), 256, 0, stream>>>(x, ldx, M, (int)D, gamma, beta, eps, y, ldy);
+    const unsigned nb = (unsigned)((M + 3) / 4);
+    if (D <= 1024 && D % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 &&
+        !(((uintptr_t)x | (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)y) & 15))
+        layernorm_reg_kernel<true><<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, gamma, beta, eps, y, ldy);
+    else
+        layernorm_any_kernel<true><<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, gamma, beta, eps, y, ldy);
     return check_launch("vc_layernorm_f32");
 }
 

@@ -13,8 +13,9 @@
 //
 // One workgroup = 4 waves = one (window, head).  The window's K and V (vol <= 448 tokens x
 // 32 dims, bf16) are staged once into LDS (57 KB, 2 workgroups per CU); each wave walks
-// 32-query blocks: S^T = K.Q'^T with the bias tile as the MFMA C operand (biasT[h][k][q],
-// pre-scaled by log2 e like Q', -inf on padded keys), the shift-region mask as -inf
+// 32-query blocks: S^T = K.Q'^T with the bias tile as the MFMA C operand (pre-scaled by
+// log2 e like Q', -inf on padded keys; stored in fragment order so each lane's 16 values
+// are one contiguous 64-B read, prefetched a tile ahead), the shift-region mask as -inf
 // (torchvision adds -100: exp(-100) ~ 4e-44 is below fp32 resolution of the row sum, so the
 // results agree), online softmax in exp2, O^T += V^T.P^T with V^T from ds_read_b64_tr_b16.
 #include "common.hpp"
@@ -44,7 +45,7 @@ __device__ __forceinline__ int region_bit(int c, int P, int w, int s) {
 
 __global__ void __launch_bounds__(256, 2)
 window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, int heads, int vol, int NP,
-                       const float* __restrict__ biasT, int masked, uint16_t* __restrict__ out, int64_t ldo) {
+                       const float* __restrict__ biasF, int masked, uint16_t* __restrict__ out, int64_t ldo) {
     __shared__ __attribute__((aligned(16))) char kv[2 * WNP_MAX * 64];
     __shared__ unsigned lab4[WNP_MAX / 8];  // 4-bit region code per window token (15: padding)
 
@@ -110,9 +111,21 @@ window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, 
     const int tq = gi >> 2, tp = gi & 3;
     const int gcol = ((lane >> 4) & 1) * 16 + tp * 4;
     const int voff = (4 * h + tq) * 64 + gcol * 2;
-    const float* bh = biasT + (int64_t)head * NP * NP;
     const int nqb = (vol + 31) / 32;
     const int ntile = NP / 64;
+    // bias fragments: biasF[head][qb][t][kb][lane][16] f32 = this lane's 16 C-operand values
+    const float* bh = biasF + (int64_t)head * (NP / 32) * ntile * 2 * 64 * 16 + lane * 16;
+    auto load_bias = [&](int qb, int t, v16f (&c)[2]) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            const float4* bp = reinterpret_cast<const float4*>(bh + (((int64_t)qb * ntile + t) * 2 + kb) * 64 * 16);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float4 u = bp[j];
+                c[kb][4 * j] = u.x; c[kb][4 * j + 1] = u.y; c[kb][4 * j + 2] = u.z; c[kb][4 * j + 3] = u.w;
+            }
+        }
+    };
 
     for (int qb = wave; qb < nqb; qb += 4) {
         const int qn = qb * 32 + rr;  // this lane's query (window-local)
@@ -125,15 +138,11 @@ window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, 
             qf[kk] = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(qkv + qrow * ld + head * 32 + 16 * kk + 8 * h));
         v16f o = {};
         float m_run = -1e30f, l_run = 0.f;
+        v16f bnext[2];
+        load_bias(qb, 0, bnext);
         for (int t = 0; t < ntile; ++t) {
-            v16f sc[2];
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb) {
-                // C = bias tile biasT[k][q]: reg e <-> key row (e&3) + 8(e>>2) + 4h, query qn
-                const float* bp = bh + (int64_t)(t * 64 + kb * 32 + 4 * h) * NP + qb * 32 + rr;
-#pragma unroll
-                for (int e = 0; e < 16; ++e) sc[kb][e] = bp[(int64_t)((e & 3) + 8 * (e >> 2)) * NP];
-            }
+            v16f sc[2] = {bnext[0], bnext[1]};  // C = bias tile (prefetched one tile ahead)
+            if (t + 1 < ntile) load_bias(qb, t + 1, bnext);
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
@@ -252,36 +261,80 @@ __global__ void __launch_bounds__(256) patch_merge_ln_kernel(const float* __rest
 // ---------------------------------------------------------------------------------
 // Final LayerNorm over every token, mean over the clip's tokens, classifier GEMV (fp32):
 // logits[b] = W . mean_n LN(x[b, n]) + bias  (torchvision SwinTransformer3d.forward:
-// norm -> avgpool -> flatten -> head).  One workgroup per clip; D <= 4096.
+// norm -> avgpool -> flatten -> head).  Two deterministic stages (no atomics, fixed sum
+// order): pool_partial_kernel — grid (B, POOL_CHUNKS), each wave normalises whole rows held
+// in registers (D <= 1024) and accumulates them, the 4 waves reduce through LDS into
+// work[b][chunk][:]; pool_final_kernel — grid B, sums the chunks in order, / ntok, GEMV.
 // ---------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) pool_head_kernel(const float* __restrict__ x, int64_t ldx, int64_t ntok, int D,
-                                                        const float* __restrict__ g, const float* __restrict__ be,
-                                                        float eps, const float* __restrict__ Wc,
-                                                        const float* __restrict__ bc, int nl,
-                                                        float* __restrict__ logits) {
-    __shared__ float acc[4][4096];
-    const int b = blockIdx.x;
+constexpr int POOL_CHUNKS = 64;
+
+__global__ void __launch_bounds__(256) pool_partial_kernel(const float* __restrict__ x, int64_t ldx, int64_t ntok,
+                                                           int D, const float* __restrict__ g,
+                                                           const float* __restrict__ be, float eps,
+                                                           float* __restrict__ work) {
+    __shared__ float red[4][1024];
+    const int b = blockIdx.x, ch = blockIdx.y;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int n = lane; n < D; n += 64) acc[w][n] = 0.f;
-    for (int64_t tk = w; tk < ntok; tk += 4) {
+    float4 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t tk = (int64_t)ch * 4 + w; tk < ntok; tk += POOL_CHUNKS * 4) {
         const float* xr = x + ((int64_t)b * ntok + tk) * ldx;
+        float4 v[4];
         float s = 0.f;
-        for (int n = lane; n < D; n += 64) s += xr[n];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int n = (i * 64 + lane) * 4;
+            v[i] = n < D ? *reinterpret_cast<const float4*>(xr + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+            s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+        }
         const float mean = wave_sum(s) / (float)D;
         float q = 0.f;
-        for (int n = lane; n < D; n += 64) {
-            const float d = xr[n] - mean;
-            q += d * d;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if ((i * 64 + lane) * 4 < D) {
+                const float a0 = v[i].x - mean, a1 = v[i].y - mean, a2 = v[i].z - mean, a3 = v[i].w - mean;
+                q += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+            }
         }
         const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
-        for (int n = lane; n < D; n += 64) acc[w][n] += (xr[n] - mean) * rstd * g[n] + be[n];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int n = (i * 64 + lane) * 4;
+            if (n < D) {
+                const float4 gg = *reinterpret_cast<const float4*>(g + n), bb = *reinterpret_cast<const float4*>(be + n);
+                acc[i].x += (v[i].x - mean) * rstd * gg.x + bb.x;
+                acc[i].y += (v[i].y - mean) * rstd * gg.y + bb.y;
+                acc[i].z += (v[i].z - mean) * rstd * gg.z + bb.z;
+                acc[i].w += (v[i].w - mean) * rstd * gg.w + bb.w;
+            }
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int n = (i * 64 + lane) * 4;
+        if (n < D) *reinterpret_cast<float4*>(&red[w][n]) = acc[i];
     }
     __syncthreads();
-    for (int n = threadIdx.x; n < D; n += 256) acc[0][n] = (acc[0][n] + acc[1][n] + acc[2][n] + acc[3][n]) / (float)ntok;
+    for (int n = threadIdx.x; n < D; n += 256)
+        work[((int64_t)b * POOL_CHUNKS + ch) * D + n] = (red[0][n] + red[1][n]) + (red[2][n] + red[3][n]);
+}
+
+__global__ void __launch_bounds__(256) pool_final_kernel(const float* __restrict__ work, int64_t ntok, int D,
+                                                         const float* __restrict__ Wc, const float* __restrict__ bc,
+                                                         int nl, float* __restrict__ logits) {
+    __shared__ float pooled[1024];
+    const int b = blockIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int n = threadIdx.x; n < D; n += 256) {
+        float s = 0.f;
+        for (int c = 0; c < POOL_CHUNKS; ++c) s += work[((int64_t)b * POOL_CHUNKS + c) * D + n];
+        pooled[n] = s / (float)ntok;
+    }
     __syncthreads();
     for (int c = w; c < nl; c += 4) {
         float a = 0.f;
-        for (int n = lane; n < D; n += 64) a += acc[0][n] * Wc[(int64_t)c * D + n];
+        for (int n = lane; n < D; n += 64) a += pooled[n] * Wc[(int64_t)c * D + n];
         a = wave_sum(a);
         if (lane == 0) logits[(int64_t)b * nl + c] = a + bc[c];
     }
@@ -294,9 +347,9 @@ using namespace vc;
 extern "C" {
 
 int vc_window_attention3d(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T, int64_t H, int64_t W, int64_t heads,
-                          int64_t head_dim, int wt, int wh, int ww, int st, int sh, int sw, const float* biasT,
+                          int64_t head_dim, int wt, int wh, int ww, int st, int sh, int sw, const float* biasF,
                           int64_t np, uint16_t* out, int64_t ldo, hipStream_t stream) {
-    if (!qkv || !biasT || !out) return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d: null pointer");
+    if (!qkv || !biasF || !out) return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d: null pointer");
     if (head_dim != 32) return fail(VC_ERR_UNSUPPORTED, "vc_window_attention3d: head_dim must be 32");
     if (wt <= 0 || wh <= 0 || ww <= 0 || T % wt || H % wh || W % ww)
         return fail(VC_ERR_UNSUPPORTED, "vc_window_attention3d: the token grid must be whole windows (no padding)");
@@ -311,7 +364,8 @@ int vc_window_attention3d(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T,
     const int64_t nwin = B * g.nwt * g.nwh * g.nww;
     if (nwin > 0x7fffffff || heads > 65535) return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d: grid too large");
     dim3 grid((unsigned)nwin, (unsigned)heads);
-    window_attn_d32_kernel<<<grid, 256, 0, stream>>>(qkv, ld, g, (int)heads, vol, (int)np, biasT,
+    if ((uintptr_t)biasF & 15) return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d: biasF must be 16-B aligned");
+    window_attn_d32_kernel<<<grid, 256, 0, stream>>>(qkv, ld, g, (int)heads, vol, (int)np, biasF,
                                                      (st | sh | sw) ? 1 : 0, out, ldo);
     return check_launch("vc_window_attention3d");
 }
@@ -330,11 +384,13 @@ int vc_patch_merge_layernorm(const float* x, int64_t ldx, int64_t B, int64_t T, 
 
 int vc_pool_head(const float* x, int64_t ldx, int64_t B, int64_t ntok, int64_t D, const float* gamma,
                  const float* beta, float eps, const float* Wc, const float* bc, int64_t num_labels, float* logits,
-                 hipStream_t stream) {
-    if (!x || !gamma || !beta || !Wc || !bc || !logits) return fail(VC_ERR_INVALID_ARG, "vc_pool_head: null pointer");
-    if (D <= 0 || D > 4096 || ntok <= 0) return fail(VC_ERR_UNSUPPORTED, "vc_pool_head: D in (0, 4096], ntok > 0");
-    pool_head_kernel<<<(unsigned)B, 256, 0, stream>>>(x, ldx, ntok, (int)D, gamma, beta, eps, Wc, bc, (int)num_labels,
-                                                      logits);
+                 float* work, hipStream_t stream) {
+    if (!x || !gamma || !beta || !Wc || !bc || !logits || !work)
+        return fail(VC_ERR_INVALID_ARG, "vc_pool_head: null pointer");
+    if (D <= 0 || D > 1024 || D % 4 || ldx % 4 || ntok <= 0 || ((uintptr_t)x & 15))
+        return fail(VC_ERR_UNSUPPORTED, "vc_pool_head: D % 4 == 0, D <= 1024, 16-B aligned rows, ntok > 0");
+    pool_partial_kernel<<<dim3((unsigned)B, POOL_CHUNKS), 256, 0, stream>>>(x, ldx, ntok, (int)D, gamma, beta, eps, work);
+    pool_final_kernel<<<(unsigned)B, 256, 0, stream>>>(work, ntok, (int)D, Wc, bc, (int)num_labels, logits);
     return check_launch("vc_pool_head");
 }
 

@@ -217,8 +217,8 @@ def divided_add_layernorm(x: torch.Tensor, y: torch.Tensor, B: int, P: int, T: i
 def window_attention3d(qkv: torch.Tensor, B: int, grid, heads: int, window, shift, biasT: torch.Tensor,
                        out: torch.Tensor) -> torch.Tensor:
     """Swin 3D shifted-window attention (head_dim 32) on the token layout [B][T][H][W]:
-    qkv bf16 [>= B*T*H*W, >= 3*heads*32] (q pre-scaled by d^-1/2 * log2 e), biasT f32
-    [heads, np, np] (see include/vclip.h) -> out bf16 [rows, >= heads*32]."""
+    qkv bf16 [>= B*T*H*W, >= 3*heads*32] (q pre-scaled by d^-1/2 * log2 e), biasT the f32
+    fragment-order bias of swin3d.expand_bias (see include/vclip.h) -> out bf16 [rows, >= heads*32]."""
     _dev(qkv, biasT, out)
     T, H, W = grid
     wt, wh, ww = window
@@ -227,8 +227,8 @@ def window_attention3d(qkv: torch.Tensor, B: int, grid, heads: int, window, shif
     np_ = (vol + 63) // 64 * 64
     _need(qkv.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and qkv.stride(1) == 1 and out.stride(1) == 1,
           "window_attention3d dtypes")
-    _need(biasT.dtype == torch.float32 and biasT.is_contiguous() and tuple(biasT.shape) == (heads, np_, np_),
-          "window_attention3d biasT [heads, np, np] f32")
+    _need(biasT.dtype == torch.float32 and biasT.is_contiguous() and biasT.numel() == heads * np_ * np_,
+          "window_attention3d bias: f32 fragment-order table of heads*np*np (swin3d.expand_bias)")
     _need(qkv.shape[0] >= B * T * H * W and out.shape[0] >= B * T * H * W, "window_attention3d rows")
     _need(qkv.shape[1] >= 3 * heads * 32 and out.shape[1] >= heads * 32, "window_attention3d columns")
     _need(T % wt == 0 and H % wh == 0 and W % ww == 0, "window_attention3d: grid must be whole windows")
@@ -252,7 +252,8 @@ def patch_merge_layernorm(x: torch.Tensor, B: int, grid, C: int, gamma, beta, ep
 
 
 def pool_head(x: torch.Tensor, B: int, ntok: int, gamma, beta, eps: float, wc: torch.Tensor, bc: torch.Tensor,
-              out: torch.Tensor | None = None) -> torch.Tensor:
+              out: torch.Tensor | None = None, work: torch.Tensor | None = None) -> torch.Tensor:
+    """logits = head(mean over each clip's ntok rows of LN(x)) (Swin3D final norm + avgpool + head)."""
     _dev(x, gamma, beta, wc, bc)
     D = gamma.numel()
     nl = wc.shape[0]
@@ -260,6 +261,8 @@ def pool_head(x: torch.Tensor, B: int, ntok: int, gamma, beta, eps: float, wc: t
           "pool_head shapes")
     if out is None:
         out = torch.empty((B, nl), dtype=torch.float32, device=x.device)
+    if work is None or work.numel() < B * 64 * D:
+        work = torch.empty(B * 64 * D, dtype=torch.float32, device=x.device)
     _lib.call("vc_pool_head", _p(x), x.stride(0), B, ntok, D, _p(gamma), _p(beta), eps, _p(wc), _p(bc), nl, _p(out),
-              _stream(x))
+              _p(work), _stream(x))
     return out

@@ -14,8 +14,8 @@ Per block: LN1 -> qkv GEMM (q pre-scaled by d^-1/2 * log2 e) -> shifted-window a
 (gather/scatter by index: no roll / partition copies; bias + shift mask inside) -> proj
 GEMM + residual -> LN2 -> fc1 + exact GELU -> fc2 + residual.  Between stages: fused
 PatchMerging gather + LN(4C), then the reduction GEMM into the next stage's residual.
-Relative-position bias tables are expanded once per (block, window) into
-biasT[h][k][q] (f32, log2 e scaled, -inf on padded keys).
+Relative-position bias tables are expanded once per (block, window) into the attention
+kernel's accumulator fragment order (f32, log2 e scaled, -inf on padded keys).
 
 Parity unpinned against torchvision itself (not installed here): checked against
 oracle/swin3d_ref.py, the restatement of torchvision's algorithm.
@@ -73,17 +73,26 @@ def window_and_shift(size_thw, window_size, shift_size):
 
 
 def expand_bias(table, full_window, window, device):
-    """biasT[h][k][q] = log2e * table[index_full[:vol,:vol]][q][k][h] (torchvision
-    _get_relative_position_bias, sliced index of the FULL window when it shrinks);
-    -inf for padded keys k >= vol, 0 for padded queries."""
+    """Relative-position bias of one block in the kernel's fragment order.
+
+    bias[h][q][k] = table[index_full[:vol,:vol]][q][k][h] (torchvision _get_relative_position_bias:
+    the FULL window's index, sliced when the window shrinks), scaled by log2 e; -inf on padded
+    keys k >= vol, 0 on padded queries.  Returned as f32 [heads, np/32, np/64, 2, 64, 16]:
+    [h][qb][t][kb][lane][e] = bias[h][q = 32qb + lane%32][k = 64t + 32kb + (e&3) + 8(e>>2) + 4(lane//32)],
+    i.e. each lane's 16 accumulator-layout values of a 32x32 S^T block are contiguous."""
     vol = window[0] * window[1] * window[2]
     npad = _ru(vol, 64)
     idx = relative_position_index(full_window)[:vol, :vol].reshape(-1).to(device)
     bias = table.to(device=device, dtype=torch.float32)[idx].view(vol, vol, -1).permute(2, 0, 1)  # [h, q, k]
-    bt = torch.full((bias.shape[0], npad, npad), float("-inf"), dtype=torch.float32, device=device)
+    heads = bias.shape[0]
+    bt = torch.full((heads, npad, npad), float("-inf"), dtype=torch.float32, device=device)  # [h, k, q]
     bt[:, :, vol:] = 0.0
     bt[:, :vol, :vol] = bias.transpose(1, 2) * LOG2E
-    return bt.contiguous()
+    ar = lambda n: torch.arange(n, device=device)  # noqa: E731
+    qb, t, kb, lane, e = torch.meshgrid(ar(npad // 32), ar(npad // 64), ar(2), ar(64), ar(16), indexing="ij")
+    k = t * 64 + kb * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)
+    q = qb * 32 + (lane & 31)
+    return bt[:, k, q].contiguous()
 
 
 class Swin3d(torch.nn.Module):
@@ -228,6 +237,7 @@ class Swin3d(torch.nn.Module):
                 st["Mg"] = z(_ru(B * t2 * h2 * w2, 256), 4 * C)
             ws["stages"].append(st)
         ws["logits"] = torch.zeros((B, self.num_classes), dtype=f32, device=device)
+        ws["pool_work"] = torch.zeros(B * 64 * c["embed_dim"] * 2 ** (len(grids) - 1), dtype=f32, device=device)
         self._ws = {key: ws}
         return ws
 
@@ -276,7 +286,7 @@ class Swin3d(torch.nn.Module):
                 ops.gemm(sw["Mg"], st["w_red"], st["b_red"], "bias_f32", nxt["X"], m=nxt["M"])
         t, h, w = grids[-1]
         return ops.pool_head(ws["stages"][-1]["X"], B, t * h * w, pk["norm"][0], pk["norm"][1], eps, pk["w_head"],
-                             pk["b_head"], out=ws["logits"])
+                             pk["b_head"], out=ws["logits"], work=ws["pool_work"])
 
 
 def create_model(logger=None, model_size="tiny", pretrained=True, num_classes=2, device="cuda", weights_seed: int = 0):

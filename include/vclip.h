@@ -191,15 +191,17 @@ int vc_divided_add_layernorm(float* x, int64_t ldx, const uint16_t* y, int64_t l
  * Shifted-window attention core, head_dim 32: for every window of (wt,wh,ww) tokens of the grid
  * rolled by -(st,sh,sw), softmax(q'.k + bias [+ shift mask]) v per head.  qkv: bf16 rows of the
  * fused q|k|v projection (head h: q at h*32, k at C + h*32, v at 2C + h*32, C = heads*32), with
- * q' = q * d^-1/2 * log2(e) (folded into the projection).  biasT: f32 [heads][np][np],
- * biasT[h][k][q] = log2(e) * relative_position_bias[h][q][k] for q, k < vol and -inf for
- * k >= vol, np = roundup(wt*wh*ww, 64) <= 448.  The shift mask (tokens of different shift
- * regions, torchvision's -100) is applied as -inf.  out: bf16 rows (head h at h*32), every
- * token written once.  T, H, W must be whole windows.  Replaces shifted_window_attention_3d
- * (torchvision.models.video.swin_transformer) between its qkv and proj Linears.
+ * q' = q * d^-1/2 * log2(e) (folded into the projection).  biasF: f32, the log2(e)-scaled
+ * relative-position bias in accumulator-fragment order [heads][np/32][np/64][2][64][16]:
+ * element [h][qb][t][kb][lane][e] = log2(e) * bias[h][q][k] with q = 32qb + lane%32,
+ * k = 64t + 32kb + (e&3) + 8(e>>2) + 4(lane/32); -inf for k >= vol (np = roundup(vol, 64) <= 448).
+ * The shift mask (tokens of different shift regions, torchvision's -100) is applied as -inf.
+ * out: bf16 rows (head h at h*32), every token written once.  T, H, W must be whole windows.
+ * Replaces shifted_window_attention_3d (torchvision.models.video.swin_transformer) between its
+ * qkv and proj Linears.
  */
 int vc_window_attention3d(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T, int64_t H, int64_t W, int64_t heads,
-                          int64_t head_dim, int wt, int wh, int ww, int st, int sh, int sw, const float* biasT,
+                          int64_t head_dim, int wt, int wh, int ww, int st, int sh, int sw, const float* biasF,
                           int64_t np, uint16_t* out, int64_t ldo, hipStream_t stream);
 
 /*
@@ -214,10 +216,11 @@ int vc_patch_merge_layernorm(const float* x, int64_t ldx, int64_t B, int64_t T, 
 /*
  * logits[b] = Wc . mean_n LN(x[b*ntok + n]) + bc (fp32): final norm, AdaptiveAvgPool3d(1) and
  * head of torchvision SwinTransformer3d.forward (head replaced by the reference, swin3d.py:43-44).
+ * work: caller scratch f32 [B * 64 * D] (fixed-order partial sums: deterministic).  D <= 1024.
  */
 int vc_pool_head(const float* x, int64_t ldx, int64_t B, int64_t ntok, int64_t D, const float* gamma,
                  const float* beta, float eps, const float* Wc, const float* bc, int64_t num_labels, float* logits,
-                 hipStream_t stream);
+                 float* work, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -26,7 +26,6 @@ def build(name, batch, dev):
         from vclip_amd.swin3d import create_model
         from vclip_amd.weights import make_synthetic_video
         m = create_model(model_size="tiny", device=dev)
-        m.forward_logits = m.forward
         return m, torch.from_numpy(make_synthetic_video(batch, 32, 224, seed=1)).to(dev)
     if name == "vivit":
         from vclip_amd.vivit import create_model
