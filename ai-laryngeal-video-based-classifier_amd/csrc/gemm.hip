@@ -86,11 +86,19 @@ __device__ __forceinline__ void store_tile(const v16f (&acc)[MI][NI], int64_t mb
                 float v1 = acc[i][j][4 * g + 1] + bb.y;
                 float v2 = acc[i][j][4 * g + 2] + bb.z;
                 float v3 = acc[i][j][4 * g + 3] + bb.w;
-                if (EPI == VC_EPI_BIAS_BF16 || EPI == VC_EPI_BIAS_GELU_TANH || EPI == VC_EPI_BIAS_GELU_ERF) {
+                if (EPI == VC_EPI_BIAS_BF16 || EPI == VC_EPI_BIAS_GELU_TANH || EPI == VC_EPI_BIAS_GELU_ERF ||
+                    EPI == VC_EPI_BIAS_RELU_BF16 || EPI == VC_EPI_BIAS_RESID_RELU_BF16) {
                     if (EPI == VC_EPI_BIAS_GELU_TANH) {
                         v0 = gelu_tanh(v0); v1 = gelu_tanh(v1); v2 = gelu_tanh(v2); v3 = gelu_tanh(v3);
                     } else if (EPI == VC_EPI_BIAS_GELU_ERF) {
                         v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+                    } else if (EPI == VC_EPI_BIAS_RELU_BF16 || EPI == VC_EPI_BIAS_RESID_RELU_BF16) {
+                        if (EPI == VC_EPI_BIAS_RESID_RELU_BF16) {
+                            const uint2 rr = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(aux) + m * ldaux + n);
+                            v0 += bf2f((unsigned short)(rr.x & 0xffff)); v1 += bf2f((unsigned short)(rr.x >> 16));
+                            v2 += bf2f((unsigned short)(rr.y & 0xffff)); v3 += bf2f((unsigned short)(rr.y >> 16));
+                        }
+                        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
                     }
                     uint2 p;
                     p.x = pack2bf(v0, v1);
@@ -564,6 +572,8 @@ gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint
                         v0 = gelu_tanh(v0); v1 = gelu_tanh(v1); v2 = gelu_tanh(v2); v3 = gelu_tanh(v3);
                     } else if (EPI == VC_EPI_BIAS_GELU_ERF) {
                         v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+                    } else if (EPI == VC_EPI_BIAS_RELU_BF16) {
+                        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
                     }
                     pk[g][0] = pack2bf(v0, v1);
                     pk[g][1] = pack2bf(v2, v3);
@@ -677,7 +687,8 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
         case 2: return launch_cfg<128, 256, 2, 4, E>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 3: return launch_big<E>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 4:
-            if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF)
+            if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
+                          E == VC_EPI_BIAS_RELU_BF16)
                 return launch_persist<E>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
             return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 4 supports bf16-output epilogues only");
         case 14: return launch_persist<E, 1>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
@@ -703,7 +714,8 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
 // and the grid is at least two rounds of 256 tiles; otherwise 128x256 (fc2-like, N = 768,
 // long K) or 128x128.
 static int pick_cfg(int64_t M, int64_t N, int64_t K, int epi) {
-    const bool bf16_out = epi == VC_EPI_BIAS_BF16 || epi == VC_EPI_BIAS_GELU_TANH || epi == VC_EPI_BIAS_GELU_ERF;
+    const bool bf16_out = epi == VC_EPI_BIAS_BF16 || epi == VC_EPI_BIAS_GELU_TANH || epi == VC_EPI_BIAS_GELU_ERF ||
+                          epi == VC_EPI_BIAS_RELU_BF16;
     if (bf16_out && M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && K >= 192 && N <= 8192 &&
         (M / 256) * (N / 256) >= 512)
         return 4;
@@ -730,6 +742,8 @@ extern "C" int vc_gemm_bf16_cfg(const uint16_t* A, int64_t lda, const uint16_t* 
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: pointers must be 16-byte aligned");
     if (epilogue == VC_EPI_EMBED_F32 && (!aux || G <= 0 || ldaux % 4))
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: EMBED epilogue needs aux, G > 0");
+    if (epilogue == VC_EPI_BIAS_RESID_RELU_BF16 && (!aux || ldaux % 4 || ldaux < N || ((uintptr_t)aux & 7)))
+        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: RESID_RELU epilogue needs a bf16 residual (aux) with ldaux >= N");
     if (cfg < 0) cfg = pick_cfg(M, N, K, epilogue);
     const int ablation = cfg >= 10 ? cfg : -1;  // x3 / x4: timing-only ablations of cfg 3 / 4 (wrong results)
     if (ablation > 0) cfg = (ablation % 10 == 4) ? 4 : 3;
@@ -737,7 +751,8 @@ extern "C" int vc_gemm_bf16_cfg(const uint16_t* A, int64_t lda, const uint16_t* 
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: no tile config divides M x N");
     if ((M / kCfgs[cfg].bm) * (N / kCfgs[cfg].bn) > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: grid too large");
     const int k = (int)K;
-    if (cfg == 4 && (K % 32 || K / 32 < 6 || N > 8192 || epilogue > VC_EPI_BIAS_GELU_ERF))
+    if (cfg == 4 && (K % 32 || K / 32 < 6 || N > 8192 ||
+                     (epilogue > VC_EPI_BIAS_GELU_ERF && epilogue != VC_EPI_BIAS_RELU_BF16)))
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 4 needs K%32==0, K>=192, N<=8192, bf16 epilogue");
     if (ablation > 0) {
         if (epilogue != VC_EPI_BIAS_BF16) return fail(VC_ERR_INVALID_ARG, "ablation: bias epilogue only");
@@ -756,6 +771,10 @@ extern "C" int vc_gemm_bf16_cfg(const uint16_t* A, int64_t lda, const uint16_t* 
             return launch_epi<VC_EPI_EMBED_F32>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
         case VC_EPI_BIAS_F32:
             return launch_epi<VC_EPI_BIAS_F32>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
+        case VC_EPI_BIAS_RELU_BF16:
+            return launch_epi<VC_EPI_BIAS_RELU_BF16>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
+        case VC_EPI_BIAS_RESID_RELU_BF16:
+            return launch_epi<VC_EPI_BIAS_RESID_RELU_BF16>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
     }
     return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad epilogue");
 }

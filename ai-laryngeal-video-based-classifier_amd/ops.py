@@ -11,7 +11,8 @@ import torch
 
 from . import _lib
 
-EPI = {"bias": 0, "bias_gelu_tanh": 1, "bias_gelu_erf": 2, "bias_resid_f32": 3, "embed_f32": 4, "bias_f32": 5}
+EPI = {"bias": 0, "bias_gelu_tanh": 1, "bias_gelu_erf": 2, "bias_resid_f32": 3, "embed_f32": 4, "bias_f32": 5,
+       "bias_relu": 6, "bias_resid_relu": 7}
 GATHER_KIND = {"u8": 0, "f32": 1, "bf16": 2}
 
 
@@ -92,10 +93,13 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: str, ou
     _need(a.stride(1) == 1 and w.stride(1) == 1 and out.stride(-1) == 1 and w.shape[1] == K, "gemm layout")
     _need(bias.numel() == N and bias.is_contiguous(), "gemm bias")
     e = EPI[epilogue]
-    if e in (0, 1, 2):
+    if e in (0, 1, 2, 6, 7):
         _need(out.dtype == torch.bfloat16, "gemm out must be bf16 for this epilogue")
     else:
         _need(out.dtype == torch.float32, "gemm out must be f32 for this epilogue")
+    if e == 7:
+        _need(aux is not None and aux.dtype == torch.bfloat16 and aux.stride(1) == 1 and aux.shape[0] >= M and
+              aux.shape[1] >= N, "resid_relu: aux must be the bf16 residual [>= M, >= N]")
     if e == 4:
         _need(aux is not None and aux.dtype == torch.float32 and aux.stride(1) == 1 and group > 0, "embed aux")
         _need((M - 1) // group * group_stride + group_offset + (M - 1) % group < out.shape[0], "embed out rows")
@@ -265,4 +269,62 @@ def pool_head(x: torch.Tensor, B: int, ntok: int, gamma, beta, eps: float, wc: t
         work = torch.empty(B * 64 * D, dtype=torch.float32, device=x.device)
     _lib.call("vc_pool_head", _p(x), x.stride(0), B, ntok, D, _p(gamma), _p(beta), eps, _p(wc), _p(bc), nl, _p(out),
               _p(work), _stream(x))
+    return out
+
+
+CONV_IN = {"ncthw_f32": 0, "cl_bf16": 1}
+
+
+def conv_out_size(size, k, s, p):
+    return tuple((n + 2 * pp - kk) // ss + 1 for n, kk, ss, pp in zip(size, k, s, p))
+
+
+def conv3d_im2col(x: torch.Tensor, kind: str, B: int, grid, C: int, kernel, stride, pad, out: torch.Tensor) -> torch.Tensor:
+    """im2col of a 3D convolution: x f32 [B,C,T,H,W] (kind "ncthw_f32") or channels-last bf16 rows
+    [>= B*T*H*W, >= C] ("cl_bf16") -> out bf16 [>= B*To*Ho*Wo, >= kvol*C]."""
+    import ctypes
+    _dev(x, out)
+    T, H, W = grid
+    To, Ho, Wo = conv_out_size(grid, kernel, stride, pad)
+    kvol = kernel[0] * kernel[1] * kernel[2]
+    _need(out.dtype == torch.bfloat16 and out.stride(1) == 1 and out.shape[0] >= B * To * Ho * Wo and
+          out.shape[1] >= kvol * C, "conv3d_im2col out")
+    if kind == "ncthw_f32":
+        _need(x.dtype == torch.float32 and x.is_contiguous() and tuple(x.shape) == (B, C, T, H, W), "conv3d_im2col x")
+        ldx = 0
+    else:
+        _need(x.dtype == torch.bfloat16 and x.stride(1) == 1 and x.shape[0] >= B * T * H * W and x.shape[1] >= C,
+              "conv3d_im2col x")
+        ldx = x.stride(0)
+    k, s, p = ((ctypes.c_int * 3)(*v) for v in (kernel, stride, pad))
+    _lib.call("vc_conv3d_im2col", _p(x), ldx, CONV_IN[kind], B, T, H, W, C, ctypes.addressof(k), ctypes.addressof(s),
+              ctypes.addressof(p), _p(out), out.stride(0), _stream(x))
+    return out
+
+
+def maxpool3d(x: torch.Tensor, B: int, grid, C: int, kernel, stride, pad, out: torch.Tensor) -> torch.Tensor:
+    import ctypes
+    _dev(x, out)
+    To, Ho, Wo = conv_out_size(grid, kernel, stride, pad)
+    T, H, W = grid
+    _need(x.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and x.shape[0] >= B * T * H * W and
+          out.shape[0] >= B * To * Ho * Wo and x.shape[1] >= C and out.shape[1] >= C, "maxpool3d shapes")
+    k, s, p = ((ctypes.c_int * 3)(*v) for v in (kernel, stride, pad))
+    _lib.call("vc_maxpool3d", _p(x), x.stride(0), B, T, H, W, C, ctypes.addressof(k), ctypes.addressof(s),
+              ctypes.addressof(p), _p(out), out.stride(0), _stream(x))
+    return out
+
+
+def avgpool_head(x: torch.Tensor, B: int, grid, C: int, pool_kernel, wc: torch.Tensor, bc: torch.Tensor,
+                 work: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+    import ctypes
+    _dev(x, wc, bc, work, out)
+    T, H, W = grid
+    nl = wc.shape[0]
+    _need(x.dtype == torch.bfloat16 and x.shape[0] >= B * T * H * W and x.shape[1] >= C, "avgpool_head x")
+    _need(wc.dtype == torch.float32 and wc.is_contiguous() and wc.shape[1] == C and work.numel() >= B * C and
+          out.shape == (B, nl), "avgpool_head shapes")
+    pk = (ctypes.c_int * 3)(*pool_kernel)
+    _lib.call("vc_avgpool_head", _p(x), x.stride(0), B, T, H, W, C, ctypes.addressof(pk), _p(wc), _p(bc), nl,
+              _p(work), _p(out), _stream(x))
     return out

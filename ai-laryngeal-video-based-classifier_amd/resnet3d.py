@@ -1,0 +1,237 @@
+"""3D ResNet-50 (pytorchvideo `create_resnet` as the reference configures it) on the
+libvclip.so kernels — drop-in for `create_model(logger)` of
+resnet50-3d-video/video_classifier/models/resnet3d.py:4-48, called as
+`model(f32[B, 3, T, H, W])` -> `f32[B, 2]` (resnet50-3d-video trainer / inference.py:399).
+
+Every Conv3d + BatchNorm(eval) [+ ReLU] [+ residual] is one GEMM: BN is folded into the
+weights and bias in fp32 before the bf16 cast, ReLU and the bottleneck's skip add are GEMM
+epilogues; 1x1x1 stride-1 convolutions read the activations directly, the others go through
+vc_conv3d_im2col.  Activations are channels-last bf16 rows ((b*T + t)*H + h)*W + w; rows are
+padded to a multiple of 256 and output channels to a multiple of 128 (zero weights, so the
+padding columns are exactly 0).  The head (AvgPool3d (4,7,7) stride 1 -> Linear ->
+global average) is one position-weighted pooling + GEMV (the Linear commutes with both means).
+
+Parity unpinned against pytorchvideo itself (not installed here): checked against
+oracle/resnet3d_ref.py, the restatement of pytorchvideo's create_resnet.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import ops
+from .weights import resnet3d_param_shapes
+
+RESNET3D_50 = dict(depths=(3, 4, 6, 3), stem_dim=64, conv_a_kernels=((1, 1, 1), (1, 1, 1), (3, 1, 1), (3, 1, 1)),
+                   spatial_strides=(1, 2, 2, 2), head_pool=(4, 7, 7), num_classes=2, bn_eps=1e-5)
+
+
+def _ru(x, m):
+    return (x + m - 1) // m * m
+
+
+class ResNet3d(torch.nn.Module):
+    """fp32 master parameters + BatchNorm running statistics in pytorchvideo naming."""
+
+    def __init__(self, cfg: dict = RESNET3D_50):
+        super().__init__()
+        self.cfg = dict(cfg)
+        shapes = resnet3d_param_shapes(self.cfg)
+        self._names = list(shapes.keys())
+        self.params = torch.nn.ParameterDict()
+        for n, s in shapes.items():
+            self.params[n.replace(".", "__")] = torch.nn.Parameter(torch.zeros(s), requires_grad=False)
+        self._packed = None
+        self._ws = {}
+
+    def state_dict(self, *a, **k):
+        return OrderedDict((n, self.params[n.replace(".", "__")].detach()) for n in self._names)
+
+    def load_state_dict(self, sd, strict: bool = True):
+        sd = {k[len("module."):] if k.startswith("module.") else k: v for k, v in sd.items()}
+        sd = {k: v for k, v in sd.items() if not k.endswith("num_batches_tracked")}
+        missing = [n for n in self._names if n not in sd]
+        unexpected = [k for k in sd if k not in self._names]
+        if strict and (missing or unexpected):
+            raise KeyError(f"load_state_dict: missing={missing[:5]} unexpected={unexpected[:5]}")
+        with torch.no_grad():
+            for n in self._names:
+                if n in sd:
+                    v = sd[n]
+                    v = torch.as_tensor(np.asarray(v)) if not isinstance(v, torch.Tensor) else v
+                    dst = self.params[n.replace(".", "__")]
+                    dst.copy_(v.reshape(dst.shape))
+        self._packed = None
+        return missing, unexpected
+
+    # ---- packing: BN folded, weights [N_pad, K] bf16 in the im2col column order --------
+    def _pack(self, device):
+        if self._packed is not None and self._packed["device"] == device:
+            return self._packed
+        c = self.cfg
+        eps = c["bn_eps"]
+        P = lambda n: self.params[n.replace(".", "__")].detach().to(device=device, dtype=torch.float64)  # noqa: E731
+
+        def fold(conv, bn, channels_last=True, k_pad=None):
+            w = P(conv + ".weight")
+            sc = P(bn + ".weight") / torch.sqrt(P(bn + ".running_var") + eps)
+            b = P(bn + ".bias") - P(bn + ".running_mean") * sc
+            w = w * sc.view(-1, 1, 1, 1, 1)
+            w = (w.permute(0, 2, 3, 4, 1) if channels_last else w).reshape(w.shape[0], -1)
+            n_p = _ru(w.shape[0], 128)
+            k = w.shape[1] if k_pad is None else k_pad
+            W = torch.zeros((n_p, k), dtype=torch.float64, device=device)
+            W[:w.shape[0], :w.shape[1]] = w
+            B = torch.zeros(n_p, dtype=torch.float64, device=device)
+            B[:b.numel()] = b
+            return W.to(torch.bfloat16).contiguous(), B.float().contiguous()
+
+        pk = {"device": device}
+        pk["stem"] = fold("blocks.0.conv", "blocks.0.norm", channels_last=False, k_pad=_ru(3 * 3 * 7 * 7, 64))
+        stages = []
+        din, dout = c["stem_dim"], c["stem_dim"] * 4
+        for s, depth in enumerate(c["depths"]):
+            blocks = []
+            for i in range(depth):
+                p = f"blocks.{s + 1}.res_blocks.{i}."
+                blk = {}
+                if p + "branch1_conv.weight" in self._names:
+                    blk["b1"] = fold(p + "branch1_conv", p + "branch1_norm")
+                blk["a"] = fold(p + "branch2.conv_a", p + "branch2.norm_a")
+                blk["b"] = fold(p + "branch2.conv_b", p + "branch2.norm_b")
+                blk["c"] = fold(p + "branch2.conv_c", p + "branch2.norm_c")
+                blocks.append(blk)
+            stages.append(dict(blocks=blocks, din=din, dout=dout, inner=dout // 4))
+            din, dout = dout, dout * 2
+        pk["stages"] = stages
+        pk["w_head"] = self.params["blocks__5__proj__weight"].detach().to(device).float().contiguous()
+        pk["b_head"] = self.params["blocks__5__proj__bias"].detach().to(device).float().contiguous()
+        self._packed = pk
+        return pk
+
+    # ---- geometry / workspace ---------------------------------------------------------
+    def geometry(self, T, H, W):
+        c = self.cfg
+        stem = ops.conv_out_size((T, H, W), (3, 7, 7), (1, 2, 2), (1, 3, 3))
+        g = [ops.conv_out_size(stem, (1, 3, 3), (1, 2, 2), (0, 1, 1))]
+        for s in range(1, len(c["depths"])):
+            st = c["spatial_strides"][s]
+            g.append(ops.conv_out_size(g[-1], (1, 3, 3), (1, st, st), (0, 1, 1)))
+        return stem, g
+
+    def _workspace(self, B, T, H, W, device):
+        key = (B, T, H, W, str(device))
+        if key in self._ws:
+            return self._ws[key]
+        c = self.cfg
+        stem, grids = self.geometry(T, H, W)
+        bf = torch.bfloat16
+        rows = lambda g: _ru(B * g[0] * g[1] * g[2], 256)  # noqa: E731
+        z = lambda r, cols: torch.zeros((r, cols), dtype=bf, device=device)  # noqa: E731
+        ws = {"stem_out": z(rows(stem), 128)}
+        # im2col scratch: the largest M x K of any convolution
+        big = rows(stem) * _ru(3 * 3 * 7 * 7, 64)
+        din, dout = c["stem_dim"], c["stem_dim"] * 4
+        g_in = grids[0]
+        acts = []
+        for s, depth in enumerate(c["depths"]):
+            g = grids[s]
+            inner = dout // 4
+            ka = c["conv_a_kernels"][s]
+            big = max(big, rows(g_in) * ka[0] * ka[1] * ka[2] * max(din, dout), rows(g) * 9 * inner,
+                      rows(g) * din)
+            acts.append(dict(x=z(rows(g), dout), x2=z(rows(g), dout), sc=z(rows(g), dout),
+                             a=z(rows(g_in) if g_in != g else rows(g), _ru(inner, 128)), b=z(rows(g), _ru(inner, 128))))
+            g_in = g
+            din, dout = dout, dout * 2
+        ws["x0"] = z(rows(grids[0]), c["stem_dim"])
+        ws["acts"] = acts
+        ws["col"] = torch.zeros(big, dtype=bf, device=device)
+        ws["head_work"] = torch.zeros(B * 2048, dtype=torch.float32, device=device)
+        ws["logits"] = torch.zeros((B, c["num_classes"]), dtype=torch.float32, device=device)
+        self._ws = {key: ws}
+        return ws
+
+    # ---- forward -----------------------------------------------------------------------
+    @torch.no_grad()
+    def forward(self, video: torch.Tensor) -> torch.Tensor:
+        if video.device.type != "cuda":
+            raise RuntimeError("ResNet3d (vclip_amd) runs on the GPU only: move the clip batch to cuda")
+        x = video.contiguous().float() if video.dtype != torch.float32 else video.contiguous()
+        return self.forward_logits(x)
+
+    def forward_logits(self, video: torch.Tensor) -> torch.Tensor:
+        c = self.cfg
+        B, C, T, H, W = video.shape
+        if C != 3:
+            raise ValueError("video must be [B, 3, T, H, W]")
+        pk = self._pack(video.device)
+        ws = self._workspace(B, T, H, W, video.device)
+        stem, grids = self.geometry(T, H, W)
+        rows = lambda g: _ru(B * g[0] * g[1] * g[2], 256)  # noqa: E731
+
+        def col(m, k):
+            return ws["col"][: m * k].view(m, k)
+
+        # stem: conv (3,7,7)/(1,2,2) + BN + ReLU, then MaxPool (1,3,3)/(1,2,2)
+        Kst = pk["stem"][0].shape[1]
+        A = col(rows(stem), Kst)
+        ops.conv3d_im2col(video, "ncthw_f32", B, (T, H, W), 3, (3, 7, 7), (1, 2, 2), (1, 3, 3), A)
+        ops.gemm(A, pk["stem"][0], pk["stem"][1], "bias_relu", ws["stem_out"])
+        x = ws["x0"]
+        ops.maxpool3d(ws["stem_out"], B, stem, c["stem_dim"], (1, 3, 3), (1, 2, 2), (0, 1, 1), x)
+        g_in, cin = grids[0], c["stem_dim"]
+        for s, (st, act) in enumerate(zip(pk["stages"], ws["acts"])):
+            g = grids[s]
+            ss = c["spatial_strides"][s]
+            ka = c["conv_a_kernels"][s]
+            inner, dout = st["inner"], st["dout"]
+            for i, blk in enumerate(st["blocks"]):
+                stride = (1, ss, ss) if i == 0 else (1, 1, 1)
+                gi = g_in if i == 0 else g
+                xin = x
+                # branch1: 1x1x1 conv (+ stride) + BN, or the identity
+                if "b1" in blk:
+                    if stride == (1, 1, 1):
+                        ops.gemm(xin, blk["b1"][0], blk["b1"][1], "bias", act["sc"], m=rows(g))
+                    else:
+                        A = col(rows(g), cin)
+                        ops.conv3d_im2col(xin, "cl_bf16", B, gi, cin, (1, 1, 1), stride, (0, 0, 0), A)
+                        ops.gemm(A, blk["b1"][0], blk["b1"][1], "bias", act["sc"])
+                    skip = act["sc"]
+                else:
+                    skip = xin
+                # conv_a (+ BN + ReLU) at the block's input resolution
+                if tuple(ka) == (1, 1, 1):
+                    ops.gemm(xin, blk["a"][0], blk["a"][1], "bias_relu", act["a"], m=rows(gi))
+                else:
+                    A = col(rows(gi), ka[0] * cin)
+                    ops.conv3d_im2col(xin, "cl_bf16", B, gi, cin, ka, (1, 1, 1), tuple(k // 2 for k in ka), A)
+                    ops.gemm(A, blk["a"][0], blk["a"][1], "bias_relu", act["a"])
+                # conv_b (1,3,3) with the stage stride (+ BN + ReLU)
+                A = col(rows(g), 9 * inner)
+                ops.conv3d_im2col(act["a"], "cl_bf16", B, gi, inner, (1, 3, 3), stride, (0, 1, 1), A)
+                ops.gemm(A, blk["b"][0], blk["b"][1], "bias_relu", act["b"])
+                # conv_c 1x1x1 + BN + skip + ReLU
+                out = act["x"] if xin is not act["x"] else act["x2"]
+                ops.gemm(act["b"][:, :inner], blk["c"][0], blk["c"][1], "bias_resid_relu", out, aux=skip)
+                x, cin = out, dout
+            g_in = g
+        t, h, w = grids[-1]
+        return ops.avgpool_head(x, B, (t, h, w), cin, c["head_pool"], pk["w_head"], pk["b_head"], ws["head_work"],
+                                ws["logits"])
+
+
+def create_model(logger=None, device="cuda", weights_seed: int = 0):
+    """Drop-in for resnet50-3d-video/video_classifier/models/resnet3d.py:4-48 (random init there
+    too: `create_resnet` without pretrained weights; here seeded synthetic weights)."""
+    if logger:
+        logger.info("Creating 3D ResNet-50 model...")
+    model = ResNet3d(RESNET3D_50)
+    from .weights import make_resnet3d_weights
+    model.load_state_dict(make_resnet3d_weights(RESNET3D_50, seed=weights_seed))
+    if logger:
+        logger.info("Model created successfully")
+    return model.to(device) if device else model

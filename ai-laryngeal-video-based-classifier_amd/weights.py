@@ -169,6 +169,64 @@ def make_swin3d_weights(cfg: dict, seed: int = 0, std: float = 0.02) -> "Ordered
     return out
 
 
+def resnet3d_param_shapes(cfg: dict) -> "OrderedDict[str, tuple]":
+    """Parameter / BatchNorm-buffer names and shapes of pytorchvideo `create_resnet` as the
+    reference configures it (resnet50-3d-video/video_classifier/models/resnet3d.py:8-45)."""
+    s = OrderedDict()
+
+    def bn(pre, c):
+        for k in ("weight", "bias", "running_mean", "running_var"):
+            s[f"{pre}.{k}"] = (c,)
+
+    d0 = cfg["stem_dim"]
+    s["blocks.0.conv.weight"] = (d0, 3, 3, 7, 7)
+    bn("blocks.0.norm", d0)
+    din, dout = d0, d0 * 4
+    for st, depth in enumerate(cfg["depths"]):
+        inner = dout // 4
+        ka = cfg["conv_a_kernels"][st]
+        for i in range(depth):
+            p = f"blocks.{st + 1}.res_blocks.{i}."
+            cin = din if i == 0 else dout
+            if i == 0 and (cin != dout or cfg["spatial_strides"][st] != 1):
+                s[p + "branch1_conv.weight"] = (dout, cin, 1, 1, 1)
+                bn(p + "branch1_norm", dout)
+            s[p + "branch2.conv_a.weight"] = (inner, cin) + tuple(ka)
+            bn(p + "branch2.norm_a", inner)
+            s[p + "branch2.conv_b.weight"] = (inner, inner, 1, 3, 3)
+            bn(p + "branch2.norm_b", inner)
+            s[p + "branch2.conv_c.weight"] = (dout, inner, 1, 1, 1)
+            bn(p + "branch2.norm_c", dout)
+        din, dout = dout, dout * 2
+    s["blocks.5.proj.weight"] = (cfg.get("num_classes", 2), din)
+    s["blocks.5.proj.bias"] = (cfg.get("num_classes", 2),)
+    return s
+
+
+def make_resnet3d_weights(cfg: dict, seed: int = 0) -> "OrderedDict[str, np.ndarray]":
+    """Convs ~ N(0, 2/fan_in) (He), BN gamma = 1 + N(0, .02), beta / running_mean ~ N(0, .02),
+    running_var = 1 + |N(0, .02)|; the last BN of every residual branch gets gamma scaled by
+    0.2 so the 16-block residual stream stays O(1) with random weights."""
+    rng = np.random.RandomState(seed)
+    out = OrderedDict()
+    for name, shape in resnet3d_param_shapes(cfg).items():
+        if name.endswith("conv.weight") or name.endswith("conv_a.weight") or name.endswith("conv_b.weight") or \
+                name.endswith("conv_c.weight"):
+            fan_in = int(np.prod(shape[1:]))
+            w = rng.standard_normal(shape) * np.sqrt(2.0 / fan_in)
+        elif name.endswith("running_var"):
+            w = 1.0 + np.abs(rng.standard_normal(shape) * 0.02)
+        elif name.endswith("norm.weight") or name.endswith("norm_a.weight") or name.endswith("norm_b.weight") or \
+                name.endswith("norm_c.weight"):
+            w = 1.0 + rng.standard_normal(shape) * 0.02
+            if name.endswith("norm_c.weight"):
+                w = w * 0.2
+        else:
+            w = rng.standard_normal(shape) * 0.02
+        out[name] = np.ascontiguousarray(w.astype(np.float32))
+    return out
+
+
 def make_synthetic_video(batch: int, num_frames: int, image_size: int, seed: int = 1) -> np.ndarray:
     """[B, 3, T, H, W] f32 (the torchvision video-model input layout, swin trainer.py:116):
     the uint8 frames of make_synthetic_frames through the Swin/ResNet3D transform's

@@ -87,6 +87,9 @@ int vc_patch_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C, 
 #define VC_EPI_EMBED_F32        4  /* out f32 [r(m)][n] = acc + bias[n] + aux[m % G][n],
                                        r(m) = (m / G) * group_stride + group_offset (tubelet -> tokens) */
 #define VC_EPI_BIAS_F32         5  /* out f32 [m][n]  = acc + bias[n]             (Swin embed / merge)  */
+#define VC_EPI_BIAS_RELU_BF16   6  /* out bf16[m][n]  = relu(acc + bias[n])       (conv + BN + ReLU)    */
+#define VC_EPI_BIAS_RESID_RELU_BF16 7 /* out bf16[m][n] = relu(acc + bias[n] + res[m][n]), res = (const
+                                       uint16_t*)aux bf16 with row stride ldaux (bottleneck conv_c + skip) */
 
 /*
  * C[M][N] = A[M][K] . W[N][K]^T  (bf16 inputs, fp32 accumulate on MFMA), fused epilogue.
@@ -183,6 +186,33 @@ int vc_temporal_attention(const uint16_t* qkv, int64_t ld, int64_t B, int64_t P,
 int vc_divided_add_layernorm(float* x, int64_t ldx, const uint16_t* y, int64_t ldy, int64_t B, int64_t P, int64_t T,
                              int64_t D, const float* gamma, const float* beta, float eps, int mode, uint16_t* h,
                              int64_t ldh, hipStream_t stream);
+
+/* ---- 3D convolutions (ResNet3D-50, pytorchvideo create_resnet) ------------
+ * A Conv3d is vc_conv3d_im2col + vc_gemm_bf16 with the BatchNorm folded into W / bias and ReLU
+ * (+ the residual) in the epilogue.  Channels-last activations: rows ((b*T + t)*H + h)*W + w. */
+#define VC_CONV_IN_NCTHW_F32 0  /* the f32 [B][C][T][H][W] clip (stem); columns (c, kt, kh, kw)      */
+#define VC_CONV_IN_CL_BF16   1  /* channels-last bf16 rows (ld = ldx), C % 8 == 0; columns (kt, kh, kw, c) */
+/*
+ * A[m][col] for output position m = ((b*To + to)*Ho + ho)*Wo + wo, zero padding, with
+ * To = (T + 2p_t - k_t)/s_t + 1 (etc.); kernel/stride/pad are int[3] host arrays (t, h, w).
+ * Replaces the input side of torch.nn.Conv3d in pytorchvideo's stem / bottleneck blocks.
+ */
+int vc_conv3d_im2col(const void* x, int64_t ldx, int input_kind, int64_t B, int64_t T, int64_t H, int64_t W,
+                     int64_t C, const int* kernel, const int* stride, const int* pad, uint16_t* A, int64_t lda,
+                     hipStream_t stream);
+
+/* MaxPool3d on channels-last bf16 (padding counts as -inf): pytorchvideo's stem pool. */
+int vc_maxpool3d(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_t H, int64_t W, int64_t C,
+                 const int* kernel, const int* stride, const int* pad, uint16_t* y, int64_t ldy, hipStream_t stream);
+
+/*
+ * ResNetBasicHead (AvgPool3d(pool_kernel, stride 1) -> Linear -> AdaptiveAvgPool3d(1)) on
+ * channels-last bf16 x: logits[b] = Wc . pooled[b] + bc, pooled = the position-weighted mean
+ * (the Linear commutes with both averages).  work: caller scratch f32 [B * C].
+ */
+int vc_avgpool_head(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_t H, int64_t W, int64_t C,
+                    const int* pool_kernel, const float* Wc, const float* bc, int64_t num_labels, float* work,
+                    float* logits, hipStream_t stream);
 
 /* ---- Video Swin 3D (torchvision swin3d_t) -------------------------------
  * Token layout: rows ((b*T + t)*H + h)*W + w (channels-last [B][T][H][W][C]). */

@@ -1,0 +1,115 @@
+"""3D ResNet-50 on the GPU: conv pieces bit-exact vs torch, end to end vs
+oracle/resnet3d_ref.py (fp32 CPU restatement of pytorchvideo create_resnet; pytorchvideo is
+not installed, so parity with the library is UNPINNED — SURVEY.md §8c).  bf16 activations
+through 16 residual blocks: logits compared at 1e-2 relative to their magnitude (north_star
+bf16 tolerance is 1e-2 absolute on O(1) logits; these random-weight logits are O(5))."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import resnet3d_ref as ref
+from vclip_amd.weights import make_resnet3d_weights, make_synthetic_video
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vclip_amd import _lib
+    _lib.load()
+
+
+def ops():
+    from vclip_amd import ops as O
+    return O
+
+
+def _unfold_ref(x, kernel, stride, pad):
+    """x [B,C,T,H,W] -> [B*To*Ho*Wo, C*kvol] with columns (c, kt, kh, kw) (nn.Conv3d weight order)."""
+    xp = torch.nn.functional.pad(x, (pad[2], pad[2], pad[1], pad[1], pad[0], pad[0]))
+    u = xp.unfold(2, kernel[0], stride[0]).unfold(3, kernel[1], stride[1]).unfold(4, kernel[2], stride[2])
+    B, C, To, Ho, Wo = u.shape[:5]
+    return u.permute(0, 2, 3, 4, 1, 5, 6, 7).reshape(B * To * Ho * Wo, C * kernel[0] * kernel[1] * kernel[2]), (To, Ho, Wo)
+
+
+@pytest.mark.parametrize("kernel,stride,pad", [((3, 7, 7), (1, 2, 2), (1, 3, 3)), ((1, 3, 3), (1, 2, 2), (0, 1, 1))])
+def test_im2col_ncthw_bit_exact(kernel, stride, pad):
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(2, 3, 5, 30, 26, generator=g)
+    want, (To, Ho, Wo) = _unfold_ref(x, kernel, stride, pad)
+    K = want.shape[1]
+    out = torch.zeros(want.shape[0] + 7, K + 5, dtype=torch.bfloat16, device=DEV)
+    ops().conv3d_im2col(x.to(DEV), "ncthw_f32", 2, (5, 30, 26), 3, kernel, stride, pad, out)
+    assert torch.equal(out[:want.shape[0], :K].cpu(), want.bfloat16())
+
+
+@pytest.mark.parametrize("kernel,stride,pad,C", [((1, 3, 3), (1, 2, 2), (0, 1, 1), 64), ((3, 1, 1), (1, 1, 1), (1, 0, 0), 16),
+                                                  ((1, 1, 1), (1, 2, 2), (0, 0, 0), 24)])
+def test_im2col_channels_last_bit_exact(kernel, stride, pad, C):
+    g = torch.Generator().manual_seed(C)
+    B, T, H, W = 2, 4, 9, 11
+    x = torch.randn(B, C, T, H, W, generator=g).bfloat16()
+    cl = x.permute(0, 2, 3, 4, 1).reshape(B * T * H * W, C)
+    ld = C + 8
+    xd = torch.zeros(B * T * H * W, ld, dtype=torch.bfloat16)
+    xd[:, :C] = cl
+    want, _ = _unfold_ref(x.float(), kernel, stride, pad)  # columns (c, taps)
+    kv = kernel[0] * kernel[1] * kernel[2]
+    want = want.view(-1, C, kv).transpose(1, 2).reshape(-1, kv * C)  # -> (taps, c)
+    out = torch.zeros(want.shape[0], kv * C, dtype=torch.bfloat16, device=DEV)
+    ops().conv3d_im2col(xd.to(DEV), "cl_bf16", B, (T, H, W), C, kernel, stride, pad, out)
+    assert torch.equal(out.cpu(), want.bfloat16())
+
+
+def test_maxpool3d():
+    g = torch.Generator().manual_seed(2)
+    B, C, T, H, W = 2, 16, 3, 13, 12
+    x = torch.randn(B, C, T, H, W, generator=g).bfloat16()
+    want = torch.nn.functional.max_pool3d(x.float(), (1, 3, 3), (1, 2, 2), (0, 1, 1))
+    To, Ho, Wo = want.shape[2:]
+    out = torch.zeros(B * To * Ho * Wo, C, dtype=torch.bfloat16, device=DEV)
+    ops().maxpool3d(x.permute(0, 2, 3, 4, 1).reshape(-1, C).contiguous().to(DEV), B, (T, H, W), C, (1, 3, 3), (1, 2, 2),
+                    (0, 1, 1), out)
+    assert torch.equal(out.cpu(), want.permute(0, 2, 3, 4, 1).reshape(-1, C).bfloat16())
+
+
+def test_avgpool_head():
+    g = torch.Generator().manual_seed(3)
+    B, C, T, H, W = 2, 256, 9, 7, 7
+    x = torch.randn(B, C, T, H, W, generator=g).bfloat16().float()
+    wc, bc = torch.randn(2, C, generator=g) * 0.05, torch.randn(2, generator=g)
+    pooled = torch.nn.functional.avg_pool3d(x, (4, 7, 7), stride=1)
+    want = (pooled.permute(0, 2, 3, 4, 1) @ wc.T + bc).mean(dim=(1, 2, 3))
+    out = torch.zeros(B, 2, device=DEV)
+    ops().avgpool_head(x.permute(0, 2, 3, 4, 1).reshape(-1, C).bfloat16().contiguous().to(DEV), B, (T, H, W), C,
+                       (4, 7, 7), wc.to(DEV), bc.to(DEV), torch.zeros(B * C, device=DEV), out)
+    assert torch.allclose(out.cpu(), want, atol=1e-4)
+
+
+def _model():
+    from vclip_amd.resnet3d import ResNet3d
+    m = ResNet3d(ref.RESNET3D_50)
+    m.load_state_dict(make_resnet3d_weights(ref.RESNET3D_50, seed=0))
+    return m.to(DEV)
+
+
+@pytest.mark.parametrize("T,B", [(8, 2), (32, 1)])
+def test_resnet3d_logits(T, B):
+    video = make_synthetic_video(B, T, 224, seed=2)
+    sd = {k: torch.from_numpy(v) for k, v in make_resnet3d_weights(ref.RESNET3D_50, seed=0).items()}
+    with torch.no_grad():
+        want = ref.resnet3d_forward(sd, ref.RESNET3D_50, torch.from_numpy(video)).numpy()
+    got = _model()(torch.from_numpy(video).to(DEV)).cpu().numpy()
+    err = np.abs(got - want).max()
+    assert err < 1e-2 * max(1.0, np.abs(want).max()), (err, got, want)
+
+
+def test_resnet3d_batch_invariance():
+    video = torch.from_numpy(make_synthetic_video(3, 8, 224, seed=4)).to(DEV)
+    m = _model()
+    full = m(video).clone()
+    one = m(video[1:2].contiguous()).clone()
+    assert torch.equal(full[1:2], one)

@@ -17,7 +17,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-GFLOP = {"vivit": 903.05, "timesformer": 391.66, "swin3d_t": 175.53}
+GFLOP = {"vivit": 903.05, "timesformer": 391.66, "swin3d_t": 175.53, "resnet3d_50": 349.03}
 
 
 def build(name, batch, dev):
@@ -26,6 +26,11 @@ def build(name, batch, dev):
         from vclip_amd.swin3d import create_model
         from vclip_amd.weights import make_synthetic_video
         m = create_model(model_size="tiny", device=dev)
+        return m, torch.from_numpy(make_synthetic_video(batch, 32, 224, seed=1)).to(dev)
+    if name == "resnet3d_50":
+        from vclip_amd.resnet3d import create_model
+        from vclip_amd.weights import make_synthetic_video
+        m = create_model(device=dev)
         return m, torch.from_numpy(make_synthetic_video(batch, 32, 224, seed=1)).to(dev)
     if name == "vivit":
         from vclip_amd.vivit import create_model
