@@ -8,8 +8,8 @@ namespace vc {
 
 // ---------------------------------------------------------------------------------
 // im2col from the f32 [B][C][T][H][W] clip (the model input; C is small, e.g. the stem's 3):
-// A[m][(c, kt, kh, kw)] (PyTorch Conv3d weight order), zero padding.  One thread per
-// (output position, c, kt, kh) writes the kw values of one kernel row.
+// A[m][(c, kt, kh, kw)] (PyTorch Conv3d weight order), zero padding, columns zero-filled up
+// to the next multiple of 8 (the GEMM's K padding).
 // ---------------------------------------------------------------------------------
 struct Conv3dGeom {
     int T, H, W, C;         // input
@@ -19,29 +19,51 @@ struct Conv3dGeom {
     int pt, ph, pw;
 };
 
-__global__ void __launch_bounds__(256) im2col_ncthw_kernel(const float* __restrict__ x, int64_t total, Conv3dGeom g,
-                                                           uint16_t* __restrict__ A, int64_t lda) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= total) return;
-    int64_t r = i;
-    const int ih = r % g.kh;
-    r /= g.kh;
-    const int it = r % g.kt;
-    r /= g.kt;
-    const int c = r % g.C;
-    r /= g.C;
-    const int64_t m = r;  // output position (b, to, ho, wo)
+// A workgroup owns 64 consecutive output positions (one per lane, so a load instruction reads
+// 64 neighbouring output pixels of one input row: coalesced) and all column chunks of their
+// rows (the 4 waves stride over the chunks, so every line of those rows is completed by one
+// workgroup).  The column -> (c, kt, kh, kw) decomposition comes from an LDS table.
+__global__ void __launch_bounds__(256) im2col_ncthw_kernel(const float* __restrict__ x, int64_t M, int nchunk, Conv3dGeom g,
+                                                           int K, uint16_t* __restrict__ A, int64_t lda) {
+    __shared__ unsigned tab[2048];  // c | it << 8 | ih << 16 | iw << 24
+    for (int k = threadIdx.x; k < nchunk * 8; k += 256) {
+        unsigned v = 0xffffffffu;
+        if (k < K) {
+            const int iw = k % g.kw, ih = (k / g.kw) % g.kh, it = (k / (g.kw * g.kh)) % g.kt, c = k / (g.kw * g.kh * g.kt);
+            v = (unsigned)c | ((unsigned)it << 8) | ((unsigned)ih << 16) | ((unsigned)iw << 24);
+        }
+        tab[k] = v;
+    }
+    __syncthreads();
+    const int64_t m = (int64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    if (m >= M) return;
+    const int wave = threadIdx.x >> 6;
     const int wo = m % g.Wo;
     const int ho = (m / g.Wo) % g.Ho;
     const int to = (m / ((int64_t)g.Wo * g.Ho)) % g.To;
     const int64_t b = m / ((int64_t)g.Wo * g.Ho * g.To);
-    const int t = to * g.st - g.pt + it, y = ho * g.sh - g.ph + ih;
-    uint16_t* dst = A + m * lda + ((int64_t)(c * g.kt + it) * g.kh + ih) * g.kw;
-    const bool rowok = t >= 0 && t < g.T && y >= 0 && y < g.H;
-    const float* src = x + (((b * g.C + c) * g.T + t) * g.H + y) * (int64_t)g.W;
-    for (int iw = 0; iw < g.kw; ++iw) {
-        const int xx = wo * g.sw - g.pw + iw;
-        dst[iw] = (rowok && xx >= 0 && xx < g.W) ? f2bf(src[xx]) : (uint16_t)0;
+    const int t0 = to * g.st - g.pt, y0 = ho * g.sh - g.ph, x0 = wo * g.sw - g.pw;
+    const float* xb = x + b * g.C * (int64_t)g.T * g.H * g.W;
+    uint16_t* arow = A + m * lda;
+    for (int kc = wave; kc < nchunk; kc += 4) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const unsigned tv = tab[kc * 8 + e];
+            float val = 0.f;
+            if (tv != 0xffffffffu) {
+                const int c = tv & 255, t = t0 + ((tv >> 8) & 255), y = y0 + ((tv >> 16) & 255), xx = x0 + (tv >> 24);
+                if (t >= 0 && t < g.T && y >= 0 && y < g.H && xx >= 0 && xx < g.W)
+                    val = xb[(((int64_t)c * g.T + t) * g.H + y) * g.W + xx];
+            }
+            v[e] = val;
+        }
+        uint4 o;
+        o.x = pack2bf(v[0], v[1]);
+        o.y = pack2bf(v[2], v[3]);
+        o.z = pack2bf(v[4], v[5]);
+        o.w = pack2bf(v[6], v[7]);
+        *reinterpret_cast<uint4*>(arow + kc * 8) = o;
     }
 }
 
@@ -124,21 +146,31 @@ __device__ __forceinline__ float pool_w(int i, int D, int k) {
     return (float)(hi - lo + 1) / (float)(nwin * k);
 }
 
+constexpr int HEAD_CHUNKS = 32;
+
+// stage 1: grid (B, C/256, HEAD_CHUNKS): each thread a channel, a strided share of positions
 __global__ void __launch_bounds__(256) head_pool_kernel(const uint16_t* __restrict__ x, int64_t ldx, int T, int H, int W,
-                                                        int C, int kt, int kh, int kw, float* __restrict__ pooled) {
+                                                        int C, int kt, int kh, int kw, float* __restrict__ part) {
+    const int b = blockIdx.x;
+    const int c = blockIdx.y * 256 + threadIdx.x;
+    const int ch = blockIdx.z;
+    if (c >= C) return;
+    const int npos = T * H * W;
+    float s = 0.f;
+    for (int pos = ch; pos < npos; pos += HEAD_CHUNKS) {
+        const int xx = pos % W, y = (pos / W) % H, t = pos / (W * H);
+        s += pool_w(t, T, kt) * pool_w(y, H, kh) * pool_w(xx, W, kw) * bf2f(x[((int64_t)b * npos + pos) * ldx + c]);
+    }
+    part[((int64_t)b * HEAD_CHUNKS + ch) * C + c] = s;
+}
+
+// stage 2: sum the chunks in order (deterministic) -> pooled
+__global__ void __launch_bounds__(256) head_reduce_kernel(const float* __restrict__ part, int C, float* __restrict__ pooled) {
     const int b = blockIdx.x;
     const int c = blockIdx.y * 256 + threadIdx.x;
     if (c >= C) return;
     float s = 0.f;
-    for (int t = 0; t < T; ++t) {
-        const float wt_ = pool_w(t, T, kt);
-        for (int y = 0; y < H; ++y) {
-            const float wty = wt_ * pool_w(y, H, kh);
-            for (int xx = 0; xx < W; ++xx)
-                s += wty * pool_w(xx, W, kw) *
-                     bf2f(x[((((int64_t)b * T + t) * H + y) * W + xx) * ldx + c]);
-        }
-    }
+    for (int ch = 0; ch < HEAD_CHUNKS; ++ch) s += part[((int64_t)b * HEAD_CHUNKS + ch) * C + c];
     pooled[(int64_t)b * C + c] = s;
 }
 
@@ -190,8 +222,12 @@ int vc_conv3d_im2col(const void* x, int64_t ldx, int input_kind, int64_t B, int6
     if (lda < kvol * C) return fail(VC_ERR_INVALID_ARG, "vc_conv3d_im2col: lda < kernel volume * C");
     const int64_t M = B * g.To * g.Ho * g.Wo;
     if (input_kind == VC_CONV_IN_NCTHW_F32) {
-        const int64_t total = M * C * g.kt * g.kh;
-        im2col_ncthw_kernel<<<(unsigned)((total + 255) / 256), 256, 0, stream>>>((const float*)x, total, g, A, lda);
+        const int K = (int)(kvol * C);
+        const int nchunk = (K + 7) / 8;
+        if (lda < nchunk * 8 || lda % 8 || ((uintptr_t)A & 15) || nchunk * 8 > 2048 || C > 255 || g.kt > 255 ||
+            g.kh > 255 || g.kw > 255)
+            return fail(VC_ERR_INVALID_ARG, "vc_conv3d_im2col: NCTHW input needs lda >= roundup(K, 8) <= 2048, 16-B rows");
+        im2col_ncthw_kernel<<<(unsigned)((M + 63) / 64), 256, 0, stream>>>((const float*)x, M, nchunk, g, K, A, lda);
     } else if (input_kind == VC_CONV_IN_CL_BF16) {
         if (C % 8 || ldx % 8 || lda % 8 || ((uintptr_t)x | (uintptr_t)A) & 15)
             return fail(VC_ERR_INVALID_ARG, "vc_conv3d_im2col: channels-last input needs C % 8 == 0 and 16-B rows");
@@ -221,8 +257,10 @@ int vc_avgpool_head(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_
     if (pool_kernel[0] > T || pool_kernel[1] > H || pool_kernel[2] > W || pool_kernel[0] <= 0 || pool_kernel[1] <= 0 ||
         pool_kernel[2] <= 0)
         return fail(VC_ERR_INVALID_ARG, "vc_avgpool_head: pool kernel larger than the feature map");
-    head_pool_kernel<<<dim3((unsigned)B, (unsigned)((C + 255) / 256)), 256, 0, stream>>>(
-        x, ldx, (int)T, (int)H, (int)W, (int)C, pool_kernel[0], pool_kernel[1], pool_kernel[2], work);
+    float* part = work + B * C;  // work: [B*C] pooled, then [B*HEAD_CHUNKS*C] partials
+    head_pool_kernel<<<dim3((unsigned)B, (unsigned)((C + 255) / 256), HEAD_CHUNKS), 256, 0, stream>>>(
+        x, ldx, (int)T, (int)H, (int)W, (int)C, pool_kernel[0], pool_kernel[1], pool_kernel[2], part);
+    head_reduce_kernel<<<dim3((unsigned)B, (unsigned)((C + 255) / 256)), 256, 0, stream>>>(part, (int)C, work);
     head_gemv_kernel<<<(unsigned)B, 256, 0, stream>>>(work, (int)C, Wc, bc, (int)num_labels, logits);
     return check_launch("vc_avgpool_head");
 }

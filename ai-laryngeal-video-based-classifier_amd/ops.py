@@ -322,7 +322,7 @@ def avgpool_head(x: torch.Tensor, B: int, grid, C: int, pool_kernel, wc: torch.T
     T, H, W = grid
     nl = wc.shape[0]
     _need(x.dtype == torch.bfloat16 and x.shape[0] >= B * T * H * W and x.shape[1] >= C, "avgpool_head x")
-    _need(wc.dtype == torch.float32 and wc.is_contiguous() and wc.shape[1] == C and work.numel() >= B * C and
+    _need(wc.dtype == torch.float32 and wc.is_contiguous() and wc.shape[1] == C and work.numel() >= B * C * 33 and
           out.shape == (B, nl), "avgpool_head shapes")
     pk = (ctypes.c_int * 3)(*pool_kernel)
     _lib.call("vc_avgpool_head", _p(x), x.stride(0), B, T, H, W, C, ctypes.addressof(pk), _p(wc), _p(bc), nl,

@@ -149,7 +149,7 @@ class ResNet3d(torch.nn.Module):
         ws["x0"] = z(rows(grids[0]), c["stem_dim"])
         ws["acts"] = acts
         ws["col"] = torch.zeros(big, dtype=bf, device=device)
-        ws["head_work"] = torch.zeros(B * 2048, dtype=torch.float32, device=device)
+        ws["head_work"] = torch.zeros(B * 2048 * 33, dtype=torch.float32, device=device)
         ws["logits"] = torch.zeros((B, c["num_classes"]), dtype=torch.float32, device=device)
         self._ws = {key: ws}
         return ws

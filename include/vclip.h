@@ -208,7 +208,8 @@ int vc_maxpool3d(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_t H
 /*
  * ResNetBasicHead (AvgPool3d(pool_kernel, stride 1) -> Linear -> AdaptiveAvgPool3d(1)) on
  * channels-last bf16 x: logits[b] = Wc . pooled[b] + bc, pooled = the position-weighted mean
- * (the Linear commutes with both averages).  work: caller scratch f32 [B * C].
+ * (the Linear commutes with both averages).  work: caller scratch f32 [B * C * 33] (pooled + 32
+ * fixed-order partial sums: deterministic).
  */
 int vc_avgpool_head(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_t H, int64_t W, int64_t C,
                     const int* pool_kernel, const float* Wc, const float* bc, int64_t num_labels, float* work,

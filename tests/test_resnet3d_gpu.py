@@ -41,7 +41,7 @@ def test_im2col_ncthw_bit_exact(kernel, stride, pad):
     x = torch.randn(2, 3, 5, 30, 26, generator=g)
     want, (To, Ho, Wo) = _unfold_ref(x, kernel, stride, pad)
     K = want.shape[1]
-    out = torch.zeros(want.shape[0] + 7, K + 5, dtype=torch.bfloat16, device=DEV)
+    out = torch.zeros(want.shape[0] + 7, (K + 7) // 8 * 8 + 8, dtype=torch.bfloat16, device=DEV)
     ops().conv3d_im2col(x.to(DEV), "ncthw_f32", 2, (5, 30, 26), 3, kernel, stride, pad, out)
     assert torch.equal(out[:want.shape[0], :K].cpu(), want.bfloat16())
 
@@ -85,7 +85,7 @@ def test_avgpool_head():
     want = (pooled.permute(0, 2, 3, 4, 1) @ wc.T + bc).mean(dim=(1, 2, 3))
     out = torch.zeros(B, 2, device=DEV)
     ops().avgpool_head(x.permute(0, 2, 3, 4, 1).reshape(-1, C).bfloat16().contiguous().to(DEV), B, (T, H, W), C,
-                       (4, 7, 7), wc.to(DEV), bc.to(DEV), torch.zeros(B * C, device=DEV), out)
+                       (4, 7, 7), wc.to(DEV), bc.to(DEV), torch.zeros(B * C * 33, device=DEV), out)
     assert torch.allclose(out.cpu(), want, atol=1e-4)
 
 
