@@ -46,6 +46,9 @@ SIGNATURES = {
     "vc_conv3d_im2col": ([c_p, c_i64, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p], c_int),
     "vc_maxpool3d": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p], c_int),
     "vc_avgpool_head": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_i64, c_p, c_p, c_p], c_int),
+    "vc_global_avgpool": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p], c_int),
+    "vc_lstm_recurrence": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_i64, c_p, c_p], c_int),
+    "vc_mlp_head": ([c_p, c_i64, c_i64, c_p, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p], c_int),
     "vc_divided_add_layernorm": ([c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_int, c_p,
                                   c_i64, c_p], c_int),
 }

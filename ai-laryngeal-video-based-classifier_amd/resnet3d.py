@@ -25,7 +25,8 @@ from . import ops
 from .weights import resnet3d_param_shapes
 
 RESNET3D_50 = dict(depths=(3, 4, 6, 3), stem_dim=64, conv_a_kernels=((1, 1, 1), (1, 1, 1), (3, 1, 1), (3, 1, 1)),
-                   spatial_strides=(1, 2, 2, 2), head_pool=(4, 7, 7), num_classes=2, bn_eps=1e-5)
+                   spatial_strides=(1, 2, 2, 2), head_pool=(4, 7, 7), num_classes=2, bn_eps=1e-5,
+                   stem_kernel=(3, 7, 7), stem_pad=(1, 3, 3))
 
 
 def _ru(x, m):
@@ -89,7 +90,8 @@ class ResNet3d(torch.nn.Module):
             return W.to(torch.bfloat16).contiguous(), B.float().contiguous()
 
         pk = {"device": device}
-        pk["stem"] = fold("blocks.0.conv", "blocks.0.norm", channels_last=False, k_pad=_ru(3 * 3 * 7 * 7, 64))
+        sk = c.get("stem_kernel", (3, 7, 7))
+        pk["stem"] = fold("blocks.0.conv", "blocks.0.norm", channels_last=False, k_pad=_ru(3 * sk[0] * sk[1] * sk[2], 64))
         stages = []
         din, dout = c["stem_dim"], c["stem_dim"] * 4
         for s, depth in enumerate(c["depths"]):
@@ -106,15 +108,16 @@ class ResNet3d(torch.nn.Module):
             stages.append(dict(blocks=blocks, din=din, dout=dout, inner=dout // 4))
             din, dout = dout, dout * 2
         pk["stages"] = stages
-        pk["w_head"] = self.params["blocks__5__proj__weight"].detach().to(device).float().contiguous()
-        pk["b_head"] = self.params["blocks__5__proj__bias"].detach().to(device).float().contiguous()
+        if "blocks.5.proj.weight" in self._names:
+            pk["w_head"] = self.params["blocks__5__proj__weight"].detach().to(device).float().contiguous()
+            pk["b_head"] = self.params["blocks__5__proj__bias"].detach().to(device).float().contiguous()
         self._packed = pk
         return pk
 
     # ---- geometry / workspace ---------------------------------------------------------
     def geometry(self, T, H, W):
         c = self.cfg
-        stem = ops.conv_out_size((T, H, W), (3, 7, 7), (1, 2, 2), (1, 3, 3))
+        stem = ops.conv_out_size((T, H, W), c.get("stem_kernel", (3, 7, 7)), (1, 2, 2), c.get("stem_pad", (1, 3, 3)))
         g = [ops.conv_out_size(stem, (1, 3, 3), (1, 2, 2), (0, 1, 1))]
         for s in range(1, len(c["depths"])):
             st = c["spatial_strides"][s]
@@ -132,7 +135,8 @@ class ResNet3d(torch.nn.Module):
         z = lambda r, cols: torch.zeros((r, cols), dtype=bf, device=device)  # noqa: E731
         ws = {"stem_out": z(rows(stem), 128)}
         # im2col scratch: the largest M x K of any convolution
-        big = rows(stem) * _ru(3 * 3 * 7 * 7, 64)
+        sk = c.get("stem_kernel", (3, 7, 7))
+        big = rows(stem) * _ru(3 * sk[0] * sk[1] * sk[2], 64)
         din, dout = c["stem_dim"], c["stem_dim"] * 4
         g_in = grids[0]
         acts = []
@@ -149,7 +153,7 @@ class ResNet3d(torch.nn.Module):
         ws["x0"] = z(rows(grids[0]), c["stem_dim"])
         ws["acts"] = acts
         ws["col"] = torch.zeros(big, dtype=bf, device=device)
-        ws["head_work"] = torch.zeros(B * 2048 * 33, dtype=torch.float32, device=device)
+        ws["head_work"] = torch.zeros(B * T * 2048 * 33, dtype=torch.float32, device=device)
         ws["logits"] = torch.zeros((B, c["num_classes"]), dtype=torch.float32, device=device)
         self._ws = {key: ws}
         return ws
@@ -163,6 +167,13 @@ class ResNet3d(torch.nn.Module):
         return self.forward_logits(x)
 
     def forward_logits(self, video: torch.Tensor) -> torch.Tensor:
+        x, B, grid, C, ws = self.forward_features(video)
+        pk = self._packed
+        return ops.avgpool_head(x, B, grid, C, self.cfg["head_pool"], pk["w_head"], pk["b_head"], ws["head_work"],
+                                ws["logits"])
+
+    def forward_features(self, video: torch.Tensor):
+        """Stem + the four stages; returns (last activations [rows, C] bf16, B, (T, H, W), C, workspace)."""
         c = self.cfg
         B, C, T, H, W = video.shape
         if C != 3:
@@ -178,7 +189,8 @@ class ResNet3d(torch.nn.Module):
         # stem: conv (3,7,7)/(1,2,2) + BN + ReLU, then MaxPool (1,3,3)/(1,2,2)
         Kst = pk["stem"][0].shape[1]
         A = col(rows(stem), Kst)
-        ops.conv3d_im2col(video, "ncthw_f32", B, (T, H, W), 3, (3, 7, 7), (1, 2, 2), (1, 3, 3), A)
+        ops.conv3d_im2col(video, "ncthw_f32", B, (T, H, W), 3, c.get("stem_kernel", (3, 7, 7)), (1, 2, 2),
+                          c.get("stem_pad", (1, 3, 3)), A)
         ops.gemm(A, pk["stem"][0], pk["stem"][1], "bias_relu", ws["stem_out"])
         x = ws["x0"]
         ops.maxpool3d(ws["stem_out"], B, stem, c["stem_dim"], (1, 3, 3), (1, 2, 2), (0, 1, 1), x)
@@ -219,9 +231,7 @@ class ResNet3d(torch.nn.Module):
                 ops.gemm(act["b"][:, :inner], blk["c"][0], blk["c"][1], "bias_resid_relu", out, aux=skip)
                 x, cin = out, dout
             g_in = g
-        t, h, w = grids[-1]
-        return ops.avgpool_head(x, B, (t, h, w), cin, c["head_pool"], pk["w_head"], pk["b_head"], ws["head_work"],
-                                ws["logits"])
+        return x, B, grids[-1], cin, ws
 
 
 def create_model(logger=None, device="cuda", weights_seed: int = 0):

@@ -179,7 +179,7 @@ def resnet3d_param_shapes(cfg: dict) -> "OrderedDict[str, tuple]":
             s[f"{pre}.{k}"] = (c,)
 
     d0 = cfg["stem_dim"]
-    s["blocks.0.conv.weight"] = (d0, 3, 3, 7, 7)
+    s["blocks.0.conv.weight"] = (d0, 3) + tuple(cfg.get("stem_kernel", (3, 7, 7)))
     bn("blocks.0.norm", d0)
     din, dout = d0, d0 * 4
     for st, depth in enumerate(cfg["depths"]):
@@ -198,8 +198,9 @@ def resnet3d_param_shapes(cfg: dict) -> "OrderedDict[str, tuple]":
             s[p + "branch2.conv_c.weight"] = (dout, inner, 1, 1, 1)
             bn(p + "branch2.norm_c", dout)
         din, dout = dout, dout * 2
-    s["blocks.5.proj.weight"] = (cfg.get("num_classes", 2), din)
-    s["blocks.5.proj.bias"] = (cfg.get("num_classes", 2),)
+    if cfg.get("num_classes", 2):
+        s["blocks.5.proj.weight"] = (cfg.get("num_classes", 2), din)
+        s["blocks.5.proj.bias"] = (cfg.get("num_classes", 2),)
     return s
 
 
@@ -224,6 +225,84 @@ def make_resnet3d_weights(cfg: dict, seed: int = 0) -> "OrderedDict[str, np.ndar
         else:
             w = rng.standard_normal(shape) * 0.02
         out[name] = np.ascontiguousarray(w.astype(np.float32))
+    return out
+
+
+# torchvision resnet50 (the per-frame feature extractor of resnet50-2d-lstm/src/models/model.py:9-12,
+# nn.Sequential(children()[:-1]) -> keys "resnet50.<child>...") <-> the pytorchvideo-style names
+# the shared conv path packs (kt = 1 kernels)
+RESNET50_2D = dict(depths=(3, 4, 6, 3), stem_dim=64, conv_a_kernels=((1, 1, 1),) * 4, spatial_strides=(1, 2, 2, 2),
+                   num_classes=0, bn_eps=1e-5, stem_kernel=(1, 7, 7), stem_pad=(0, 3, 3))
+
+
+def torchvision_resnet50_to_blocks(name: str):
+    """'resnet50.4.0.conv1.weight' -> 'blocks.1.res_blocks.0.branch2.conv_a.weight' (None if not a
+    ResNet key).  Children: 0 conv1, 1 bn1, 4..7 layer1..4 (Bottleneck v1.5: stride on conv2)."""
+    parts = name.split(".")
+    if parts[0] != "resnet50":
+        return None
+    child = int(parts[1])
+    if child == 0:
+        return "blocks.0.conv." + parts[-1]
+    if child == 1:
+        return "blocks.0.norm." + parts[-1]
+    stage, blk, mod = child - 3, parts[2], parts[3]
+    pre = f"blocks.{stage}.res_blocks.{blk}."
+    if mod == "downsample":
+        return pre + ("branch1_conv." if parts[4] == "0" else "branch1_norm.") + parts[-1]
+    m = {"conv1": "branch2.conv_a", "bn1": "branch2.norm_a", "conv2": "branch2.conv_b", "bn2": "branch2.norm_b",
+         "conv3": "branch2.conv_c", "bn3": "branch2.norm_c"}[mod]
+    return pre + m + "." + parts[-1]
+
+
+def resnet50_lstm_param_shapes(hidden: int = 256, layers: int = 2) -> "OrderedDict[str, tuple]":
+    """Reference VideoResNet50LSTM state_dict names / shapes (resnet50-2d-lstm/src/models/model.py)."""
+    inv = {}
+    s = OrderedDict()
+    for n, shp in resnet3d_param_shapes(RESNET50_2D).items():
+        inv[n] = shp
+    # torchvision order: conv1, bn1, layer1..4
+    for n, shp in inv.items():
+        tv = blocks_to_torchvision_resnet50(n)
+        s[tv] = shp[:2] + shp[3:] if len(shp) == 5 else shp  # 2D conv weights drop the kt = 1 axis
+    for l in range(layers):
+        din = 2048 if l == 0 else hidden
+        s[f"lstm.weight_ih_l{l}"] = (4 * hidden, din)
+        s[f"lstm.weight_hh_l{l}"] = (4 * hidden, hidden)
+        s[f"lstm.bias_ih_l{l}"] = (4 * hidden,)
+        s[f"lstm.bias_hh_l{l}"] = (4 * hidden,)
+    s["classifier.0.weight"] = (64, hidden)
+    s["classifier.0.bias"] = (64,)
+    s["classifier.3.weight"] = (1, 64)
+    s["classifier.3.bias"] = (1,)
+    return s
+
+
+def blocks_to_torchvision_resnet50(name: str) -> str:
+    parts = name.split(".")
+    if parts[1] == "0":
+        return ("resnet50.0." if parts[2] == "conv" else "resnet50.1.") + parts[-1]
+    stage, blk = int(parts[1]), parts[3]
+    pre = f"resnet50.{stage + 3}.{blk}."
+    if parts[4].startswith("branch1"):
+        return pre + ("downsample.0." if parts[4] == "branch1_conv" else "downsample.1.") + parts[-1]
+    m = {"conv_a": "conv1", "norm_a": "bn1", "conv_b": "conv2", "norm_b": "bn2", "conv_c": "conv3", "norm_c": "bn3"}[parts[5]]
+    return pre + m + "." + parts[-1]
+
+
+def make_resnet50_lstm_weights(seed: int = 0, hidden: int = 256) -> "OrderedDict[str, np.ndarray]":
+    """ResNet part as make_resnet3d_weights (He convs, near-identity BN); LSTM / classifier ~
+    U(-1/sqrt(hidden), 1/sqrt(hidden)) like torch's default init."""
+    base = make_resnet3d_weights(RESNET50_2D, seed=seed)
+    rng = np.random.RandomState(seed + 1)
+    out = OrderedDict()
+    for n, shp in resnet50_lstm_param_shapes(hidden).items():
+        if n.startswith("resnet50."):
+            b = base[torchvision_resnet50_to_blocks(n)]
+            out[n] = np.ascontiguousarray(b.reshape(shp))
+        else:
+            k = 1.0 / np.sqrt(hidden if n.startswith("lstm") else shp[-1])
+            out[n] = np.ascontiguousarray(rng.uniform(-k, k, shp).astype(np.float32))
     return out
 
 
