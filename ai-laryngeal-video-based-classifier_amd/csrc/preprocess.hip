@@ -1,0 +1,146 @@
+// Clip preprocessing on the GPU:
+//  * resample_u8_kernel — one axis of Pillow's BILINEAR resize of uint8 images, bit-exact:
+//    fixed-point coefficients (22 fraction bits) precomputed on the host exactly as Pillow's
+//    precompute_coeffs + normalize_coeffs_8bpc do, accumulation from 1 << 21, clip8 per pass
+//    (Pillow Resample.c ImagingResampleHorizontal_8bpc / Vertical_8bpc).  The ViViT processor
+//    (VivitImageProcessor: PIL bilinear shortest edge 224 -> 256, centre crop 224, x/63.75 - 3;
+//    vivit_transformer/vivit_classifier/trainers/trainer.py:22-26, 62-95) is two passes plus
+//    video_transform_kernel.
+//  * video_transform_kernel — frame-index gather (pytorchvideo UniformTemporalSubsample /
+//    the sampled indices), optional torch-semantics bilinear resize (F.interpolate,
+//    align_corners=False: pytorchvideo ShortSideScale), crop (torchvision CenterCrop), per-channel
+//    affine x*scale[c] + shift[c] (Normalize / the /255 of the inference scripts), and the output
+//    layout [B][T][C][h][w] (HF pixel_values) or [B][C][T][h][w] (torchvision video models).
+#include "common.hpp"
+
+namespace vc {
+
+constexpr int PIL_PRECISION_BITS = 32 - 8 - 2;
+
+__device__ __forceinline__ unsigned char clip8(int in) {
+    if (in >= (1 << PIL_PRECISION_BITS << 8)) return 255;
+    if (in <= 0) return 0;
+    return (unsigned char)(in >> PIL_PRECISION_BITS);
+}
+
+// axis 0: horizontal (W -> Wo), axis 1: vertical (H -> Ho).  One thread per output pixel.
+__global__ void __launch_bounds__(256) resample_u8_kernel(const uint8_t* __restrict__ src, int64_t N, int H, int W, int C,
+                                                          int axis, int outsz, const int* __restrict__ bounds,
+                                                          const int* __restrict__ coef, int ksize,
+                                                          uint8_t* __restrict__ dst) {
+    const int Ho = axis ? outsz : H, Wo = axis ? W : outsz;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= N * Ho * Wo) return;
+    const int xo = i % Wo;
+    const int yo = (i / Wo) % Ho;
+    const int64_t n = i / ((int64_t)Wo * Ho);
+    const int o = axis ? yo : xo;
+    const int mn = bounds[2 * o], cnt = bounds[2 * o + 1];
+    const int* k = coef + (int64_t)o * ksize;
+    const uint8_t* base = src + n * H * W * C;
+    for (int c = 0; c < C; ++c) {
+        int ss = 1 << (PIL_PRECISION_BITS - 1);
+        for (int x = 0; x < cnt; ++x) {
+            const int sy = axis ? mn + x : yo, sx = axis ? xo : mn + x;
+            ss += (int)base[((int64_t)sy * W + sx) * C + c] * k[x];
+        }
+        dst[((n * Ho + yo) * (int64_t)Wo + xo) * C + c] = clip8(ss);
+    }
+}
+
+struct VideoXform {
+    int F, H, W;        // source frames per clip, frame size (uint8 HxWx3)
+    int T;              // frames per output clip
+    int Hr, Wr;         // resize target (== H, W: no resize)
+    int top, left;      // crop origin in the (resized) frame
+    int ch, cw;         // crop size = output frame size
+    float sc[3], sh[3]; // per-channel affine
+    int layout;         // 0: [B][T][C][ch][cw], 1: [B][C][T][ch][cw]
+    int bf16;
+};
+
+__global__ void __launch_bounds__(256) video_transform_kernel(const uint8_t* __restrict__ frames,
+                                                              const int64_t* __restrict__ idx, int64_t nclip, VideoXform p,
+                                                              void* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t per_frame = (int64_t)p.ch * p.cw;
+    if (i >= nclip * p.T * per_frame) return;
+    const int j = i % p.cw;
+    const int r = (i / p.cw) % p.ch;
+    const int t = (i / per_frame) % p.T;
+    const int64_t b = i / (per_frame * p.T);
+    int64_t f = idx[b * p.T + t];
+    f = f < 0 ? 0 : (f >= p.F ? p.F - 1 : f);
+    const uint8_t* fr = frames + (b * p.F + f) * (int64_t)p.H * p.W * 3;
+    const int y = r + p.top, x = j + p.left;
+    float v[3];
+    if (p.Hr == p.H && p.Wr == p.W) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c) v[c] = (float)fr[((int64_t)y * p.W + x) * 3 + c];
+    } else {
+        // torch upsample_bilinear2d, align_corners=False: src = max((dst + 0.5) * in/out - 0.5, 0)
+        const float rh = (float)p.H / (float)p.Hr, rw = (float)p.W / (float)p.Wr;
+        float hr = (y + 0.5f) * rh - 0.5f, wr = (x + 0.5f) * rw - 0.5f;
+        hr = hr < 0.f ? 0.f : hr;
+        wr = wr < 0.f ? 0.f : wr;
+        const int h1 = (int)hr, w1 = (int)wr;
+        const int h1p = h1 < p.H - 1 ? 1 : 0, w1p = w1 < p.W - 1 ? 1 : 0;
+        const float l1h = hr - (float)h1, l0h = 1.f - l1h, l1w = wr - (float)w1, l0w = 1.f - l1w;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const float p00 = fr[((int64_t)h1 * p.W + w1) * 3 + c], p01 = fr[((int64_t)h1 * p.W + w1 + w1p) * 3 + c];
+            const float p10 = fr[((int64_t)(h1 + h1p) * p.W + w1) * 3 + c];
+            const float p11 = fr[((int64_t)(h1 + h1p) * p.W + w1 + w1p) * 3 + c];
+            v[c] = l0h * (l0w * p00 + l1w * p01) + l1h * (l0w * p10 + l1w * p11);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float o = v[c] * p.sc[c] + p.sh[c];
+        const int64_t oi = p.layout == 0 ? (((b * p.T + t) * 3 + c) * per_frame + (int64_t)r * p.cw + j)
+                                         : (((b * 3 + c) * p.T + t) * per_frame + (int64_t)r * p.cw + j);
+        if (p.bf16)
+            reinterpret_cast<uint16_t*>(out)[oi] = f2bf(o);
+        else
+            reinterpret_cast<float*>(out)[oi] = o;
+    }
+}
+
+}  // namespace vc
+
+using namespace vc;
+
+extern "C" {
+
+int vc_resample_u8(const uint8_t* src, int64_t N, int64_t H, int64_t W, int64_t C, int axis, int64_t out_size,
+                   const int* bounds, const int* coeffs, int64_t ksize, uint8_t* dst, hipStream_t stream) {
+    if (!src || !bounds || !coeffs || !dst) return fail(VC_ERR_INVALID_ARG, "vc_resample_u8: null pointer");
+    if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C > 4 || out_size <= 0 || ksize <= 0 || (axis != 0 && axis != 1))
+        return fail(VC_ERR_INVALID_ARG, "vc_resample_u8: bad shape");
+    const int64_t total = N * (axis ? out_size * W : H * out_size);
+    resample_u8_kernel<<<(unsigned)((total + 255) / 256), 256, 0, stream>>>(src, N, (int)H, (int)W, (int)C, axis,
+                                                                           (int)out_size, bounds, coeffs, (int)ksize, dst);
+    return check_launch("vc_resample_u8");
+}
+
+int vc_video_transform(const uint8_t* frames, int64_t nclips, int64_t F, int64_t H, int64_t W, const int64_t* idx,
+                       int64_t T, int64_t resize_h, int64_t resize_w, int64_t top, int64_t left, int64_t crop_h,
+                       int64_t crop_w, const float* scale3, const float* shift3, int layout, int out_bf16, void* out,
+                       hipStream_t stream) {
+    if (!frames || !idx || !scale3 || !shift3 || !out) return fail(VC_ERR_INVALID_ARG, "vc_video_transform: null pointer");
+    if (nclips <= 0 || F <= 0 || H <= 0 || W <= 0 || T <= 0 || resize_h <= 0 || resize_w <= 0 || top < 0 || left < 0 ||
+        crop_h <= 0 || crop_w <= 0 || top + crop_h > resize_h || left + crop_w > resize_w || (layout != 0 && layout != 1))
+        return fail(VC_ERR_INVALID_ARG, "vc_video_transform: bad geometry");
+    VideoXform p;
+    p.F = (int)F; p.H = (int)H; p.W = (int)W; p.T = (int)T;
+    p.Hr = (int)resize_h; p.Wr = (int)resize_w;
+    p.top = (int)top; p.left = (int)left; p.ch = (int)crop_h; p.cw = (int)crop_w;
+    for (int c = 0; c < 3; ++c) { p.sc[c] = scale3[c]; p.sh[c] = shift3[c]; }
+    p.layout = layout;
+    p.bf16 = out_bf16 ? 1 : 0;
+    const int64_t total = nclips * T * crop_h * crop_w;
+    video_transform_kernel<<<(unsigned)((total + 255) / 256), 256, 0, stream>>>(frames, idx, nclips, p, out);
+    return check_launch("vc_video_transform");
+}
+
+}  // extern "C"

@@ -155,6 +155,36 @@ int vc_cls_head(const float* x, int64_t ldx, int64_t B, int64_t S, int64_t D,
                 const float* gamma, const float* beta, float eps,
                 const float* Wc, const float* bc, int64_t num_labels, float* logits, hipStream_t stream);
 
+/* ---- Clip preprocessing ------------------------------------------- */
+
+/*
+ * One axis of Pillow's BILINEAR resize of uint8 images [N][H][W][C] (C <= 4), bit-exact:
+ * axis 0 resizes W -> out_size, axis 1 resizes H -> out_size.  bounds (int32 [out_size][2]:
+ * first source index, tap count) and coeffs (int32 [out_size][ksize], 22 fraction bits) are
+ * DEVICE tables built on the host exactly as Pillow's precompute_coeffs + normalize_coeffs_8bpc
+ * (vclip_amd/preprocess.py); each pass rounds to uint8 as Pillow's clip8 does.  Two passes
+ * (horizontal, then vertical) = PIL Image.resize(..., BILINEAR), which the ViViT processor
+ * applies per frame (VivitImageProcessor, vivit_transformer/.../trainers/trainer.py:22-26).
+ */
+int vc_resample_u8(const uint8_t* src, int64_t N, int64_t H, int64_t W, int64_t C, int axis, int64_t out_size,
+                   const int* bounds, const int* coeffs, int64_t ksize, uint8_t* dst, hipStream_t stream);
+
+/*
+ * frames u8 [nclips][F][H][W][3] -> out[clip][t] = affine(crop(resize(frames[clip][idx[clip][t]]))):
+ * idx int64 [nclips][T] (clamped to [0, F-1]); resize to (resize_h, resize_w) with torch
+ * F.interpolate bilinear, align_corners=False semantics (skipped when equal to (H, W)); crop
+ * (top, left, crop_h, crop_w); per-channel out = v * scale3[c] + shift3[c] (scale3 / shift3 are
+ * HOST float[3]); layout 0: [clip][T][3][h][w] (HF pixel_values), 1: [clip][3][T][h][w]
+ * (torchvision video models); f32 or (out_bf16) bf16.  Replaces pytorchvideo
+ * UniformTemporalSubsample + ShortSideScale + CenterCrop + Normalize (videoswintransformer/.../
+ * dataset.py:162-170, resnet50-3d-video/.../dataset.py:186-192), the inference scripts' /255 +
+ * normalise (resnet50-3d-video/inference.py:382-394) and, after vc_resample_u8, the ViViT affine.
+ */
+int vc_video_transform(const uint8_t* frames, int64_t nclips, int64_t F, int64_t H, int64_t W, const int64_t* idx,
+                       int64_t T, int64_t resize_h, int64_t resize_w, int64_t top, int64_t left, int64_t crop_h,
+                       int64_t crop_w, const float* scale3, const float* shift3, int layout, int out_bf16, void* out,
+                       hipStream_t stream);
+
 /* ---- TimeSformer divided space-time attention ------------------------
  * Clip layout: rows b*S + r, S = 1 + P*T, r = 0 (CLS) or 1 + p*T + t (patch-major, time-minor).
  * Frame layout: rows (b*T + t)*(1 + P) + j, j = 0 (CLS copy) or 1 + p (the spatial sequences). */

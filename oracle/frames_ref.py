@@ -35,3 +35,33 @@ def tubelet_im2col(pix, tubelet=(2, 16, 16), order="time_major"):
     # -> B, nt, nh, nw, C, kt, kh, kw   (or B, nh, nw, nt, ... for patch-major)
     x = x.transpose(0, 1, 4, 6, 3, 2, 5, 7) if order == "time_major" else x.transpose(0, 4, 6, 1, 3, 2, 5, 7)
     return np.ascontiguousarray(x.reshape(B * (T // kt) * (H // kh) * (W // kw), C * kt * kh * kw))
+
+
+def pil_resize_emulated(img, out_hw, coeffs):
+    """Pillow BILINEAR resize of one uint8 image [H, W, C] restated in numpy integer arithmetic
+    (Resample.c: horizontal pass, then vertical, each accumulating from 1 << 21 with 22-bit
+    fixed-point coefficients and clip8).  `coeffs(in, out)` -> (bounds, coef, ksize)."""
+    H, W, C = img.shape
+    H2, W2 = out_hw
+
+    def pas(x, axis, n_in, n_out):
+        b, c, _ = coeffs(n_in, n_out)
+        shape = list(x.shape)
+        shape[axis] = n_out
+        out = np.zeros(shape, np.int64)
+        for o in range(n_out):
+            s = np.full([d for i, d in enumerate(x.shape) if i != axis], 1 << 21, np.int64)
+            for t in range(b[o, 1]):
+                s = s + np.take(x, b[o, 0] + t, axis=axis) * int(c[o, t])
+            if axis == 0:
+                out[o] = s
+            else:
+                out[:, o] = s
+        return np.where(out >= (1 << 30), 255, np.where(out <= 0, 0, out >> 22))
+
+    x = img.astype(np.int64)
+    if W2 != W:
+        x = pas(x, 1, W, W2)
+    if H2 != H:
+        x = pas(x, 0, H, H2)
+    return x.astype(np.uint8)

@@ -1,0 +1,62 @@
+"""GPU preprocessing vs the reference's own transforms: Pillow (bit-exact uint8 resize),
+transformers VivitImageProcessor (the ViViT trainer's processor), and the pytorchvideo
+eval chain restated with torch ops (F.interpolate bilinear, CenterCrop, Normalize)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+PIL = pytest.importorskip("PIL.Image")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vclip_amd import _lib
+    _lib.load()
+
+
+@pytest.mark.parametrize("H,W,H2,W2", [(224, 224, 256, 256), (240, 320, 256, 341), (300, 200, 200, 133)])
+def test_pil_resize_bit_exact(H, W, H2, W2):
+    from vclip_amd.preprocess import pil_resize_u8
+    rng = np.random.RandomState(H * W)
+    imgs = rng.randint(0, 256, (3, H, W, 3)).astype(np.uint8)
+    got = pil_resize_u8(torch.from_numpy(imgs).to(DEV), (H2, W2)).cpu().numpy()
+    for i in range(3):
+        ref = np.asarray(PIL.fromarray(imgs[i]).resize((W2, H2), PIL.BILINEAR))
+        assert np.array_equal(got[i], ref)
+
+
+def test_vivit_preprocess_vs_hf_processor():
+    transformers = pytest.importorskip("transformers")
+    from vclip_amd.preprocess import vivit_preprocess
+    proc = transformers.VivitImageProcessor(num_frames=4, image_size=224, patch_size=16)
+    rng = np.random.RandomState(1)
+    frames = rng.randint(0, 256, (2, 4, 224, 224, 3)).astype(np.uint8)
+    want = np.concatenate([proc(list(frames[b]), return_tensors="np")["pixel_values"] for b in range(2)])
+    got = vivit_preprocess(torch.from_numpy(frames).to(DEV)).cpu().numpy()
+    assert got.shape == want.shape
+    assert np.abs(got - want).max() < 1e-5
+
+
+@pytest.mark.parametrize("F,H,W,T,div255", [(40, 240, 320, 16, False), (12, 224, 224, 32, True), (9, 300, 256, 8, False)])
+def test_video_eval_transform(F, H, W, T, div255):
+    from vclip_amd.preprocess import short_side_size, uniform_temporal_subsample_indices, video_eval_transform
+    rng = np.random.RandomState(F)
+    frames = rng.randint(0, 256, (2, F, H, W, 3)).astype(np.uint8)
+    got = video_eval_transform(torch.from_numpy(frames).to(DEV), T, div255=div255).cpu()
+    x = torch.from_numpy(frames).float().permute(0, 4, 1, 2, 3)  # [B, C, F, H, W] as EncodedVideo gives
+    x = x[:, :, uniform_temporal_subsample_indices(F, T)]
+    rh, rw = short_side_size(H, W, 256)
+    B = x.shape[0]
+    x = torch.nn.functional.interpolate(x.reshape(B * 3, T, H, W), size=(rh, rw), mode="bilinear",
+                                        align_corners=False).reshape(B, 3, T, rh, rw)
+    top, left = int(round((rh - 224) / 2.0)), int(round((rw - 224) / 2.0))
+    x = x[..., top:top + 224, left:left + 224]
+    if div255:
+        x = x / 255.0
+    want = (x - 0.45) / 0.225
+    tol = 1e-4 * (1.0 if div255 else 255.0)
+    assert got.shape == want.shape and (got - want).abs().max().item() < tol
