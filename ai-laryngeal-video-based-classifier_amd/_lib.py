@@ -54,6 +54,19 @@ SIGNATURES = {
                             c_p, c_int, c_int, c_p, c_p], c_int),
     "vc_divided_add_layernorm": ([c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_int, c_p,
                                   c_i64, c_p], c_int),
+    # train step
+    "vc_attention_fwd_lse": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_int, c_p, c_i64, c_p, c_p], c_int),
+    "vc_attention_bwd": ([c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p],
+                         c_int),
+    "vc_layernorm_bwd": ([c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_f, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_i64,
+                          c_p], c_int),
+    "vc_colsum": ([c_p, c_int, c_i64, c_i64, c_i64, c_i64, c_f, c_p, c_p, c_i64, c_p], c_int),
+    "vc_wgrad_bf16": ([c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_p, c_i64, c_p, c_i64, c_p], c_int),
+    "vc_cls_head_bwd": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_p, c_i64, c_p, c_p, c_i64, c_p, c_i64, c_p,
+                         c_p, c_p, c_p, c_p], c_int),
+    "vc_embed_bwd": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_i64, c_p], c_int),
+    "vc_adamw": ([c_p, c_p, c_p, c_p, c_i64, c_f, c_f, c_f, c_f, c_f, c_i64, c_f, c_p], c_int),
+    "vc_pack_weight": ([c_p, c_i64, c_i64, c_i64, c_f, c_p, c_p, c_p], c_int),
 }
 
 

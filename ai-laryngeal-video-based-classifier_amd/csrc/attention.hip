@@ -78,10 +78,12 @@ __device__ __forceinline__ void attn_sync() {
 // results are wrong by design; 16 re-bases on every tile (the LIM = 0 build of the
 // threshold sweep, cdna_hip_programming.md rule 26: must agree with the shipped build);
 // 32 drops the MFMA/VALU interleave directives (correct, timing comparison only).
-template <int QB, int ABL>
+// WLSE: also store the base-2 log-sum-exp of each query's scores, lse[(b*H + h)*S + q] =
+// m + log2(l) (running max and row sum), from which the backward kernels recompute P.
+template <int QB, int ABL, bool WLSE = false>
 __global__ void __launch_bounds__(256, 2)
 attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, float c_log2,
-                    uint16_t* __restrict__ out, int64_t ldo) {
+                    uint16_t* __restrict__ out, int64_t ldo, float* __restrict__ lse = nullptr) {
     static_assert(QB == 1, "see the QB note above");
     constexpr int AQ = 128 * QB;  // query rows per workgroup (4 waves x QB x 32)
     __shared__ __attribute__((aligned(16))) char smem[NSLOT * KV_SLOT];
@@ -383,6 +385,9 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
         const float l_own = l_run[qb][0] + l_run[qb][1];
         const float l_tot = l_own + __shfl_xor(l_own, 32, 64);
         const float inv = 1.0f / l_tot;
+        if constexpr (WLSE) {
+            if (h == 0 && q < S) lse[(int64_t)bh * S + q] = -minit[qb][0] + __log2f(l_tot);
+        }
         unsigned pk[2][4][2];
 #pragma unroll
         for (int db = 0; db < 2; ++db)
@@ -405,12 +410,12 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
     }
 }
 
-template <int QB, int ABL>
+template <int QB, int ABL, bool WLSE = false>
 static void launch_attn(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, float c_log2, uint16_t* out,
-                        int64_t ldo, hipStream_t stream) {
+                        int64_t ldo, hipStream_t stream, float* lse = nullptr) {
     constexpr int AQ = 128 * QB;
     dim3 grid((unsigned)((S + AQ - 1) / AQ), (unsigned)(B * H));
-    attn_fwd_d64_kernel<QB, ABL><<<grid, 256, 0, stream>>>(qkv, ld, (int)S, (int)H, c_log2, out, ldo);
+    attn_fwd_d64_kernel<QB, ABL, WLSE><<<grid, 256, 0, stream>>>(qkv, ld, (int)S, (int)H, c_log2, out, ldo, lse);
 }
 
 }  // namespace vc
@@ -435,6 +440,17 @@ extern "C" int vc_attention_fwd(const uint16_t* qkv, int64_t ld, int64_t B, int6
     const float c_log2 = q_prescaled ? 1.0f : scale * 1.4426950408889634f;
     launch_attn<1, 0>(qkv, ld, B, S, H, c_log2, out, ldo, stream);
     return check_launch("vc_attention_fwd");
+}
+
+// Training forward: vc_attention_fwd plus the base-2 log-sum-exp per (clip, head, query).
+extern "C" int vc_attention_fwd_lse(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, int64_t head_dim,
+                                    float scale, int q_prescaled, uint16_t* out, int64_t ldo, float* lse,
+                                    hipStream_t stream) {
+    if (int rc = attn_checks(qkv, ld, B, S, H, head_dim, out, ldo)) return rc;
+    if (!lse) return fail(VC_ERR_INVALID_ARG, "vc_attention_fwd_lse: null lse");
+    const float c_log2 = q_prescaled ? 1.0f : scale * 1.4426950408889634f;
+    launch_attn<1, 0, true>(qkv, ld, B, S, H, c_log2, out, ldo, stream, lse);
+    return check_launch("vc_attention_fwd_lse");
 }
 
 // Timing-only ablations / variants of the attention kernel (tools/ablate_attn.py).

@@ -44,6 +44,12 @@ __device__ __forceinline__ float gelu_tanh(float x) {
     const float e = __builtin_amdgcn_exp2f(-2.8853900817779268f * u);  // 2*log2(e)
     return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
+// d/dx gelu_fast = 0.5(1 + tanh u) + 0.5 x (1 - tanh^2 u) * 0.7978845608 (1 + 3*0.044715 x^2)
+__device__ __forceinline__ float dgelu_tanh(float x) {
+    const float u = 0.7978845608f * x * (1.0f + 0.044715f * x * x);
+    const float t = tanhf(u);
+    return 0.5f * (1.0f + t) + 0.5f * x * (1.0f - t * t) * 0.7978845608f * (1.0f + 0.134145f * x * x);
+}
 __device__ __forceinline__ float gelu_erf(float x) {
     return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
 }

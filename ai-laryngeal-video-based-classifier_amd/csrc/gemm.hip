@@ -86,7 +86,31 @@ __device__ __forceinline__ void store_tile(const v16f (&acc)[MI][NI], int64_t mb
                 float v1 = acc[i][j][4 * g + 1] + bb.y;
                 float v2 = acc[i][j][4 * g + 2] + bb.z;
                 float v3 = acc[i][j][4 * g + 3] + bb.w;
-                if (EPI == VC_EPI_BIAS_BF16 || EPI == VC_EPI_BIAS_GELU_TANH || EPI == VC_EPI_BIAS_GELU_ERF ||
+                if (EPI == VC_EPI_BIAS_GELU_TANH_SAVE || EPI == VC_EPI_DGELU_TANH) {
+                    uint2* ap = reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(const_cast<float*>(aux)) + m * ldaux + n);
+                    if (EPI == VC_EPI_BIAS_GELU_TANH_SAVE) {
+                        // keep the bf16 pre-activation for the backward's gelu'
+                        uint2 pre;
+                        pre.x = pack2bf(v0, v1);
+                        pre.y = pack2bf(v2, v3);
+                        *ap = pre;
+                        v0 = gelu_tanh(v0); v1 = gelu_tanh(v1); v2 = gelu_tanh(v2); v3 = gelu_tanh(v3);
+                    } else {
+                        const uint2 pre = *ap;
+                        v0 *= dgelu_tanh(bf2f((unsigned short)(pre.x & 0xffff)));
+                        v1 *= dgelu_tanh(bf2f((unsigned short)(pre.x >> 16)));
+                        v2 *= dgelu_tanh(bf2f((unsigned short)(pre.y & 0xffff)));
+                        v3 *= dgelu_tanh(bf2f((unsigned short)(pre.y >> 16)));
+                    }
+                    uint2 p;
+                    p.x = pack2bf(v0, v1);
+                    p.y = pack2bf(v2, v3);
+                    *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + m * ldo + n) = p;
+                } else if (EPI == VC_EPI_BIAS_ADD_F32) {
+                    const float4 a = *reinterpret_cast<const float4*>(aux + m * ldaux + n);
+                    *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + m * ldo + n) =
+                        make_float4(a.x + v0, a.y + v1, a.z + v2, a.w + v3);
+                } else if (EPI == VC_EPI_BIAS_BF16 || EPI == VC_EPI_BIAS_GELU_TANH || EPI == VC_EPI_BIAS_GELU_ERF ||
                     EPI == VC_EPI_BIAS_RELU_BF16 || EPI == VC_EPI_BIAS_RESID_RELU_BF16) {
                     if (EPI == VC_EPI_BIAS_GELU_TANH) {
                         v0 = gelu_tanh(v0); v1 = gelu_tanh(v1); v2 = gelu_tanh(v2); v3 = gelu_tanh(v3);
@@ -744,6 +768,13 @@ extern "C" int vc_gemm_bf16_cfg(const uint16_t* A, int64_t lda, const uint16_t* 
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: EMBED epilogue needs aux, G > 0");
     if (epilogue == VC_EPI_BIAS_RESID_RELU_BF16 && (!aux || ldaux % 4 || ldaux < N || ((uintptr_t)aux & 7)))
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: RESID_RELU epilogue needs a bf16 residual (aux) with ldaux >= N");
+    if ((epilogue == VC_EPI_BIAS_GELU_TANH_SAVE || epilogue == VC_EPI_DGELU_TANH) &&
+        (!aux || ldaux % 4 || ldaux < N || ((uintptr_t)aux & 7)))
+        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: GELU_SAVE / DGELU epilogues need a bf16 aux with ldaux >= N");
+    if (epilogue == VC_EPI_BIAS_ADD_F32 && (!aux || ldaux % 4 || ldaux < N || ((uintptr_t)aux & 15)))
+        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: BIAS_ADD_F32 epilogue needs an f32 aux with ldaux >= N");
+    if (epilogue >= VC_EPI_BIAS_ADD_F32 && cfg >= 3)
+        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: training epilogues run on cfg 0-2");
     if (cfg < 0) cfg = pick_cfg(M, N, K, epilogue);
     const int ablation = cfg >= 10 ? cfg : -1;  // x3 / x4: timing-only ablations of cfg 3 / 4 (wrong results)
     if (ablation > 0) cfg = (ablation % 10 == 4) ? 4 : 3;
@@ -775,6 +806,12 @@ extern "C" int vc_gemm_bf16_cfg(const uint16_t* A, int64_t lda, const uint16_t* 
             return launch_epi<VC_EPI_BIAS_RELU_BF16>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
         case VC_EPI_BIAS_RESID_RELU_BF16:
             return launch_epi<VC_EPI_BIAS_RESID_RELU_BF16>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
+        case VC_EPI_BIAS_ADD_F32:
+            return launch_epi<VC_EPI_BIAS_ADD_F32>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
+        case VC_EPI_BIAS_GELU_TANH_SAVE:
+            return launch_epi<VC_EPI_BIAS_GELU_TANH_SAVE>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
+        case VC_EPI_DGELU_TANH:
+            return launch_epi<VC_EPI_DGELU_TANH>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
     }
     return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad epilogue");
 }

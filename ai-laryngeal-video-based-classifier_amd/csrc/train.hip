@@ -1,0 +1,593 @@
+// Training-step kernels of the ViViT train step: the backward of every
+// non-attention op of VivitLayer / VivitEmbeddings / the classifier, the weight-gradient GEMM,
+// and the optimizer.  Reference: vivit_transformer/vivit_classifier/trainers/trainer.py:140-146
+// (criterion(outputs.logits, labels); loss.backward(); optimizer.step()) with
+// AdamW(lr 1e-3, weight_decay 0.01) from vivit_transformer/main.py:150-155.
+//
+// Every reduction is deterministic (fixed-order partial sums, no atomics), so a gradient is
+// bit-identical run to run and across data-parallel replicas fed the same shard.
+#include "common.hpp"
+
+#include <algorithm>
+#include <cmath>
+
+namespace vc {
+namespace trn {
+
+// ---------------------------------------------------------------------------------
+// LayerNorm backward, fused with the residual-gradient add and its bf16 copy.
+// One wave per row (D = 256*V), rows grid-strided; per-lane column partials of dgamma /
+// dbeta in registers, combined across the 4 waves in LDS -> part[block][2][D].
+//   xhat = (x - mean) * rstd,  g = dy * gamma,
+//   dx  += rstd * (g - mean(g) - xhat * mean(g * xhat))     (nn.LayerNorm backward)
+// ---------------------------------------------------------------------------------
+template <int V>
+__global__ void __launch_bounds__(256) ln_bwd_kernel(const float* __restrict__ dy, int64_t lddy,
+                                                     const float* __restrict__ x, int64_t ldx,
+                                                     const float* __restrict__ gamma, float eps, int64_t M,
+                                                     float* __restrict__ dx, int64_t lddx, uint16_t* __restrict__ dxb,
+                                                     int64_t lddxb, float* __restrict__ part) {
+    constexpr int D = V * 256;
+    __shared__ float red[4][2 * D];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float4 pg[V], pb[V], g4[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        pg[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        pb[i] = pg[i];
+        g4[i] = reinterpret_cast<const float4*>(gamma)[i * 64 + lane];
+    }
+    for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < M; row += (int64_t)gridDim.x * 4) {
+        const float4* xr = reinterpret_cast<const float4*>(x + row * ldx);
+        const float4* dr = reinterpret_cast<const float4*>(dy + row * lddy);
+        float4 xv[V], dv[V];
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            xv[i] = xr[i * 64 + lane];
+            dv[i] = dr[i * 64 + lane];
+            s += (xv[i].x + xv[i].y) + (xv[i].z + xv[i].w);
+        }
+        const float mean = wave_sum(s) * (1.0f / D);
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            const float a = xv[i].x - mean, b = xv[i].y - mean, c = xv[i].z - mean, d = xv[i].w - mean;
+            q += (a * a + b * b) + (c * c + d * d);
+        }
+        const float rstd = rsqrtf(wave_sum(q) * (1.0f / D) + eps);
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            xv[i].x = (xv[i].x - mean) * rstd; xv[i].y = (xv[i].y - mean) * rstd;
+            xv[i].z = (xv[i].z - mean) * rstd; xv[i].w = (xv[i].w - mean) * rstd;
+            const float a = dv[i].x * g4[i].x, b = dv[i].y * g4[i].y, c = dv[i].z * g4[i].z, d = dv[i].w * g4[i].w;
+            s1 += (a + b) + (c + d);
+            s2 += (a * xv[i].x + b * xv[i].y) + (c * xv[i].z + d * xv[i].w);
+            pg[i].x += dv[i].x * xv[i].x; pg[i].y += dv[i].y * xv[i].y;
+            pg[i].z += dv[i].z * xv[i].z; pg[i].w += dv[i].w * xv[i].w;
+            pb[i].x += dv[i].x; pb[i].y += dv[i].y; pb[i].z += dv[i].z; pb[i].w += dv[i].w;
+        }
+        const float c1 = wave_sum(s1) * (1.0f / D), c2 = wave_sum(s2) * (1.0f / D);
+        float4* dxr = reinterpret_cast<float4*>(dx + row * lddx);
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            float4 o = dxr[i * 64 + lane];
+            o.x += rstd * (dv[i].x * g4[i].x - c1 - xv[i].x * c2);
+            o.y += rstd * (dv[i].y * g4[i].y - c1 - xv[i].y * c2);
+            o.z += rstd * (dv[i].z * g4[i].z - c1 - xv[i].z * c2);
+            o.w += rstd * (dv[i].w * g4[i].w - c1 - xv[i].w * c2);
+            dxr[i * 64 + lane] = o;
+            uint2 ob;
+            ob.x = pack2bf(o.x, o.y);
+            ob.y = pack2bf(o.z, o.w);
+            *reinterpret_cast<uint2*>(dxb + row * lddxb + (i * 64 + lane) * 4) = ob;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        reinterpret_cast<float4*>(red[w])[i * 64 + lane] = pg[i];
+        reinterpret_cast<float4*>(red[w] + D)[i * 64 + lane] = pb[i];
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < 2 * D; c += 256)
+        part[(int64_t)blockIdx.x * 2 * D + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+}
+
+// ---------------------------------------------------------------------------------
+// Column sums (bias gradients, partial-sum reductions).  Pass 1: block (x, y) sums rows
+// [y*rps, (y+1)*rps) of its 256 columns -> out[y][col].  The final pass (one row split)
+// applies the per-column scale and writes either one output or two (cols < n0 -> out0,
+// else out1: dgamma | dbeta of a LayerNorm).
+// ---------------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ float ld_as_f32(const T* p);
+template <>
+__device__ __forceinline__ float ld_as_f32<float>(const float* p) { return *p; }
+template <>
+__device__ __forceinline__ float ld_as_f32<uint16_t>(const uint16_t* p) { return bf2f(*p); }
+
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ in, int64_t ld, int64_t R, int64_t N,
+                                                     int64_t rps, float* __restrict__ out0, int64_t n0,
+                                                     float* __restrict__ out1, int64_t nscaled, float scale) {
+    const int64_t col = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (col >= N) return;
+    const int64_t r0 = (int64_t)blockIdx.y * rps;
+    const int64_t r1 = r0 + rps < R ? r0 + rps : R;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int64_t r = r0;
+    for (; r + 4 <= r1; r += 4) {
+        s0 += ld_as_f32<T>(in + r * ld + col);
+        s1 += ld_as_f32<T>(in + (r + 1) * ld + col);
+        s2 += ld_as_f32<T>(in + (r + 2) * ld + col);
+        s3 += ld_as_f32<T>(in + (r + 3) * ld + col);
+    }
+    for (; r < r1; ++r) s0 += ld_as_f32<T>(in + r * ld + col);
+    float s = (s0 + s1) + (s2 + s3);
+    if (col < nscaled) s *= scale;
+    if (gridDim.y > 1)
+        out0[(int64_t)blockIdx.y * N + col] = s;
+    else if (col < n0)
+        out0[col] = s;
+    else
+        out1[col - n0] = s;
+}
+
+template <typename T>
+static int colsum_launch(const T* in, int64_t ld, int64_t R, int64_t N, float* out0, int64_t n0, float* out1,
+                         int64_t nscaled, float scale, float* work, int64_t work_elems, hipStream_t stream) {
+    const unsigned nbx = (unsigned)((N + 255) / 256);
+    int64_t splits = (R + 127) / 128;  // ~128 rows per block in pass 1
+    if (splits > 256) splits = 256;
+    if (splits * N > work_elems) splits = work_elems / N;
+    if (splits <= 1) {
+        colsum_kernel<T><<<dim3(nbx, 1), 256, 0, stream>>>(in, ld, R, N, R, out0, n0, out1, nscaled, scale);
+        return 0;
+    }
+    const int64_t rps = (R + splits - 1) / splits;
+    splits = (R + rps - 1) / rps;
+    colsum_kernel<T><<<dim3(nbx, (unsigned)splits), 256, 0, stream>>>(in, ld, R, N, rps, work, N, nullptr, 0, 1.0f);
+    colsum_kernel<float><<<dim3(nbx, 1), 256, 0, stream>>>(work, N, splits, N, splits, out0, n0, out1, nscaled, scale);
+    return 0;
+}
+
+// ---------------------------------------------------------------------------------
+// Weight-gradient GEMM: dW[n1][n2] = rowscale(n1) * sum_m G[m][n1] * X[m][n2]
+// (G = output gradient, X = layer input, both bf16 row-major [M][*], fp32 accumulate).
+// The reduction index m is the ROW index of both operands, so both MFMA operands are read
+// from row-major LDS images with ds_read_b64_tr_b16 (T10).  Block tile 128 (n1) x 128 (n2),
+// 4 waves as 2 x 2 of 64 x 64; split-K over m (grid.y) into fp32 partials + a reduce pass,
+// because the weight shapes give only 36-144 output tiles for 256 CUs.
+// Operands swapped (A = X, B = G) so each lane holds 4 consecutive n2 -> float4 stores.
+// ---------------------------------------------------------------------------------
+constexpr int WTILE = 64 * 128 * 2;  // one [64 m][128 cols] bf16 tile = two [64][64] panels
+constexpr int WSLOT = 2 * WTILE;
+
+__device__ __forceinline__ int bswz(int r, int c) {
+    const int m = (r >> 1) & 7;
+    return c ^ (((m & 1) << 2) | (m & 2) | ((m >> 2) & 1));
+}
+
+__device__ __forceinline__ v8bf tr_frag(const char* tile, int offa, int offb) {
+    v4s va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(tile + offa));
+    v4s vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(tile + offb));
+    v8s vv;
+    vv[0] = va[0]; vv[1] = va[1]; vv[2] = va[2]; vv[3] = va[3];
+    vv[4] = vb[0]; vv[5] = vb[1]; vv[6] = vb[2]; vv[7] = vb[3];
+    return __builtin_bit_cast(v8bf, vv);
+}
+
+__global__ void __launch_bounds__(256, 2)
+wgrad_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __restrict__ X, int64_t ldx, int64_t M,
+             int nJ, int64_t mchunk, float* __restrict__ out, int64_t ldo, int64_t split_stride, int64_t nscaled,
+             float scale) {
+    __shared__ __attribute__((aligned(16))) char smem[2 * WSLOT];
+    const int ntiles = gridDim.x;
+    const int L = blockIdx.x;
+    const int xq = ntiles >> 3, xr = ntiles & 7, xcd = L & 7;
+    const int tile = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (L >> 3);
+    const int ti = tile / nJ, tj = tile % nJ;
+    const int64_t n1_0 = (int64_t)ti * 128, n2_0 = (int64_t)tj * 128;
+    const int64_t mb = (int64_t)blockIdx.y * mchunk;
+    const int64_t me = mb + mchunk < M ? mb + mchunk : M;
+    const int nt = (int)((me - mb) / 64);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = tid >> 6;
+    const int w1 = wave >> 1, w2 = wave & 1;  // n1 panel, n2 panel of this wave
+    const int r = lane & 31, h = lane >> 5;
+
+    // transposed-read offsets (rows 4h+tq, +8; 32-column blocks db)
+    const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+    const int gcol = ((lane >> 4) & 1) * 16 + tp * 4;
+    int offa[2], offb[2];
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+        const int col = db * 32 + gcol;
+        const int ra = 4 * h + tq, rb = ra + 8;
+        offa[db] = ra * 128 + bswz(ra, col >> 3) * 16 + (col & 7) * 2;
+        offb[db] = rb * 128 + bswz(rb, col >> 3) * 16 + (col & 7) * 2;
+    }
+
+    // staging: 64 rows x 16 chunks of each operand, 4 chunks per thread per operand
+    uint4 rg[4], rx[4];
+    auto load = [&](int t) {
+        const int64_t m0 = mb + (int64_t)t * 64;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int idx = tid + 256 * i, row = idx >> 4, cc = idx & 15;
+            rg[i] = *reinterpret_cast<const uint4*>(G + (m0 + row) * ldg + n1_0 + cc * 8);
+            rx[i] = *reinterpret_cast<const uint4*>(X + (m0 + row) * ldx + n2_0 + cc * 8);
+        }
+    };
+    auto store = [&](char* slot) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int idx = tid + 256 * i, row = idx >> 4, cc = idx & 15;
+            const int off = (cc >> 3) * 8192 + row * 128 + bswz(row, cc & 7) * 16;
+            *reinterpret_cast<uint4*>(slot + off) = rg[i];
+            *reinterpret_cast<uint4*>(slot + WTILE + off) = rx[i];
+        }
+    };
+
+    v16f acc[2][2];  // [n2 block i][n1 block j]: lane -> n1, regs -> n2
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    if (nt > 0) {
+        load(0);
+        store(smem);
+    }
+    __syncthreads();
+    for (int t = 0; t < nt; ++t) {
+        const char* gt = smem + (t & 1) * WSLOT + w1 * 8192;
+        const char* xt = smem + (t & 1) * WSLOT + WTILE + w2 * 8192;
+        if (t + 1 < nt) load(t + 1);
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+            const int kr = ks * 16 * 128;
+            v8bf a[2], b[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) a[i] = tr_frag(xt, offa[i] + kr, offb[i] + kr);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) b[j] = tr_frag(gt, offa[j] + kr, offb[j] + kr);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        }
+        if (t + 1 < nt) store(smem + ((t + 1) & 1) * WSLOT);
+        __syncthreads();
+    }
+
+    float* o = out + (int64_t)blockIdx.y * split_stride;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int64_t n1 = n1_0 + w1 * 64 + j * 32 + r;
+        const float sc = n1 < nscaled ? scale : 1.0f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int64_t n2 = n2_0 + w2 * 64 + i * 32 + 8 * g + 4 * h;
+                *reinterpret_cast<float4*>(o + n1 * ldo + n2) =
+                    make_float4(acc[i][j][4 * g] * sc, acc[i][j][4 * g + 1] * sc, acc[i][j][4 * g + 2] * sc,
+                                acc[i][j][4 * g + 3] * sc);
+            }
+    }
+}
+
+// out[n1][n2] = sum_z ws[z][n1][n2] (the scale was applied per split)
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, int64_t n4, int splits,
+                                                           int64_t N2, float* __restrict__ out, int64_t ldo) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n4) return;
+    const float4* w = reinterpret_cast<const float4*>(ws);
+    float4 s = w[i];
+    for (int z = 1; z < splits; ++z) {
+        const float4 v = w[(int64_t)z * n4 + i];
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    const int64_t e = i * 4, n1 = e / N2, n2 = e - n1 * N2;
+    *reinterpret_cast<float4*>(out + n1 * ldo + n2) = s;
+}
+
+// ---------------------------------------------------------------------------------
+// Classifier head backward (one workgroup, B clips in order: deterministic).
+// Forward per clip: y = LN(x[b*S]) (final layernorm on the CLS row), logits = Wc y + bc.
+// Given dlogits: dWc += dl (x) y, dbc += dl, dy = Wc^T dl, dgamma += dy*xhat, dbeta += dy,
+// dx[b*S] = LN backward of dy (written; the dx rows of other tokens are left untouched).
+// D <= 1024 (4 columns per thread).
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ float block_sum(float v, float* red) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ void __launch_bounds__(256) cls_head_bwd_kernel(const float* __restrict__ x, int64_t ldx, int B, int64_t S,
+                                                           int D, const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, float eps,
+                                                           const float* __restrict__ Wc, int nl,
+                                                           const float* __restrict__ dlogits, float* __restrict__ dx,
+                                                           int64_t lddx, uint16_t* __restrict__ dxb, int64_t lddxb,
+                                                           float* __restrict__ dWc, float* __restrict__ dbc,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta) {
+    __shared__ float red[4];
+    const int tid = threadIdx.x;
+    float dg[4] = {0.f, 0.f, 0.f, 0.f}, dbt[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < nl; ++c)
+        for (int k = 0; k < 4; ++k) {
+            const int n = tid + 256 * k;
+            if (n < D) dWc[c * D + n] = 0.f;
+        }
+    for (int b = 0; b < B; ++b) {
+        const float* xr = x + (int64_t)b * S * ldx;
+        float xv[4];
+        float s = 0.f;
+        for (int k = 0; k < 4; ++k) {
+            const int n = tid + 256 * k;
+            xv[k] = n < D ? xr[n] : 0.f;
+            s += xv[k];
+        }
+        const float mean = block_sum(s, red) / (float)D;
+        float q = 0.f;
+        for (int k = 0; k < 4; ++k) {
+            const int n = tid + 256 * k;
+            if (n < D) q += (xv[k] - mean) * (xv[k] - mean);
+        }
+        const float rstd = rsqrtf(block_sum(q, red) / (float)D + eps);
+        float gdy[4], s1 = 0.f, s2 = 0.f;
+        for (int k = 0; k < 4; ++k) {
+            const int n = tid + 256 * k;
+            gdy[k] = 0.f;
+            if (n < D) {
+                xv[k] = (xv[k] - mean) * rstd;  // xhat
+                const float y = xv[k] * gamma[n] + beta[n];
+                float dy = 0.f;
+                for (int c = 0; c < nl; ++c) {
+                    const float dl = dlogits[b * nl + c];
+                    dWc[c * D + n] += dl * y;
+                    dy += dl * Wc[c * D + n];
+                }
+                dg[k] += dy * xv[k];
+                dbt[k] += dy;
+                gdy[k] = dy * gamma[n];
+                s1 += gdy[k];
+                s2 += gdy[k] * xv[k];
+            }
+        }
+        const float c1 = block_sum(s1, red) / (float)D;
+        const float c2 = block_sum(s2, red) / (float)D;
+        for (int k = 0; k < 4; ++k) {
+            const int n = tid + 256 * k;
+            if (n < D) {
+                const float v = rstd * (gdy[k] - c1 - xv[k] * c2);
+                dx[(int64_t)b * S * lddx + n] = v;
+                dxb[(int64_t)b * S * lddxb + n] = f2bf(v);
+            }
+        }
+    }
+    for (int k = 0; k < 4; ++k) {
+        const int n = tid + 256 * k;
+        if (n < D) { dgamma[n] = dg[k]; dbeta[n] = dbt[k]; }
+    }
+    if (tid < nl) {
+        float s = 0.f;
+        for (int b = 0; b < B; ++b) s += dlogits[b * nl + tid];
+        dbc[tid] = s;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Embedding backward: dpos[s] = sum_b dx[b*S + s]; dcls = dpos[0];
+// demb[b*(S-1) + p] = bf16(dx[b*S + 1 + p]) (the patch rows, for the embed weight gradient).
+// ---------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) embed_bwd_kernel(const float* __restrict__ dx, int64_t lddx, int B, int64_t S,
+                                                        int D, float* __restrict__ dpos, float* __restrict__ dcls,
+                                                        uint16_t* __restrict__ demb, int64_t ldde) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int d4 = D / 4;
+    if (i >= S * d4) return;
+    const int64_t s = i / d4;
+    const int c = (int)(i - s * d4) * 4;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int b = 0; b < B; ++b) {
+        const float4 v = *reinterpret_cast<const float4*>(dx + ((int64_t)b * S + s) * lddx + c);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        if (s >= 1) {
+            uint2 o;
+            o.x = pack2bf(v.x, v.y);
+            o.y = pack2bf(v.z, v.w);
+            *reinterpret_cast<uint2*>(demb + ((int64_t)b * (S - 1) + s - 1) * ldde + c) = o;
+        }
+    }
+    *reinterpret_cast<float4*>(dpos + s * D + c) = acc;
+    if (s == 0) *reinterpret_cast<float4*>(dcls + c) = acc;
+}
+
+// ---------------------------------------------------------------------------------
+// AdamW over flat fp32 buffers, the arithmetic of torch.optim.AdamW (decoupled decay):
+//   p *= 1 - lr*wd;  m += (1-b1)(g - m);  v = b2 v + (1-b2) g^2;
+//   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+// ---------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v, int64_t n, float lr,
+                                                    float b1, float b2, float eps, float wd, float step_size,
+                                                    float bc2_sqrt, float gscale) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+        const float gg = g[i] * gscale;
+        float pp = p[i] * (1.0f - lr * wd);
+        float mm = m[i];
+        mm = mm + (1.0f - b1) * (gg - mm);
+        const float vv = v[i] * b2 + (1.0f - b2) * gg * gg;
+        const float denom = sqrtf(vv) / bc2_sqrt + eps;
+        pp = pp - step_size * (mm / denom);
+        p[i] = pp;
+        m[i] = mm;
+        v[i] = vv;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Weight packing after each optimizer step: fp32 master [N][K] -> bf16 [N][K] and/or
+// bf16 [K][N] (the dgrad GEMMs' operand), rows < nscaled multiplied by `scale` (the
+// softmax scale * log2 e folded into the q projection).  64 x 64 tiles through LDS.
+// ---------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) pack_weight_kernel(const float* __restrict__ src, int64_t N, int64_t K,
+                                                          int64_t nscaled, float scale, uint16_t* __restrict__ dst,
+                                                          uint16_t* __restrict__ dstT) {
+    __shared__ float tile[64][65];
+    const int64_t n0 = (int64_t)blockIdx.y * 64, k0 = (int64_t)blockIdx.x * 64;
+    for (int i = threadIdx.x; i < 4096; i += 256) {
+        const int rr = i >> 6, cc = i & 63;
+        const int64_t n = n0 + rr, k = k0 + cc;
+        float v = 0.f;
+        if (n < N && k < K) {
+            v = src[n * K + k];
+            if (n < nscaled) v *= scale;
+            if (dst) dst[n * K + k] = f2bf(v);
+        }
+        tile[rr][cc] = v;
+    }
+    if (!dstT) return;
+    __syncthreads();
+    for (int i = threadIdx.x; i < 4096; i += 256) {
+        const int rr = i >> 6, cc = i & 63;  // rr: k, cc: n
+        const int64_t k = k0 + rr, n = n0 + cc;
+        if (n < N && k < K) dstT[k * N + n] = f2bf(tile[cc][rr]);
+    }
+}
+
+}  // namespace trn
+}  // namespace vc
+
+using namespace vc;
+using namespace vc::trn;
+
+extern "C" {
+
+int vc_layernorm_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx, int64_t M, int64_t D,
+                     const float* gamma, float eps, float* dx, int64_t lddx, uint16_t* dxb, int64_t lddxb,
+                     float* dgamma, float* dbeta, float* work, int64_t work_elems, hipStream_t stream) {
+    if (!dy || !x || !gamma || !dx || !dxb || !dgamma || !dbeta || !work)
+        return fail(VC_ERR_INVALID_ARG, "vc_layernorm_bwd: null pointer");
+    if (D != 256 && D != 512 && D != 768 && D != 1024)
+        return fail(VC_ERR_UNSUPPORTED, "vc_layernorm_bwd: D must be 256, 512, 768 or 1024");
+    if (lddy % 4 || ldx % 4 || lddx % 4 || lddxb % 4 || M <= 0)
+        return fail(VC_ERR_INVALID_ARG, "vc_layernorm_bwd: leading dimensions must be multiples of 4");
+    int64_t nb = (M + 3) / 4;
+    if (nb > 512) nb = 512;
+    const int64_t need = nb * 2 * D + 16 * 2 * D;
+    if (work_elems < need) return fail(VC_ERR_INVALID_ARG, "vc_layernorm_bwd: work too small (need " + std::to_string(need) + ")");
+    switch (D) {
+        case 256: ln_bwd_kernel<1><<<(unsigned)nb, 256, 0, stream>>>(dy, lddy, x, ldx, gamma, eps, M, dx, lddx, dxb, lddxb, work); break;
+        case 512: ln_bwd_kernel<2><<<(unsigned)nb, 256, 0, stream>>>(dy, lddy, x, ldx, gamma, eps, M, dx, lddx, dxb, lddxb, work); break;
+        case 768: ln_bwd_kernel<3><<<(unsigned)nb, 256, 0, stream>>>(dy, lddy, x, ldx, gamma, eps, M, dx, lddx, dxb, lddxb, work); break;
+        default: ln_bwd_kernel<4><<<(unsigned)nb, 256, 0, stream>>>(dy, lddy, x, ldx, gamma, eps, M, dx, lddx, dxb, lddxb, work); break;
+    }
+    colsum_launch<float>(work, 2 * D, nb, 2 * D, dgamma, D, dbeta, 0, 1.0f, work + nb * 2 * D, 16 * 2 * D, stream);
+    return check_launch("vc_layernorm_bwd");
+}
+
+int vc_colsum(const void* in, int dtype, int64_t ld, int64_t R, int64_t N, int64_t nscaled, float scale, float* out,
+              float* work, int64_t work_elems, hipStream_t stream) {
+    if (!in || !out) return fail(VC_ERR_INVALID_ARG, "vc_colsum: null pointer");
+    if (R <= 0 || N <= 0 || ld < N) return fail(VC_ERR_INVALID_ARG, "vc_colsum: bad shape");
+    if (!work) work_elems = 0;
+    if (dtype == 0)
+        colsum_launch<float>((const float*)in, ld, R, N, out, N, nullptr, nscaled, scale, work, work_elems, stream);
+    else if (dtype == 1)
+        colsum_launch<uint16_t>((const uint16_t*)in, ld, R, N, out, N, nullptr, nscaled, scale, work, work_elems, stream);
+    else
+        return fail(VC_ERR_INVALID_ARG, "vc_colsum: dtype must be 0 (f32) or 1 (bf16)");
+    return check_launch("vc_colsum");
+}
+
+int vc_wgrad_bf16(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, int64_t M, int64_t N1, int64_t N2,
+                  int64_t nscaled, float scale, float* out, int64_t ldo, float* work, int64_t work_elems,
+                  hipStream_t stream) {
+    if (!G || !X || !out) return fail(VC_ERR_INVALID_ARG, "vc_wgrad_bf16: null pointer");
+    if (M <= 0 || M % 64 || N1 % 128 || N2 % 128 || N1 <= 0 || N2 <= 0)
+        return fail(VC_ERR_INVALID_ARG, "vc_wgrad_bf16: need M % 64 == 0, N1 % 128 == 0, N2 % 128 == 0");
+    if (ldg % 8 || ldx % 8 || ldo % 4 || ldg < N1 || ldx < N2 || ldo < N2 ||
+        ((((uintptr_t)G) | ((uintptr_t)X) | ((uintptr_t)out)) & 15))
+        return fail(VC_ERR_INVALID_ARG, "vc_wgrad_bf16: bad leading dimension / alignment");
+    const int nI = (int)(N1 / 128), nJ = (int)(N2 / 128);
+    const int ntiles = nI * nJ;
+    const int64_t kt = M / 64;
+    int64_t splits = (512 + ntiles - 1) / ntiles;
+    if (splits > kt / 2) splits = kt / 2;
+    if (!work || work_elems < 2 * N1 * N2) splits = 1;
+    else if (splits * N1 * N2 > work_elems) splits = work_elems / (N1 * N2);
+    if (splits < 1) splits = 1;
+    const int64_t mchunk = (kt + splits - 1) / splits * 64;
+    splits = (M + mchunk - 1) / mchunk;
+    if (splits == 1) {
+        wgrad_kernel<<<dim3((unsigned)ntiles, 1), 256, 0, stream>>>(G, ldg, X, ldx, M, nJ, mchunk, out, ldo, 0, nscaled,
+                                                                  scale);
+    } else {
+        wgrad_kernel<<<dim3((unsigned)ntiles, (unsigned)splits), 256, 0, stream>>>(G, ldg, X, ldx, M, nJ, mchunk, work,
+                                                                                 N2, N1 * N2, nscaled, scale);
+        const int64_t n4 = N1 * N2 / 4;
+        wgrad_reduce_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, stream>>>(work, n4, (int)splits, N2, out, ldo);
+    }
+    return check_launch("vc_wgrad_bf16");
+}
+
+int vc_cls_head_bwd(const float* x, int64_t ldx, int64_t B, int64_t S, int64_t D, const float* gamma, const float* beta,
+                    float eps, const float* Wc, int64_t num_labels, const float* dlogits, float* dx, int64_t lddx,
+                    uint16_t* dxb, int64_t lddxb, float* dWc, float* dbc, float* dgamma, float* dbeta,
+                    hipStream_t stream) {
+    if (!x || !gamma || !beta || !Wc || !dlogits || !dx || !dxb || !dWc || !dbc || !dgamma || !dbeta)
+        return fail(VC_ERR_INVALID_ARG, "vc_cls_head_bwd: null pointer");
+    if (D > 1024 || num_labels > 256 || B <= 0) return fail(VC_ERR_UNSUPPORTED, "vc_cls_head_bwd: D <= 1024, labels <= 256");
+    cls_head_bwd_kernel<<<1, 256, 0, stream>>>(x, ldx, (int)B, S, (int)D, gamma, beta, eps, Wc, (int)num_labels, dlogits,
+                                               dx, lddx, dxb, lddxb, dWc, dbc, dgamma, dbeta);
+    return check_launch("vc_cls_head_bwd");
+}
+
+int vc_embed_bwd(const float* dx, int64_t lddx, int64_t B, int64_t S, int64_t D, float* dpos, float* dcls,
+                 uint16_t* demb, int64_t ldde, hipStream_t stream) {
+    if (!dx || !dpos || !dcls || !demb) return fail(VC_ERR_INVALID_ARG, "vc_embed_bwd: null pointer");
+    if (D % 4 || lddx % 4 || ldde % 4 || S < 2 || ((uintptr_t)dx & 15) || ((uintptr_t)dpos & 15) || ((uintptr_t)dcls & 15))
+        return fail(VC_ERR_INVALID_ARG, "vc_embed_bwd: D % 4, alignment");
+    const int64_t n = S * (D / 4);
+    embed_bwd_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(dx, lddx, (int)B, S, (int)D, dpos, dcls, demb, ldde);
+    return check_launch("vc_embed_bwd");
+}
+
+int vc_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr, float beta1,
+             float beta2, float eps, float weight_decay, int64_t step, float grad_scale, hipStream_t stream) {
+    if (!param || !grad || !exp_avg || !exp_avg_sq) return fail(VC_ERR_INVALID_ARG, "vc_adamw: null pointer");
+    if (n <= 0 || step <= 0) return fail(VC_ERR_INVALID_ARG, "vc_adamw: n > 0, step >= 1");
+    const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+    const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+    const float step_size = (float)(lr / bc1);
+    const float bc2_sqrt = (float)std::sqrt(bc2);
+    int64_t nb = (n + 255) / 256;
+    if (nb > 8192) nb = 8192;
+    adamw_kernel<<<(unsigned)nb, 256, 0, stream>>>(param, grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps,
+                                                   weight_decay, step_size, bc2_sqrt, grad_scale);
+    return check_launch("vc_adamw");
+}
+
+int vc_pack_weight(const float* src, int64_t N, int64_t K, int64_t nscaled, float scale, uint16_t* dst, uint16_t* dstT,
+                   hipStream_t stream) {
+    if (!src || (!dst && !dstT)) return fail(VC_ERR_INVALID_ARG, "vc_pack_weight: null pointer");
+    if (N <= 0 || K <= 0) return fail(VC_ERR_INVALID_ARG, "vc_pack_weight: bad shape");
+    dim3 grid((unsigned)((K + 63) / 64), (unsigned)((N + 63) / 64));
+    pack_weight_kernel<<<grid, 256, 0, stream>>>(src, N, K, nscaled, scale, dst, dstT);
+    return check_launch("vc_pack_weight");
+}
+
+}  // extern "C"

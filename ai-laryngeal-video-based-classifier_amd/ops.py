@@ -12,7 +12,7 @@ import torch
 from . import _lib
 
 EPI = {"bias": 0, "bias_gelu_tanh": 1, "bias_gelu_erf": 2, "bias_resid_f32": 3, "embed_f32": 4, "bias_f32": 5,
-       "bias_relu": 6, "bias_resid_relu": 7}
+       "bias_relu": 6, "bias_resid_relu": 7, "bias_add_f32": 8, "bias_gelu_tanh_save": 9, "dgelu_tanh": 10}
 GATHER_KIND = {"u8": 0, "f32": 1, "bf16": 2}
 
 
@@ -93,13 +93,16 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: str, ou
     _need(a.stride(1) == 1 and w.stride(1) == 1 and out.stride(-1) == 1 and w.shape[1] == K, "gemm layout")
     _need(bias.numel() == N and bias.is_contiguous(), "gemm bias")
     e = EPI[epilogue]
-    if e in (0, 1, 2, 6, 7):
+    if e in (0, 1, 2, 6, 7, 9, 10):
         _need(out.dtype == torch.bfloat16, "gemm out must be bf16 for this epilogue")
     else:
         _need(out.dtype == torch.float32, "gemm out must be f32 for this epilogue")
-    if e == 7:
+    if e in (7, 9, 10):
         _need(aux is not None and aux.dtype == torch.bfloat16 and aux.stride(1) == 1 and aux.shape[0] >= M and
-              aux.shape[1] >= N, "resid_relu: aux must be the bf16 residual [>= M, >= N]")
+              aux.shape[1] >= N, f"{epilogue}: aux must be bf16 [>= M, >= N]")
+    if e == 8:
+        _need(aux is not None and aux.dtype == torch.float32 and aux.stride(1) == 1 and aux.shape[0] >= M and
+              aux.shape[1] >= N, "bias_add_f32: aux must be the f32 residual [>= M, >= N]")
     if e == 4:
         _need(aux is not None and aux.dtype == torch.float32 and aux.stride(1) == 1 and group > 0, "embed aux")
         _need((M - 1) // group * group_stride + group_offset + (M - 1) % group < out.shape[0], "embed out rows")
@@ -358,3 +361,128 @@ def mlp_head(h: torch.Tensor, B: int, w1, b1, w2, b2, out: torch.Tensor) -> torc
     _lib.call("vc_mlp_head", _p(h), B, w1.shape[1], _p(w1), _p(b1), w1.shape[0], _p(w2), _p(b2), w2.shape[0], _p(out),
               _stream(h))
     return out
+
+
+# ---- train step -----------------------------------------------------------
+
+def attention_fwd_lse(qkv: torch.Tensor, B: int, S: int, H: int, out: torch.Tensor, lse: torch.Tensor,
+                      scale: float = 0.125, q_prescaled: bool = True) -> torch.Tensor:
+    """vc_attention_fwd that also stores the base-2 log-sum-exp lse f32 [B*H*S]."""
+    _dev(qkv, out, lse)
+    _need(lse.dtype == torch.float32 and lse.is_contiguous() and lse.numel() >= B * H * S, "lse: f32 [B*H*S]")
+    _need(qkv.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and qkv.stride(1) == 1 and out.stride(1) == 1,
+          "attention dtypes/layout")
+    _need(qkv.shape[1] >= 3 * H * 64 and out.shape[1] >= H * 64, "attention columns")
+    _need(qkv.shape[0] >= (B - 1) * S + (S + 63) // 64 * 64, "attention: qkv needs row padding to a 64-key tile")
+    _need(out.shape[0] >= B * S, "attention out rows")
+    _lib.call("vc_attention_fwd_lse", _p(qkv), qkv.stride(0), B, S, H, 64, scale, int(bool(q_prescaled)), _p(out),
+              out.stride(0), _p(lse), _stream(qkv))
+    return out
+
+
+def attention_bwd(qkv: torch.Tensor, out: torch.Tensor, dout: torch.Tensor, lse: torch.Tensor, delta: torch.Tensor,
+                  B: int, S: int, H: int, dqkv: torch.Tensor) -> torch.Tensor:
+    """dqkv (q part = dL/dq' of the stored pre-scaled q', then dk, dv) of the joint attention."""
+    _dev(qkv, out, dout, lse, delta, dqkv)
+    for t, nm in ((qkv, "qkv"), (out, "out"), (dout, "dout"), (dqkv, "dqkv")):
+        _need(t.dtype == torch.bfloat16 and t.stride(1) == 1, f"attention_bwd: {nm} bf16 with unit column stride")
+    _need(lse.dtype == torch.float32 and delta.dtype == torch.float32 and lse.numel() >= B * H * S and
+          delta.numel() >= B * H * S, "attention_bwd: lse / delta f32 [B*H*S]")
+    pad = (B - 1) * S + (S + 63) // 64 * 64
+    _need(qkv.shape[0] >= pad and dout.shape[0] >= pad, "attention_bwd: qkv / dout need row padding to a 64-row tile")
+    _need(out.shape[0] >= B * S and dqkv.shape[0] >= B * S, "attention_bwd rows")
+    _need(qkv.shape[1] >= 3 * H * 64 and dqkv.shape[1] >= 3 * H * 64 and out.shape[1] >= H * 64 and
+          dout.shape[1] >= H * 64, "attention_bwd columns")
+    _lib.call("vc_attention_bwd", _p(qkv), qkv.stride(0), _p(out), out.stride(0), _p(dout), dout.stride(0), _p(lse),
+              _p(delta), B, S, H, 64, _p(dqkv), dqkv.stride(0), _stream(qkv))
+    return dqkv
+
+
+def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, gamma: torch.Tensor, eps: float, dx: torch.Tensor,
+                  dxb: torch.Tensor, dgamma: torch.Tensor, dbeta: torch.Tensor, work: torch.Tensor,
+                  m: int | None = None) -> torch.Tensor:
+    """dx += LayerNorm backward of dy (f32, in place), dxb = bf16(dx); dgamma / dbeta overwritten."""
+    _dev(dy, x, gamma, dx, dxb, dgamma, dbeta, work)
+    M = x.shape[0] if m is None else m
+    D = gamma.numel()
+    _need(dy.dtype == torch.float32 and x.dtype == torch.float32 and dx.dtype == torch.float32 and
+          dxb.dtype == torch.bfloat16 and work.dtype == torch.float32, "layernorm_bwd dtypes")
+    _need(all(t.shape[0] >= M and t.shape[1] >= D and t.stride(1) == 1 for t in (dy, x, dx, dxb)), "layernorm_bwd shapes")
+    _need(dgamma.numel() == D and dbeta.numel() == D and dgamma.is_contiguous() and dbeta.is_contiguous(),
+          "layernorm_bwd dgamma/dbeta")
+    _lib.call("vc_layernorm_bwd", _p(dy), dy.stride(0), _p(x), x.stride(0), M, D, _p(gamma), eps, _p(dx), dx.stride(0),
+              _p(dxb), dxb.stride(0), _p(dgamma), _p(dbeta), _p(work), work.numel(), _stream(x))
+    return dx
+
+
+def colsum(x: torch.Tensor, out: torch.Tensor, work: torch.Tensor | None = None, m: int | None = None,
+           nscaled: int = 0, scale: float = 1.0) -> torch.Tensor:
+    """out[n] = s(n) * sum over the first m rows of x[:, n] (x f32 or bf16 2-D, unit column stride)."""
+    _dev(x, out)
+    R = x.shape[0] if m is None else m
+    N = out.numel()
+    _need(x.dtype in (torch.float32, torch.bfloat16) and x.dim() == 2 and x.stride(1) == 1 and x.shape[1] >= N and
+          x.shape[0] >= R, "colsum input")
+    _need(out.dtype == torch.float32 and out.is_contiguous(), "colsum out f32")
+    wp, wn = (_p(work), work.numel()) if work is not None else (None, 0)
+    _lib.call("vc_colsum", _p(x), 0 if x.dtype == torch.float32 else 1, x.stride(0), R, N, nscaled, scale, _p(out), wp,
+              wn, _stream(x))
+    return out
+
+
+def wgrad(g: torch.Tensor, x: torch.Tensor, out: torch.Tensor, work: torch.Tensor | None = None,
+          nscaled: int = 0, scale: float = 1.0, m: int | None = None) -> torch.Tensor:
+    """out[n1][n2] = s(n1) * sum_m g[m][n1] x[m][n2]  (g bf16 [M, N1], x bf16 [M, N2], out f32 [N1, N2])."""
+    _dev(g, x, out)
+    M = g.shape[0] if m is None else m
+    N1, N2 = out.shape
+    _need(g.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and out.dtype == torch.float32, "wgrad dtypes")
+    _need(g.stride(1) == 1 and x.stride(1) == 1 and out.stride(1) == 1 and g.shape[1] >= N1 and x.shape[1] >= N2 and
+          g.shape[0] >= M and x.shape[0] >= M, "wgrad shapes")
+    wp, wn = (_p(work), work.numel()) if work is not None else (None, 0)
+    _lib.call("vc_wgrad_bf16", _p(g), g.stride(0), _p(x), x.stride(0), M, N1, N2, nscaled, scale, _p(out),
+              out.stride(0), wp, wn, _stream(g))
+    return out
+
+
+def cls_head_bwd(x, B, S, gamma, beta, eps, wc, dlogits, dx, dxb, dwc, dbc, dgamma, dbeta):
+    _dev(x, gamma, beta, wc, dlogits, dx, dxb, dwc, dbc, dgamma, dbeta)
+    D = gamma.numel()
+    nl = wc.shape[0]
+    _need(dlogits.dtype == torch.float32 and dlogits.is_contiguous() and tuple(dlogits.shape) == (B, nl),
+          "cls_head_bwd dlogits f32 [B, nl]")
+    _need(x.shape[0] >= B * S and dx.shape[0] >= B * S and dxb.shape[0] >= B * S, "cls_head_bwd rows")
+    _lib.call("vc_cls_head_bwd", _p(x), x.stride(0), B, S, D, _p(gamma), _p(beta), eps, _p(wc), nl, _p(dlogits),
+              _p(dx), dx.stride(0), _p(dxb), dxb.stride(0), _p(dwc), _p(dbc), _p(dgamma), _p(dbeta), _stream(x))
+
+
+def embed_bwd(dx: torch.Tensor, B: int, S: int, dpos: torch.Tensor, dcls: torch.Tensor, demb: torch.Tensor):
+    _dev(dx, dpos, dcls, demb)
+    D = dcls.numel()
+    _need(dx.dtype == torch.float32 and dx.shape[0] >= B * S and dx.stride(1) == 1, "embed_bwd dx")
+    _need(dpos.dtype == torch.float32 and dpos.is_contiguous() and dpos.numel() == S * D, "embed_bwd dpos")
+    _need(demb.dtype == torch.bfloat16 and demb.shape[0] >= B * (S - 1) and demb.shape[1] >= D and demb.stride(1) == 1,
+          "embed_bwd demb")
+    _lib.call("vc_embed_bwd", _p(dx), dx.stride(0), B, S, D, _p(dpos), _p(dcls), _p(demb), demb.stride(0), _stream(dx))
+
+
+def adamw(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0):
+    _dev(param, grad, exp_avg, exp_avg_sq)
+    n = param.numel()
+    _need(all(t.dtype == torch.float32 and t.is_contiguous() and t.numel() == n for t in
+              (param, grad, exp_avg, exp_avg_sq)), "adamw: contiguous f32 buffers of one size")
+    _lib.call("vc_adamw", _p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), n, lr, beta1, beta2, eps, weight_decay,
+              int(step), grad_scale, _stream(param))
+
+
+def pack_weight(src: torch.Tensor, dst: torch.Tensor | None = None, dst_t: torch.Tensor | None = None,
+                nscaled: int = 0, scale: float = 1.0):
+    _dev(src)
+    N, K = src.shape
+    _need(src.dtype == torch.float32 and src.is_contiguous(), "pack_weight src f32 contiguous [N, K]")
+    if dst is not None:
+        _need(dst.dtype == torch.bfloat16 and dst.is_contiguous() and tuple(dst.shape) == (N, K), "pack_weight dst")
+    if dst_t is not None:
+        _need(dst_t.dtype == torch.bfloat16 and dst_t.is_contiguous() and tuple(dst_t.shape) == (K, N), "pack_weight dst_t")
+    _lib.call("vc_pack_weight", _p(src), N, K, nscaled, scale, _p(dst) if dst is not None else None,
+              _p(dst_t) if dst_t is not None else None, _stream(src))

@@ -90,6 +90,13 @@ int vc_patch_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C, 
 #define VC_EPI_BIAS_RELU_BF16   6  /* out bf16[m][n]  = relu(acc + bias[n])       (conv + BN + ReLU)    */
 #define VC_EPI_BIAS_RESID_RELU_BF16 7 /* out bf16[m][n] = relu(acc + bias[n] + res[m][n]), res = (const
                                        uint16_t*)aux bf16 with row stride ldaux (bottleneck conv_c + skip) */
+/* Training epilogues (ViViT train step; block configs 0-2 only): */
+#define VC_EPI_BIAS_ADD_F32     8  /* out f32 [m][n]  = aux[m][n] + acc + bias[n]  (residual into a new buffer,
+                                       so the layer input stays saved for the backward)                    */
+#define VC_EPI_BIAS_GELU_TANH_SAVE 9 /* out bf16[m][n] = gelu_fast(acc + bias[n]); (uint16_t*)aux[m][n] =
+                                       bf16(acc + bias[n]), the pre-activation kept for the backward      */
+#define VC_EPI_DGELU_TANH      10  /* out bf16[m][n]  = (acc + bias[n]) * gelu_fast'((uint16_t*)aux[m][n]):
+                                       the fc2 dgrad fused with the gelu backward                          */
 
 /*
  * C[M][N] = A[M][K] . W[N][K]^T  (bf16 inputs, fp32 accumulate on MFMA), fused epilogue.
@@ -302,6 +309,88 @@ int vc_patch_merge_layernorm(const float* x, int64_t ldx, int64_t B, int64_t T, 
 int vc_pool_head(const float* x, int64_t ldx, int64_t B, int64_t ntok, int64_t D, const float* gamma,
                  const float* beta, float eps, const float* Wc, const float* bc, int64_t num_labels, float* logits,
                  float* work, hipStream_t stream);
+
+/* ---- ViViT train step: trainers/trainer.py:140-146 — forward, CE loss,
+ * loss.backward(), AdamW.step() — and its data-parallel gradient all-reduce (§8e) ----------- */
+
+/*
+ * vc_attention_fwd + lse[(b*H + h)*S + q] = base-2 log-sum-exp of q's scaled scores (f32), kept
+ * for the backward.  Requires the same row padding as vc_attention_fwd.
+ */
+int vc_attention_fwd_lse(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, int64_t head_dim,
+                         float scale, int q_prescaled, uint16_t* out, int64_t ldo, float* lse, hipStream_t stream);
+
+/*
+ * Attention backward (autograd of eager_attention_forward, TF5/models/vivit/modeling_vivit.py:
+ * 149-174).  qkv: the forward's q'|k|v rows (q' = q*scale*log2 e, q_prescaled); out: the forward
+ * output O; dout: dL/dO (same layout as out); lse from vc_attention_fwd_lse; delta: caller
+ * scratch f32 [B*H*S].  Writes dqkv (layout of qkv): the q part is dL/dq' (the gradient of the
+ * STORED q'), then dL/dk, dL/dv; rows of a clip past S are not written.  dout rows must be
+ * readable to (B-1)*S + roundup(S,64) - 1, as qkv.  Deterministic (no atomics).
+ */
+int vc_attention_bwd(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ldo, const uint16_t* dout,
+                     int64_t lddo, const float* lse, float* delta, int64_t B, int64_t S, int64_t H, int64_t head_dim,
+                     uint16_t* dqkv, int64_t lddq, hipStream_t stream);
+
+/*
+ * LayerNorm backward fused with the residual-gradient add (nn.LayerNorm layernorm_before /
+ * layernorm_after backward, TF5/.../modeling_vivit.py:245-266):
+ * dx[m] += LN'(x[m]) . dy[m] (f32, in place), dxb[m] = bf16(dx[m]); dgamma / dbeta = column
+ * sums over the M rows (overwritten).  D in {256, 512, 768, 1024};
+ * work: f32 scratch of >= (min(512, ceil(M/4)) + 16) * 2D elements.
+ */
+int vc_layernorm_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx, int64_t M, int64_t D,
+                     const float* gamma, float eps, float* dx, int64_t lddx, uint16_t* dxb, int64_t lddxb,
+                     float* dgamma, float* dbeta, float* work, int64_t work_elems, hipStream_t stream);
+
+/*
+ * out[n] = (n < nscaled ? scale : 1) * sum over R rows of in[r][n]; dtype 0 = f32, 1 = bf16
+ * (bias gradients of nn.Linear).  work: optional f32 scratch (row-split partials), deterministic.
+ */
+int vc_colsum(const void* in, int dtype, int64_t ld, int64_t R, int64_t N, int64_t nscaled, float scale, float* out,
+              float* work, int64_t work_elems, hipStream_t stream);
+
+/*
+ * Weight gradient of nn.Linear / the tubelet Conv3d: out[n1][n2] = s(n1) * sum_m G[m][n1] X[m][n2]
+ * (G = output gradient, X = layer input, bf16 [M][*] row-major; fp32 out, overwritten),
+ * s(n1) = scale for n1 < nscaled (the q-scale fold), else 1.  M % 64 == 0, N1 % 128 == 0,
+ * N2 % 128 == 0.  work: f32 scratch for split-K partials (>= 2*N1*N2 enables splitting).
+ */
+int vc_wgrad_bf16(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, int64_t M, int64_t N1, int64_t N2,
+                  int64_t nscaled, float scale, float* out, int64_t ldo, float* work, int64_t work_elems,
+                  hipStream_t stream);
+
+/*
+ * Backward of the final LayerNorm on the CLS rows + classifier (TF5/.../modeling_vivit.py:427,556)
+ * given dlogits f32 [B][num_labels]: writes dx / dxb of the B CLS rows (row b*S; other rows are
+ * not touched), dWc [num_labels][D], dbc, dgamma, dbeta (all overwritten).  D <= 1024.
+ */
+int vc_cls_head_bwd(const float* x, int64_t ldx, int64_t B, int64_t S, int64_t D, const float* gamma, const float* beta,
+                    float eps, const float* Wc, int64_t num_labels, const float* dlogits, float* dx, int64_t lddx,
+                    uint16_t* dxb, int64_t lddxb, float* dWc, float* dbc, float* dgamma, float* dbeta,
+                    hipStream_t stream);
+
+/*
+ * Embedding backward (VivitEmbeddings, TF5/.../modeling_vivit.py:126-146): dpos[s] = sum_b dx[b*S+s],
+ * dcls = dpos[0], demb[b*(S-1) + p] = bf16(dx[b*S + 1 + p]) (input of the tubelet weight gradient).
+ */
+int vc_embed_bwd(const float* dx, int64_t lddx, int64_t B, int64_t S, int64_t D, float* dpos, float* dcls,
+                 uint16_t* demb, int64_t ldde, hipStream_t stream);
+
+/*
+ * torch.optim.AdamW step (decoupled weight decay, bias-corrected) over flat f32 buffers, with the
+ * gradient multiplied by grad_scale first (1/world_size after a SUM all-reduce).  step >= 1.
+ * Replaces optimizer.step() of trainer.py:146 (AdamW, vivit_transformer/main.py:150-155).
+ */
+int vc_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr, float beta1,
+             float beta2, float eps, float weight_decay, int64_t step, float grad_scale, hipStream_t stream);
+
+/*
+ * fp32 master weight [N][K] -> bf16 [N][K] (dst) and/or bf16 [K][N] (dstT, the dgrad operand);
+ * rows < nscaled are multiplied by scale first (q projection * softmax scale * log2 e).
+ */
+int vc_pack_weight(const float* src, int64_t N, int64_t K, int64_t nscaled, float scale, uint16_t* dst, uint16_t* dstT,
+                   hipStream_t stream);
 
 #ifdef __cplusplus
 }
