@@ -25,6 +25,7 @@ import numpy as np
 import torch
 
 from . import ops
+from .vivit_train import FlatLayout, TrainEngine, VivitTrainFn
 from .weights import vivit_param_shapes
 
 
@@ -98,9 +99,16 @@ class VivitForVideoClassification(torch.nn.Module):
         if c.hidden_size // c.num_attention_heads != 64:
             raise ValueError("libvclip attention supports head_dim 64 only")
         self.params = torch.nn.ParameterDict()
-        self._names = list(vivit_param_shapes(c.as_shape_cfg()).keys())
-        for name, shape in vivit_param_shapes(c.as_shape_cfg()).items():
-            self.params[name.replace(".", "__")] = torch.nn.Parameter(torch.zeros(shape), requires_grad=False)
+        shapes = vivit_param_shapes(c.as_shape_cfg())
+        self._names = list(shapes.keys())
+        for name, shape in shapes.items():
+            self.params[name.replace(".", "__")] = torch.nn.Parameter(torch.zeros(shape))
+        self._layout = FlatLayout(c, shapes)
+        self._flat = None      # fp32 masters, one device buffer (params are views), built for training
+        self._gflat = None     # gradients, same layout (p.grad are views)
+        self._gscratch = None  # backward target when gradients accumulate across calls
+        self._engine = None
+        self.grad_ready_hooks = []  # fn(stage, start, end, gflat): a slice of gflat is final (enqueued)
         self._packed = None
         self._ws = {}
         self.kernel_events = None
@@ -131,9 +139,76 @@ class VivitForVideoClassification(torch.nn.Module):
     def P(self, name):
         return self.params[name.replace(".", "__")]
 
+    def _param_list(self):
+        return [self.P(n) for n in self._names]
+
+    def _apply(self, fn, *args, **kwargs):  # .to() / .cuda(): parameters move one by one
+        out = super()._apply(fn, *args, **kwargs)
+        self._flat = self._gflat = self._gscratch = self._engine = None
+        self._packed = None
+        self._ws = {}
+        return out
+
+    # ---- training (vclip_amd/vivit_train.py) --------------------------
+    def _ensure_flat(self, device):
+        """Move the fp32 masters into one flat device buffer, parameters becoming views of it
+        (the same Parameter objects, so an optimizer built earlier keeps working)."""
+        if self._flat is not None and self._flat.device == device:
+            return
+        flat = torch.zeros(self._layout.total, dtype=torch.float32, device=device)
+        with torch.no_grad():
+            for n in self._names:
+                v = self._layout.view(flat, n)
+                v.copy_(self.P(n).detach().reshape(v.shape))
+                self.P(n).data = v
+        self._flat = flat
+        self._gflat = torch.zeros_like(flat)
+        self._gscratch = None
+        self._engine = None
+
+    def _train_engine(self, B, device):
+        self._ensure_flat(device)
+        if self._engine is None or self._engine.B != B or self._engine.device != device:
+            self._engine = None
+            self._engine = TrainEngine(self, B, device)
+        return self._engine
+
+    def _run_backward(self, eng, dlogits):
+        params = self._param_list()
+        accumulate = any(p.grad is not None for p in params)
+        if not accumulate:
+            target = self._gflat
+        else:
+            if self._gscratch is None:
+                self._gscratch = torch.zeros_like(self._gflat)
+            target = self._gscratch
+
+        def ready(stage, start, end):
+            if not accumulate:
+                for h in self.grad_ready_hooks:
+                    h(stage, start, end, target)
+
+        eng.backward(dlogits, target, ready)
+        lay = self._layout
+        if not accumulate:
+            for n, p in zip(self._names, params):
+                p.grad = lay.view(self._gflat, n)
+            return
+        for n, p in zip(self._names, params):
+            g = lay.view(target, n)
+            if p.grad is None:
+                p.grad = lay.view(self._gflat, n).copy_(g)
+            else:
+                p.grad.add_(g)
+
+    def _weights_version(self):
+        from . import vivit_train
+        return (vivit_train.MASTER_EPOCH[0], sum(p._version for p in self._param_list()))
+
     # ---- device packing ----------------------------------------------------------
     def _pack(self, device):
-        if self._packed is not None and self._packed["device"] == device:
+        ver = self._weights_version()
+        if self._packed is not None and self._packed["device"] == device and self._packed["version"] == ver:
             return self._packed
         c = self.config
         bf = torch.bfloat16
@@ -141,7 +216,7 @@ class VivitForVideoClassification(torch.nn.Module):
         P = lambda n: self.P(n).detach().to(device)  # noqa: E731
         D = c.hidden_size
         kt, kh, kw = c.tubelet_size
-        pk = {"device": device}
+        pk = {"device": device, "version": ver}
         pk["w_emb"] = P("vivit.embeddings.patch_embeddings.projection.weight").reshape(D, -1).to(bf).contiguous()
         pk["b_emb"] = P("vivit.embeddings.patch_embeddings.projection.bias").to(f32).contiguous()
         pk["pos"] = P("vivit.embeddings.position_embeddings").reshape(-1, D).to(f32).contiguous()
@@ -201,7 +276,6 @@ class VivitForVideoClassification(torch.nn.Module):
         return ws
 
     # ---- forward -----------------------------------------------------------------
-    @torch.no_grad()
     def forward(self, pixel_values: torch.Tensor = None, labels: torch.Tensor = None, **kw):
         if pixel_values is None:
             raise ValueError("pixel_values required")
@@ -209,12 +283,18 @@ class VivitForVideoClassification(torch.nn.Module):
             raise RuntimeError("VivitForVideoClassification (vclip_amd) runs on the GPU only: move pixel_values "
                                "to cuda (the reference's `.to(device)`, trainer.py:92)")
         x = pixel_values.contiguous().float() if pixel_values.dtype != torch.float32 else pixel_values.contiguous()
-        logits = self.forward_logits(x)
+        params = self._param_list()
+        if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            logits = VivitTrainFn.apply(self, x, *params)  # forward saving activations; HIP backward
+        else:
+            with torch.no_grad():
+                logits = self.forward_logits(x)
         loss = None
         if labels is not None:
             loss = torch.nn.functional.cross_entropy(logits, labels.to(logits.device))
         return ClassifierOutput(logits, loss)
 
+    @torch.no_grad()
     def forward_logits(self, pix: torch.Tensor) -> torch.Tensor:
         c = self.config
         B, T, C, H, W = pix.shape
@@ -269,4 +349,5 @@ def create_model(model_name="google/vivit-b-16x2-kinetics400", num_classes=2, cl
     model = VivitForVideoClassification(cfg)
     from .weights import make_vivit_weights
     model.load_state_dict(make_vivit_weights(cfg.as_shape_cfg(), seed=weights_seed))
-    return model.to(device) if device else model
+    model = model.to(device) if device else model
+    return model.eval()  # like transformers' from_pretrained; the trainer calls model.train()

@@ -1,0 +1,155 @@
+"""ViViT train step through the drop-in model: the reference's loop
+(vivit_transformer/vivit_classifier/trainers/trainer.py:140-146 — zero_grad, model(**inputs),
+CrossEntropyLoss, loss.backward(), AdamW.step()) run on vclip_amd's model and optimizer,
+against the same loop on the fp32 oracle (oracle/vivit_ref.py, pinned to HF ViViT goldens)
+with torch autograd + torch.optim.AdamW.
+
+Tolerances: the HIP path computes in bf16 with fp32 accumulation, so per-parameter gradients
+are compared by relative L2 error (<= 5e-2) and cosine (>= 0.998) against fp32 autograd;
+losses to 1e-2 absolute (the logits' bf16 bound); AdamW trajectories by the relative error of
+each tensor's accumulated update (<= 0.1).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+SMALL = dict(image_size=32, num_frames=4, tubelet_size=[2, 16, 16], num_channels=3, hidden_size=256,
+             num_hidden_layers=2, num_attention_heads=4, intermediate_size=512, hidden_act="gelu_fast",
+             layer_norm_eps=1e-6, qkv_bias=True)
+# full ViViT-B per-layer geometry (S = 3137 tokens, D = 768, 12 heads), 2 layers to keep the CPU autograd short
+WIDE = dict(SMALL, image_size=224, num_frames=32, hidden_size=768, num_attention_heads=12, intermediate_size=3072)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vclip_amd import _lib as L
+    L.load()
+
+
+def _setup(cfg, B, seed=0):
+    from vclip_amd.vivit import VivitConfig, VivitForVideoClassification
+    from vclip_amd.weights import make_synthetic_clips, make_vivit_weights
+    sd = make_vivit_weights(cfg, seed=seed)
+    pix = make_synthetic_clips(B, cfg["num_frames"], cfg["image_size"], seed=1)
+    labels = np.random.RandomState(2).randint(0, 2, size=B)
+    model = VivitForVideoClassification(VivitConfig(**cfg, id2label={0: "non-referral", 1: "referral"}))
+    model.load_state_dict(sd)
+    model = model.to(DEV).train()
+    return model, sd, torch.from_numpy(pix), torch.from_numpy(labels).long()
+
+
+def _oracle_grads(sd, cfg, pix, labels):
+    from oracle.vivit_ref import vivit_forward
+    ref = {k: torch.from_numpy(v).clone().requires_grad_() for k, v in sd.items()}
+    logits = vivit_forward(ref, cfg, pix)
+    loss = torch.nn.functional.cross_entropy(logits, labels)
+    loss.backward()
+    return float(loss), logits.detach(), {k: v.grad for k, v in ref.items()}
+
+
+def _compare(model, ref_grads, l2_tol=5e-2, cos_tol=0.998):
+    worst = []
+    for n, p in model.hf_state_dict().items():
+        g = p.grad.detach().cpu().double().reshape(-1)
+        r = ref_grads[n].double().reshape(-1)
+        if n.endswith("k_proj.bias"):
+            # softmax is invariant to a key bias (it adds q.b_k to a whole score row): the exact
+            # gradient is 0 and both sides hold rounding noise; bound it against the key weight's
+            scale = ref_grads[n.replace("bias", "weight")].double().norm()
+            assert g.norm() < 1e-2 * scale and r.norm() < 1e-2 * scale, (n, float(g.norm()), float(scale))
+            continue
+        if r.norm() < 1e-12:
+            assert g.norm() < 1e-6, n
+            continue
+        l2 = float((g - r).norm() / r.norm())
+        cos = float(g @ r / (g.norm() * r.norm()))
+        worst.append((l2, n, cos))
+        assert l2 < l2_tol and cos > cos_tol, (n, l2, cos)
+    return max(worst)
+
+
+@pytest.mark.parametrize("cfg,B", [(SMALL, 2), (SMALL, 3), (WIDE, 1)])
+def test_train_gradients_match_autograd(cfg, B):
+    model, sd, pix, labels = _setup(cfg, B)
+    out = model(pixel_values=pix.to(DEV))
+    loss = torch.nn.functional.cross_entropy(out.logits, labels.to(DEV))
+    loss.backward()
+    ref_loss, ref_logits, ref_grads = _oracle_grads(sd, cfg, pix, labels)
+    np.testing.assert_allclose(out.logits.detach().cpu().numpy(), ref_logits.numpy(), rtol=0, atol=1e-2)
+    assert abs(float(loss) - ref_loss) < 1e-2  # follows from the 1e-2 logit bound
+    print("worst gradient (rel L2, name, cos):", _compare(model, ref_grads))
+
+
+def test_reference_training_loop_with_fused_adamw():
+    """Three steps of the reference loop: vclip AdamW on the HIP model vs torch AdamW on the oracle."""
+    from oracle.vivit_ref import vivit_forward
+    from vclip_amd.optim import AdamW
+    cfg, B = SMALL, 2
+    model, sd, pix, labels = _setup(cfg, B)
+    opt = AdamW(model.parameters(), lr=1e-3, weight_decay=0.01)
+    ref = {k: torch.from_numpy(v).clone().requires_grad_() for k, v in sd.items()}
+    ropt = torch.optim.AdamW(list(ref.values()), lr=1e-3, weight_decay=0.01)
+    crit = torch.nn.CrossEntropyLoss()
+    losses, rlosses = [], []
+    for step in range(3):
+        opt.zero_grad()
+        outputs = model(pixel_values=pix.to(DEV))
+        loss = crit(outputs.logits, labels.to(DEV))
+        loss.backward()
+        opt.step()
+        losses.append(float(loss))
+        ropt.zero_grad()
+        rl = crit(vivit_forward(ref, cfg, pix), labels)
+        rl.backward()
+        ropt.step()
+        rlosses.append(float(rl))
+    np.testing.assert_allclose(losses, rlosses, rtol=0, atol=2e-2)
+    # the accumulated AdamW update of every tensor (early AdamW steps move each weight by ~lr *
+    # sign(m); weights whose gradient is ~0 may take either sign on either side, so compare the
+    # whole tensor's update, not single elements)
+    for n, p in model.hf_state_dict().items():
+        if n.endswith("k_proj.bias"):
+            continue  # exact gradient 0: AdamW normalises rounding noise to +-lr steps on both sides
+        du = p.detach().cpu().double() - torch.from_numpy(sd[n]).double()
+        dr = ref[n].detach().double() - torch.from_numpy(sd[n]).double()
+        e = float((du - dr).abs().mean() / dr.abs().mean().clamp_min(1e-12))
+        assert e < 0.1, (n, e)
+    # eval after training uses the updated masters (the inference bf16 pack is refreshed)
+    model.eval()
+    with torch.no_grad():
+        ev = model(pixel_values=pix.to(DEV)).logits.cpu()
+        rv = vivit_forward({k: v.cpu() for k, v in model.state_dict().items()}, cfg, pix)
+    np.testing.assert_allclose(ev.numpy(), rv.numpy(), rtol=0, atol=1e-2)
+
+
+def test_torch_adamw_on_vclip_grads_and_accumulation():
+    """p.grad are ordinary tensors: torch's own AdamW steps them; a second backward without
+    zero_grad accumulates (torch semantics)."""
+    model, sd, pix, labels = _setup(SMALL, 2)
+    x, y = pix.to(DEV), labels.to(DEV)
+    torch.nn.functional.cross_entropy(model(pixel_values=x).logits, y).backward()
+    g1 = {n: p.grad.detach().clone() for n, p in model.hf_state_dict().items()}
+    torch.nn.functional.cross_entropy(model(pixel_values=x).logits, y).backward()
+    for n, p in model.hf_state_dict().items():
+        torch.testing.assert_close(p.grad, 2 * g1[n], rtol=1e-5, atol=1e-7)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=0.01)
+    w0 = model.P("classifier.weight").detach().clone()
+    opt.step()
+    assert (model.P("classifier.weight").detach() - w0).abs().max().item() > 1e-4
+
+
+def test_train_step_deterministic():
+    model, sd, pix, labels = _setup(SMALL, 2)
+    x, y = pix.to(DEV), labels.to(DEV)
+    gs = []
+    for _ in range(2):
+        model.zero_grad(set_to_none=True)
+        torch.nn.functional.cross_entropy(model(pixel_values=x).logits, y).backward()
+        gs.append(model._gflat.clone())
+    assert torch.equal(gs[0], gs[1])
