@@ -132,6 +132,7 @@ class TrainEngine:
         self.W = [dict(qkv=z(3 * D, D), qkvT=z(D, 3 * D), o=z(D, D), oT=z(D, D), f1=z(I, D), f1T=z(D, I),
                        f2=z(D, I), f2T=z(I, D), bqkv=z(3 * D, dt=f32)) for _ in range(L)]
         self.W_emb = z(D, self.Kemb)
+        self.kernel_events = None
 
     # ---- weights ------------------------------------------------------------------------------
     def pack(self):
@@ -217,7 +218,14 @@ class TrainEngine:
             ops.gemm(dXb, W["oT"], self.zeros[:D], "bias", dO)
             ops.wgrad(dXb, self.O[i], G(p + "attention.o_proj.weight"), self.work)
             ops.colsum(dX, G(p + "attention.o_proj.bias"), self.work)
+            ev = self.kernel_events  # optional HIP-event timing of the attention backward (bench.py)
+            if ev is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
             ops.attention_bwd(self.QKV[i], self.O[i], dO, self.LSE[i], self.delta, B, S, H, dQKV)
+            if ev is not None:
+                e1.record()
+                ev.append((e0, e1))
             ops.gemm(dQKV, W["qkvT"], self.zeros[:D], "bias_f32", dY)
             ops.wgrad(dQKV, self.Y1[i], lay.span(gflat, p + "attention.q_proj.weight", 3 * D * D, (3 * D, D)),
                       self.work, nscaled=D, scale=qs)

@@ -3,6 +3,8 @@ per GPU, bf16 MFMA compute (BASELINE.json `metric`, configs[1]), plus the logit
 max-abs-error vs the fp32 CPU reference and a roofline line for the dominant kernel.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline]
+  python bench.py --mode train [...]   # BASELINE configs[4]: ViViT-B train step (fwd + bwd +
+                                       # AdamW) bf16, 4 clips per GPU, RCCL gradient all-reduce
 
 One process per GPU (torch.distributed.run for N > 1, backend nccl = RCCL).  Clips
 shard as independent data-parallel units: each rank runs its own batch and no
@@ -107,19 +109,122 @@ def cpu_baseline(model_cfg, n_clips, gpu_logits_fn):
                       f"(eager attention), torch CPU {cores} threads"}, err
 
 
+TRAIN_ATTN_GFLOP_PER_CLIP_LAYER = 2 * ATTN_GFLOP_PER_CLIP_LAYER  # dV, dP, dK, dQ (recompute of S not counted)
+
+
+def cpu_train_baseline(n_clips):
+    """The fp32 oracle's train step on the host cores (torch autograd + torch AdamW over the
+    oracle/vivit_ref.py forward): a bounded sample of n_clips one-clip steps."""
+    from oracle.vivit_ref import vivit_forward
+    from vclip_amd.weights import make_synthetic_clips, make_vivit_weights
+    cfg = dict(hidden_size=768, intermediate_size=3072, tubelet_size=[2, 16, 16], num_channels=3, num_frames=32,
+               image_size=224, num_hidden_layers=12, num_labels=2, num_attention_heads=12, layer_norm_eps=1e-6)
+    sd = {k: torch.from_numpy(v).requires_grad_() for k, v in make_vivit_weights(cfg, seed=0).items()}
+    opt = torch.optim.AdamW(list(sd.values()), lr=1e-3, weight_decay=0.01)
+    pix = torch.from_numpy(make_synthetic_clips(n_clips, 32, 224, seed=1))
+    labels = torch.zeros(n_clips, dtype=torch.long)
+    cores = torch.get_num_threads()
+    t0 = time.perf_counter()
+    for i in range(n_clips):
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(vivit_forward(sd, cfg, pix[i:i + 1]), labels[i:i + 1]).backward()
+        opt.step()
+    dt = time.perf_counter() - t0
+    return {"value": n_clips / dt, "unit": "clips/s", "cores": cores, "kind": "port",
+            "sample": f"{n_clips} one-clip train steps (fwd + autograd bwd + torch AdamW) of the fp32 oracle "
+                      f"(oracle/vivit_ref.py, eager attention), torch CPU {cores} threads"}
+
+
+def run_train(a, dist, rank, world, dev):
+    """BASELINE configs[4]: the reference's train step (trainers/trainer.py:140-146) on the HIP
+    model: zero_grad, forward, CrossEntropyLoss, backward (+ RCCL all-reduce for N > 1), AdamW."""
+    from vclip_amd.dp import GradAllReduce
+    from vclip_amd.optim import AdamW
+    from vclip_amd.vivit import create_model
+    from vclip_amd.weights import make_synthetic_clips
+
+    model = create_model(num_frames=32, device=dev).train()
+    opt = AdamW(model.parameters(), lr=1e-3, weight_decay=0.01)
+    sync = GradAllReduce(model) if dist else None
+    pix = torch.from_numpy(make_synthetic_clips(a.batch, 32, 224, seed=1 + rank)).to(dev)
+    labels = torch.from_numpy(np.random.RandomState(2 + rank).randint(0, 2, size=a.batch)).long().to(dev)
+    crit = torch.nn.CrossEntropyLoss()
+    losses = []
+
+    def step():
+        opt.zero_grad()
+        outputs = model(pixel_values=pix)
+        loss = crit(outputs.logits, labels)
+        loss.backward()
+        if sync:
+            sync.wait()
+        opt.step()
+        losses.append(loss.detach())
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = []
+    model._engine.kernel_events = evs
+    dt = timed_loop(step, a.steps, 0, dist, torch.cuda.synchronize)
+    model._engine.kernel_events = None
+    attn_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    clips = a.batch * a.steps * world
+    value = clips / dt
+    ms_per_step = dt / a.steps * 1e3
+    attn_tflops = TRAIN_ATTN_GFLOP_PER_CLIP_LAYER * a.batch / (attn_ms * 1e-3) / 1e3
+    step_tflops = 3 * VIVIT_GFLOP_PER_CLIP * a.batch / (ms_per_step * 1e-3) / 1e3
+    out = None
+    if rank == 0:
+        cpu = None if (world > 1 or a.no_cpu_baseline) else cpu_train_baseline(a.cpu_clips)
+        out = {
+            "metric": "clips/sec train step (fwd+bwd+AdamW) ViViT-B 32x224^2 bf16",
+            "value": round(value, 2), "unit": "clips/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (uint8 frames RandomState(1+rank) -> ViViT processor affine, labels RandomState(2+rank); "
+                    "weights RandomState(0))",
+            "config": {"workload": f"ViViT-B/16x2 train step, 32x224x224 clips, batch {a.batch} per GPU, AdamW(lr 1e-3, "
+                                   "wd 0.01), RCCL gradient all-reduce for N > 1 (BASELINE configs[4])",
+                       "model": "ViViT-B/16x2 (joint space-time, 12L, d768, 12H, 3137 tokens)",
+                       "global_batch": a.batch * world, "seq_len": 3137, "parallelism": f"dp{world}"},
+            "loss_first_last": [round(float(losses[0]), 5), round(float(losses[-1]), 5)],
+            "roofline": {"bound": "mfma", "kernel": "attention backward (attn_bwd_dkdv + attn_bwd_dq + prep)",
+                         "achieved": round(attn_tflops, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                         "avg_launch_ms": round(attn_ms, 4),
+                         "flop_per_launch": f"{TRAIN_ATTN_GFLOP_PER_CLIP_LAYER:.2f} GF/clip x {a.batch} clips"},
+            "step_tflops": round(step_tflops, 1), "step_frac_of_peak": round(step_tflops / PEAK_BF16_TFLOPS, 4),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=8, help="clips per GPU per step")
-    ap.add_argument("--cpu-clips", type=int, default=3)
+    ap.add_argument("--mode", choices=["fwd", "train"], default="fwd")
+    ap.add_argument("--batch", type=int, default=None, help="clips per GPU per step (fwd 8, train 4)")
+    ap.add_argument("--cpu-clips", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     a = ap.parse_args()
+    if a.batch is None:
+        a.batch = 8 if a.mode == "fwd" else 4
+    if a.cpu_clips is None:
+        a.cpu_clips = 3 if a.mode == "fwd" else 1
 
     dist, rank, world, local = _dist()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if a.mode == "train":
+        out = run_train(a, dist, rank, world, dev)
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return out
 
     from vclip_amd.vivit import create_model
     from vclip_amd.weights import make_synthetic_clips
