@@ -35,10 +35,12 @@ def convert_state_dict(sd) -> "OrderedDict":
     return OrderedDict((convert_key(k), v) for k, v in sd.items())
 
 
-def load_reference_checkpoint(path: str, map_location="cpu"):
-    """Load a reference `.pth` training checkpoint dict safely (weights_only=True)."""
+def load_reference_checkpoint(path: str, map_location="cpu", vivit_keys: bool = True):
+    """Load a reference `.pth` training checkpoint dict safely (weights_only=True).  vivit_keys:
+    rename transformers-4.48 ViViT keys (the other families' models strip `module.` themselves)."""
     import torch
     ck = torch.load(path, map_location=map_location, weights_only=True)
+    conv = convert_state_dict if vivit_keys else (lambda sd: OrderedDict(sd))
     if isinstance(ck, dict) and "model_state_dict" in ck:
-        return ck, convert_state_dict(ck["model_state_dict"])
-    return {}, convert_state_dict(ck)
+        return ck, conv(ck["model_state_dict"])
+    return {}, conv(ck)

@@ -1,0 +1,107 @@
+"""End-to-end CLI drop-ins on the GPU, on a tiny synthetic dataset of
+raw uint8 clips (.npy, the build's decode-free format: PyAV / OpenCV are absent from the image) in
+the reference's <root>/{train,val,test}/{class}/ layout:
+
+  vivit_transformer/main.py      1 epoch of the reference loop on the HIP train step, best
+                                 checkpoint (trainer.py:291-305 schema), test metrics JSON;
+  vivit_transformer/inference.py that checkpoint -> prediction JSON;
+  timesformer / videoswintransformer / resnet50-3d-video: main.py --skip_train --checkpoint_path
+  (test metrics) and inference.py on a saved state dict.
+Checked: the files the reference writes exist with its keys, and the CLI's prediction equals the
+model's own softmax on the same clip.
+"""
+import json
+import os
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vclip_amd import _lib as L
+    L.load()
+
+
+@pytest.fixture(scope="module")
+def dataset(tmp_path_factory):
+    root = tmp_path_factory.mktemp("clips")
+    rng = np.random.RandomState(0)
+    for split, n in (("train", 2), ("val", 1), ("test", 2)):
+        for c in ("non-referral", "referral"):
+            d = root / split / c
+            d.mkdir(parents=True)
+            for k in range(n):
+                F = 40 if k == 0 else 20  # one video shorter than num_frames (the total < T branch)
+                np.save(d / f"{c}_{split}_{k}.npy", rng.randint(0, 256, (F, 224, 224, 3)).astype(np.uint8))
+    return root
+
+
+def _exp_dir(log_dir):
+    ds = sorted(Path(log_dir).iterdir())
+    assert ds, log_dir
+    return ds[-1]
+
+
+def test_vivit_main_trains_and_inference_predicts(dataset, tmp_path):
+    from vclip_amd.apps import run_inference, run_main
+    log_dir, model_dir = tmp_path / "logs", tmp_path / "models"
+    m, history, exp = run_main("vivit", ["--data_dir", str(dataset), "--log_dir", str(log_dir), "--model_dir",
+                                         str(model_dir), "--epochs", "1", "--batch_size", "2",
+                                         "--train_sampling", "random_window"])
+    assert len(history["train_loss"]) == 1 and np.isfinite(history["train_loss"][0])
+    metrics = json.load(open(exp / "test_metrics_uniform.json"))
+    for k in ("accuracy", "confusion_matrix", "f1_score", "precision", "recall", "auroc"):
+        assert k in metrics
+    ck_path = model_dir / "best_model_random_window.pth"
+    ck = torch.load(ck_path, weights_only=True)
+    for k in ("epoch", "model_state_dict", "optimizer_state_dict", "val_loss", "val_acc", "history", "config",
+              "id2label", "label2id", "num_frames", "train_sampling", "val_sampling", "test_sampling"):
+        assert k in ck
+    assert ck["id2label"] == {0: "non-referral", 1: "referral"}
+    video = sorted((dataset / "test" / "referral").iterdir())[0]
+    res = run_inference("vivit", ["--video_path", str(video), "--model_path", str(ck_path), "--log_dir",
+                                  str(tmp_path / "ilogs")])
+    assert res["predicted_class"] in ("non-referral", "referral") and 0.5 <= res["confidence"] <= 1.0
+    saved = json.load(open(_exp_dir(tmp_path / "ilogs") / "inference_results" / f"{video.stem}_result.json"))
+    assert saved["predicted_class"] == res["predicted_class"]
+    # == the model's own softmax on that clip (uniform sampling of 40 frames, processor on the GPU)
+    from vclip_amd import preprocess, sampling
+    from vclip_amd.vivit import VivitConfig, VivitForVideoClassification
+    model = VivitForVideoClassification(VivitConfig.from_dict(ck["config"])).cuda().eval()
+    model.load_state_dict(ck["model_state_dict"])
+    idx = sampling.VivitSampler(32, "uniform").get_sampling_indices(str(video), 40)
+    fr = torch.from_numpy(np.load(video)[idx]).cuda().unsqueeze(0)
+    with torch.no_grad():
+        p = torch.softmax(model(pixel_values=preprocess.vivit_preprocess(fr)).logits, 1)[0]
+    assert abs(float(p.max()) - res["confidence"]) < 1e-5
+
+
+@pytest.mark.parametrize("fam,extra", [("timesformer", []), ("swin", ["--model_size", "tiny"]), ("resnet3d", [])])
+def test_eval_and_inference_clis(dataset, tmp_path, fam, extra):
+    from vclip_amd.apps import FAMILIES, build_parser, run_inference, run_main
+    f = FAMILIES[fam]
+    args = build_parser(f, inference=False).parse_args(["--data_dir", str(dataset), "--log_dir", "x", "--model_dir", "y"]
+                                                       + extra)
+    if not hasattr(args, "num_classes"):
+        args.num_classes = 2
+    model = f.create_model(args, ["non-referral", "referral"], torch.device("cuda", 0), None)
+    ck_path = tmp_path / "ck.pth"
+    torch.save({"model_state_dict": model.state_dict(), "id2label": {0: "non-referral", 1: "referral"}}, ck_path)
+    m, _, exp = run_main(fam, ["--data_dir", str(dataset), "--log_dir", str(tmp_path / "logs"), "--model_dir",
+                               str(tmp_path / "models"), "--skip_train", "--checkpoint_path", str(ck_path),
+                               "--batch_size", "2"] + extra)
+    assert (exp / "test_metrics_uniform.json").exists() and 0.0 <= m["accuracy"] <= 1.0
+    with pytest.raises(NotImplementedError):
+        run_main(fam, ["--data_dir", str(dataset), "--log_dir", str(tmp_path / "l2"), "--model_dir",
+                       str(tmp_path / "m2"), "--epochs", "1"] + extra)
+    video = sorted((dataset / "test" / "referral").iterdir())[0]
+    res = run_inference(fam, ["--video_path", str(video), "--model_path", str(ck_path), "--log_dir",
+                              str(tmp_path / "ilogs")] + extra)
+    assert res["predicted_class"] in ("non-referral", "referral") and 0.5 <= res["confidence"] <= 1.0
