@@ -34,22 +34,6 @@ __device__ __forceinline__ int bswz(int r, int c) {
     return c ^ (((m & 1) << 2) | (m & 2) | ((m >> 2) & 1));
 }
 
-struct TileRegs {
-    uint4 a, b;
-};
-
-// 64 rows x 64 bf16 at `base` (row stride ld elements) -> registers: 256 threads, 2 x 16 B each
-__device__ __forceinline__ void tile_load(const uint16_t* base, int64_t ld, int tid, TileRegs& t) {
-    const int r0 = tid >> 3, c = tid & 7;
-    t.a = *reinterpret_cast<const uint4*>(base + (int64_t)r0 * ld + c * 8);
-    t.b = *reinterpret_cast<const uint4*>(base + (int64_t)(r0 + 32) * ld + c * 8);
-}
-__device__ __forceinline__ void tile_store(char* lds, int tid, const TileRegs& t) {
-    const int r0 = tid >> 3, c = tid & 7;
-    *reinterpret_cast<uint4*>(lds + r0 * 128 + bswz(r0, c) * 16) = t.a;
-    *reinterpret_cast<uint4*>(lds + (r0 + 32) * 128 + bswz(r0 + 32, c) * 16) = t.b;
-}
-
 // A/B fragment of k-step kk from a row image: lane (r, h) gets row `row`, columns 16kk+8h..+7
 __device__ __forceinline__ v8bf row_frag(const char* tile, int off) {
     return __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(tile + off));
@@ -198,24 +182,37 @@ attn_bwd_dkdv_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const uint16_
     for (int e = 0; e < 16; ++e) { dv[0][e] = 0.f; dv[1][e] = 0.f; dk[0][e] = 0.f; dk[1][e] = 0.f; }
 
     const int nt = (S + 63) / 64;
-    TileRegs tq, tdo;
+    // tile prefetch lives in plain registers (a struct captured by lambdas ended up in scratch)
+    uint4 pq0, pq1, pd0, pd1;
     float tf = 0.f;
-    auto load = [&](int t) {
-        tile_load(qbase + (int64_t)t * 64 * ld, ld, tid, tq);
-        tile_load(dobase + (int64_t)t * 64 * lddo, lddo, tid, tdo);
-        if (tid < 128) {
-            int q = t * 64 + (tid & 63);
-            q = q < S ? q : S - 1;
-            tf = tid < 64 ? lseb[q] : delb[q];
-        }
-    };
-    auto store = [&](char* slot) {
-        tile_store(slot, tid, tq);
-        tile_store(slot + TILE_BYTES, tid, tdo);
-        if (tid < 128) reinterpret_cast<float*>(slot + 2 * TILE_BYTES)[tid] = tf;
-    };
-    load(0);
-    store(smem);
+    const int sr0 = tid >> 3, sc = tid & 7;
+    const int so0 = sr0 * 128 + bswz(sr0, sc) * 16, so1 = (sr0 + 32) * 128 + bswz(sr0 + 32, sc) * 16;
+    // LDS holds -lse and -Delta: they initialise the S and dP accumulators (so the MFMAs emit
+    // S - lse and dP - Delta directly); a query past S gets -lse = -inf, i.e. P = 0
+#define ABWD_LOAD_A(t)                                                                                  \
+    {                                                                                                   \
+        const uint16_t* qs = qbase + ((int64_t)(t) * 64 + sr0) * ld + sc * 8;                           \
+        const uint16_t* ds = dobase + ((int64_t)(t) * 64 + sr0) * lddo + sc * 8;                        \
+        pq0 = *reinterpret_cast<const uint4*>(qs);                                                      \
+        pq1 = *reinterpret_cast<const uint4*>(qs + 32 * ld);                                            \
+        pd0 = *reinterpret_cast<const uint4*>(ds);                                                      \
+        pd1 = *reinterpret_cast<const uint4*>(ds + 32 * lddo);                                          \
+        if (tid < 128) {                                                                                \
+            const int q = (t) * 64 + (tid & 63);                                                        \
+            const int qc = q < S ? q : S - 1;                                                           \
+            tf = tid < 64 ? (q < S ? -lseb[qc] : -INFINITY) : -delb[qc];                                \
+        }                                                                                               \
+    }
+#define ABWD_STORE_A(slot)                                                                              \
+    {                                                                                                   \
+        *reinterpret_cast<uint4*>((slot) + so0) = pq0;                                                  \
+        *reinterpret_cast<uint4*>((slot) + so1) = pq1;                                                  \
+        *reinterpret_cast<uint4*>((slot) + TILE_BYTES + so0) = pd0;                                     \
+        *reinterpret_cast<uint4*>((slot) + TILE_BYTES + so1) = pd1;                                     \
+        if (tid < 128) reinterpret_cast<float*>((slot) + 2 * TILE_BYTES)[tid] = tf;                     \
+    }
+    ABWD_LOAD_A(0);
+    ABWD_STORE_A(smem);
     __syncthreads();
 
     for (int t = 0; t < nt; ++t) {
@@ -223,31 +220,25 @@ attn_bwd_dkdv_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const uint16_
         const char* qi = cur;
         const char* di = cur + TILE_BYTES;
         const float* fl = reinterpret_cast<const float*>(cur + 2 * TILE_BYTES);  // [0,64) lse, [64,128) Delta
-        if (t + 1 < nt) load(t + 1);
-        const int q0 = t * 64;
+        if (t + 1 < nt) ABWD_LOAD_A(t + 1);
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb) {
-            v16f s;
-#pragma unroll
-            for (int e = 0; e < 16; ++e) s[e] = 0.f;
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-                s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(qi, qb * 4096 + roff[kk]), kf[kk], s, 0, 0, 0);
-            // P = exp2(S - lse[q]); register 4g+e holds query 32qb + 8g + 4h + e
-            v16f p;
+            // accumulator inits: register 4g+e holds query 32qb + 8g + 4h + e
+            v16f s, dp;
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const float4 L = *reinterpret_cast<const float4*>(fl + qb * 32 + 8 * g + 4 * h);
-                p[4 * g + 0] = __builtin_amdgcn_exp2f(s[4 * g + 0] - L.x);
-                p[4 * g + 1] = __builtin_amdgcn_exp2f(s[4 * g + 1] - L.y);
-                p[4 * g + 2] = __builtin_amdgcn_exp2f(s[4 * g + 2] - L.z);
-                p[4 * g + 3] = __builtin_amdgcn_exp2f(s[4 * g + 3] - L.w);
+                const float4 Dl = *reinterpret_cast<const float4*>(fl + 64 + qb * 32 + 8 * g + 4 * h);
+                s[4 * g + 0] = L.x; s[4 * g + 1] = L.y; s[4 * g + 2] = L.z; s[4 * g + 3] = L.w;
+                dp[4 * g + 0] = Dl.x; dp[4 * g + 1] = Dl.y; dp[4 * g + 2] = Dl.z; dp[4 * g + 3] = Dl.w;
             }
-            if (q0 + 64 > S) {
 #pragma unroll
-                for (int e = 0; e < 16; ++e)
-                    if (q0 + qb * 32 + 8 * (e >> 2) + 4 * h + (e & 3) >= S) p[e] = 0.f;
-            }
+            for (int kk = 0; kk < 4; ++kk)
+                s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(qi, qb * 4096 + roff[kk]), kf[kk], s, 0, 0, 0);
+            // P = exp2(S - lse[q])
+            v16f p;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) p[e] = __builtin_amdgcn_exp2f(s[e]);
             // dV^T += dO^T . P
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
@@ -258,22 +249,13 @@ attn_bwd_dkdv_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const uint16_
                     dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(di, tro.a[db] + kr, tro.b[db] + kr), pf,
                                                                      dv[db], 0, 0, 0);
             }
-            // dP = dO . V^T
-            v16f dp;
-#pragma unroll
-            for (int e = 0; e < 16; ++e) dp[e] = 0.f;
+            // dP - Delta = dO . V^T - Delta[q]
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk)
                 dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(di, qb * 4096 + roff[kk]), vf[kk], dp, 0, 0, 0);
-            // dS = P o (dP - Delta[q])
+            // dS = P o (dP - Delta)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float4 Dl = *reinterpret_cast<const float4*>(fl + 64 + qb * 32 + 8 * g + 4 * h);
-                dp[4 * g + 0] = p[4 * g + 0] * (dp[4 * g + 0] - Dl.x);
-                dp[4 * g + 1] = p[4 * g + 1] * (dp[4 * g + 1] - Dl.y);
-                dp[4 * g + 2] = p[4 * g + 2] * (dp[4 * g + 2] - Dl.z);
-                dp[4 * g + 3] = p[4 * g + 3] * (dp[4 * g + 3] - Dl.w);
-            }
+            for (int e = 0; e < 16; ++e) dp[e] = p[e] * dp[e];
             // dK^T += Q'^T . dS
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
@@ -285,9 +267,11 @@ attn_bwd_dkdv_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const uint16_
                                                                      dk[db], 0, 0, 0);
             }
         }
-        if (t + 1 < nt) store(smem + ((t + 1) & 1) * SLOT_A);
+        if (t + 1 < nt) ABWD_STORE_A(smem + ((t + 1) & 1) * SLOT_A);
         __syncthreads();
     }
+#undef ABWD_LOAD_A
+#undef ABWD_STORE_A
     uint16_t* drow = dqkv + (tok0 + kc) * lddq + hh * 64;
     store_rows(drow + (int64_t)H * 64, dk, LN2, h, key < S);
     store_rows(drow + (int64_t)2 * H * 64, dv, 1.0f, h, key < S);
@@ -343,41 +327,57 @@ attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const uint16_t*
     for (int e = 0; e < 16; ++e) { dq[0][e] = 0.f; dq[1][e] = 0.f; }
 
     const int nt = (S + 63) / 64;
-    TileRegs tk, tv;
-    auto load = [&](int t) {
-        tile_load(kbase + (int64_t)t * 64 * ld, ld, tid, tk);
-        tile_load(vbase + (int64_t)t * 64 * ld, ld, tid, tv);
-    };
-    auto store = [&](char* slot) {
-        tile_store(slot, tid, tk);
-        tile_store(slot + TILE_BYTES, tid, tv);
-    };
-    load(0);
-    store(smem);
+    uint4 pk0, pk1, pv0, pv1;
+    const int sr0 = tid >> 3, sc = tid & 7;
+    const int so0 = sr0 * 128 + bswz(sr0, sc) * 16, so1 = (sr0 + 32) * 128 + bswz(sr0 + 32, sc) * 16;
+#define ABWD_LOAD_B(t)                                                                                  \
+    {                                                                                                   \
+        const uint16_t* ks = kbase + ((int64_t)(t) * 64 + sr0) * ld + sc * 8;                           \
+        const uint16_t* vs = vbase + ((int64_t)(t) * 64 + sr0) * ld + sc * 8;                           \
+        pk0 = *reinterpret_cast<const uint4*>(ks);                                                      \
+        pk1 = *reinterpret_cast<const uint4*>(ks + 32 * ld);                                            \
+        pv0 = *reinterpret_cast<const uint4*>(vs);                                                      \
+        pv1 = *reinterpret_cast<const uint4*>(vs + 32 * ld);                                            \
+    }
+#define ABWD_STORE_B(slot)                                                                              \
+    {                                                                                                   \
+        *reinterpret_cast<uint4*>((slot) + so0) = pk0;                                                  \
+        *reinterpret_cast<uint4*>((slot) + so1) = pk1;                                                  \
+        *reinterpret_cast<uint4*>((slot) + TILE_BYTES + so0) = pv0;                                     \
+        *reinterpret_cast<uint4*>((slot) + TILE_BYTES + so1) = pv1;                                     \
+    }
+    ABWD_LOAD_B(0);
+    ABWD_STORE_B(smem);
     __syncthreads();
 
+    // accumulator inits: S^T - lse (keys past S of the last tile: -inf, i.e. P = 0) and dP^T - Delta;
+    // register 4g+e of key block kb holds key t*64 + 32kb + 8g + 4h + e
+    v16f negL, negD, negL_last[2];
+    const int klast = (nt - 1) * 64;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        negL[e] = -lq;
+        negD[e] = -dq_delta;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+            negL_last[kb][e] = klast + kb * 32 + 8 * (e >> 2) + 4 * h + (e & 3) < S ? -lq : -INFINITY;
+    }
     for (int t = 0; t < nt; ++t) {
         const char* ki = smem + (t & 1) * SLOT_B;
         const char* vi = ki + TILE_BYTES;
-        if (t + 1 < nt) load(t + 1);
-        const int k0 = t * 64;
+        if (t + 1 < nt) ABWD_LOAD_B(t + 1);
+        const bool last = t == nt - 1;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
-            v16f st, dpt;
-#pragma unroll
-            for (int e = 0; e < 16; ++e) { st[e] = 0.f; dpt[e] = 0.f; }
+            v16f st = last ? negL_last[kb] : negL, dpt = negD;
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
                 st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(ki, kb * 4096 + roff[kk]), qf[kk], st, 0, 0, 0);
                 dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(vi, kb * 4096 + roff[kk]), df[kk], dpt, 0, 0, 0);
             }
-            // register 4g+e holds key k0 + 32kb + 8g + 4h + e
+            // dS^T = P^T o (dP^T - Delta)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                float p = __builtin_amdgcn_exp2f(st[e] - lq);
-                if (k0 + 64 > S && k0 + kb * 32 + 8 * (e >> 2) + 4 * h + (e & 3) >= S) p = 0.f;
-                st[e] = p * (dpt[e] - dq_delta);
-            }
+            for (int e = 0; e < 16; ++e) st[e] = __builtin_amdgcn_exp2f(st[e]) * dpt[e];
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
                 const v8bf sf = to_bf8(st, s2);
@@ -388,9 +388,11 @@ attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const uint16_t*
                                                                      dq[db], 0, 0, 0);
             }
         }
-        if (t + 1 < nt) store(smem + ((t + 1) & 1) * SLOT_B);
+        if (t + 1 < nt) ABWD_STORE_B(smem + ((t + 1) & 1) * SLOT_B);
         __syncthreads();
     }
+#undef ABWD_LOAD_B
+#undef ABWD_STORE_B
     store_rows(dqkv + (tok0 + qc) * lddq + hh * 64, dq, LN2, h, q < S);
 }
 

@@ -282,6 +282,165 @@ wgrad_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __rest
     }
 }
 
+// ---------------------------------------------------------------------------------
+// The same weight gradient on the forward GEMM's 256x256 machinery (gemm.hip
+// gemm_bf16_big_kernel): 8 waves as 2 (n2) x 4 (n1), wave tile 128 (n2) x 64 (n1); 32-row
+// half-tiles of both operands staged HBM->LDS by LDS-DMA into a 4-slot ring (2 x 16 KiB per
+// slot: four [32 rows][64 cols] panels per operand, chunk-swizzled on the SOURCE address so
+// the lane-linear DMA image is the bswz image), tile t+3 issued while t is computed, a counted
+// vmcnt retiring only t+1 before the one barrier per half-tile; both MFMA operands read with
+// ds_read_b64_tr_b16 (the reduction index m is the row index of the images).  N1, N2 % 256 == 0.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ void wg_glds16(const void* gsrc, uint32_t lds_addr) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_addr)
+                 : "memory");
+}
+template <int NW>
+__device__ __forceinline__ void wg_wait_vm() {
+    static_assert(NW >= 0 && NW < 16, "vmcnt immediate");
+    __builtin_amdgcn_s_waitcnt(NW | 0x0F70);
+}
+__device__ __forceinline__ void wg_sync() {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");  // LDS was written by DMA behind the compiler's back
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+constexpr int WPANEL = 32 * 128;    // [32 rows][64 bf16]
+constexpr int WOPND = 4 * WPANEL;   // 256 columns of one operand
+constexpr int WBSLOT = 2 * WOPND;   // G then X: 32 KiB
+constexpr int WBNS = 4;
+
+__global__ void __launch_bounds__(512, 1)
+wgrad_big_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __restrict__ X, int64_t ldx, int64_t M,
+                 int nJ, int64_t mchunk, float* __restrict__ out, int64_t ldo, int64_t split_stride, int64_t nscaled,
+                 float scale) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int MI = 4, NI = 2;
+    const int ntiles = gridDim.x;
+    const int L = blockIdx.x;
+    const int xq = ntiles >> 3, xr = ntiles & 7, xcd = L & 7;
+    const int tile = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (L >> 3);
+    const int ti = tile / nJ, tj = tile % nJ;
+    const int64_t n1_0 = (int64_t)ti * 256, n2_0 = (int64_t)tj * 256;
+    const int64_t mb = (int64_t)blockIdx.y * mchunk;
+    const int64_t me = mb + mchunk < M ? mb + mchunk : M;
+    const int nk = (int)((me - mb) / 32);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int w2 = wave >> 2, w1 = wave & 3;
+    const int r = lane & 31, h = lane >> 5;
+
+    // staging: wave w DMAs pieces q = 2w, 2w+1 of each operand (piece = 8 rows of one panel)
+    int64_t gsrc[2], xsrc[2];
+    uint32_t ldst[2];
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+        const int q = 2 * wave + pp, panel = q >> 2, row = (q & 3) * 8 + (lane >> 3);
+        const int lch = bswz(row, lane & 7);  // xor swizzle: its own inverse
+        gsrc[pp] = (int64_t)row * ldg + n1_0 + panel * 64 + lch * 8;
+        xsrc[pp] = (int64_t)row * ldx + n2_0 + panel * 64 + lch * 8;
+        ldst[pp] = panel * WPANEL + (q & 3) * 8 * 128;
+    }
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem);
+    auto stage = [&](int t) {
+        const uint32_t s = lds0 + (t % WBNS) * WBSLOT;
+        const int64_t m0 = mb + (int64_t)t * 32;
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+            wg_glds16(G + m0 * ldg + gsrc[pp], __builtin_amdgcn_readfirstlane(s + ldst[pp]));
+            wg_glds16(X + m0 * ldx + xsrc[pp], __builtin_amdgcn_readfirstlane(s + WOPND + ldst[pp]));
+        }
+    };
+
+    // transposed-read offsets within a panel (rows 4h+tq and +8; 32-column block db)
+    const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
+    const int gcol = ((lane >> 4) & 1) * 16 + tp * 4;
+    int offa[2], offb[2];
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+        const int col = db * 32 + gcol;
+        const int ra = 4 * h + tq, rb = ra + 8;
+        offa[db] = ra * 128 + bswz(ra, col >> 3) * 16 + (col & 7) * 2;
+        offb[db] = rb * 128 + bswz(rb, col >> 3) * 16 + (col & 7) * 2;
+    }
+    auto read_frags = [&](int t, int kk, v8bf (&fa)[MI], v8bf (&fb)[NI]) {
+        const char* gt = smem + (t % WBNS) * WBSLOT;
+        const char* xt = gt + WOPND;
+        const int kr = kk * 16 * 128;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {  // n2 block: panel 2*w2 + i/2, db = i & 1
+            const char* pn = xt + (2 * w2 + (i >> 1)) * WPANEL + kr;
+            fa[i] = tr_frag(pn, offa[i & 1], offb[i & 1]);
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {  // n1 block: panel w1, db = j
+            const char* pn = gt + w1 * WPANEL + kr;
+            fb[j] = tr_frag(pn, offa[j], offb[j]);
+        }
+    };
+    v16f acc[MI][NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    auto mfmas = [&](const v8bf (&fa)[MI], const v8bf (&fb)[NI]) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    };
+
+    if (nk > 0) {
+        v8bf fa0[MI], fb0[NI], fa1[MI], fb1[NI];
+        stage(0);
+        if (nk > 1) stage(1);
+        if (nk > 2) stage(2);
+        if (nk > 2) wg_wait_vm<8>();
+        else if (nk > 1) wg_wait_vm<4>();
+        else wg_wait_vm<0>();
+        wg_sync();
+        read_frags(0, 0, fa0, fb0);
+        for (int t = 0; t < nk - 1; ++t) {
+            if (t + 3 < nk) stage(t + 3);
+            read_frags(t, 1, fa1, fb1);
+            mfmas(fa0, fb0);
+            if (t + 3 < nk) wg_wait_vm<8>();
+            else if (t + 2 < nk) wg_wait_vm<4>();
+            else wg_wait_vm<0>();
+            wg_sync();
+            read_frags(t + 1, 0, fa0, fb0);
+            mfmas(fa1, fb1);
+        }
+        read_frags(nk - 1, 1, fa1, fb1);
+        mfmas(fa0, fb0);
+        mfmas(fa1, fb1);
+    }
+
+    float* o = out + (int64_t)blockIdx.y * split_stride;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+        const int64_t n1 = n1_0 + w1 * 64 + j * 32 + r;
+        const float sc = n1 < nscaled ? scale : 1.0f;
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int64_t n2 = n2_0 + w2 * 128 + i * 32 + 8 * g + 4 * h;
+                *reinterpret_cast<float4*>(o + n1 * ldo + n2) =
+                    make_float4(acc[i][j][4 * g] * sc, acc[i][j][4 * g + 1] * sc, acc[i][j][4 * g + 2] * sc,
+                                acc[i][j][4 * g + 3] * sc);
+            }
+    }
+}
+
 // out[n1][n2] = sum_z ws[z][n1][n2] (the scale was applied per split)
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, int64_t n4, int splits,
                                                            int64_t N2, float* __restrict__ out, int64_t ldo) {
@@ -517,11 +676,43 @@ int vc_wgrad_bf16(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx
                   int64_t nscaled, float scale, float* out, int64_t ldo, float* work, int64_t work_elems,
                   hipStream_t stream) {
     if (!G || !X || !out) return fail(VC_ERR_INVALID_ARG, "vc_wgrad_bf16: null pointer");
-    if (M <= 0 || M % 64 || N1 % 128 || N2 % 128 || N1 <= 0 || N2 <= 0)
-        return fail(VC_ERR_INVALID_ARG, "vc_wgrad_bf16: need M % 64 == 0, N1 % 128 == 0, N2 % 128 == 0");
+    const bool big = N1 % 256 == 0 && N2 % 256 == 0;
+    if (M <= 0 || M % (big ? 32 : 64) || N1 % 128 || N2 % 128 || N1 <= 0 || N2 <= 0)
+        return fail(VC_ERR_INVALID_ARG, "vc_wgrad_bf16: need N1 % 128 == 0, N2 % 128 == 0, M % 64 == 0 "
+                                        "(M % 32 when N1, N2 % 256 == 0)");
     if (ldg % 8 || ldx % 8 || ldo % 4 || ldg < N1 || ldx < N2 || ldo < N2 ||
         ((((uintptr_t)G) | ((uintptr_t)X) | ((uintptr_t)out)) & 15))
         return fail(VC_ERR_INVALID_ARG, "vc_wgrad_bf16: bad leading dimension / alignment");
+    if (big) {
+        // 256 x 256 LDS-DMA kernel, split-K sized for ~one workgroup per CU
+        const int nJ2 = (int)(N2 / 256);
+        const int nt2 = (int)(N1 / 256) * nJ2;
+        const int64_t kt2 = M / 32;
+        int64_t sp = (256 + nt2 - 1) / nt2;
+        if (sp > kt2 / 4) sp = kt2 / 4;
+        if (!work || work_elems < 2 * N1 * N2) sp = 1;
+        else if (sp * N1 * N2 > work_elems) sp = work_elems / (N1 * N2);
+        if (sp < 1) sp = 1;
+        const int64_t mch = (kt2 + sp - 1) / sp * 32;
+        sp = (M + mch - 1) / mch;
+        static bool attr = false;
+        if (!attr) {
+            hipError_t e = hipFuncSetAttribute((const void*)wgrad_big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               WBNS * WBSLOT);
+            if (e != hipSuccess) return fail((int)e, std::string("vc_wgrad_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
+            attr = true;
+        }
+        if (sp == 1) {
+            wgrad_big_kernel<<<dim3((unsigned)nt2, 1), 512, WBNS * WBSLOT, stream>>>(G, ldg, X, ldx, M, nJ2, mch, out, ldo,
+                                                                                     0, nscaled, scale);
+        } else {
+            wgrad_big_kernel<<<dim3((unsigned)nt2, (unsigned)sp), 512, WBNS * WBSLOT, stream>>>(
+                G, ldg, X, ldx, M, nJ2, mch, work, N2, N1 * N2, nscaled, scale);
+            const int64_t n4 = N1 * N2 / 4;
+            wgrad_reduce_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, stream>>>(work, n4, (int)sp, N2, out, ldo);
+        }
+        return check_launch("vc_wgrad_bf16");
+    }
     const int nI = (int)(N1 / 128), nJ = (int)(N2 / 128);
     const int ntiles = nI * nJ;
     const int64_t kt = M / 64;

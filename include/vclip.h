@@ -353,8 +353,8 @@ int vc_colsum(const void* in, int dtype, int64_t ld, int64_t R, int64_t N, int64
 /*
  * Weight gradient of nn.Linear / the tubelet Conv3d: out[n1][n2] = s(n1) * sum_m G[m][n1] X[m][n2]
  * (G = output gradient, X = layer input, bf16 [M][*] row-major; fp32 out, overwritten),
- * s(n1) = scale for n1 < nscaled (the q-scale fold), else 1.  M % 64 == 0, N1 % 128 == 0,
- * N2 % 128 == 0.  work: f32 scratch for split-K partials (>= 2*N1*N2 enables splitting).
+ * s(n1) = scale for n1 < nscaled (the q-scale fold), else 1.  N1 % 128 == 0, N2 % 128 == 0,
+ * M % 64 == 0 (M % 32 when N1 and N2 are multiples of 256: the 256 x 256 kernel).  work: f32 scratch for split-K partials (>= 2*N1*N2 enables splitting).
  */
 int vc_wgrad_bf16(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, int64_t M, int64_t N1, int64_t N2,
                   int64_t nscaled, float scale, float* out, int64_t ldo, float* work, int64_t work_elems,
