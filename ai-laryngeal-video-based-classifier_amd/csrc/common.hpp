@@ -47,7 +47,9 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 // d/dx gelu_fast = 0.5(1 + tanh u) + 0.5 x (1 - tanh^2 u) * 0.7978845608 (1 + 3*0.044715 x^2)
 __device__ __forceinline__ float dgelu_tanh(float x) {
     const float u = 0.7978845608f * x * (1.0f + 0.044715f * x * x);
-    const float t = tanhf(u);
+    // tanh(u) = 1 - 2 / (exp(2u) + 1): one v_exp_f32 + one v_rcp_f32 (libm tanhf is a long
+    // branchy sequence in the epilogue); exp -> inf / 0 gives the +-1 limits exactly
+    const float t = 1.0f - 2.0f * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(2.8853900817779268f * u) + 1.0f);
     return 0.5f * (1.0f + t) + 0.5f * x * (1.0f - t * t) * 0.7978845608f * (1.0f + 0.134145f * x * x);
 }
 __device__ __forceinline__ float gelu_erf(float x) {

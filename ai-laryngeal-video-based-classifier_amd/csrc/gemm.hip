@@ -733,16 +733,21 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
     return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad config");
 }
 
-// Default tile choice (measured on MI355X at the ViViT-B/16x2 B=8 projection shapes,
-// tools/tune_gemm.py): the persistent 256x256 kernel whenever the epilogue is a bf16 store
-// and the grid is at least two rounds of 256 tiles; otherwise 128x256 (fc2-like, N = 768,
-// long K) or 128x128.
+// Default tile choice (measured on MI355X, tools/tune_gemm.py at the ViViT-B B=8 inference
+// shapes and tools/tune_train_gemm.py at the B=4 train-step shapes):
+//   * bf16-output epilogues the persistent 256x256 kernel supports: cfg 4 whenever M, N % 256
+//     (q|k|v 805 vs 652 TF/s at B=8, 776 vs 479 at B=4; o_proj dgrad 583 vs 458);
+//   * otherwise the 256x256 kernel when its tiles fit in one round of CUs (B=4: fc2 698 vs 545,
+//     fc1 dgrad 781 vs 599, q|k|v dgrad 730 vs 566, o_proj 380 vs 363 TF/s); at B=8 (297 tiles
+//     for N = 768) 128x256 (fc2, long K) or 128x128 (o_proj) are faster.
 static int pick_cfg(int64_t M, int64_t N, int64_t K, int epi) {
     const bool bf16_out = epi == VC_EPI_BIAS_BF16 || epi == VC_EPI_BIAS_GELU_TANH || epi == VC_EPI_BIAS_GELU_ERF ||
                           epi == VC_EPI_BIAS_RELU_BF16;
     if (bf16_out && M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && K >= 192 && N <= 8192 &&
-        (M / 256) * (N / 256) >= 512)
+        (M / 256) * (N / 256) >= 64)
         return 4;
+    if (M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && (M / 256) * (N / 256) >= 64 && (M / 256) * (N / 256) <= 256)
+        return 3;
     if (M % 128 == 0 && N % 256 == 0 && K >= 1536) return 2;
     if (M % 256 == 0 && N % 128 == 0 && (M / 256) * (N / 128) >= 1024) return 0;
     return 1;
@@ -773,8 +778,6 @@ extern "C" int vc_gemm_bf16_cfg(const uint16_t* A, int64_t lda, const uint16_t* 
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: GELU_SAVE / DGELU epilogues need a bf16 aux with ldaux >= N");
     if (epilogue == VC_EPI_BIAS_ADD_F32 && (!aux || ldaux % 4 || ldaux < N || ((uintptr_t)aux & 15)))
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: BIAS_ADD_F32 epilogue needs an f32 aux with ldaux >= N");
-    if (epilogue >= VC_EPI_BIAS_ADD_F32 && cfg >= 3)
-        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: training epilogues run on cfg 0-2");
     if (cfg < 0) cfg = pick_cfg(M, N, K, epilogue);
     const int ablation = cfg >= 10 ? cfg : -1;  // x3 / x4: timing-only ablations of cfg 3 / 4 (wrong results)
     if (ablation > 0) cfg = (ablation % 10 == 4) ? 4 : 3;

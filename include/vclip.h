@@ -90,7 +90,7 @@ int vc_patch_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C, 
 #define VC_EPI_BIAS_RELU_BF16   6  /* out bf16[m][n]  = relu(acc + bias[n])       (conv + BN + ReLU)    */
 #define VC_EPI_BIAS_RESID_RELU_BF16 7 /* out bf16[m][n] = relu(acc + bias[n] + res[m][n]), res = (const
                                        uint16_t*)aux bf16 with row stride ldaux (bottleneck conv_c + skip) */
-/* Training epilogues (ViViT train step; block configs 0-2 only): */
+/* Training epilogues (ViViT train step; block configs 0-3): */
 #define VC_EPI_BIAS_ADD_F32     8  /* out f32 [m][n]  = aux[m][n] + acc + bias[n]  (residual into a new buffer,
                                        so the layer input stays saved for the backward)                    */
 #define VC_EPI_BIAS_GELU_TANH_SAVE 9 /* out bf16[m][n] = gelu_fast(acc + bias[n]); (uint16_t*)aux[m][n] =

@@ -27,7 +27,7 @@ def _model(cfg):
     c = VivitConfig(**cfg, id2label={0: "non-referral", 1: "referral"})
     m = VivitForVideoClassification(c)
     m.load_state_dict(make_vivit_weights(cfg, seed=0))
-    return m.cuda()
+    return m.cuda().eval()  # constructed models start in train mode, as HF's
 
 
 def test_vivit_tiny_logits():
