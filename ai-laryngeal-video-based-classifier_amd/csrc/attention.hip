@@ -77,7 +77,9 @@ __device__ __forceinline__ void attn_sync() {
 // ABL: timing-only ablations (1 no loop loads, 2 no exp, 4 no PV MFMA, 8 no QK MFMA) —
 // results are wrong by design; 16 re-bases on every tile (the LIM = 0 build of the
 // threshold sweep, cdna_hip_programming.md rule 26: must agree with the shipped build);
-// 32 drops the MFMA/VALU interleave directives (correct, timing comparison only).
+// 32 adds sched_group_barrier directives interleaving tile t+1's QK^T MFMAs with tile t's
+// exp2 / sum VALU (correct; measured 3 % SLOWER than hipcc's own schedule at B = 8 and B = 4,
+// tools/ab_attn_interleave.py, so the shipped build leaves the scheduling to the compiler).
 // WLSE: also store the base-2 log-sum-exp of each query's scores, lse[(b*H + h)*S + q] =
 // m + log2(l) (running max and row sum), from which the backward kernels recompute P.
 template <int QB, int ABL, bool WLSE = false>
@@ -276,7 +278,7 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
         //      against an exact re-based max.
         v2f ps[QB];
         expsum(scur, ps);
-        if constexpr (NEXT == 0 && !(ABL & 32)) {
+        if constexpr (NEXT == 0 && (ABL & 32)) {
             // full next tile: no mask branch, so its QK^T MFMAs share one scheduling region
             // with this tile's exp2/sum; interleave them (VALU in every MFMA gap)
             __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
