@@ -349,14 +349,17 @@ gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
             for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(fw[j]));
             return;
         }
+        if constexpr (ABL & 16) __builtin_amdgcn_s_setprio(1);  // T5: keep the cluster between barriers
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int j = 0; j < NI; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[j], fa[i], acc[i][j], 0, 0, 0);
+        if constexpr (ABL & 16) __builtin_amdgcn_s_setprio(0);
     };
     // 6 fragment reads ride between 8 MFMAs
     auto interleave = [&]() {
+        if constexpr (ABL & 32) return;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -491,13 +494,16 @@ gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint
             for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(fw[j]));
             return;
         }
+        if constexpr (ABL & 16) __builtin_amdgcn_s_setprio(1);  // T5: keep the cluster between barriers
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int j = 0; j < NI; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[j], fa[i], acc[i][j], 0, 0, 0);
+        if constexpr (ABL & 16) __builtin_amdgcn_s_setprio(0);
     };
     auto interleave = [&]() {
+        if constexpr (ABL & 32) return;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -729,6 +735,15 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
         case 73: return launch_big<E, 7>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 83: return launch_big<E, 8>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 153: return launch_big<E, 15>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        // scheduling variants (correct results; tools/ab_gemm_sched.py): 16 s_setprio around each MFMA
+        // cluster (cdna_hip_programming.md T5) measured 4-15 % SLOWER on every ViViT shape, 32 without the
+        // sched_group_barrier interleave within +-1 %: neither ships
+        case 163: return launch_big<E, 16>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 323: return launch_big<E, 32>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 483: return launch_big<E, 48>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 164: return launch_persist<E, 16>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
+        case 324: return launch_persist<E, 32>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
+        case 484: return launch_persist<E, 48>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
     }
     return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad config");
 }
