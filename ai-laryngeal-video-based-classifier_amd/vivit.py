@@ -111,6 +111,9 @@ class VivitForVideoClassification(torch.nn.Module):
         self.grad_ready_hooks = []  # fn(stage, start, end, gflat): a slice of gflat is final (enqueued)
         self._packed = None
         self._ws = {}
+        self._streams = None
+        self.concurrent_streams = None  # None / 1: one stream; n > 1: batch split over n HIP streams
+        self.last_streams = 1
         self.kernel_events = None
 
     # ---- state dict in HF naming ---------------------------------------------------
@@ -147,6 +150,7 @@ class VivitForVideoClassification(torch.nn.Module):
         self._flat = self._gflat = self._gscratch = self._engine = None
         self._packed = None
         self._ws = {}
+        self._streams = None
         return out
 
     # ---- training (vclip_amd/vivit_train.py) --------------------------
@@ -260,10 +264,12 @@ class VivitForVideoClassification(torch.nn.Module):
         Memb = _round_up(B * npatch, 128)
         return npatch, S, Mpad, Memb
 
-    def _workspace(self, B, device):
-        key = (B, str(device))
+    def _workspace(self, B, device, part: int = 0):
+        key = (B, str(device), part)
         if key in self._ws:
             return self._ws[key]
+        if len(self._ws) >= 4:
+            self._ws = {}
         c = self.config
         D, I = c.hidden_size, c.intermediate_size
         kt, kh, kw = c.tubelet_size
@@ -272,7 +278,7 @@ class VivitForVideoClassification(torch.nn.Module):
         z = lambda *s, dt=bf: torch.zeros(s, dtype=dt, device=device)  # noqa: E731
         ws = dict(A_emb=z(Memb, c.num_channels * kt * kh * kw), X=z(Mpad, D, dt=torch.float32), Y=z(Mpad, D),
                   QKV=z(Mpad, 3 * D), O=z(Mpad, D), Hd=z(Mpad, I), logits=z(B, c.num_labels, dt=torch.float32))
-        self._ws = {key: ws}  # keep one shape resident
+        self._ws[key] = ws
         return ws
 
     # ---- forward -----------------------------------------------------------------
@@ -288,7 +294,7 @@ class VivitForVideoClassification(torch.nn.Module):
             logits = VivitTrainFn.apply(self, x, *params)  # forward saving activations; HIP backward
         else:
             with torch.no_grad():
-                logits = self.forward_logits(x)
+                logits = self.forward_logits(x).clone()  # the workspace buffer is reused by the next call
         loss = None
         if labels is not None:
             loss = torch.nn.functional.cross_entropy(logits, labels.to(logits.device))
@@ -296,13 +302,48 @@ class VivitForVideoClassification(torch.nn.Module):
 
     @torch.no_grad()
     def forward_logits(self, pix: torch.Tensor) -> torch.Tensor:
+        """logits f32 [B, labels] (a workspace buffer, overwritten by the next call).
+
+        `concurrent_streams = n > 1` splits the batch over n HIP streams, each part with its own
+        workspace, so one part's GEMM epilogues and kernel tails overlap another part's work:
+        +3-5 % clips/s at B = 8 with 2 streams (tools/try_streams.py; 4 streams were slower).
+        Off by default: under overlap a kernel's stream-event duration includes time queued
+        behind the other stream's kernels and no longer matches its rocprof kernel-trace
+        duration, which the benchmark's per-kernel roofline is checked against.  Logits are
+        bit-identical either way (every kernel is batch-invariant)."""
         c = self.config
         B, T, C, H, W = pix.shape
         if T != c.num_frames or H != c.image_size or W != c.image_size or C != c.num_channels:
             raise ValueError(f"pixel_values {tuple(pix.shape)} do not match config "
                              f"(T={c.num_frames}, C={c.num_channels}, {c.image_size}^2)")
+        ns = self.concurrent_streams or 1
+        ns = max(1, min(int(ns), B))
+        self.last_streams = ns
+        if ns == 1:
+            return self._forward_part(pix, 0)
+        dev = pix.device
+        if self._streams is None or len(self._streams) < ns or self._streams[0].device != dev:
+            self._streams = [torch.cuda.Stream(device=dev) for _ in range(ns)]
+        key = (B, str(dev), "logits")
+        if key not in self._ws:
+            self._ws[key] = torch.zeros(B, c.num_labels, dtype=torch.float32, device=dev)
+        logits = self._ws[key]
+        cur = torch.cuda.current_stream(dev)
+        bounds = [B * i // ns for i in range(ns + 1)]
+        for i in range(ns):
+            st = self._streams[i]
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                self._forward_part(pix[bounds[i]:bounds[i + 1]], i, out=logits[bounds[i]:bounds[i + 1]])
+        for i in range(ns):
+            cur.wait_stream(self._streams[i])
+        return logits
+
+    def _forward_part(self, pix: torch.Tensor, part: int, out=None) -> torch.Tensor:
+        c = self.config
+        B = pix.shape[0]
         pk = self._pack(pix.device)
-        ws = self._workspace(B, pix.device)
+        ws = self._workspace(B, pix.device, part)
         D = c.hidden_size
         npatch, S, Mpad, Memb = self.geometry(B)
         eps = c.layer_norm_eps
@@ -317,7 +358,7 @@ class VivitForVideoClassification(torch.nn.Module):
         for L in pk["layers"]:
             ops.layernorm(X, L["ln1_g"], L["ln1_b"], eps, Y)
             ops.gemm(Y, L["w_qkv"], L["b_qkv"], "bias", QKV)
-            if ev is not None:
+            if ev is not None:  # recorded on this part's stream, the one the kernel runs on
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
             ops.attention(QKV, B, S, c.num_attention_heads, scale, O, q_prescaled=True)
@@ -328,7 +369,8 @@ class VivitForVideoClassification(torch.nn.Module):
             ops.layernorm(X, L["ln2_g"], L["ln2_b"], eps, Y)
             ops.gemm(Y, L["w_1"], L["b_1"], act, Hd)
             ops.gemm(Hd, L["w_2"], L["b_2"], "bias_resid_f32", X)
-        return ops.cls_head(X, B, S, pk["lnf_g"], pk["lnf_b"], eps, pk["w_cls"], pk["b_cls"], out=ws["logits"])
+        return ops.cls_head(X, B, S, pk["lnf_g"], pk["lnf_b"], eps, pk["w_cls"], pk["b_cls"],
+                            out=ws["logits"] if out is None else out)
 
 
 def create_model(model_name="google/vivit-b-16x2-kinetics400", num_classes=2, class_labels=None, num_frames=32,

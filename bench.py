@@ -245,12 +245,16 @@ def main():
     model.kernel_events = evs
     dt = timed_loop(step, a.steps, 0, dist, torch.cuda.synchronize)
     model.kernel_events = None
+    streams = model.last_streams
     attn_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
 
     clips = a.batch * a.steps * world
     value = clips / dt
     ms_per_step = dt / a.steps * 1e3
-    attn_tflops = ATTN_GFLOP_PER_CLIP_LAYER * a.batch / (attn_ms * 1e-3) / 1e3
+    # the batch runs as model.last_streams concurrent halves: each attention launch holds
+    # batch / streams clips (events are recorded on the stream each launch runs on)
+    launch_clips = a.batch / streams
+    attn_tflops = ATTN_GFLOP_PER_CLIP_LAYER * launch_clips / (attn_ms * 1e-3) / 1e3
     model_tflops = VIVIT_GFLOP_PER_CLIP * a.batch / (ms_per_step * 1e-3) / 1e3
 
     out = None
@@ -286,8 +290,9 @@ def main():
             "roofline": {"bound": "mfma", "kernel": "attn_fwd_d64_kernel", "achieved": round(attn_tflops, 1),
                          "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "algorithmic_bytes": ATTN_IO_BYTES_PER_CLIP * a.batch, "avg_launch_ms": round(attn_ms, 4),
-                         "flop_per_launch": f"{ATTN_GFLOP_PER_CLIP_LAYER:.2f} GF/clip x {a.batch} clips"},
+                         "algorithmic_bytes": ATTN_IO_BYTES_PER_CLIP * launch_clips, "avg_launch_ms": round(attn_ms, 4),
+                         "flop_per_launch": f"{ATTN_GFLOP_PER_CLIP_LAYER:.2f} GF/clip x {launch_clips:g} clips",
+                         "streams": streams},
             "model_tflops": round(model_tflops, 1),
             "model_frac_of_peak": round(model_tflops / PEAK_BF16_TFLOPS, 4),
             "cpu_baseline": cpu,

@@ -60,3 +60,19 @@ def test_vivit_batch_invariance():
     full = m(pixel_values=pix).logits.clone()
     one = m(pixel_values=pix[1:2].contiguous()).logits.clone()
     assert torch.equal(full[1:2], one)
+
+
+def test_vivit_two_stream_split_bit_exact():
+    """With concurrent_streams = 2 the forward splits the batch over two HIP streams; the logits
+    must equal the one-stream run bit for bit (clips are independent, kernels batch-invariant)."""
+    from vclip_amd.vivit import create_model
+    from vclip_amd.weights import make_synthetic_clips
+    m = create_model(num_frames=32, device="cuda")
+    pix = torch.from_numpy(make_synthetic_clips(8, 32, 224, seed=5)).cuda()
+    m.concurrent_streams = 1
+    one = m.forward_logits(pix).clone()
+    m.concurrent_streams = 2
+    two = m.forward_logits(pix).clone()
+    assert m.last_streams == 2
+    assert torch.equal(one, two)
+    torch.testing.assert_close(m(pixel_values=pix).logits, one, rtol=0, atol=0)
