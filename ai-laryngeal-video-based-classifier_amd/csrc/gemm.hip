@@ -147,13 +147,15 @@ __device__ __forceinline__ void store_tile(const v16f (&acc)[MI][NI], int64_t mb
     }
 }
 
-template <int BM, int BN, int WM, int WN, int EPI>
-__global__ void __launch_bounds__(512, 1)
+// ST: LDS ring depth in tiles (prefetch distance ST - 1).  ST = 2 at 128x128 needs 64 KiB of
+// LDS, so two workgroups share a CU and one's epilogue overlaps the other's main loop.
+template <int BM, int BN, int WM, int WN, int EPI, int ST = 3>
+__global__ void __launch_bounds__(512, ST == 2 ? 2 : 1)
 gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
                  int nbm, int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
                  const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride, int64_t goff) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int ST = 3;                       // LDS ring depth (tiles)
+    static_assert(ST == 2 || ST == 3, "ring depth");
     constexpr int SLOT = (BM + BN) * 128;       // bytes per ring slot (A then W, 128-B rows)
     constexpr int TM = BM / WM, TN = BN / WN;   // wave tile
     constexpr int MI = TM / 32, NI = TN / 32;
@@ -208,7 +210,7 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
 
     const int nk = K / GBK;
     stage(0, 0);
-    if (nk > 1) {
+    if (ST == 3 && nk > 1) {
         stage(1, 1);
         wait_vm<LPT>();
     } else {
@@ -218,7 +220,7 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
 
     for (int t = 0; t < nk; ++t) {
         const int slot = t % ST;
-        if (t + 2 < nk) stage(t + 2, (t + 2) % ST);
+        if (t + ST - 1 < nk) stage(t + ST - 1, (t + ST - 1) % ST);
         const char* At = smem + slot * SLOT;
         const char* Wt = At + BM * 128;
 
@@ -243,8 +245,8 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
                 for (int j = 0; j < NI; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[cb][j], af[cb][i], acc[i][j], 0, 0, 0);
         }
-        // retire tile t+1 (tile t+2 may stay in flight), then all waves pass the barrier
-        if (t + 2 < nk) wait_vm<LPT>();
+        // retire tile t+1 (with ST = 3, tile t+2 may stay in flight), then all waves pass the barrier
+        if (ST == 3 && t + 2 < nk) wait_vm<LPT>();
         else wait_vm<0>();
         block_sync_lds();
     }
@@ -637,22 +639,22 @@ gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint
 struct GemmCfg {
     int bm, bn;
 };
-static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}};
-constexpr int kNumCfgs = 5;
+static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}, {128, 128}};
+constexpr int kNumCfgs = 6;
 
-template <int BM, int BN, int WM, int WN, int E>
+template <int BM, int BN, int WM, int WN, int E, int ST = 3>
 static int launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
                       const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
                       int64_t gs, int64_t go, hipStream_t stream) {
-    constexpr int lds = 3 * (BM + BN) * 128;
+    constexpr int lds = ST * (BM + BN) * 128;
     static bool attr_set = false;  // per instantiation; benign race (idempotent)
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, WM, WN, E>,
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, WM, WN, E, ST>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
         attr_set = true;
     }
-    gemm_bf16_kernel<BM, BN, WM, WN, E><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(
+    gemm_bf16_kernel<BM, BN, WM, WN, E, ST><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(
         A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go);
     return check_launch("vc_gemm_bf16");
 }
@@ -716,6 +718,7 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
         case 1: return launch_cfg<128, 128, 2, 4, E>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 2: return launch_cfg<128, 256, 2, 4, E>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 3: return launch_big<E>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 5: return launch_cfg<128, 128, 2, 4, E, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 4:
             if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
                           E == VC_EPI_BIAS_RELU_BF16)
@@ -751,21 +754,21 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
 // Default tile choice (measured on MI355X, tools/tune_gemm.py at the ViViT-B B=8 inference
 // shapes and tools/tune_train_gemm.py at the B=4 train-step shapes):
 //   * bf16-output epilogues the persistent 256x256 kernel supports: cfg 4 whenever M, N % 256
-//     (q|k|v 805 vs 652 TF/s at B=8, 776 vs 479 at B=4; o_proj dgrad 583 vs 458);
-//   * otherwise the 256x256 kernel when its tiles fit in one round of CUs (B=4: fc2 698 vs 545,
-//     fc1 dgrad 781 vs 599, q|k|v dgrad 730 vs 566, o_proj 380 vs 363 TF/s); at B=8 (297 tiles
-//     for N = 768) 128x256 (fc2, long K) or 128x128 (o_proj) are faster.
+//     (q|k|v 785 vs 675 TF/s at B=8, 769 vs 619 at B=4; o_proj dgrad 578 vs 527);
+//   * the 256x256 kernel when its tiles fit one round of CUs and the GEMM is not tiny (B=4:
+//     fc2 683 vs 647, fc1 dgrad 771 vs 694, q|k|v dgrad 727 vs 668 TF/s);
+//   * otherwise the 128x128 two-workgroups-per-CU kernel (cfg 5), which beat cfgs 0-2 on every
+//     shape measured: B=8 fc2 768 vs 677, o_proj 491 vs 430, fc1 (erf/other epilogues) 664 vs 602.
 static int pick_cfg(int64_t M, int64_t N, int64_t K, int epi) {
     const bool bf16_out = epi == VC_EPI_BIAS_BF16 || epi == VC_EPI_BIAS_GELU_TANH || epi == VC_EPI_BIAS_GELU_ERF ||
                           epi == VC_EPI_BIAS_RELU_BF16;
     if (bf16_out && M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && K >= 192 && N <= 8192 &&
         (M / 256) * (N / 256) >= 64)
         return 4;
-    if (M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && (M / 256) * (N / 256) >= 64 && (M / 256) * (N / 256) <= 256)
+    const int64_t t256 = (M / 256) * (N / 256);
+    if (M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && t256 >= 64 && t256 <= 256 && !(N <= 768 && K <= 768))
         return 3;
-    if (M % 128 == 0 && N % 256 == 0 && K >= 1536) return 2;
-    if (M % 256 == 0 && N % 128 == 0 && (M / 256) * (N / 128) >= 1024) return 0;
-    return 1;
+    return 5;
 }
 
 }  // namespace vc

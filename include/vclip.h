@@ -113,7 +113,9 @@ int vc_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
 
 /*
  * Same as vc_gemm_bf16 with an explicit block-tile configuration (tuning hook):
- *   cfg 0: 256x128, cfg 1: 128x128, cfg 2: 128x256 (rows x cols of C); -1 = automatic.
+ *   cfg 0: 256x128, cfg 1: 128x128, cfg 2: 128x256, cfg 3: 256x256, cfg 4: 256x256 persistent
+ *   (bf16-output epilogues 0/1/2/6 only), cfg 5: 128x128 with a 2-tile LDS ring (two workgroups
+ *   per CU); -1 = automatic (measured choice, gemm.hip pick_cfg).
  */
 int vc_gemm_bf16_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
                      int64_t M, int64_t N, int64_t K, const float* bias, int epilogue,

@@ -45,7 +45,7 @@ def main():
         fl = 2.0 * M * N * K
         cands = {}
         for c in [int(x) for x in a.cfgs.split(",")]:
-            bm, bn = {0: (256, 128), 1: (128, 128), 2: (128, 256), 3: (256, 256), 4: (256, 256)}[c]
+            bm, bn = {0: (256, 128), 1: (128, 128), 2: (128, 256), 3: (256, 256), 4: (256, 256), 5: (128, 128)}[c]
             if c == 4 and 'f32' in epi:
                 continue
             if M % bm or N % bn:
