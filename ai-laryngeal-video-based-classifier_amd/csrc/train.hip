@@ -21,14 +21,22 @@ namespace trn {
 //   xhat = (x - mean) * rstd,  g = dy * gamma,
 //   dx  += rstd * (g - mean(g) - xhat * mean(g * xhat))     (nn.LayerNorm backward)
 // ---------------------------------------------------------------------------------
-template <int V>
+// SUMS: also the column sums of dx before and after the update (the bias gradients of the
+// Linear layers whose outputs these residual gradients are) -> part[block][4][D].
+template <int V, bool SUMS>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const float* __restrict__ dy, int64_t lddy,
                                                      const float* __restrict__ x, int64_t ldx,
                                                      const float* __restrict__ gamma, float eps, int64_t M,
                                                      float* __restrict__ dx, int64_t lddx, uint16_t* __restrict__ dxb,
                                                      int64_t lddxb, float* __restrict__ part) {
     constexpr int D = V * 256;
-    __shared__ float red[4][2 * D];
+    constexpr int NP = SUMS ? 4 : 2;
+    __shared__ float red[4][NP * D];
+    float4 so[SUMS ? V : 1], sn[SUMS ? V : 1];
+    if constexpr (SUMS) {
+#pragma unroll
+        for (int i = 0; i < V; ++i) { so[i] = make_float4(0.f, 0.f, 0.f, 0.f); sn[i] = so[i]; }
+    }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     float4 pg[V], pb[V], g4[V];
 #pragma unroll
@@ -73,11 +81,13 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const float* __restrict__ d
 #pragma unroll
         for (int i = 0; i < V; ++i) {
             float4 o = dxr[i * 64 + lane];
+            if constexpr (SUMS) { so[i].x += o.x; so[i].y += o.y; so[i].z += o.z; so[i].w += o.w; }
             o.x += rstd * (dv[i].x * g4[i].x - c1 - xv[i].x * c2);
             o.y += rstd * (dv[i].y * g4[i].y - c1 - xv[i].y * c2);
             o.z += rstd * (dv[i].z * g4[i].z - c1 - xv[i].z * c2);
             o.w += rstd * (dv[i].w * g4[i].w - c1 - xv[i].w * c2);
             dxr[i * 64 + lane] = o;
+            if constexpr (SUMS) { sn[i].x += o.x; sn[i].y += o.y; sn[i].z += o.z; sn[i].w += o.w; }
             uint2 ob;
             ob.x = pack2bf(o.x, o.y);
             ob.y = pack2bf(o.z, o.w);
@@ -88,10 +98,14 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const float* __restrict__ d
     for (int i = 0; i < V; ++i) {
         reinterpret_cast<float4*>(red[w])[i * 64 + lane] = pg[i];
         reinterpret_cast<float4*>(red[w] + D)[i * 64 + lane] = pb[i];
+        if constexpr (SUMS) {
+            reinterpret_cast<float4*>(red[w] + 2 * D)[i * 64 + lane] = so[i];
+            reinterpret_cast<float4*>(red[w] + 3 * D)[i * 64 + lane] = sn[i];
+        }
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < 2 * D; c += 256)
-        part[(int64_t)blockIdx.x * 2 * D + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+    for (int c = threadIdx.x; c < NP * D; c += 256)
+        part[(int64_t)blockIdx.x * NP * D + c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
 }
 
 // ---------------------------------------------------------------------------------
@@ -106,6 +120,26 @@ template <>
 __device__ __forceinline__ float ld_as_f32<float>(const float* p) { return *p; }
 template <>
 __device__ __forceinline__ float ld_as_f32<uint16_t>(const uint16_t* p) { return bf2f(*p); }
+
+// Column sums of the per-block LayerNorm partials: segment s of D columns -> outs[s].
+struct Outs4 {
+    float* p[4];
+};
+__global__ void __launch_bounds__(256) seg_colsum_kernel(const float* __restrict__ in, int64_t R, int64_t D, int nseg,
+                                                         Outs4 outs) {
+    __shared__ float red[4][64];
+    const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+    const int64_t W = D * nseg, col = (int64_t)blockIdx.x * 64 + c;
+    float s = 0.f;
+    if (col < W)
+        for (int64_t r = g; r < R; r += 4) s += in[r * W + col];
+    red[g][c] = s;
+    __syncthreads();
+    if (g == 0 && col < W) {
+        const int seg = (int)(col / D);
+        outs.p[seg][col - seg * D] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+    }
+}
 
 template <typename T>
 __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ in, int64_t ld, int64_t R, int64_t N,
@@ -637,24 +671,41 @@ extern "C" {
 
 int vc_layernorm_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx, int64_t M, int64_t D,
                      const float* gamma, float eps, float* dx, int64_t lddx, uint16_t* dxb, int64_t lddxb,
-                     float* dgamma, float* dbeta, float* work, int64_t work_elems, hipStream_t stream) {
+                     float* dgamma, float* dbeta, float* dsum_in, float* dsum_out, float* work, int64_t work_elems,
+                     hipStream_t stream) {
     if (!dy || !x || !gamma || !dx || !dxb || !dgamma || !dbeta || !work)
         return fail(VC_ERR_INVALID_ARG, "vc_layernorm_bwd: null pointer");
     if (D != 256 && D != 512 && D != 768 && D != 1024)
         return fail(VC_ERR_UNSUPPORTED, "vc_layernorm_bwd: D must be 256, 512, 768 or 1024");
     if (lddy % 4 || ldx % 4 || lddx % 4 || lddxb % 4 || M <= 0)
         return fail(VC_ERR_INVALID_ARG, "vc_layernorm_bwd: leading dimensions must be multiples of 4");
+    if ((dsum_in == nullptr) != (dsum_out == nullptr))
+        return fail(VC_ERR_INVALID_ARG, "vc_layernorm_bwd: dsum_in and dsum_out go together");
+    const bool sums = dsum_in != nullptr;
+    const int np = sums ? 4 : 2;
     int64_t nb = (M + 3) / 4;
     if (nb > 512) nb = 512;
-    const int64_t need = nb * 2 * D + 16 * 2 * D;
+    const int64_t nsp = (nb + 31) / 32;  // row splits of the partial reduction
+    const int64_t need = (nb + nsp) * np * D;
     if (work_elems < need) return fail(VC_ERR_INVALID_ARG, "vc_layernorm_bwd: work too small (need " + std::to_string(need) + ")");
+#define VC_LNB(V)                                                                                                   \
+    (sums ? (ln_bwd_kernel<V, true><<<(unsigned)nb, 256, 0, stream>>>(dy, lddy, x, ldx, gamma, eps, M, dx, lddx, dxb,  \
+                                                                      lddxb, work), 0)                             \
+          : (ln_bwd_kernel<V, false><<<(unsigned)nb, 256, 0, stream>>>(dy, lddy, x, ldx, gamma, eps, M, dx, lddx, dxb, \
+                                                                       lddxb, work), 0))
     switch (D) {
-        case 256: ln_bwd_kernel<1><<<(unsigned)nb, 256, 0, stream>>>(dy, lddy, x, ldx, gamma, eps, M, dx, lddx, dxb, lddxb, work); break;
-        case 512: ln_bwd_kernel<2><<<(unsigned)nb, 256, 0, stream>>>(dy, lddy, x, ldx, gamma, eps, M, dx, lddx, dxb, lddxb, work); break;
-        case 768: ln_bwd_kernel<3><<<(unsigned)nb, 256, 0, stream>>>(dy, lddy, x, ldx, gamma, eps, M, dx, lddx, dxb, lddxb, work); break;
-        default: ln_bwd_kernel<4><<<(unsigned)nb, 256, 0, stream>>>(dy, lddy, x, ldx, gamma, eps, M, dx, lddx, dxb, lddxb, work); break;
+        case 256: VC_LNB(1); break;
+        case 512: VC_LNB(2); break;
+        case 768: VC_LNB(3); break;
+        default: VC_LNB(4); break;
     }
-    colsum_launch<float>(work, 2 * D, nb, 2 * D, dgamma, D, dbeta, 0, 1.0f, work + nb * 2 * D, 16 * 2 * D, stream);
+#undef VC_LNB
+    // partials [nb][np*D] -> [nsp][np*D] (32 rows per block) -> the np outputs
+    float* tmp = work + nb * np * D;
+    colsum_kernel<float><<<dim3((unsigned)((np * D + 255) / 256), (unsigned)nsp), 256, 0, stream>>>(
+        work, np * D, nb, np * D, 32, tmp, np * D, nullptr, 0, 1.0f);
+    Outs4 o{{dgamma, dbeta, dsum_in, dsum_out}};
+    seg_colsum_kernel<<<(unsigned)((np * D + 63) / 64), 256, 0, stream>>>(tmp, nsp, D, np, o);
     return check_launch("vc_layernorm_bwd");
 }
 

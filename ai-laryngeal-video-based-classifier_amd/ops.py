@@ -400,8 +400,10 @@ def attention_bwd(qkv: torch.Tensor, out: torch.Tensor, dout: torch.Tensor, lse:
 
 def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, gamma: torch.Tensor, eps: float, dx: torch.Tensor,
                   dxb: torch.Tensor, dgamma: torch.Tensor, dbeta: torch.Tensor, work: torch.Tensor,
-                  m: int | None = None) -> torch.Tensor:
-    """dx += LayerNorm backward of dy (f32, in place), dxb = bf16(dx); dgamma / dbeta overwritten."""
+                  m: int | None = None, dsum_in: torch.Tensor | None = None,
+                  dsum_out: torch.Tensor | None = None) -> torch.Tensor:
+    """dx += LayerNorm backward of dy (f32, in place), dxb = bf16(dx); dgamma / dbeta overwritten;
+    optional dsum_in / dsum_out = column sums of dx before / after (bias gradients)."""
     _dev(dy, x, gamma, dx, dxb, dgamma, dbeta, work)
     M = x.shape[0] if m is None else m
     D = gamma.numel()
@@ -410,8 +412,14 @@ def layernorm_bwd(dy: torch.Tensor, x: torch.Tensor, gamma: torch.Tensor, eps: f
     _need(all(t.shape[0] >= M and t.shape[1] >= D and t.stride(1) == 1 for t in (dy, x, dx, dxb)), "layernorm_bwd shapes")
     _need(dgamma.numel() == D and dbeta.numel() == D and dgamma.is_contiguous() and dbeta.is_contiguous(),
           "layernorm_bwd dgamma/dbeta")
+    _need((dsum_in is None) == (dsum_out is None), "layernorm_bwd: dsum_in and dsum_out go together")
+    if dsum_in is not None:
+        _dev(dsum_in, dsum_out)
+        _need(all(t.dtype == torch.float32 and t.is_contiguous() and t.numel() == D for t in (dsum_in, dsum_out)),
+              "layernorm_bwd dsum_in / dsum_out f32 [D]")
     _lib.call("vc_layernorm_bwd", _p(dy), dy.stride(0), _p(x), x.stride(0), M, D, _p(gamma), eps, _p(dx), dx.stride(0),
-              _p(dxb), dxb.stride(0), _p(dgamma), _p(dbeta), _p(work), work.numel(), _stream(x))
+              _p(dxb), dxb.stride(0), _p(dgamma), _p(dbeta), _p(dsum_in) if dsum_in is not None else None,
+              _p(dsum_out) if dsum_out is not None else None, _p(work), work.numel(), _stream(x))
     return dx
 
 

@@ -208,16 +208,16 @@ class TrainEngine:
             # MLP block: out = R1 + fc2(gelu(fc1(LN2(R1))))
             ops.gemm(dXb, W["f2T"], self.zeros[:I], "dgelu_tanh", dH, aux=self.Hpre[i])
             ops.wgrad(dXb, self.Hd[i], G(p + "mlp.fc2.weight"), self.work)
-            ops.colsum(dX, G(p + "mlp.fc2.bias"), self.work)
             ops.gemm(dH, W["f1T"], self.zeros[:D], "bias_f32", dY)
             ops.wgrad(dH, self.Y2[i], G(p + "mlp.fc1.weight"), self.work)
             ops.colsum(dH, G(p + "mlp.fc1.bias"), self.work)
+            # + the fc2 / o_proj bias gradients: column sums of dX before / after this update
             ops.layernorm_bwd(dY, self.R[2 * i + 1], P(p + "layernorm_after.weight"), eps, dX, dXb,
-                              G(p + "layernorm_after.weight"), G(p + "layernorm_after.bias"), self.work, m=B * S)
+                              G(p + "layernorm_after.weight"), G(p + "layernorm_after.bias"), self.work, m=B * S,
+                              dsum_in=G(p + "mlp.fc2.bias"), dsum_out=G(p + "attention.o_proj.bias"))
             # attention block: R1 = R0 + o_proj(attn(qkv(LN1(R0))))
             ops.gemm(dXb, W["oT"], self.zeros[:D], "bias", dO)
             ops.wgrad(dXb, self.O[i], G(p + "attention.o_proj.weight"), self.work)
-            ops.colsum(dX, G(p + "attention.o_proj.bias"), self.work)
             ev = self.kernel_events  # optional HIP-event timing of the attention backward (bench.py)
             if ev is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -338,12 +338,15 @@ int vc_attention_bwd(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64
  * LayerNorm backward fused with the residual-gradient add (nn.LayerNorm layernorm_before /
  * layernorm_after backward, TF5/.../modeling_vivit.py:245-266):
  * dx[m] += LN'(x[m]) . dy[m] (f32, in place), dxb[m] = bf16(dx[m]); dgamma / dbeta = column
- * sums over the M rows (overwritten).  D in {256, 512, 768, 1024};
- * work: f32 scratch of >= (min(512, ceil(M/4)) + 16) * 2D elements.
+ * sums over the M rows (overwritten).  Optional (both or neither): dsum_in / dsum_out = column
+ * sums of dx before / after the update — the bias gradients of the Linear layers whose outputs
+ * these residual gradients are (fc2 and o_proj around layernorm_after).  D in {256, 512, 768,
+ * 1024}; work: f32 scratch of >= (nb + ceil(nb/32)) * 4D elements, nb = min(512, ceil(M/4)).
  */
 int vc_layernorm_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx, int64_t M, int64_t D,
                      const float* gamma, float eps, float* dx, int64_t lddx, uint16_t* dxb, int64_t lddxb,
-                     float* dgamma, float* dbeta, float* work, int64_t work_elems, hipStream_t stream);
+                     float* dgamma, float* dbeta, float* dsum_in, float* dsum_out, float* work, int64_t work_elems,
+                     hipStream_t stream);
 
 /*
  * out[n] = (n < nscaled ? scale : 1) * sum over R rows of in[r][n]; dtype 0 = f32, 1 = bf16

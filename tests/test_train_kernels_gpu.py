@@ -124,10 +124,19 @@ def test_layernorm_bwd(M, D):
     dxb = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
     dg = torch.zeros(D, device=DEV)
     db = torch.zeros(D, device=DEV)
-    work = torch.empty((min(512, (M + 3) // 4) + 16) * 2 * D, device=DEV)
-    O.layernorm_bwd(dy.to(DEV), x.to(DEV), gamma.to(DEV), 1e-6, dx, dxb, dg, db, work)
+    nb = min(512, (M + 3) // 4)
+    work = torch.empty((nb + (nb + 31) // 32) * 4 * D, device=DEV)
+    s_in, s_out = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+    O.layernorm_bwd(dy.to(DEV), x.to(DEV), gamma.to(DEV), 1e-6, dx, dxb, dg, db, work, dsum_in=s_in, dsum_out=s_out)
     ref = dx0 + xr.grad
     np.testing.assert_allclose(dx.cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
+    # the fused bias gradients: column sums of dx before and after the update
+    np.testing.assert_allclose(s_in.cpu().numpy(), dx0.double().sum(0).numpy(), rtol=1e-4, atol=1e-3)
+    np.testing.assert_allclose(s_out.cpu().numpy(), ref.double().sum(0).numpy(), rtol=1e-4, atol=1e-3)
+    # without the sums (the layernorm_before call of the train step)
+    dx2 = dx0.to(DEV).clone()
+    O.layernorm_bwd(dy.to(DEV), x.to(DEV), gamma.to(DEV), 1e-6, dx2, dxb, dg, db, work)
+    torch.testing.assert_close(dx2, dx)
     np.testing.assert_array_equal(dxb.cpu().float().numpy(), dx.cpu().bfloat16().float().numpy())
     np.testing.assert_allclose(dg.cpu().numpy(), gr.grad.numpy(), rtol=1e-4, atol=1e-3)
     np.testing.assert_allclose(db.cpu().numpy(), br.grad.numpy(), rtol=1e-4, atol=1e-3)
