@@ -40,9 +40,10 @@ __device__ __forceinline__ float gelu_tanh(float x) {
     // gelu_fast: 0.5x(1+tanh(u)), u = 0.7978845608 x (1 + 0.044715 x^2)  (TF5/activations.py)
     // evaluated as x * sigmoid(2u) = x / (1 + 2^(-2u log2 e)): one v_exp_f32 + one v_rcp_f32
     // instead of libm tanhf (rel. error ~1e-7, far below the bf16 rounding of the output).
-    const float u = 0.7978845608f * x * (1.0f + 0.044715f * x * x);
-    const float e = __builtin_amdgcn_exp2f(-2.8853900817779268f * u);  // 2*log2(e)
-    return x * __builtin_amdgcn_rcpf(1.0f + e);
+    // constants folded: -2 log2(e) u = x (k1 + k2 x^2), k1 = -2 log2(e) 0.7978845608, k2 = k1 0.044715
+    // (5 VALU + 2 transcendental per element in the fc1 epilogue)
+    const float z = x * __builtin_fmaf(-0.10294324f, x * x, -2.3022082f);
+    return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z));
 }
 // d/dx gelu_fast = 0.5(1 + tanh u) + 0.5 x (1 - tanh^2 u) * 0.7978845608 (1 + 3*0.044715 x^2)
 __device__ __forceinline__ float dgelu_tanh(float x) {
