@@ -424,12 +424,13 @@ template <int EPI, int ABL = 0>  // ABL: timing ablations (1 no loop loads, 2 no
 __global__ void __launch_bounds__(512, 1)
 gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
                          int nbm, int nbn, int K, int N, const float* __restrict__ bias, uint16_t* __restrict__ out,
-                         int64_t ldo) {
+                         int64_t ldo, uint16_t* __restrict__ pre_out, int64_t ldpre) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int BM = 256, BN = 256, BKH = 32, NS = 4;
     constexpr int SLOT = (BM + BN) * 64;   // 32 KiB
     constexpr int TM = 128, TN = 64, MI = 4, NI = 2;
-    constexpr int NST = MI * NI * 2;       // 16-B stores per wave per tile epilogue
+    constexpr bool SAVE = EPI == VC_EPI_BIAS_GELU_TANH_SAVE;  // + bf16 pre-activation to pre_out
+    constexpr int NST = MI * NI * 2 * (SAVE ? 2 : 1);          // 16-B stores per wave per tile epilogue
     float* bias_lds = reinterpret_cast<float*>(smem + NS * SLOT);
 
     const int ntiles = nbm * nbn;
@@ -589,9 +590,10 @@ gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint
         for (int i = 0; i < MI; ++i) {
             const int64_t m = m0 + wm * TM + i * 32 + r;
             uint16_t* orow = out + m * ldo;
+            uint16_t* prow = SAVE ? pre_out + m * ldpre : nullptr;
 #pragma unroll
             for (int j = 0; j < NI; ++j) {
-                unsigned pk[4][2];
+                unsigned pk[4][2], pp[4][2];
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     const int nl = (int)n0 + wn * TN + j * 32 + g * 8 + h * 4;
@@ -600,7 +602,11 @@ gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint
                     float v1 = acc[i][j][4 * g + 1] + bb.y;
                     float v2 = acc[i][j][4 * g + 2] + bb.z;
                     float v3 = acc[i][j][4 * g + 3] + bb.w;
-                    if (EPI == VC_EPI_BIAS_GELU_TANH) {
+                    if constexpr (SAVE) {
+                        pp[g][0] = pack2bf(v0, v1);
+                        pp[g][1] = pack2bf(v2, v3);
+                    }
+                    if (EPI == VC_EPI_BIAS_GELU_TANH || SAVE) {
                         v0 = gelu_tanh(v0); v1 = gelu_tanh(v1); v2 = gelu_tanh(v2); v3 = gelu_tanh(v3);
                     } else if (EPI == VC_EPI_BIAS_GELU_ERF) {
                         v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
@@ -620,6 +626,13 @@ gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint
                     v.x = s0[0]; v.y = s1[0]; v.z = s0[1]; v.w = s1[1];
                     if constexpr (ABL & 4) asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w), "v"(orow + col));
                     else *reinterpret_cast<uint4*>(orow + col) = v;
+                    if constexpr (SAVE) {
+                        auto q0 = __builtin_amdgcn_permlane32_swap(pp[g][0], pp[g + 1][0], false, false);
+                        auto q1 = __builtin_amdgcn_permlane32_swap(pp[g][1], pp[g + 1][1], false, false);
+                        uint4 u;
+                        u.x = q0[0]; u.y = q1[0]; u.z = q0[1]; u.w = q1[1];
+                        *reinterpret_cast<uint4*>(prow + col) = u;
+                    }
                 }
             }
         }
@@ -690,7 +703,8 @@ static int num_cus() {
 
 template <int E, int ABL = 0>
 static int launch_persist(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
-                          int N, const float* bias, void* out, int64_t ldo, hipStream_t stream) {
+                          int N, const float* bias, void* out, int64_t ldo, hipStream_t stream,
+                          const float* aux = nullptr, int64_t ldaux = 0) {
     const int lds = 4 * 512 * 64 + N * 4;
     static int attr_set = 0;
     if (attr_set < lds) {
@@ -703,7 +717,8 @@ static int launch_persist(const uint16_t* A, int64_t lda, const uint16_t* W, int
     int grid = num_cus() / 8 * 8;
     if (grid > (ntiles + 7) / 8 * 8) grid = (ntiles + 7) / 8 * 8;
     gemm_bf16_persist_kernel<E, ABL><<<(unsigned)grid, 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, N, bias,
-                                                                      (uint16_t*)out, ldo);
+                                                                      (uint16_t*)out, ldo,
+                                                                      (uint16_t*)const_cast<float*>(aux), ldaux);
     return check_launch("vc_gemm_bf16");
 }
 
@@ -721,8 +736,8 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
         case 5: return launch_cfg<128, 128, 2, 4, E, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 4:
             if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
-                          E == VC_EPI_BIAS_RELU_BF16)
-                return launch_persist<E>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
+                          E == VC_EPI_BIAS_RELU_BF16 || E == VC_EPI_BIAS_GELU_TANH_SAVE)
+                return launch_persist<E>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s, aux, ldaux);
             return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 4 supports bf16-output epilogues only");
         case 14: return launch_persist<E, 1>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
         case 24: return launch_persist<E, 2>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
@@ -761,7 +776,7 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
 //     shape measured: B=8 fc2 768 vs 677, o_proj 491 vs 430, fc1 (erf/other epilogues) 664 vs 602.
 static int pick_cfg(int64_t M, int64_t N, int64_t K, int epi) {
     const bool bf16_out = epi == VC_EPI_BIAS_BF16 || epi == VC_EPI_BIAS_GELU_TANH || epi == VC_EPI_BIAS_GELU_ERF ||
-                          epi == VC_EPI_BIAS_RELU_BF16;
+                          epi == VC_EPI_BIAS_RELU_BF16 || epi == VC_EPI_BIAS_GELU_TANH_SAVE;
     if (bf16_out && M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && K >= 192 && N <= 8192 &&
         (M / 256) * (N / 256) >= 64)
         return 4;
@@ -796,16 +811,22 @@ extern "C" int vc_gemm_bf16_cfg(const uint16_t* A, int64_t lda, const uint16_t* 
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: GELU_SAVE / DGELU epilogues need a bf16 aux with ldaux >= N");
     if (epilogue == VC_EPI_BIAS_ADD_F32 && (!aux || ldaux % 4 || ldaux < N || ((uintptr_t)aux & 15)))
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: BIAS_ADD_F32 epilogue needs an f32 aux with ldaux >= N");
-    if (cfg < 0) cfg = pick_cfg(M, N, K, epilogue);
+    // the persistent kernel writes 16-byte row chunks of out (and of the saved pre-activation)
+    const bool st16_ok = ldo % 8 == 0 && (epilogue != VC_EPI_BIAS_GELU_TANH_SAVE || (ldaux % 8 == 0 && !((uintptr_t)aux & 15)));
+    if (cfg < 0) {
+        cfg = pick_cfg(M, N, K, epilogue);
+        if (cfg == 4 && !st16_ok) cfg = 5;
+    }
     const int ablation = cfg >= 10 ? cfg : -1;  // x3 / x4: timing-only ablations of cfg 3 / 4 (wrong results)
     if (ablation > 0) cfg = (ablation % 10 == 4) ? 4 : 3;
     if (cfg < 0 || cfg >= kNumCfgs || M % kCfgs[cfg].bm || N % kCfgs[cfg].bn)
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: no tile config divides M x N");
     if ((M / kCfgs[cfg].bm) * (N / kCfgs[cfg].bn) > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: grid too large");
     const int k = (int)K;
-    if (cfg == 4 && (K % 32 || K / 32 < 6 || N > 8192 ||
-                     (epilogue > VC_EPI_BIAS_GELU_ERF && epilogue != VC_EPI_BIAS_RELU_BF16)))
-        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 4 needs K%32==0, K>=192, N<=8192, bf16 epilogue");
+    if (cfg == 4 && (K % 32 || K / 32 < 6 || N > 8192 || !st16_ok ||
+                     (epilogue > VC_EPI_BIAS_GELU_ERF && epilogue != VC_EPI_BIAS_RELU_BF16 &&
+                      epilogue != VC_EPI_BIAS_GELU_TANH_SAVE)))
+        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 4 needs K%32==0, K>=192, N<=8192, ldo%8==0, bf16 epilogue");
     if (ablation > 0) {
         if (epilogue != VC_EPI_BIAS_BF16) return fail(VC_ERR_INVALID_ARG, "ablation: bias epilogue only");
         return launch_epi<VC_EPI_BIAS_BF16>(ablation, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);

@@ -207,6 +207,26 @@ def test_gemm_training_epilogues():
     np.testing.assert_allclose(dh.cpu().float().numpy(), ref.numpy(), rtol=1e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("cfg", [4, 5, -1])
+def test_gemm_gelu_save_configs(cfg):
+    """GELU_SAVE on the persistent 256x256 kernel (cfg 4, two bf16 outputs per tile) vs cfg 5:
+    identical bits (same fp32 accumulation order per output is not guaranteed, so compare to the
+    double reference), at a shape with several tiles per workgroup."""
+    O = ops()
+    g = torch.Generator().manual_seed(6)
+    M, N, K = 4096, 3072, 768
+    a = (torch.randn(M, K, generator=g) * 0.5).bfloat16()
+    w = (torch.randn(N, K, generator=g) * 0.05).bfloat16()
+    bias = torch.randn(N, generator=g) * 0.1
+    acc = (a.double() @ w.double().T + bias.double()).float()
+    h = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    pre = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    O.gemm(a.to(DEV), w.to(DEV), bias.to(DEV), "bias_gelu_tanh_save", h, aux=pre, cfg=cfg)
+    np.testing.assert_allclose(pre.cpu().float().numpy(), acc.bfloat16().float().numpy(), rtol=0, atol=1.6e-2)
+    from oracle.vivit_ref import gelu_fast
+    np.testing.assert_allclose(h.cpu().float().numpy(), gelu_fast(acc).numpy(), rtol=1e-2, atol=1e-2)
+
+
 # ------------------------------------------------------------------------- classifier head / embeddings
 def test_cls_head_bwd():
     O = ops()

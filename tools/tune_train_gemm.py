@@ -51,7 +51,7 @@ def main():
         fl = 2.0 * M * N * K
         cands = {}
         for c, (bm, bn) in TILES.items():
-            if c == 4 and epi != "bias":
+            if c == 4 and epi not in ("bias", "bias_gelu_tanh_save"):
                 continue
             if M % bm or N % bn:
                 continue
