@@ -29,8 +29,12 @@ __device__ __forceinline__ unsigned short f2bf(float x) {
     __bf16 b = (__bf16)x;
     return __builtin_bit_cast(unsigned short, b);
 }
+// two f32 -> packed bf16 pair in ONE v_cvt_pk_bf16_f32 (RNE; the scalar casts + shift/or
+// form costs four VALU ops)
+typedef __bf16 v2bf __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ unsigned int pack2bf(float lo, float hi) {
-    return (unsigned int)f2bf(lo) | ((unsigned int)f2bf(hi) << 16);
+    const v2f x = {lo, hi};
+    return __builtin_bit_cast(unsigned int, __builtin_convertvector(x, v2bf));
 }
 __device__ __forceinline__ float bf2f(unsigned short u) {
     return __builtin_bit_cast(float, ((unsigned int)u) << 16);

@@ -107,7 +107,7 @@ def test_gemm_bias_bf16(M, N, K):
     assert err < 8e-3, err
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("epi", ["bias", "bias_gelu_tanh"])
 def test_gemm_every_tile_config(cfg, epi):
     """Every block-tile configuration on a shape with more tiles than CUs (the persistent
@@ -120,6 +120,25 @@ def test_gemm_every_tile_config(cfg, epi):
     ops().gemm(a.to(DEV), w.to(DEV), bias.to(DEV), epi, out, cfg=cfg)
     err = ((out.float().cpu() - ref).abs() / (ref.abs() + 1.0)).max().item()
     assert err < 8e-3, err
+
+
+@pytest.mark.parametrize("M,N,K", [(768, 768, 192), (256, 256, 768), (2304, 768, 3072), (25344, 3072, 768),
+                                   (4096, 2304, 256), (12800, 768, 768)])
+@pytest.mark.parametrize("epi", ["bias", "bias_gelu_erf", "bias_relu"])
+def test_gemm_pingpong_matches_persistent(M, N, K, epi):
+    """cfg 6 (staggered ping-pong schedule, staging cursor running across tiles) computes the
+    same MFMAs in the same k order as cfg 4: bit-identical outputs, at shapes with one tile
+    per workgroup, tile counts not a multiple of 8, the minimum K (6 half-tiles) and long K."""
+    a, w, bias, ref = _gemm_case(M, N, K, M + 7 * N + K)
+    ad, wd, bd = a.to(DEV), w.to(DEV), bias.to(DEV)
+    o4 = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    o6 = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+    ops().gemm(ad, wd, bd, epi, o4, cfg=4)
+    ops().gemm(ad, wd, bd, epi, o6, cfg=6)
+    assert torch.equal(o4, o6)
+    if epi == "bias":
+        err = ((o6.float().cpu() - ref).abs() / (ref.abs() + 1.0)).max().item()
+        assert err < 8e-3, err
 
 
 def test_gemm_orientation_asymmetric():

@@ -15,7 +15,7 @@ from vclip_amd import ops  # noqa: E402
 SHAPES = [("qkv", 2304, 768, "bias"), ("o_proj", 768, 768, "bias_add_f32"), ("fc1", 3072, 768, "bias_gelu_tanh_save"),
           ("fc2", 768, 3072, "bias_add_f32"), ("dgrad_fc2", 3072, 768, "dgelu_tanh"), ("dgrad_fc1", 768, 3072, "bias_f32"),
           ("dgrad_o", 768, 768, "bias"), ("dgrad_qkv", 768, 2304, "bias_f32")]
-TILES = {0: (256, 128), 1: (128, 128), 2: (128, 256), 3: (256, 256), 4: (256, 256), 5: (128, 128)}
+TILES = {0: (256, 128), 1: (128, 128), 2: (128, 256), 3: (256, 256), 4: (256, 256), 5: (128, 128), 6: (256, 256)}
 
 
 def timeit(fn, iters):
@@ -51,7 +51,7 @@ def main():
         fl = 2.0 * M * N * K
         cands = {}
         for c, (bm, bn) in TILES.items():
-            if c == 4 and epi not in ("bias", "bias_gelu_tanh_save"):
+            if c in (4, 6) and epi not in ("bias", "bias_gelu_tanh_save"):
                 continue
             if M % bm or N % bn:
                 continue
