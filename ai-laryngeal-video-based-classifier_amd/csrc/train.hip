@@ -639,25 +639,35 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
 __global__ void __launch_bounds__(256) pack_weight_kernel(const float* __restrict__ src, int64_t N, int64_t K,
                                                           int64_t nscaled, float scale, uint16_t* __restrict__ dst,
                                                           uint16_t* __restrict__ dstT) {
+    // 64 x 64 tile; each thread moves 4 consecutive elements per pass (float4 in, 8-B bf16 out),
+    // the transposed write goes through LDS as 4 consecutive n per thread (host: N, K % 4 == 0)
     __shared__ float tile[64][65];
     const int64_t n0 = (int64_t)blockIdx.y * 64, k0 = (int64_t)blockIdx.x * 64;
-    for (int i = threadIdx.x; i < 4096; i += 256) {
-        const int rr = i >> 6, cc = i & 63;
-        const int64_t n = n0 + rr, k = k0 + cc;
-        float v = 0.f;
+    const int t = threadIdx.x, rr0 = t >> 4, c4 = (t & 15) * 4;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int rr = rr0 + p * 16;
+        const int64_t n = n0 + rr, k = k0 + c4;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
         if (n < N && k < K) {
-            v = src[n * K + k];
-            if (n < nscaled) v *= scale;
-            if (dst) dst[n * K + k] = f2bf(v);
+            v = *reinterpret_cast<const float4*>(src + n * K + k);
+            if (n < nscaled) { v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale; }
+            if (dst) *reinterpret_cast<uint2*>(dst + n * K + k) = make_uint2(pack2bf(v.x, v.y), pack2bf(v.z, v.w));
         }
-        tile[rr][cc] = v;
+        tile[rr][c4 + 0] = v.x;
+        tile[rr][c4 + 1] = v.y;
+        tile[rr][c4 + 2] = v.z;
+        tile[rr][c4 + 3] = v.w;
     }
     if (!dstT) return;
     __syncthreads();
-    for (int i = threadIdx.x; i < 4096; i += 256) {
-        const int rr = i >> 6, cc = i & 63;  // rr: k, cc: n
-        const int64_t k = k0 + rr, n = n0 + cc;
-        if (n < N && k < K) dstT[k * N + n] = f2bf(tile[cc][rr]);
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int kr = rr0 + p * 16;  // k within the tile; c4: 4 consecutive n
+        const int64_t k = k0 + kr, n = n0 + c4;
+        if (n < N && k < K)
+            *reinterpret_cast<uint2*>(dstT + k * N + n) =
+                make_uint2(pack2bf(tile[c4][kr], tile[c4 + 1][kr]), pack2bf(tile[c4 + 2][kr], tile[c4 + 3][kr]));
     }
 }
 
@@ -826,7 +836,9 @@ int vc_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
 int vc_pack_weight(const float* src, int64_t N, int64_t K, int64_t nscaled, float scale, uint16_t* dst, uint16_t* dstT,
                    hipStream_t stream) {
     if (!src || (!dst && !dstT)) return fail(VC_ERR_INVALID_ARG, "vc_pack_weight: null pointer");
-    if (N <= 0 || K <= 0) return fail(VC_ERR_INVALID_ARG, "vc_pack_weight: bad shape");
+    if (N <= 0 || K <= 0 || N % 4 || K % 4) return fail(VC_ERR_INVALID_ARG, "vc_pack_weight: need N, K % 4 == 0");
+    if ((((uintptr_t)src) & 15) || (((uintptr_t)dst) & 7) || (((uintptr_t)dstT) & 7))
+        return fail(VC_ERR_INVALID_ARG, "vc_pack_weight: src 16-B / dst 8-B alignment");
     dim3 grid((unsigned)((K + 63) / 64), (unsigned)((N + 63) / 64));
     pack_weight_kernel<<<grid, 256, 0, stream>>>(src, N, K, nscaled, scale, dst, dstT);
     return check_launch("vc_pack_weight");

@@ -393,6 +393,7 @@ int vc_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
 /*
  * fp32 master weight [N][K] -> bf16 [N][K] (dst) and/or bf16 [K][N] (dstT, the dgrad operand);
  * rows < nscaled are multiplied by scale first (q projection * softmax scale * log2 e).
+ * N, K % 4 == 0; src 16-byte, dst / dstT 8-byte aligned.
  */
 int vc_pack_weight(const float* src, int64_t N, int64_t K, int64_t nscaled, float scale, uint16_t* dst, uint16_t* dstT,
                    hipStream_t stream);

@@ -284,14 +284,15 @@ def test_adamw_matches_torch():
     np.testing.assert_allclose(p.cpu().numpy(), ref.detach().numpy(), rtol=1e-6, atol=1e-7)
 
 
-def test_pack_weight():
+@pytest.mark.parametrize("N,K,ns", [(200, 132, 70), (2304, 768, 768), (68, 4, 0)])
+def test_pack_weight(N, K, ns):
     O = ops()
     g = torch.Generator().manual_seed(14)
-    w = torch.randn(200, 130, generator=g)
-    dst = torch.zeros(200, 130, dtype=torch.bfloat16, device=DEV)
-    dst_t = torch.zeros(130, 200, dtype=torch.bfloat16, device=DEV)
-    O.pack_weight(w.to(DEV), dst, dst_t, nscaled=70, scale=0.3)
+    w = torch.randn(N, K, generator=g)
+    dst = torch.zeros(N, K, dtype=torch.bfloat16, device=DEV)
+    dst_t = torch.zeros(K, N, dtype=torch.bfloat16, device=DEV)
+    O.pack_weight(w.to(DEV), dst, dst_t, nscaled=ns, scale=0.3)
     ref = w.clone()
-    ref[:70] *= 0.3
+    ref[:ns] *= 0.3
     np.testing.assert_array_equal(dst.cpu().float().numpy(), ref.bfloat16().float().numpy())
     np.testing.assert_array_equal(dst_t.cpu().float().numpy(), ref.T.bfloat16().float().numpy())
