@@ -4,7 +4,7 @@ set -o pipefail
 mkdir -p gpurun_out
 STEPS=${STEPS:-30}
 echo "== pytest -m gpu"
-timeout -k 10 480 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 480 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; tail -5 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || { tail -60 gpurun_out/pytest_gpu.log; exit $rc; }
 echo "== smoke"
 timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
