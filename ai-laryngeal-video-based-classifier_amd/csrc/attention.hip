@@ -80,6 +80,13 @@ __device__ __forceinline__ void attn_sync() {
 // 32 adds sched_group_barrier directives interleaving tile t+1's QK^T MFMAs with tile t's
 // exp2 / sum VALU (correct; measured 3 % SLOWER than hipcc's own schedule at B = 8 and B = 4,
 // tools/ab_attn_interleave.py, so the shipped build leaves the scheduling to the compiler).
+// Correct variants measured at B = 8 (tools/ablate_attn.py, interleaved rounds, r01 session 4):
+// 64 / 128 static s_setprio for one of the two co-resident workgroups: +1.5 % / 0 (noise band);
+// 256 split-half softmax + P.V (three scheduling regions): 1.5 % slower; 512 K-fragment
+// prefetch across the barrier (vmcnt(0) per tile): 0.  PMC of the shipped build
+// (tools/pmc_attn.sh): MFMA busy 46 % of cycles at 1.98 GHz, wave cycles 44 % issuing /
+// 33 % issue-stalled (matrix pipe or dependency) / 23 % in s_waitcnt or barrier; zero LDS
+// bank conflicts; ~84 non-MFMA VALU per wave per 64-key tile.
 // WLSE: also store the base-2 log-sum-exp of each query's scores, lse[(b*H + h)*S + q] =
 // m + log2(l) (running max and row sum), from which the backward kernels recompute P.
 template <int QB, int ABL, bool WLSE = false>
@@ -243,10 +250,16 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
     };
 
     const int ntiles = (S + AK - 1) / AK;
+    // ABL 64 / 128: static wave priority for one of the two workgroups that share a CU
+    // (MI355X_MICROARCH.md "Two waves per SIMD" item 4); initially co-resident blocks are
+    // L and L + 256 (64 = prio by bit 8 of L), 128 = by bit 3 (neighbours within an XCD)
+    if constexpr (ABL & 64) { if ((L >> 8) & 1) __builtin_amdgcn_s_setprio(1); }
+    if constexpr (ABL & 128) { if ((L >> 3) & 1) __builtin_amdgcn_s_setprio(1); }
     stage(0);
     if (ntiles > 1) stage(1);
     if (ntiles > 2) stage(2);
-    if (ntiles > 2) attn_wait_vm<4>();  // tiles 0 and 1 resident, 2 in flight
+    // ABL & 512 (K-fragment prefetch) keeps no tile in flight across the per-tile barrier
+    if (!(ABL & 512) && ntiles > 2) attn_wait_vm<4>();  // tiles 0 and 1 resident, 2 in flight
     else attn_wait_vm<0>();
     attn_sync();
     // tile 0 establishes the running max m
@@ -362,20 +375,180 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
         }
     };
 
+    // ---- split-half iteration (ABL & 256): the tile's two 32-key blocks go through
+    //      softmax and P.V one after the other, each behind its own overflow check, so the
+    //      P.V MFMAs of block 0 and the QK^T MFMAs of tile t+1's block 1 sit beside block 1's
+    //      exp2 / sum VALU (three scheduling regions of 4 / 8 / 4 MFMAs instead of 8 / 8 with
+    //      all of the transcendental work in the first).  A re-base found in block 1 scales
+    //      O and l, which already hold block 0's terms at the old base: O_new = alpha O_old.
+    auto qk_half = [&](const char* slot, int kb, v16f& sc) __attribute__((always_inline)) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            const v8bf kf = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(slot + koff[kk] + kb * 4096));
+            sc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[0][kk], kk == 0 ? minit[0] : sc, 0, 0, 0);
+        }
+    };
+    auto mask_half = [&](int t, int kb, v16f& sc) __attribute__((always_inline)) {
+        const int kv0 = t * AK + kb * 32;
+        if (kv0 + 32 > S) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int key = (e & 3) + 8 * (e >> 2) + 4 * h;
+                if (kv0 + key >= S) sc[e] = -INFINITY;
+            }
+        }
+    };
+    auto expsum_half = [&](v16f& sc) __attribute__((always_inline)) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) sc[e] = __builtin_amdgcn_exp2f(sc[e]);
+        v2f u[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) u[j] = v2f{sc[4 * j], sc[4 * j + 1]} + v2f{sc[4 * j + 2], sc[4 * j + 3]};
+        return (u[0] + u[1]) + (u[2] + u[3]);
+    };
+    auto pv_half = [&](const char* slot, int kb, const v16f& sc) __attribute__((always_inline)) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            v8bf pf;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) pf[jj] = (__bf16)sc[8 * s2 + jj];
+#pragma unroll
+            for (int db = 0; db < 2; ++db) {
+                const char* pa = slot + voff[db] + (kb * 32 + 16 * s2) * 128;
+                v4s va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)pa);
+                v4s vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(pa + 8 * 128));
+                v8s vv;
+                vv[0] = va[0]; vv[1] = va[1]; vv[2] = va[2]; vv[3] = va[3];
+                vv[4] = vb[0]; vv[5] = vb[1]; vv[6] = vb[2]; vv[7] = vb[3];
+                o[0][db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf, vv), pf, o[0][db], 0, 0, 0);
+            }
+        }
+    };
+    // exact re-base of tile t (both blocks recomputed into scur); returns nothing, updates state
+    auto rebase = [&](const char* slot, int t, v16f (&snx)[2], int nvalid_next) __attribute__((always_inline)) {
+        qk(slot, t, scur);
+        const float delta = fmaxf(rowmax_of(scur[0]), 0.f);
+        const float alpha = __builtin_amdgcn_exp2f(-delta);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            scur[0][0][e] -= delta;
+            scur[0][1][e] -= delta;
+            o[0][0][e] *= alpha;
+            o[0][1][e] *= alpha;
+            minit[0][e] -= delta;
+        }
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+            if (kb < nvalid_next) {
+#pragma unroll
+                for (int e = 0; e < 16; ++e) snx[kb][e] -= delta;
+            }
+        l_run[0] *= alpha;
+    };
+    auto iter_split = [&](auto next_c, const char* slot, const char* nslot, int t) __attribute__((always_inline)) {
+        constexpr int NEXT = decltype(next_c)::value;
+        if (!(ABL & 1) && t + 3 < ntiles) stage(t + 3);
+        v16f snext[2];
+        // region 1: QK^T of tile t+1 block 0 beside block 0's exp2 / sum
+        if constexpr (NEXT != 2) {
+            qk_half(nslot, 0, snext[0]);
+            if constexpr (NEXT == 1) mask_half(t + 1, 0, snext[0]);
+        }
+        v2f ps = expsum_half(scur[0][0]);
+        if (__any(!(ps[0] + ps[1] <= LIM))) {
+            rebase(slot, t, snext, NEXT != 2 ? 1 : 0);
+            ps = expsum_half(scur[0][0]);
+        }
+        l_run[0] += ps;
+        // region 2: P.V of block 0, QK^T of tile t+1 block 1, block 1's exp2 / sum
+        pv_half(slot, 0, scur[0][0]);
+        if constexpr (NEXT != 2) {
+            qk_half(nslot, 1, snext[1]);
+            if constexpr (NEXT == 1) mask_half(t + 1, 1, snext[1]);
+        }
+        ps = expsum_half(scur[0][1]);
+        if (__any(!(ps[0] + ps[1] <= LIM))) {
+            rebase(slot, t, snext, NEXT != 2 ? 2 : 0);
+            ps = expsum_half(scur[0][1]);
+        }
+        l_run[0] += ps;
+        // region 3: P.V of block 1
+        pv_half(slot, 1, scur[0][1]);
+        if (t + 2 < ntiles) {
+            if (t + 3 < ntiles) attn_wait_vm<4>();
+            else attn_wait_vm<0>();
+            attn_sync();
+        }
+        if constexpr (NEXT != 2) { scur[0][0] = snext[0]; scur[0][1] = snext[1]; }
+    };
+    // ---- K-fragment prefetch (ABL & 512): the K fragments of tile t+1 are read into
+    //      registers during the P.V phase of tile t-1, so the QK^T MFMAs after the barrier
+    //      start without an LDS round trip.  That needs K_{t+2} resident during iteration t:
+    //      each iteration ends with vmcnt(0) (tile t+3, staged at its start, has landed)
+    //      instead of keeping one tile in flight across the barrier.
+    v8bf kfr[4][2];
+    auto read_k = [&](const char* slot) __attribute__((always_inline)) {
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+            kfr[kk][0] = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(slot + koff[kk]));
+            kfr[kk][1] = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(slot + koff[kk] + 4096));
+        }
+    };
+    if constexpr (ABL & 512) {
+        if (ntiles > 1) read_k(smem + KV_SLOT);
+    }
+    auto iter_pf = [&](auto next_c, const char* slot, const char* nslot, const char* n2slot, int t) __attribute__((always_inline)) {
+        constexpr int NEXT = decltype(next_c)::value;
+        if (!(ABL & 1) && t + 3 < ntiles) stage(t + 3);
+        v16f snext[2];
+        if constexpr (NEXT != 2) {
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                snext[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[kk][0], qf[0][kk], kk == 0 ? minit[0] : snext[0], 0, 0, 0);
+                snext[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kfr[kk][1], qf[0][kk], kk == 0 ? minit[0] : snext[1], 0, 0, 0);
+            }
+            if constexpr (NEXT == 1) {
+                mask_half(t + 1, 0, snext[0]);
+                mask_half(t + 1, 1, snext[1]);
+            }
+        }
+        v2f ps[1];
+        expsum(scur, ps);
+        if (__any(!(ps[0][0] + ps[0][1] <= LIM))) {
+            rebase(slot, t, snext, NEXT != 2 ? 2 : 0);
+            expsum(scur, ps);
+        }
+        l_run[0] += ps[0];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) pv_half(slot, kb, scur[0][kb]);
+        if (t + 2 < ntiles) read_k(n2slot);  // K_{t+2}: resident since the last barrier
+        if (t + 1 < ntiles) {
+            attn_wait_vm<0>();
+            attn_sync();
+        }
+        if constexpr (NEXT != 2) { scur[0][0] = snext[0]; scur[0][1] = snext[1]; }
+    };
+    auto step = [&](auto next_c, const char* slot, const char* nslot, const char* n2slot, int t) __attribute__((always_inline)) {
+        if constexpr ((ABL & 512) && QB == 1) iter_pf(next_c, slot, nslot, n2slot, t);
+        else if constexpr ((ABL & 256) && QB == 1) iter_split(next_c, slot, nslot, t);
+        else iter(next_c, slot, nslot, t);
+    };
+
     using full_c = std::integral_constant<int, 0>;
     const int nfull = S / AK;  // full tiles
     int t = 0;
     for (; t + 5 <= nfull; t += NSLOT) {  // iterations t..t+3 all have a full next tile
-        iter(full_c{}, smem + 0 * KV_SLOT, smem + 1 * KV_SLOT, t);
-        iter(full_c{}, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, t + 1);
-        iter(full_c{}, smem + 2 * KV_SLOT, smem + 3 * KV_SLOT, t + 2);
-        iter(full_c{}, smem + 3 * KV_SLOT, smem + 0 * KV_SLOT, t + 3);
+        step(full_c{}, smem + 0 * KV_SLOT, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, t);
+        step(full_c{}, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, smem + 3 * KV_SLOT, t + 1);
+        step(full_c{}, smem + 2 * KV_SLOT, smem + 3 * KV_SLOT, smem + 0 * KV_SLOT, t + 2);
+        step(full_c{}, smem + 3 * KV_SLOT, smem + 0 * KV_SLOT, smem + 1 * KV_SLOT, t + 3);
     }
     for (; t < ntiles; ++t) {  // at most 4 + 1 iterations: runtime slot, mask-checked next tile
         const char* slot = smem + (t % NSLOT) * KV_SLOT;
         const char* nslot = smem + ((t + 1) % NSLOT) * KV_SLOT;
-        if (t + 1 < ntiles) iter(std::integral_constant<int, 1>{}, slot, nslot, t);
-        else iter(std::integral_constant<int, 2>{}, slot, nslot, t);
+        const char* n2slot = smem + ((t + 2) % NSLOT) * KV_SLOT;
+        if (t + 1 < ntiles) step(std::integral_constant<int, 1>{}, slot, nslot, n2slot, t);
+        else step(std::integral_constant<int, 2>{}, slot, nslot, n2slot, t);
     }
 
     // ---- normalise and store O[q][d]: reg 4g+e of block db -> d = 32db + 8g + 4h + e;
@@ -464,7 +637,7 @@ extern "C" int vc_attention_fwd_ablation(const uint16_t* qkv, int64_t ld, int64_
 #define VC_ABL(QB, N) case 100 * (QB - 1) + N: launch_attn<QB, N>(qkv, ld, B, S, H, c_log2, out, ldo, stream); break;
     switch (abl) {
         VC_ABL(1, 0) VC_ABL(1, 1) VC_ABL(1, 2) VC_ABL(1, 4) VC_ABL(1, 6) VC_ABL(1, 8) VC_ABL(1, 12) VC_ABL(1, 14)
-        VC_ABL(1, 15) VC_ABL(1, 16) VC_ABL(1, 32)
+        VC_ABL(1, 15) VC_ABL(1, 16) VC_ABL(1, 32) VC_ABL(1, 64) VC_ABL(1, 128) VC_ABL(1, 256) VC_ABL(1, 320) VC_ABL(1, 512) VC_ABL(1, 576)
         default: return fail(VC_ERR_INVALID_ARG, "bad ablation");
     }
 #undef VC_ABL
