@@ -831,8 +831,9 @@ gemm_bf16_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t*
 struct GemmCfg {
     int bm, bn;
 };
-static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}, {128, 128}, {256, 256}};
-constexpr int kNumCfgs = 7;
+static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}, {128, 128}, {256, 256},
+                                 {64, 128}};
+constexpr int kNumCfgs = 8;
 
 template <int BM, int BN, int WM, int WN, int E, int ST = 3>
 static int launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
@@ -965,6 +966,7 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
         case 2: return launch_cfg<128, 256, 2, 4, E>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 3: return launch_big<E>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 5: return launch_cfg<128, 128, 2, 4, E, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 7: return launch_cfg<64, 128, 2, 4, E, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 4:
             if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
                           E == VC_EPI_BIAS_RELU_BF16 || E == VC_EPI_BIAS_GELU_TANH_SAVE)

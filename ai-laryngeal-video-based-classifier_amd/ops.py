@@ -116,6 +116,47 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: str, ou
     return out
 
 
+# tile rows, tile cols and workgroups per CU of the GEMM configs gemm_rounds() composes
+# (csrc/gemm.hip kCfgs; cfg 4 is the persistent 256x256 kernel, one workgroup per CU)
+_GEMM_TILES = {1: (128, 128, 1), 4: (256, 256, 1), 5: (128, 128, 2), 7: (64, 128, 2)}
+_NUM_CUS = {}
+
+
+def _num_cus(dev: torch.device) -> int:
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _NUM_CUS:
+        _NUM_CUS[key] = torch.cuda.get_device_properties(key).multi_processor_count
+    return _NUM_CUS[key]
+
+
+def gemm_rounds(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: str, out: torch.Tensor,
+                main_cfg: int, tail_cfg: int, m: int | None = None) -> torch.Tensor:
+    """gemm() as two launches when the tiles of `main_cfg` leave a partial last round on the
+    CUs: the main launch covers whole rounds (rows rounded down to its row tile), the tail
+    launch the remaining rows with the smaller tiles of `tail_cfg` in one round of its own.
+    Each output element runs the same MFMA sequence over K in either launch, so the result is
+    bit-identical to one launch (and stays batch-invariant).  Measured at ViViT-B B = 8
+    (tools/quant_probe.py): q|k|v 111.1 -> 105.5 us (cfg 4 + tail cfg 5), fc2 149.1 -> 139.2 us
+    (cfg 5 + tail cfg 1); o_proj and fc1 are slower split.  Inside the model forward the split
+    q|k|v + fc2 came out 0.6 % slower end to end (tools/ab_model.py round_split), so the ViViT
+    forward keeps one launch by default (VivitForVideoClassification.round_split)."""
+    M = a.shape[0] if m is None else m
+    N = w.shape[0]
+    bm, bn, per_cu = _GEMM_TILES[main_cfg]
+    tbm, tbn, tper_cu = _GEMM_TILES[tail_cfg]
+    cus = _num_cus(a.device)
+    slots, nbn = cus * per_cu, N // bn
+    rounds = (M // bm) * nbn // slots
+    m1 = (rounds * slots // nbn) * bm if rounds else 0
+    tail_tiles = (M - m1) // tbm * (N // tbn)
+    if (rounds == 0 or M % bm or N % bn or N % tbn or (M - m1) % tbm or m1 >= M
+            or tail_tiles > cus * tper_cu):
+        return gemm(a, w, bias, epilogue, out, m=M)
+    gemm(a, w, bias, epilogue, out, m=m1, cfg=main_cfg)
+    gemm(a[m1:], w, bias, epilogue, out[m1:], m=M - m1, cfg=tail_cfg)
+    return out
+
+
 def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, out: torch.Tensor,
               m: int | None = None) -> torch.Tensor:
     """LayerNorm of the first gamma.numel() columns of each row (x f32 -> out bf16)."""

@@ -17,6 +17,7 @@ fp32 biases / LayerNorm / position table / classifier.
 """
 from __future__ import annotations
 
+import functools
 import json
 import math
 from collections import OrderedDict
@@ -115,6 +116,10 @@ class VivitForVideoClassification(torch.nn.Module):
         self.concurrent_streams = None  # None / 1: one stream; n > 1: batch split over n HIP streams
         self.last_streams = 1
         self.kernel_events = None
+        # q|k|v and fc2 as whole-round + tail launches (ops.gemm_rounds): bit-identical, 5-7 %
+        # faster per GEMM in isolation but 0.6 % SLOWER in the model (tools/ab_model.py
+        # round_split, interleaved, B = 8: 9.340 vs 9.285 ms/step), so off by default
+        self.round_split = False
 
     # ---- state dict in HF naming ---------------------------------------------------
     def hf_state_dict(self):
@@ -348,27 +353,39 @@ class VivitForVideoClassification(torch.nn.Module):
         npatch, S, Mpad, Memb = self.geometry(B)
         eps = c.layer_norm_eps
         X, Y, QKV, O, Hd = ws["X"], ws["Y"], ws["QKV"], ws["O"], ws["Hd"]
-        ops.tubelet_im2col(pix, c.tubelet_size, ws["A_emb"])
-        ops.gemm(ws["A_emb"], pk["w_emb"], pk["b_emb"], "embed_f32", X, aux=pk["pos"][1:], group=npatch,
-                 group_stride=S, group_offset=1, m=Memb)
+        # optional per-launch HIP-event timing (bench.py), recorded on this part's stream, the
+        # one each kernel runs on: a list collects the attention launches only, a dict every op
+        ev = self.kernel_events
+
+        def run(name, fn, *args, **kw):
+            if ev is None or (not isinstance(ev, dict) and name != "attention"):
+                return fn(*args, **kw)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            r = fn(*args, **kw)
+            e1.record()
+            (ev.setdefault(name, []) if isinstance(ev, dict) else ev).append((e0, e1))
+            return r
+
+        run("im2col", ops.tubelet_im2col, pix, c.tubelet_size, ws["A_emb"])
+        run("embed", ops.gemm, ws["A_emb"], pk["w_emb"], pk["b_emb"], "embed_f32", X, aux=pk["pos"][1:],
+            group=npatch, group_stride=S, group_offset=1, m=Memb)
         ops.cls_init(pk["cls"], pk["pos"], X, B, S)
         act = "bias_gelu_tanh" if c.hidden_act in ("gelu_fast", "gelu_pytorch_tanh", "gelu_new") else "bias_gelu_erf"
         scale = 1.0 / math.sqrt(D // c.num_attention_heads)
-        ev = self.kernel_events  # optional per-launch HIP-event timing of the attention kernel (bench.py)
+        if self.round_split:
+            qkv_gemm = functools.partial(ops.gemm_rounds, main_cfg=4, tail_cfg=5)
+            fc2_gemm = functools.partial(ops.gemm_rounds, main_cfg=5, tail_cfg=1)
+        else:
+            qkv_gemm = fc2_gemm = ops.gemm
         for L in pk["layers"]:
-            ops.layernorm(X, L["ln1_g"], L["ln1_b"], eps, Y)
-            ops.gemm(Y, L["w_qkv"], L["b_qkv"], "bias", QKV)
-            if ev is not None:  # recorded on this part's stream, the one the kernel runs on
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-            ops.attention(QKV, B, S, c.num_attention_heads, scale, O, q_prescaled=True)
-            if ev is not None:
-                e1.record()
-                ev.append((e0, e1))
-            ops.gemm(O, L["w_o"], L["b_o"], "bias_resid_f32", X)
-            ops.layernorm(X, L["ln2_g"], L["ln2_b"], eps, Y)
-            ops.gemm(Y, L["w_1"], L["b_1"], act, Hd)
-            ops.gemm(Hd, L["w_2"], L["b_2"], "bias_resid_f32", X)
+            run("layernorm", ops.layernorm, X, L["ln1_g"], L["ln1_b"], eps, Y)
+            run("qkv", qkv_gemm, Y, L["w_qkv"], L["b_qkv"], "bias", QKV)
+            run("attention", ops.attention, QKV, B, S, c.num_attention_heads, scale, O, q_prescaled=True)
+            run("o_proj", ops.gemm, O, L["w_o"], L["b_o"], "bias_resid_f32", X)
+            run("layernorm", ops.layernorm, X, L["ln2_g"], L["ln2_b"], eps, Y)
+            run("fc1", ops.gemm, Y, L["w_1"], L["b_1"], act, Hd)
+            run("fc2", fc2_gemm, Hd, L["w_2"], L["b_2"], "bias_resid_f32", X)
         return ops.cls_head(X, B, S, pk["lnf_g"], pk["lnf_b"], eps, pk["w_cls"], pk["b_cls"],
                             out=ws["logits"] if out is None else out)
 

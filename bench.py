@@ -46,6 +46,25 @@ def measured_traffic(kernel: str):
     return (k["hbm_bytes_per_launch"] if k else None), os.path.relpath(fs[-1], ROOT)
 
 
+def measured_mfma_busy():
+    """Fraction of SIMD cycles the matrix pipe was busy during the attention kernel, from the
+    newest committed PMC summary (profiles/rNN_*attn_pmc.txt, written by tools/pmc_attn.sh):
+    SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs).  None without one."""
+    import glob
+    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_attn_pmc.txt")))
+    if not fs:
+        return None, None
+    c = {}
+    for line in open(fs[-1]):
+        parts = line.split()
+        if len(parts) >= 2:
+            c[parts[0]] = float(parts[1])
+    if "SQ_VALU_MFMA_BUSY_CYCLES" not in c or "GRBM_GUI_ACTIVE" not in c:
+        return None, None
+    busy = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * c["GRBM_GUI_ACTIVE"] / 8)
+    return round(busy, 4), os.path.relpath(fs[-1], ROOT)
+
+
 def _dist():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws > 1:
@@ -83,6 +102,52 @@ def timed_loop(step, steps: int, warmup: int, dist=None, sync=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     return dt
+
+
+PEAK_HBM_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def kernel_breakdown(model, step, clips, streams, n_steps):
+    """Per-op table of the ViViT-B forward: `n_steps` extra (untimed) steps with HIP events
+    around EVERY launch, on the stream each launch runs on; per op the mean launch duration,
+    its share of the step and the achieved rate against the op's own roofline (MFMA for the
+    GEMMs / attention in algorithmic FLOPs, HBM for LayerNorm / im2col in algorithmic bytes).
+    `clips` = clips per launch."""
+    S, D, F, P = 3137, 768, 3072, 3136
+    M = clips * S
+    work = {  # (amount per launch, unit, bound)
+        "im2col": (clips * (32 * 3 * 224 * 224 * 4 + P * 1536 * 2), "GB/s", "hbm"),
+        "embed": (2.0 * clips * P * D * 1536, "TFLOP/s", "mfma"),
+        "layernorm": (M * D * (4 + 2), "GB/s", "hbm"),
+        "qkv": (2.0 * M * 3 * D * D, "TFLOP/s", "mfma"),
+        "attention": (4.0 * S * S * 64 * 12 * clips, "TFLOP/s", "mfma"),
+        "o_proj": (2.0 * M * D * D, "TFLOP/s", "mfma"),
+        "fc1": (2.0 * M * F * D, "TFLOP/s", "mfma"),
+        "fc2": (2.0 * M * D * F, "TFLOP/s", "mfma"),
+    }
+    ev = {}
+    model.kernel_events = ev
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n_steps):
+        step()
+    torch.cuda.synchronize()
+    step_ms = (time.perf_counter() - t0) / n_steps * 1e3
+    model.kernel_events = None
+    out = {}
+    for name, (amt, unit, bound) in work.items():
+        ms = [e0.elapsed_time(e1) for e0, e1 in ev.get(name, [])]
+        if not ms:
+            continue
+        avg = float(np.mean(ms))
+        rate = amt / (avg * 1e-3) / (1e12 if unit == "TFLOP/s" else 1e9)
+        peak = PEAK_BF16_TFLOPS if bound == "mfma" else PEAK_HBM_GBS
+        out[name] = {"launches_per_step": len(ms) // n_steps, "avg_launch_ms": round(avg, 4),
+                     "share_of_step": round(sum(ms) / n_steps / step_ms, 4), "bound": bound,
+                     "achieved": round(rate, 1), "unit": unit, "peak": peak, "frac": round(rate / peak, 4)}
+    out["note"] = (f"{n_steps} extra untimed steps with HIP events around every launch; step {step_ms:.3f} ms "
+                   "under that instrumentation; algorithmic work (M = clips x 3137 rows, no padding)")
+    return out
 
 
 def cpu_baseline(model_cfg, n_clips, gpu_logits_fn):
@@ -248,6 +313,8 @@ def main():
     streams = model.last_streams
     attn_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
 
+    breakdown = kernel_breakdown(model, step, a.batch // streams, streams, 3)
+
     clips = a.batch * a.steps * world
     value = clips / dt
     ms_per_step = dt / a.steps * 1e3
@@ -262,6 +329,7 @@ def main():
         cpu = None
         logit_err = None
         traffic, traffic_src = measured_traffic("attn_fwd_d64_kernel")
+        mfma_busy, mfma_busy_src = measured_mfma_busy()
         if world == 1 and not a.no_cpu_baseline:
             shape_cfg = dict(cfg.as_shape_cfg(), num_attention_heads=cfg.num_attention_heads,
                              layer_norm_eps=cfg.layer_norm_eps)
@@ -292,7 +360,8 @@ def main():
                          "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes": ATTN_IO_BYTES_PER_CLIP * launch_clips, "avg_launch_ms": round(attn_ms, 4),
                          "flop_per_launch": f"{ATTN_GFLOP_PER_CLIP_LAYER:.2f} GF/clip x {launch_clips:g} clips",
-                         "streams": streams},
+                         "streams": streams, "mfma_busy": mfma_busy, "mfma_busy_source": mfma_busy_src},
+            "kernel_breakdown": breakdown,
             "model_tflops": round(model_tflops, 1),
             "model_frac_of_peak": round(model_tflops / PEAK_BF16_TFLOPS, 4),
             "cpu_baseline": cpu,

@@ -107,7 +107,7 @@ def test_gemm_bias_bf16(M, N, K):
     assert err < 8e-3, err
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("epi", ["bias", "bias_gelu_tanh"])
 def test_gemm_every_tile_config(cfg, epi):
     """Every block-tile configuration on a shape with more tiles than CUs (the persistent
@@ -139,6 +139,31 @@ def test_gemm_pingpong_matches_persistent(M, N, K, epi):
     if epi == "bias":
         err = ((o6.float().cpu() - ref).abs() / (ref.abs() + 1.0)).max().item()
         assert err < 8e-3, err
+
+
+@pytest.mark.parametrize("M,N,K,epi,main_cfg,tail_cfg", [
+    (25344, 2304, 768, "bias", 4, 5),              # ViViT-B B=8 q|k|v: 3 rounds of 256 + a 28-row-block tail
+    (25344, 768, 3072, "bias_resid_f32", 5, 1),    # ViViT-B B=8 fc2: 2 rounds of 512 + tail
+    (12800, 768, 3072, "bias_resid_f32", 5, 1),    # B=4: 1 round + tail
+    (12800, 2304, 768, "bias", 4, 7),
+    (3328, 768, 3072, "bias_resid_f32", 5, 1),     # B=1: no whole round, one launch
+])
+def test_gemm_rounds_bit_identical(M, N, K, epi, main_cfg, tail_cfg):
+    """gemm_rounds (main launch over whole rounds of tiles + a small-tile tail launch) equals one
+    launch bit for bit: every output element runs the same MFMA sequence over K."""
+    a, w, bias, ref = _gemm_case(M, N, K, M + 3 * N + K)
+    ad, wd, bd = a.to(DEV), w.to(DEV), bias.to(DEV)
+    dt = torch.float32 if "f32" in epi else torch.bfloat16
+    x0 = (torch.randn(M, N, generator=torch.Generator().manual_seed(1)) if "f32" in epi
+          else torch.zeros(M, N)).to(DEV, dt)
+    one, two = x0.clone(), x0.clone()
+    ops().gemm(ad, wd, bd, epi, one)
+    ops().gemm_rounds(ad, wd, bd, epi, two, main_cfg, tail_cfg)
+    assert torch.equal(one, two)
+    if "f32" in epi:
+        ref = ref + x0.float().cpu()
+    err = ((two.float().cpu() - ref).abs() / (ref.abs() + 1.0)).max().item()
+    assert err < 8e-3, err
 
 
 def test_gemm_orientation_asymmetric():
