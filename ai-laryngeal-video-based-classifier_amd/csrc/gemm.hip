@@ -149,7 +149,12 @@ __device__ __forceinline__ void store_tile(const v16f (&acc)[MI][NI], int64_t mb
 
 // ST: LDS ring depth in tiles (prefetch distance ST - 1).  ST = 2 at 128x128 needs 64 KiB of
 // LDS, so two workgroups share a CU and one's epilogue overlaps the other's main loop.
-template <int BM, int BN, int WM, int WN, int EPI, int ST = 3>
+// PRE (f32 residual epilogue only): load this wave's residual elements into registers before
+// the K loop, so their latency overlaps the main loop instead of opening the epilogue
+// (+20 VGPRs at 128x128).  Bit-identical; ViViT-B B=8 forward 9.224 vs 9.265 ms/step with
+// every residual GEMM on cfg 5 vs cfg 8 (= cfg 5 without it), interleaved, tools/ab_rpre.py:
+// +0.4 %, inside the noise band; isolated o_proj / fc2 within 1-2 % either way.
+template <int BM, int BN, int WM, int WN, int EPI, int ST = 3, bool PRE = true>
 __global__ void __launch_bounds__(512, ST == 2 ? 2 : 1)
 gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
                  int nbm, int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
@@ -210,6 +215,18 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
 
     const int nk = K / GBK;
     stage(0, 0);
+    constexpr bool RPRE = PRE && EPI == VC_EPI_BIAS_RESID_F32;
+    float4 xres[RPRE ? MI : 1][RPRE ? NI : 1][4];
+    if constexpr (RPRE) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    xres[i][j][g] = *reinterpret_cast<const float4*>(
+                        reinterpret_cast<const float*>(out) + (m0 + wm * TM + i * 32 + r) * ldo + n0 + wn * TN + j * 32 + g * 8 + h * 4);
+    }
     if (ST == 3 && nk > 1) {
         stage(1, 1);
         wait_vm<LPT>();
@@ -251,7 +268,25 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
         block_sync_lds();
     }
 
-    store_tile<EPI, MI, NI>(acc, m0 + wm * TM, n0 + wn * TN, r, h, bias, out, ldo, aux, ldaux, G, gstride, goff);
+    if constexpr (RPRE) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int64_t m = m0 + wm * TM + i * 32 + r, n = n0 + wn * TN + j * 32 + g * 8 + h * 4;
+                    const float4 bb = *reinterpret_cast<const float4*>(bias + n);
+                    float4 x = xres[i][j][g];
+                    x.x += acc[i][j][4 * g + 0] + bb.x;
+                    x.y += acc[i][j][4 * g + 1] + bb.y;
+                    x.z += acc[i][j][4 * g + 2] + bb.z;
+                    x.w += acc[i][j][4 * g + 3] + bb.w;
+                    *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + m * ldo + n) = x;
+                }
+    } else {
+        store_tile<EPI, MI, NI>(acc, m0 + wm * TM, n0 + wn * TN, r, h, bias, out, ldo, aux, ldaux, G, gstride, goff);
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -832,22 +867,22 @@ struct GemmCfg {
     int bm, bn;
 };
 static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}, {128, 128}, {256, 256},
-                                 {64, 128}};
-constexpr int kNumCfgs = 8;
+                                 {64, 128}, {128, 128}};  // 8: cfg 5 without the residual prefetch (A/B)
+constexpr int kNumCfgs = 9;
 
-template <int BM, int BN, int WM, int WN, int E, int ST = 3>
+template <int BM, int BN, int WM, int WN, int E, int ST = 3, bool PRE = true>
 static int launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
                       const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
                       int64_t gs, int64_t go, hipStream_t stream) {
     constexpr int lds = ST * (BM + BN) * 128;
     static bool attr_set = false;  // per instantiation; benign race (idempotent)
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, WM, WN, E, ST>,
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, WM, WN, E, ST, PRE>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
         attr_set = true;
     }
-    gemm_bf16_kernel<BM, BN, WM, WN, E, ST><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(
+    gemm_bf16_kernel<BM, BN, WM, WN, E, ST, PRE><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(
         A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go);
     return check_launch("vc_gemm_bf16");
 }
@@ -967,6 +1002,7 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
         case 3: return launch_big<E>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 5: return launch_cfg<128, 128, 2, 4, E, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 7: return launch_cfg<64, 128, 2, 4, E, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 8: return launch_cfg<128, 128, 2, 4, E, 2, false>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 4:
             if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
                           E == VC_EPI_BIAS_RELU_BF16 || E == VC_EPI_BIAS_GELU_TANH_SAVE)

@@ -107,7 +107,7 @@ def test_gemm_bias_bf16(M, N, K):
     assert err < 8e-3, err
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("epi", ["bias", "bias_gelu_tanh"])
 def test_gemm_every_tile_config(cfg, epi):
     """Every block-tile configuration on a shape with more tiles than CUs (the persistent
@@ -188,13 +188,20 @@ def test_gemm_gelu(act):
     assert err < 8e-3, err
 
 
-def test_gemm_resid_f32():
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 5, 7, 8])
+def test_gemm_resid_f32(cfg):
+    """f32 residual epilogue on every 128/64-row config: cfgs 0-2, 5, 7 prefetch the residual
+    into registers before the K loop, cfg 8 reads it in the epilogue (bit-identical to 5)."""
     M, N, K = 512, 768, 3072
     a, w, bias, ref = _gemm_case(M, N, K, 12)
     x0 = torch.randn(M, N)
     x = x0.clone().to(DEV)
-    ops().gemm(a.to(DEV), w.to(DEV), bias.to(DEV), "bias_resid_f32", x)
+    ops().gemm(a.to(DEV), w.to(DEV), bias.to(DEV), "bias_resid_f32", x, cfg=cfg)
     np.testing.assert_allclose(x.cpu().numpy(), (x0 + ref).numpy(), rtol=1e-4, atol=1e-4)
+    if cfg == 5:
+        x8 = x0.clone().to(DEV)
+        ops().gemm(a.to(DEV), w.to(DEV), bias.to(DEV), "bias_resid_f32", x8, cfg=8)
+        assert torch.equal(x, x8)
 
 
 def test_gemm_embed_remap():
