@@ -33,36 +33,44 @@ ATTN_IO_BYTES_PER_CLIP = 3137 * 768 * 2 * 4  # q,k,v read + o written once, bf16
 PEAK_BF16_TFLOPS = 2500.0       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 
 
+def _newest(pattern: str):
+    """Newest committed profile matching profiles/<pattern> by round and version number
+    (r01_v10 after r01_v7: a natural sort, not a string sort)."""
+    import glob
+    import re
+    fs = glob.glob(os.path.join(ROOT, "profiles", pattern))
+    key = lambda f: [int(x) for x in re.findall(r"\d+", os.path.basename(f))]  # noqa: E731
+    return max(fs, key=key) if fs else None
+
+
 def measured_traffic(kernel: str):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/rNN_*traffic.json, written by tools/traffic.sh: rocprofv3 FETCH_SIZE x2 +
     WRITE_SIZE passes over this same bench command).  None when no summary exists."""
-    import glob
-    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
-    if not fs:
+    f = _newest("r*_traffic.json")
+    if not f:
         return None, None
-    with open(fs[-1]) as fh:
+    with open(f) as fh:
         k = json.load(fh)["kernels"].get(kernel)
-    return (k["hbm_bytes_per_launch"] if k else None), os.path.relpath(fs[-1], ROOT)
+    return (k["hbm_bytes_per_launch"] if k else None), os.path.relpath(f, ROOT)
 
 
 def measured_mfma_busy():
     """Fraction of SIMD cycles the matrix pipe was busy during the attention kernel, from the
     newest committed PMC summary (profiles/rNN_*attn_pmc.txt, written by tools/pmc_attn.sh):
     SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs).  None without one."""
-    import glob
-    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_attn_pmc.txt")))
-    if not fs:
+    f = _newest("r*_attn_pmc.txt")
+    if not f:
         return None, None
     c = {}
-    for line in open(fs[-1]):
+    for line in open(f):
         parts = line.split()
         if len(parts) >= 2:
             c[parts[0]] = float(parts[1])
     if "SQ_VALU_MFMA_BUSY_CYCLES" not in c or "GRBM_GUI_ACTIVE" not in c:
         return None, None
     busy = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * c["GRBM_GUI_ACTIVE"] / 8)
-    return round(busy, 4), os.path.relpath(fs[-1], ROOT)
+    return round(busy, 4), os.path.relpath(f, ROOT)
 
 
 def _dist():

@@ -44,3 +44,18 @@ def test_ops_reject_cpu_tensors():
     x = torch.zeros(256, 768)
     with pytest.raises(L.VclipError):
         ops.layernorm(x, torch.ones(768), torch.zeros(768), 1e-6, torch.zeros(256, 768, dtype=torch.bfloat16))
+
+
+def test_bench_reads_newest_profile(tmp_path, monkeypatch):
+    """bench.py's roofline traffic / MFMA-busy come from the newest committed PMC summary:
+    r01_v10 must win over r01_v7 (natural, not string, order) and r02 over r01."""
+    import bench
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    for n in ("r01_v7_traffic.json", "r01_v10_traffic.json", "r01_v9_traffic.json"):
+        (prof / n).write_text("{}")
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench._newest("r*_traffic.json").endswith("r01_v10_traffic.json")
+    (prof / "r02_v1_traffic.json").write_text("{}")
+    assert bench._newest("r*_traffic.json").endswith("r02_v1_traffic.json")
+    assert bench._newest("r*_nothing.json") is None
