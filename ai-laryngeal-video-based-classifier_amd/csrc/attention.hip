@@ -81,9 +81,11 @@ __device__ __forceinline__ void attn_sync() {
 // exp2 / sum VALU (correct; measured 3 % SLOWER than hipcc's own schedule at B = 8 and B = 4,
 // tools/ab_attn_interleave.py, so the shipped build leaves the scheduling to the compiler).
 // Correct variants measured at B = 8 (tools/ablate_attn.py, interleaved rounds, r01 session 4):
-// 64 / 128 static s_setprio for one of the two co-resident workgroups: +1.5 % / 0 (noise band);
-// 256 split-half softmax + P.V (three scheduling regions): 1.5 % slower; 512 K-fragment
-// prefetch across the barrier (vmcnt(0) per tile): 0.  PMC of the shipped build
+// 64 without the static s_setprio of one co-resident workgroup: 1.2 % slower (the shipped
+// build sets it); 128 priority by another block-id bit: neutral; 256 split-half softmax + P.V
+// (three scheduling regions): 1.5 % slower; 512 K-fragment prefetch across the barrier
+// (vmcnt(0) per tile): 0; 1024 a 5-slot ring (two tiles in flight across the barrier, 80 KiB):
+// 3 % slower (254 VGPRs) — the loads' cost (ABL 1: -10 %) is issue, not latency.  PMC of the shipped build
 // (tools/pmc_attn.sh): MFMA busy 46 % of cycles at 1.98 GHz, wave cycles 44 % issuing /
 // 33 % issue-stalled (matrix pipe or dependency) / 23 % in s_waitcnt or barrier; zero LDS
 // bank conflicts; ~84 non-MFMA VALU per wave per 64-key tile.
@@ -95,7 +97,11 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
                     uint16_t* __restrict__ out, int64_t ldo, float* __restrict__ lse = nullptr) {
     static_assert(QB == 1, "see the QB note above");
     constexpr int AQ = 128 * QB;  // query rows per workgroup (4 waves x QB x 32)
-    __shared__ __attribute__((aligned(16))) char smem[NSLOT * KV_SLOT];
+    // ABL & 1024: a 5-slot ring (80 KiB, two workgroups fill the CU's 160 KiB) keeping two
+    // tiles in flight across each barrier instead of one
+    constexpr int NS = (ABL & 1024) ? 5 : NSLOT;
+    static_assert(!((ABL & 1024) && (ABL & (256 | 512))), "5-slot ring: default iteration only");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
 
     // XCD-aware order: the workgroups of one (clip, head) share its K/V; give every XCD a
     // contiguous range of linear ids so they meet in that XCD's L2 (blocks L and L+8 share
@@ -145,7 +151,7 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
     const uint32_t vo0 = (uint32_t)(srow * ld + vswz(srow, spc) * 8) * 2;
     const uint32_t vo1 = (uint32_t)((srow + 8) * ld + vswz(srow + 8, spc) * 8) * 2;
     auto stage = [&](int t) {
-        const uint32_t s = lds0 + (t % NSLOT) * KV_SLOT + wave * 16 * 128;
+        const uint32_t s = lds0 + (t % NS) * KV_SLOT + wave * 16 * 128;
         const uint16_t* kt = kbase + (int64_t)t * AK * ld;
         const uint16_t* vt = vbase + (int64_t)t * AK * ld;
         adma16s(kt, ko0, __builtin_amdgcn_readfirstlane(s));
@@ -250,16 +256,23 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
     };
 
     const int ntiles = (S + AK - 1) / AK;
-    // ABL 64 / 128: static wave priority for one of the two workgroups that share a CU
-    // (MI355X_MICROARCH.md "Two waves per SIMD" item 4); initially co-resident blocks are
-    // L and L + 256 (64 = prio by bit 8 of L), 128 = by bit 3 (neighbours within an XCD)
-    if constexpr (ABL & 64) { if ((L >> 8) & 1) __builtin_amdgcn_s_setprio(1); }
-    if constexpr (ABL & 128) { if ((L >> 3) & 1) __builtin_amdgcn_s_setprio(1); }
+    // Static wave priority for one of the two workgroups that share a CU (MI355X_MICROARCH.md
+    // "Two waves per SIMD" item 4: priority outranks age, so one fixed winner instead of the
+    // age-based arbitration flipping between them): initially co-resident blocks are L and
+    // L + 256, so prio 1 by bit 8 of L.  +1.2 % (three interleaved A/Bs at B = 8: 259/263,
+    // 256/259, 258/261 us).  ABL 64 drops it; ABL 128 picks by bit 3 instead (neutral).
+    if constexpr (ABL & 128) {
+        if ((L >> 3) & 1) __builtin_amdgcn_s_setprio(1);
+    } else if constexpr (!(ABL & 64)) {
+        if ((L >> 8) & 1) __builtin_amdgcn_s_setprio(1);
+    }
     stage(0);
     if (ntiles > 1) stage(1);
     if (ntiles > 2) stage(2);
+    if (NS == 5 && ntiles > 3) stage(3);
     // ABL & 512 (K-fragment prefetch) keeps no tile in flight across the per-tile barrier
-    if (!(ABL & 512) && ntiles > 2) attn_wait_vm<4>();  // tiles 0 and 1 resident, 2 in flight
+    if (NS == 5 && ntiles > 3) attn_wait_vm<8>();  // tiles 0 and 1 resident, 2 and 3 in flight
+    else if (!(ABL & 512) && ntiles > 2) attn_wait_vm<4>();  // tiles 0 and 1 resident, 2 in flight
     else attn_wait_vm<0>();
     attn_sync();
     // tile 0 establishes the running max m
@@ -280,7 +293,7 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
     // a loop-invariant per-lane VGPR plus an immediate offset.
     auto iter = [&](auto next_c, const char* slot, const char* nslot, int t) {
         constexpr int NEXT = decltype(next_c)::value;
-        if (!(ABL & 1) && t + 3 < ntiles) stage(t + 3);
+        if (!(ABL & 1) && t + NS - 1 < ntiles) stage(t + NS - 1);
         v16f snext[QB][2];
         if constexpr (NEXT == 0) qk_mfma(nslot, snext);
         else if constexpr (NEXT == 1) qk(nslot, t + 1, snext);
@@ -365,7 +378,8 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
         //      flight); the barrier also retires every wave's reads of slot t before the
         //      next iteration stages t+4 into it
         if (t + 2 < ntiles) {
-            if (t + 3 < ntiles) attn_wait_vm<4>();
+            if (NS == 5 && t + 4 < ntiles) attn_wait_vm<8>();
+            else if (t + 3 < ntiles) attn_wait_vm<4>();
             else attn_wait_vm<0>();
             attn_sync();
         }
@@ -537,16 +551,26 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
     using full_c = std::integral_constant<int, 0>;
     const int nfull = S / AK;  // full tiles
     int t = 0;
-    for (; t + 5 <= nfull; t += NSLOT) {  // iterations t..t+3 all have a full next tile
-        step(full_c{}, smem + 0 * KV_SLOT, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, t);
-        step(full_c{}, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, smem + 3 * KV_SLOT, t + 1);
-        step(full_c{}, smem + 2 * KV_SLOT, smem + 3 * KV_SLOT, smem + 0 * KV_SLOT, t + 2);
-        step(full_c{}, smem + 3 * KV_SLOT, smem + 0 * KV_SLOT, smem + 1 * KV_SLOT, t + 3);
+    if constexpr (NS == 5) {
+        for (; t + 6 <= nfull; t += NS) {  // iterations t..t+4 all have a full next tile
+            step(full_c{}, smem + 0 * KV_SLOT, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, t);
+            step(full_c{}, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, smem + 3 * KV_SLOT, t + 1);
+            step(full_c{}, smem + 2 * KV_SLOT, smem + 3 * KV_SLOT, smem + 4 * KV_SLOT, t + 2);
+            step(full_c{}, smem + 3 * KV_SLOT, smem + 4 * KV_SLOT, smem + 0 * KV_SLOT, t + 3);
+            step(full_c{}, smem + 4 * KV_SLOT, smem + 0 * KV_SLOT, smem + 1 * KV_SLOT, t + 4);
+        }
+    } else {
+        for (; t + 5 <= nfull; t += NS) {  // iterations t..t+3 all have a full next tile
+            step(full_c{}, smem + 0 * KV_SLOT, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, t);
+            step(full_c{}, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, smem + 3 * KV_SLOT, t + 1);
+            step(full_c{}, smem + 2 * KV_SLOT, smem + 3 * KV_SLOT, smem + 0 * KV_SLOT, t + 2);
+            step(full_c{}, smem + 3 * KV_SLOT, smem + 0 * KV_SLOT, smem + 1 * KV_SLOT, t + 3);
+        }
     }
-    for (; t < ntiles; ++t) {  // at most 4 + 1 iterations: runtime slot, mask-checked next tile
-        const char* slot = smem + (t % NSLOT) * KV_SLOT;
-        const char* nslot = smem + ((t + 1) % NSLOT) * KV_SLOT;
-        const char* n2slot = smem + ((t + 2) % NSLOT) * KV_SLOT;
+    for (; t < ntiles; ++t) {  // at most NS + 1 iterations: runtime slot, mask-checked next tile
+        const char* slot = smem + (t % NS) * KV_SLOT;
+        const char* nslot = smem + ((t + 1) % NS) * KV_SLOT;
+        const char* n2slot = smem + ((t + 2) % NS) * KV_SLOT;
         if (t + 1 < ntiles) step(std::integral_constant<int, 1>{}, slot, nslot, n2slot, t);
         else step(std::integral_constant<int, 2>{}, slot, nslot, n2slot, t);
     }
@@ -589,8 +613,15 @@ template <int QB, int ABL, bool WLSE = false>
 static void launch_attn(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, float c_log2, uint16_t* out,
                         int64_t ldo, hipStream_t stream, float* lse = nullptr) {
     constexpr int AQ = 128 * QB;
+    constexpr int lds = ((ABL & 1024) ? 5 : NSLOT) * KV_SLOT;
+    static bool attr_set = false;  // per instantiation; idempotent
+    if (lds > 64 * 1024 && !attr_set) {
+        (void)hipFuncSetAttribute((const void*)attn_fwd_d64_kernel<QB, ABL, WLSE>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        attr_set = true;
+    }
     dim3 grid((unsigned)((S + AQ - 1) / AQ), (unsigned)(B * H));
-    attn_fwd_d64_kernel<QB, ABL, WLSE><<<grid, 256, 0, stream>>>(qkv, ld, (int)S, (int)H, c_log2, out, ldo, lse);
+    attn_fwd_d64_kernel<QB, ABL, WLSE><<<grid, 256, lds, stream>>>(qkv, ld, (int)S, (int)H, c_log2, out, ldo, lse);
 }
 
 }  // namespace vc
@@ -637,7 +668,7 @@ extern "C" int vc_attention_fwd_ablation(const uint16_t* qkv, int64_t ld, int64_
 #define VC_ABL(QB, N) case 100 * (QB - 1) + N: launch_attn<QB, N>(qkv, ld, B, S, H, c_log2, out, ldo, stream); break;
     switch (abl) {
         VC_ABL(1, 0) VC_ABL(1, 1) VC_ABL(1, 2) VC_ABL(1, 4) VC_ABL(1, 6) VC_ABL(1, 8) VC_ABL(1, 12) VC_ABL(1, 14)
-        VC_ABL(1, 15) VC_ABL(1, 16) VC_ABL(1, 32) VC_ABL(1, 64) VC_ABL(1, 128) VC_ABL(1, 256) VC_ABL(1, 320) VC_ABL(1, 512) VC_ABL(1, 576)
+        VC_ABL(1, 15) VC_ABL(1, 16) VC_ABL(1, 32) VC_ABL(1, 64) VC_ABL(1, 128) VC_ABL(1, 256) VC_ABL(1, 320) VC_ABL(1, 512) VC_ABL(1, 576) VC_ABL(1, 1024) VC_ABL(1, 1088) VC_ABL(1, 1152)
         default: return fail(VC_ERR_INVALID_ARG, "bad ablation");
     }
 #undef VC_ABL

@@ -154,7 +154,11 @@ __device__ __forceinline__ void store_tile(const v16f (&acc)[MI][NI], int64_t mb
 // (+20 VGPRs at 128x128).  Bit-identical; ViViT-B B=8 forward 9.224 vs 9.265 ms/step with
 // every residual GEMM on cfg 5 vs cfg 8 (= cfg 5 without it), interleaved, tools/ab_rpre.py:
 // +0.4 %, inside the noise band; isolated o_proj / fc2 within 1-2 % either way.
-template <int BM, int BN, int WM, int WN, int EPI, int ST = 3, bool PRE = true>
+// PRIO: static s_setprio 1 for one of two co-resident workgroups (bit 8 of the block id; cfg 9).
+// Measured slower (o_proj 67.0 vs 64.4 us, fc2 152.6 vs 151.0, model 9.792 vs 9.755 ms/step,
+// tools/ab_rpre.py 5,9): unlike the attention kernel's, the GEMM's two workgroups per CU gain
+// nothing from a fixed arbitration winner; cfg 5 ships without it.
+template <int BM, int BN, int WM, int WN, int EPI, int ST = 3, bool PRE = true, bool PRIO = false>
 __global__ void __launch_bounds__(512, ST == 2 ? 2 : 1)
 gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
                  int nbm, int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
@@ -174,6 +178,9 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
     const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
     const int tm = wgid / nbn, tn = wgid % nbn;
     const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+    if constexpr (PRIO) {
+        if ((bid >> 8) & 1) __builtin_amdgcn_s_setprio(1);
+    }
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -867,22 +874,22 @@ struct GemmCfg {
     int bm, bn;
 };
 static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}, {128, 128}, {256, 256},
-                                 {64, 128}, {128, 128}};  // 8: cfg 5 without the residual prefetch (A/B)
-constexpr int kNumCfgs = 9;
+                                 {64, 128}, {128, 128}, {128, 128}};  // 8: cfg 5 without the residual prefetch,
+constexpr int kNumCfgs = 10;                                          // 9: cfg 5 + static priority (A/Bs)
 
-template <int BM, int BN, int WM, int WN, int E, int ST = 3, bool PRE = true>
+template <int BM, int BN, int WM, int WN, int E, int ST = 3, bool PRE = true, bool PRIO = false>
 static int launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
                       const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
                       int64_t gs, int64_t go, hipStream_t stream) {
     constexpr int lds = ST * (BM + BN) * 128;
     static bool attr_set = false;  // per instantiation; benign race (idempotent)
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, WM, WN, E, ST, PRE>,
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, WM, WN, E, ST, PRE, PRIO>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
         attr_set = true;
     }
-    gemm_bf16_kernel<BM, BN, WM, WN, E, ST, PRE><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(
+    gemm_bf16_kernel<BM, BN, WM, WN, E, ST, PRE, PRIO><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(
         A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go);
     return check_launch("vc_gemm_bf16");
 }
@@ -1003,6 +1010,7 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
         case 5: return launch_cfg<128, 128, 2, 4, E, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 7: return launch_cfg<64, 128, 2, 4, E, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 8: return launch_cfg<128, 128, 2, 4, E, 2, false>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 9: return launch_cfg<128, 128, 2, 4, E, 2, true, true>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 4:
             if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
                           E == VC_EPI_BIAS_RELU_BF16 || E == VC_EPI_BIAS_GELU_TANH_SAVE)

@@ -13,6 +13,7 @@ from vclip_amd.weights import make_synthetic_clips  # noqa: E402
 from tools.tune_gemm import timeit  # noqa: E402
 
 dev = torch.device("cuda", 0)
+CFGS = [int(c) for c in (sys.argv[1] if len(sys.argv) > 1 else "5,8").split(",")]
 g = torch.Generator(device=dev).manual_seed(0)
 M = 25344
 for name, N, K in [("o_proj", 768, 768), ("fc2", 768, 3072)]:
@@ -21,15 +22,15 @@ for name, N, K in [("o_proj", 768, 768), ("fc2", 768, 3072)]:
     b = torch.randn(N, device=dev, generator=g) * 0.1
     X0 = torch.randn(M, N, device=dev, generator=g)
     outs = {}
-    for c in (5, 8):
+    for c in CFGS:
         X = X0.clone()
         ops.gemm(A, W, b, "bias_resid_f32", X, cfg=c)
         outs[c] = X
-    print(name, "bit-identical:", bool(torch.equal(outs[5], outs[8])), flush=True)
+    print(name, "bit-identical:", all(torch.equal(outs[CFGS[0]], o) for o in outs.values()), flush=True)
     X = X0.clone()
-    res = {5: [], 8: []}
+    res = {c: [] for c in CFGS}
     for _ in range(5):
-        for c in (5, 8):
+        for c in CFGS:
             res[c].append(timeit(lambda: ops.gemm(A, W, b, "bias_resid_f32", X, cfg=c), 20))
     print(name, {c: f"{sorted(v)[2] * 1e3:.1f}us" for c, v in res.items()}, flush=True)
 
@@ -47,13 +48,13 @@ ops.gemm = patched
 pix = torch.from_numpy(make_synthetic_clips(8, 32, 224, seed=1)).to(dev)
 m = create_model(num_frames=32, device=dev)
 lg = {}
-for c in (5, 8):
+for c in CFGS:
     mode["cfg"] = c
     lg[c] = m.forward_logits(pix).clone()
-print("model logits bit-identical:", bool(torch.equal(lg[5], lg[8])), flush=True)
-res = {5: [], 8: []}
+print("model logits bit-identical:", all(torch.equal(lg[CFGS[0]], o) for o in lg.values()), flush=True)
+res = {c: [] for c in CFGS}
 for _ in range(6):
-    for c in (5, 8):
+    for c in CFGS:
         mode["cfg"] = c
         for _ in range(2):
             m.forward_logits(pix)

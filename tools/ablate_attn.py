@@ -14,7 +14,7 @@ o = torch.zeros(25344, 768, device="cuda", dtype=torch.bfloat16)
 st = torch.cuda.current_stream().cuda_stream
 fl = 4.0 * S * S * 64 * H * B
 res = {}
-abls = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "0,1,2,4,6,8,12,14,15,16,32,64,128").split(",")]
+abls = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "0,1,2,4,6,8,12,14,15,16,32,64,128,256,512,1024").split(",")]
 for a in abls:
     f(qkv.data_ptr(), 2304, B, S, H, 0.125, o.data_ptr(), 768, a, st)
 torch.cuda.synchronize()
