@@ -113,6 +113,7 @@ class Swin3d(torch.nn.Module):
         self._packed = None
         self._bias_cache = {}
         self._ws = {}
+        self.kernel_events = None  # list: HIP events around each window-attention launch (bench.py)
 
     def state_dict(self, *a, **k):
         return OrderedDict((n, self.params[n.replace(".", "__")].detach()) for n in self._names)
@@ -275,7 +276,16 @@ class Swin3d(torch.nn.Module):
                 biasT = self._biasT(s, i, window, video.device)
                 ops.layernorm(X, blk["ln1"][0], blk["ln1"][1], eps, Y, m=ntok)
                 ops.gemm(Y, blk["w_qkv"], blk["b_qkv"], "bias", QKV)
+                ev = self.kernel_events
+                if ev is not None:  # recorded on the current stream, the one the kernel runs on
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
                 ops.window_attention3d(QKV, B, (t, h, w), st["heads"], window, shift, biasT, O)
+                if ev is not None:
+                    e1.record()
+                    # QK^T + PV over each token's window (window clipped to the grid), head_dim 32
+                    n = window[0] * window[1] * window[2]
+                    ev.append((e0, e1, 4.0 * ntok * n * 32 * st["heads"]))
                 ops.gemm(O, blk["w_proj"], blk["b_proj"], "bias_resid_f32", X)
                 ops.layernorm(X, blk["ln2"][0], blk["ln2"][1], eps, Y, m=ntok)
                 ops.gemm(Y, blk["w_1"], blk["b_1"], "bias_gelu_erf", Hd)

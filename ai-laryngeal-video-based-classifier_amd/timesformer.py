@@ -97,6 +97,7 @@ class TimesformerForVideoClassification(torch.nn.Module):
         self.params = torch.nn.ParameterDict()
         shapes = timesformer_param_shapes(c.as_shape_cfg())
         self._names = list(shapes.keys())
+        self.kernel_events = None  # list: HIP events around each spatial-attention launch (bench.py)
         for name, shape in shapes.items():
             self.params[name.replace(".", "__")] = torch.nn.Parameter(torch.zeros(shape), requires_grad=False)
         self._packed = None
@@ -243,7 +244,14 @@ class TimesformerForVideoClassification(torch.nn.Module):
             # spatial branch (frame layout)
             ops.divided_add_layernorm(X, Yb, B, P, T, L["ln1_g"], L["ln1_b"], eps, "temporal_to_spatial", Hf)
             ops.gemm(Hf, L["w_qkv_s"], L["b_qkv_s"], "bias", QKV)
+            ev = self.kernel_events
+            if ev is not None:  # recorded on the current stream, the one the kernel runs on
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
             ops.attention(QKV, B * T, 1 + P, Hn, scale, O, q_prescaled=True)
+            if ev is not None:
+                e1.record()
+                ev.append((e0, e1, 4.0 * (1 + P) * (1 + P) * 64 * Hn * B * T))
             ops.gemm(O, L["w_o"], L["b_o"], "bias", Yb)
             # MLP (clip layout)
             ops.divided_add_layernorm(X, Yb, B, P, T, L["ln2_g"], L["ln2_b"], eps, "spatial_to_mlp", Hc)

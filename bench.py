@@ -5,6 +5,8 @@ max-abs-error vs the fp32 CPU reference and a roofline line for the dominant ker
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline]
   python bench.py --mode train [...]   # BASELINE configs[4]: ViViT-B train step (fwd + bwd +
                                        # AdamW) bf16, 4 clips per GPU, RCCL gradient all-reduce
+  python bench.py --mode timesformer   # BASELINE configs[2]: TimeSformer-B 8f, 16 clips per GPU
+  python bench.py --mode swin          # BASELINE configs[3]: Video Swin-T 32f, 4 clips per GPU
 
 One process per GPU (torch.distributed.run for N > 1, backend nccl = RCCL).  Clips
 shard as independent data-parallel units: each rank runs its own batch and no
@@ -208,6 +210,103 @@ def cpu_train_baseline(n_clips):
                       f"(oracle/vivit_ref.py, eager attention), torch CPU {cores} threads"}
 
 
+FAMILIES = {
+    # mode: (metric, GFLOP per clip, default clips per GPU, BASELINE config, attention kernel)
+    "timesformer": ("clips/sec fwd TimeSformer-B 8x224^2 bf16", 391.66, 16,
+                    "TimeSformer-B divided space-time attention, 8x224x224 clips, batch 16 per GPU (BASELINE configs[2])",
+                    "attn_fwd_d64_kernel (spatial branch: B*T sequences of 197 tokens)"),
+    "swin": ("clips/sec fwd Video Swin-T 32x224^2 bf16", 175.53, 4,
+             "Video Swin-T 3D shifted-window attention, 32x224x224 clips, batch 4 per GPU = 32 over DP=8 "
+             "(BASELINE configs[3])", "window_attn_d32_kernel (all 12 blocks, head_dim 32)"),
+}
+
+
+def cpu_family_baseline(mode, n_clips, gpu_logits_fn):
+    """The family's fp32 CPU oracle (oracle/timesformer_ref.py, oracle/swin3d_ref.py) on the host
+    cores, one clip at a time, plus the GPU logit error on the same clips."""
+    from vclip_amd.weights import (make_swin3d_weights, make_synthetic_clips, make_synthetic_video,
+                                   make_timesformer_weights)
+    if mode == "timesformer":
+        from oracle.timesformer_ref import timesformer_forward as fwd
+        from vclip_amd.timesformer import TimesformerConfig
+        c = TimesformerConfig(num_frames=8)
+        cfg = dict(c.as_shape_cfg(), num_attention_heads=c.num_attention_heads, layer_norm_eps=c.layer_norm_eps,
+                   hidden_act=c.hidden_act)
+        sd = make_timesformer_weights(c.as_shape_cfg(), seed=0)
+        x = make_synthetic_clips(n_clips, 8, 224, seed=1)
+    else:
+        from oracle.swin3d_ref import swin3d_forward as fwd
+        from vclip_amd.swin3d import SWIN3D_CONFIGS
+        cfg = dict(SWIN3D_CONFIGS["tiny"], num_classes=2)
+        sd = make_swin3d_weights(cfg, seed=0)
+        x = make_synthetic_video(n_clips, 32, 224, seed=1)
+    sd = {k: torch.from_numpy(v) for k, v in sd.items()}
+    cores = torch.get_num_threads()
+    with torch.no_grad():
+        fwd(sd, cfg, torch.from_numpy(x[:1]))  # warm-up
+        t0 = time.perf_counter()
+        ref = [fwd(sd, cfg, torch.from_numpy(x[i:i + 1])) for i in range(n_clips)]
+        dt = time.perf_counter() - t0
+    err = float(np.abs(gpu_logits_fn(x) - torch.cat(ref).numpy()).max())
+    name = "oracle/timesformer_ref.py" if mode == "timesformer" else "oracle/swin3d_ref.py"
+    return {"value": n_clips / dt, "unit": "clips/s", "cores": cores, "kind": "port",
+            "sample": f"{n_clips} clips fp32 forward, B=1 each, {name}, torch CPU {cores} threads"}, err
+
+
+def run_family(a, dist, rank, world, dev):
+    """BASELINE configs[2] / [3]: TimeSformer-B (divided space-time attention) and Video Swin-T
+    (3D shifted windows) forwards, clips sharded per rank like the ViViT bench (no collective)."""
+    from vclip_amd.weights import make_synthetic_clips, make_synthetic_video
+    metric, gflop, _, workload, kname = FAMILIES[a.mode]
+    if a.mode == "timesformer":
+        from vclip_amd.timesformer import create_model
+        model = create_model(num_frames=8, device=dev)
+        x = torch.from_numpy(make_synthetic_clips(a.batch, 8, 224, seed=1 + rank)).to(dev)
+    else:
+        from vclip_amd.swin3d import create_model
+        model = create_model(model_size="tiny", device=dev)
+        x = torch.from_numpy(make_synthetic_video(a.batch, 32, 224, seed=1 + rank)).to(dev)
+
+    def step():
+        model.forward_logits(x)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = []
+    model.kernel_events = evs
+    dt = timed_loop(step, a.steps, 0, dist, torch.cuda.synchronize)
+    model.kernel_events = None
+    attn_s = sum(e0.elapsed_time(e1) for e0, e1, _ in evs) * 1e-3
+    attn_flop = sum(f for _, _, f in evs)
+    attn_tflops = attn_flop / attn_s / 1e12
+    value = a.batch * a.steps * world / dt
+    ms_per_step = dt / a.steps * 1e3
+    model_tflops = gflop * a.batch / (ms_per_step * 1e-3) / 1e3
+    out = None
+    if rank == 0:
+        cpu, err = None, None
+        if world == 1 and not a.no_cpu_baseline:
+            cpu, err = cpu_family_baseline(
+                a.mode, a.cpu_clips, lambda p: model.forward_logits(torch.from_numpy(p).to(dev)).cpu().numpy().copy())
+        out = {
+            "metric": metric, "value": round(value, 2), "unit": "clips/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (uint8 frames RandomState(1+rank) -> the family's processor affine; weights RandomState(0))",
+            "config": {"workload": workload, "global_batch": a.batch * world, "parallelism": f"dp{world}"},
+            "logit_max_abs_err": err,
+            "roofline": {"bound": "mfma", "kernel": kname, "achieved": round(attn_tflops, 1), "peak": PEAK_BF16_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                         "avg_launch_ms": round(attn_s * 1e3 / len(evs), 4),
+                         "flop_per_step": round(attn_flop / a.steps / 1e9, 2)},
+            "model_tflops": round(model_tflops, 1), "model_frac_of_peak": round(model_tflops / PEAK_BF16_TFLOPS, 4),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    return out
+
+
 def run_train(a, dist, rank, world, dev):
     """BASELINE configs[4]: the reference's train step (trainers/trainer.py:140-146) on the HIP
     model: zero_grad, forward, CrossEntropyLoss, backward (+ RCCL all-reduce for N > 1), AdamW."""
@@ -279,19 +378,25 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--mode", choices=["fwd", "train"], default="fwd")
+    ap.add_argument("--mode", choices=["fwd", "train", "timesformer", "swin"], default="fwd")
     ap.add_argument("--batch", type=int, default=None, help="clips per GPU per step (fwd 8, train 4)")
     ap.add_argument("--cpu-clips", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     a = ap.parse_args()
     if a.batch is None:
-        a.batch = 8 if a.mode == "fwd" else 4
+        a.batch = {"fwd": 8, "train": 4}.get(a.mode) or FAMILIES[a.mode][2]
     if a.cpu_clips is None:
-        a.cpu_clips = 3 if a.mode == "fwd" else 1
+        a.cpu_clips = {"fwd": 3, "timesformer": 3}.get(a.mode, 1)
 
     dist, rank, world, local = _dist()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if a.mode in FAMILIES:
+        out = run_family(a, dist, rank, world, dev)
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return out
     if a.mode == "train":
         out = run_train(a, dist, rank, world, dev)
         if dist:
