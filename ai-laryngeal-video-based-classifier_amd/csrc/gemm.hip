@@ -34,12 +34,13 @@ __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
 // see it: with a compiler-visible global_load_lds in the loop hipcc falls back to
 // lgkmcnt(0) before every MFMA; here its ds_read waits stay counted, and the DMA is
 // retired by our own vmcnt(N) (cdna_hip_programming.md §5.7 item 1, glds16_asm recipe).
+// m0 is declared clobbered rather than saved and restored around each piece (2 SALU fewer;
+// hipcc re-materialises m0 itself wherever it needs it).
 __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_addr) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :
                  : "v"(gsrc), "s"(lds_addr)
-                 : "memory");
+                 : "memory", "m0");
 }
 
 __device__ __forceinline__ uint32_t lds_addr_of(const void* p) {

@@ -325,12 +325,11 @@ wgrad_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __rest
 // vmcnt retiring only t+1 before the one barrier per half-tile; both MFMA operands read with
 // ds_read_b64_tr_b16 (the reduction index m is the row index of the images).  N1, N2 % 256 == 0.
 // ---------------------------------------------------------------------------------
-__device__ __forceinline__ void wg_glds16(const void* gsrc, uint32_t lds_addr) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep)
+__device__ __forceinline__ void wg_glds16(const void* gsrc, uint32_t lds_addr) {  // m0 clobbered, not restored
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+                 :
                  : "v"(gsrc), "s"(lds_addr)
-                 : "memory");
+                 : "memory", "m0");
 }
 template <int NW>
 __device__ __forceinline__ void wg_wait_vm() {

@@ -1,0 +1,46 @@
+"""Forward (or train-step) time of one libvclip.so build, for process-level A/B of two builds
+on the same box (tools/ab_build.sh makes ab/<name>/libvclip.so from a git revision):
+  python tools/ab_lib.py <path/to/libvclip.so> [fwd|train] [steps]
+The library is bound before any op runs, so every kernel of the run comes from it."""
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+from vclip_amd import _lib  # noqa: E402
+
+path, mode = sys.argv[1], (sys.argv[2] if len(sys.argv) > 2 else "fwd")
+steps = int(sys.argv[3]) if len(sys.argv) > 3 else 30
+_lib.load(path)
+from vclip_amd.vivit import create_model  # noqa: E402
+from vclip_amd.weights import make_synthetic_clips  # noqa: E402
+
+dev = torch.device("cuda", 0)
+B = 8 if mode == "fwd" else 4
+m = create_model(num_frames=32, device=dev)
+pix = torch.from_numpy(make_synthetic_clips(B, 32, 224, seed=1)).to(dev)
+if mode == "fwd":
+    step = lambda: m.forward_logits(pix)  # noqa: E731
+else:
+    from vclip_amd.optim import AdamW
+    m.train()
+    opt = AdamW(m.parameters(), lr=1e-3, weight_decay=0.01)
+    y = torch.from_numpy(np.random.RandomState(2).randint(0, 2, size=B)).long().to(dev)
+
+    def step():
+        opt.zero_grad()
+        torch.nn.functional.cross_entropy(m(pixel_values=pix).logits, y).backward()
+        opt.step()
+for _ in range(5):
+    step()
+torch.cuda.synchronize()
+ts = []
+for _ in range(3):
+    t0 = time.perf_counter()
+    for _ in range(steps // 3):
+        step()
+    torch.cuda.synchronize()
+    ts.append((time.perf_counter() - t0) / (steps // 3) * 1e3)
+print(f"{path} {mode}: {min(ts):.3f} ms/step (min of 3), {B / min(ts) * 1e3:.1f} clips/s", flush=True)
