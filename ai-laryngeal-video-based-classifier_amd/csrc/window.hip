@@ -20,6 +20,8 @@
 // results agree), online softmax in exp2, O^T += V^T.P^T with V^T from ds_read_b64_tr_b16.
 #include "common.hpp"
 
+#include <cstdlib>
+
 namespace vc {
 
 constexpr int WNP_MAX = 448;  // max padded window volume (8*7*7 = 392 -> 448)
@@ -43,6 +45,19 @@ __device__ __forceinline__ int region_bit(int c, int P, int w, int s) {
     return c >= P - s ? 1 : 0;
 }
 
+// DEFER (default): the ViViT kernel's deferred running max (attention.hip) — scores are taken
+// relative to a running max m fixed by the first key tile; per tile only exp2, the row sum and
+// the convert run; a lane's partial row sum <= LIM bounds every P of the tile, and only when
+// that fails is m re-based on the tile's exact max (O and l scaled by 2^-delta).  DEFER = false
+// is the online-softmax form with a per-tile max (and its rescale of O and l).  Swin-T B=4
+// (tools/swin_attn_stages.py, VCLIP_WINDOW_VARIANT A/B on one box): DEFER 1-5 % faster per
+// launch.  Where the rest goes: the fragment-order f32 bias stream (784 KB per (window, head)
+// workgroup, one tile of prefetch) costs 15-20 % (variant 2: no bias loads, timing only); the
+// shift-region mask +15-25 % on the shifted blocks; stages 3-4 fill only 384 / 192 of the 512
+// workgroup slots; 13 query blocks over 4 waves leave one wave a block longer than the rest.
+constexpr float WLIM = 256.0f;
+
+template <bool DEFER, int ABL = 0>  // ABL 1: no bias loads (timing only, wrong results)
 __global__ void __launch_bounds__(256, 2)
 window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, int heads, int vol, int NP,
                        const float* __restrict__ biasF, int masked, uint16_t* __restrict__ out, int64_t ldo) {
@@ -116,6 +131,13 @@ window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, 
     // bias fragments: biasF[head][qb][t][kb][lane][16] f32 = this lane's 16 C-operand values
     const float* bh = biasF + (int64_t)head * (NP / 32) * ntile * 2 * 64 * 16 + lane * 16;
     auto load_bias = [&](int qb, int t, v16f (&c)[2]) {
+        if constexpr (ABL & 1) {
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) c[kb][e] = (float)(t + kb);
+            return;
+        }
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
             const float4* bp = reinterpret_cast<const float4*>(bh + (((int64_t)qb * ntile + t) * 2 + kb) * 64 * 16);
@@ -140,6 +162,86 @@ window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, 
         float m_run = -1e30f, l_run = 0.f;
         v16f bnext[2];
         load_bias(qb, 0, bnext);
+        if constexpr (DEFER) {
+            v2f l2 = {0.f, 0.f};
+            for (int t = 0; t < ntile; ++t) {
+                v16f sc[2] = {bnext[0], bnext[1]};
+                if (t + 1 < ntile) load_bias(qb, t + 1, bnext);
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+                    for (int kb = 0; kb < 2; ++kb) {
+                        const v8bf kf = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(Ks + (t * 64 + kb * 32) * 64 + koff[kk]));
+                        sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kk], sc[kb], 0, 0, 0);
+                    }
+                }
+                if (masked) {
+#pragma unroll
+                    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+                        for (int g4 = 0; g4 < 4; ++g4) {
+                            const int k0 = t * 64 + kb * 32 + 8 * g4 + 4 * h;
+                            const unsigned wv = lab4[k0 >> 3] >> (4 * (k0 & 7));
+#pragma unroll
+                            for (int e = 0; e < 4; ++e)
+                                if ((int)((wv >> (4 * e)) & 15) != qlab) sc[kb][4 * g4 + e] = -INFINITY;
+                        }
+                    }
+                }
+                auto rowmax = [&]() {
+                    float a = fmaxf(sc[0][0], sc[1][0]), c = fmaxf(sc[0][1], sc[1][1]);
+#pragma unroll
+                    for (int e = 2; e < 16; e += 2) {
+                        a = fmaxf(a, fmaxf(sc[0][e], sc[1][e]));
+                        c = fmaxf(c, fmaxf(sc[0][e + 1], sc[1][e + 1]));
+                    }
+                    const float x = fmaxf(a, c);
+                    return fmaxf(x, __shfl_xor(x, 32, 64));
+                };
+                if (t == 0) m_run = fmaxf(rowmax(), -1e30f);  // first tile fixes m (fully masked rows: -1e30)
+                v16f p[2];
+                auto expsum = [&]() {
+#pragma unroll
+                    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                        for (int e = 0; e < 16; ++e) p[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e] - m_run);
+                    v2f u[8];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        u[j] = v2f{p[0][4 * j], p[0][4 * j + 1]} + v2f{p[0][4 * j + 2], p[0][4 * j + 3]};
+                        u[4 + j] = v2f{p[1][4 * j], p[1][4 * j + 1]} + v2f{p[1][4 * j + 2], p[1][4 * j + 3]};
+                    }
+                    return ((u[0] + u[1]) + (u[2] + u[3])) + ((u[4] + u[5]) + (u[6] + u[7]));
+                };
+                v2f ps = expsum();
+                if (__any(!(ps[0] + ps[1] <= WLIM))) {  // rare: re-base m on this tile's exact max
+                    const float delta = fmaxf(rowmax() - m_run, 0.f);
+                    const float alpha = __builtin_amdgcn_exp2f(-delta);
+                    m_run += delta;
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) o[e] *= alpha;
+                    l2 *= alpha;
+                    ps = expsum();
+                }
+                l2 += ps;
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) {
+                        v8bf pf;
+#pragma unroll
+                        for (int jj = 0; jj < 8; ++jj) pf[jj] = (__bf16)p[kb][8 * s2 + jj];
+                        const char* pa = Vs + (t * 64 + kb * 32 + 16 * s2) * 64 + voff;
+                        const v4s va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)pa);
+                        const v4s vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(pa + 8 * 64));
+                        v8s vv;
+                        vv[0] = va[0]; vv[1] = va[1]; vv[2] = va[2]; vv[3] = va[3];
+                        vv[4] = vb[0]; vv[5] = vb[1]; vv[6] = vb[2]; vv[7] = vb[3];
+                        o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf, vv), pf, o, 0, 0, 0);
+                    }
+            }
+            l_run = l2[0] + l2[1];
+        } else
         for (int t = 0; t < ntile; ++t) {
             v16f sc[2] = {bnext[0], bnext[1]};  // C = bias tile (prefetched one tile ahead)
             if (t + 1 < ntile) load_bias(qb, t + 1, bnext);
@@ -365,8 +467,19 @@ int vc_window_attention3d(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T,
     if (nwin > 0x7fffffff || heads > 65535) return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d: grid too large");
     dim3 grid((unsigned)nwin, (unsigned)heads);
     if ((uintptr_t)biasF & 15) return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d: biasF must be 16-B aligned");
-    window_attn_d32_kernel<<<grid, 256, 0, stream>>>(qkv, ld, g, (int)heads, vol, (int)np, biasF,
-                                                     (st | sh | sw) ? 1 : 0, out, ldo);
+    static const int variant = [] {  // VCLIP_WINDOW_VARIANT=0: per-tile-max form (A/B only)
+        const char* v = getenv("VCLIP_WINDOW_VARIANT");
+        return v ? atoi(v) : 1;
+    }();
+    if (variant == 2)  // timing-only ablation: no bias loads
+        window_attn_d32_kernel<true, 1><<<grid, 256, 0, stream>>>(qkv, ld, g, (int)heads, vol, (int)np, biasF,
+                                                                  (st | sh | sw) ? 1 : 0, out, ldo);
+    else if (variant == 0)
+        window_attn_d32_kernel<false><<<grid, 256, 0, stream>>>(qkv, ld, g, (int)heads, vol, (int)np, biasF,
+                                                                (st | sh | sw) ? 1 : 0, out, ldo);
+    else
+        window_attn_d32_kernel<true><<<grid, 256, 0, stream>>>(qkv, ld, g, (int)heads, vol, (int)np, biasF,
+                                                               (st | sh | sw) ? 1 : 0, out, ldo);
     return check_launch("vc_window_attention3d");
 }
 
