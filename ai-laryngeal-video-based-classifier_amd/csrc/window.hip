@@ -60,7 +60,8 @@ constexpr float WLIM = 256.0f;
 template <bool DEFER, int ABL = 0>  // ABL 1: no bias loads (timing only, wrong results)
 __global__ void __launch_bounds__(256, 2)
 window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, int heads, int vol, int NP,
-                       const float* __restrict__ biasF, int masked, uint16_t* __restrict__ out, int64_t ldo) {
+                       const float* __restrict__ biasF, int masked, uint16_t* __restrict__ out, int64_t ldo,
+                       int qsplit) {
     __shared__ __attribute__((aligned(16))) char kv[2 * WNP_MAX * 64];
     __shared__ unsigned lab4[WNP_MAX / 8];  // 4-bit region code per window token (15: padding)
 
@@ -149,7 +150,8 @@ window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, 
         }
     };
 
-    for (int qb = wave; qb < nqb; qb += 4) {
+    // query blocks of this (window, head) are dealt over qsplit workgroups (blockIdx.z) x 4 waves
+    for (int qb = blockIdx.z + qsplit * wave; qb < nqb; qb += 4 * qsplit) {
         const int qn = qb * 32 + rr;  // this lane's query (window-local)
         const int qc = qn < vol ? qn : vol - 1;
         int qlab = 0;
@@ -163,6 +165,7 @@ window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, 
         v16f bnext[2];
         load_bias(qb, 0, bnext);
         if constexpr (DEFER) {
+            // (bias fragments two tiles ahead instead of one: 238 VGPRs, 2 % slower per forward)
             v2f l2 = {0.f, 0.f};
             for (int t = 0; t < ntile; ++t) {
                 v16f sc[2] = {bnext[0], bnext[1]};
@@ -467,19 +470,33 @@ int vc_window_attention3d(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T,
     if (nwin > 0x7fffffff || heads > 65535) return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d: grid too large");
     dim3 grid((unsigned)nwin, (unsigned)heads);
     if ((uintptr_t)biasF & 15) return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d: biasF must be 16-B aligned");
-    static const int variant = [] {  // VCLIP_WINDOW_VARIANT=0: per-tile-max form (A/B only)
+    static const int variant = [] {  // VCLIP_WINDOW_VARIANT (A/B only): 0 per-tile max, 1 no query split
         const char* v = getenv("VCLIP_WINDOW_VARIANT");
         return v ? atoi(v) : 1;
     }();
+    // Variant 3 (A/B only): later Swin stages have few (window, head) pairs (Swin-T B=4: 384 and
+    // 192 workgroups for 512 slots); split each pair's query blocks over qsplit workgroups (each
+    // stages the window's K/V itself) until the grid holds >= 3 rounds of two workgroups per CU.
+    // Measured SLOWER (stage 4: 41.6 vs 36.4 us): those launches are bound by each workgroup's
+    // staging and single-wave latency, not by the empty slots, so the default keeps qsplit = 1.
+    static const int slots = [] {
+        int dev = 0, n = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        return 2 * n;
+    }();
+    int qsplit = 1;
+    const int nqb = (vol + 31) / 32;
+    if (variant == 3)
+        while (qsplit < 8 && 2 * qsplit <= nqb && nwin * heads * qsplit < 3LL * slots) qsplit *= 2;
+    grid.z = (unsigned)qsplit;
+    const int mk = (st | sh | sw) ? 1 : 0;
     if (variant == 2)  // timing-only ablation: no bias loads
-        window_attn_d32_kernel<true, 1><<<grid, 256, 0, stream>>>(qkv, ld, g, (int)heads, vol, (int)np, biasF,
-                                                                  (st | sh | sw) ? 1 : 0, out, ldo);
+        window_attn_d32_kernel<true, 1><<<grid, 256, 0, stream>>>(qkv, ld, g, (int)heads, vol, (int)np, biasF, mk, out, ldo, qsplit);
     else if (variant == 0)
-        window_attn_d32_kernel<false><<<grid, 256, 0, stream>>>(qkv, ld, g, (int)heads, vol, (int)np, biasF,
-                                                                (st | sh | sw) ? 1 : 0, out, ldo);
+        window_attn_d32_kernel<false><<<grid, 256, 0, stream>>>(qkv, ld, g, (int)heads, vol, (int)np, biasF, mk, out, ldo, qsplit);
     else
-        window_attn_d32_kernel<true><<<grid, 256, 0, stream>>>(qkv, ld, g, (int)heads, vol, (int)np, biasF,
-                                                               (st | sh | sw) ? 1 : 0, out, ldo);
+        window_attn_d32_kernel<true><<<grid, 256, 0, stream>>>(qkv, ld, g, (int)heads, vol, (int)np, biasF, mk, out, ldo, qsplit);
     return check_launch("vc_window_attention3d");
 }
 
