@@ -109,8 +109,16 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
     constexpr int AQ = 128 * QB;  // query rows per workgroup (4 waves x QB x 32)
     // ABL & 1024: a 5-slot ring (80 KiB, two workgroups fill the CU's 160 KiB) keeping two
     // tiles in flight across each barrier instead of one
-    constexpr int NS = (ABL & 1024) ? 5 : NSLOT;
-    static_assert(!((ABL & 1024) && (ABL & (256 | 512))), "5-slot ring: default iteration only");
+    // ABL & 4096: "P.V lag" — tile t-1's P.V MFMAs move into iteration t beside tile t+1's QK^T
+    // MFMAs and tile t's exp2 / sum (one scheduling region of 16 MFMAs and all of the softmax
+    // VALU); V_{t-1} stays live one iteration longer, so the ring needs 5 slots (prefetch
+    // distance stays 3 tiles).  Bit-identical to the shipped build but 8.5 % slower at B = 8
+    // (280 vs 258 us): S(t+1), P(t), bf16 P(t-1), O and the hoisted K / V^T fragments of one
+    // merged region exceed 256 VGPRs (22 spilled to scratch).
+    constexpr bool LAG = (ABL & 4096) != 0;
+    constexpr int NS = (ABL & (1024 | 4096)) ? 5 : NSLOT;
+    static_assert(!((ABL & (1024 | 4096)) && (ABL & (256 | 512))), "5-slot ring: default iteration only");
+    static_assert(!((ABL & 1024) && LAG), "one 5-slot variant at a time");
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     // XCD-aware order: the workgroups of one (clip, head) share its K/V; give every XCD a
@@ -286,9 +294,9 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
     stage(0);
     if (ntiles > 1) stage(1);
     if (ntiles > 2) stage(2);
-    if (NS == 5 && ntiles > 3) stage(3);
+    if (NS == 5 && !LAG && ntiles > 3) stage(3);
     // ABL & 512 (K-fragment prefetch) keeps no tile in flight across the per-tile barrier
-    if (NS == 5 && ntiles > 3) attn_wait_vm<8>();  // tiles 0 and 1 resident, 2 and 3 in flight
+    if (NS == 5 && !LAG && ntiles > 3) attn_wait_vm<8>();  // tiles 0 and 1 resident, 2 and 3 in flight
     else if (!(ABL & 512) && ntiles > 2) attn_wait_vm<4>();  // tiles 0 and 1 resident, 2 in flight
     else attn_wait_vm<0>();
     attn_sync();
@@ -559,6 +567,69 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
         }
         if constexpr (NEXT != 2) { scur[0][0] = snext[0]; scur[0][1] = snext[1]; }
     };
+    // ---- P.V lag iteration (ABL & 4096, QB = 1)
+    v8bf pprev[2][2];  // bf16 P of tile t-1, [key block][k-step]
+    auto pv_prev = [&](const char* pslot) __attribute__((always_inline)) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                for (int db = 0; db < 2; ++db) {
+                    const char* pa = pslot + voff[db] + (kb * 32 + 16 * s2) * 128;
+                    v4s va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)pa);
+                    v4s vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(pa + 8 * 128));
+                    v8s vv;
+                    vv[0] = va[0]; vv[1] = va[1]; vv[2] = va[2]; vv[3] = va[3];
+                    vv[4] = vb[0]; vv[5] = vb[1]; vv[6] = vb[2]; vv[7] = vb[3];
+                    o[0][db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf, vv), pprev[kb][s2], o[0][db], 0, 0, 0);
+                }
+    };
+    auto iter_lag = [&](auto next_c, auto first_c, const char* pslot, const char* slot, const char* nslot, int t)
+        __attribute__((always_inline)) {
+        constexpr int NEXT = decltype(next_c)::value;
+        constexpr bool FIRST = decltype(first_c)::value;
+        if (!(ABL & 1) && t + 3 < ntiles) stage(t + 3);  // into slot t-2, free since the last barrier
+        v16f snext[QB][2];
+        if constexpr (NEXT == 0) qk_mfma(nslot, snext);
+        else if constexpr (NEXT == 1) qk(nslot, t + 1, snext);
+        if constexpr (!FIRST) pv_prev(pslot);
+        v2f ps[QB];
+        expsum(scur, ps);
+        if (__any(!(ps[0][0] + ps[0][1] <= ((ABL & 16) ? -1.0f : LIM)))) {
+            qk(slot, t, scur);
+            const float delta = fmaxf(rowmax_of(scur[0]), 0.f);
+            const float alpha = __builtin_amdgcn_exp2f(-delta);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                scur[0][0][e] -= delta;
+                scur[0][1][e] -= delta;
+                o[0][0][e] *= alpha;  // O holds tiles <= t-1, all at the old base
+                o[0][1][e] *= alpha;
+                minit[0][e] -= delta;
+            }
+            if constexpr (NEXT != 2) {
+#pragma unroll
+                for (int e = 0; e < 16; ++e) { snext[0][0][e] -= delta; snext[0][1][e] -= delta; }
+            }
+            l_run[0] *= alpha;
+            expsum(scur, ps);
+        }
+        l_run[0] += ps[0];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj) pprev[kb][s2][jj] = (__bf16)scur[0][kb][8 * s2 + jj];
+        if (t + 2 < ntiles) {
+            if (t + 3 < ntiles) attn_wait_vm<4>();
+            else attn_wait_vm<0>();
+            attn_sync();
+        }
+        if constexpr (NEXT != 2) { scur[0][0] = snext[0][0]; scur[0][1] = snext[0][1]; }
+    };
+
     auto step = [&](auto next_c, const char* slot, const char* nslot, const char* n2slot, int t) __attribute__((always_inline)) {
         if constexpr ((ABL & 512) && QB == 1) iter_pf(next_c, slot, nslot, n2slot, t);
         else if constexpr ((ABL & 256) && QB == 1) iter_split(next_c, slot, nslot, t);
@@ -568,7 +639,26 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
     using full_c = std::integral_constant<int, 0>;
     const int nfull = S / AK;  // full tiles
     int t = 0;
-    if constexpr (NS == 5) {
+    if constexpr (LAG && QB == 1) {
+        using no_c = std::false_type;
+        auto slotp = [&](int i) { return smem + ((i + NS) % NS) * KV_SLOT; };
+        if (ntiles > 1) iter_lag(std::integral_constant<int, 1>{}, std::true_type{}, slotp(-1), slotp(0), slotp(1), 0);
+        else iter_lag(std::integral_constant<int, 2>{}, std::true_type{}, slotp(-1), slotp(0), slotp(1), 0);
+        t = 1;
+        for (; t + 6 <= nfull; t += NS) {  // t = 1 mod 5: iterations t..t+4 all have a full next tile
+            iter_lag(full_c{}, no_c{}, smem + 0 * KV_SLOT, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, t);
+            iter_lag(full_c{}, no_c{}, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, smem + 3 * KV_SLOT, t + 1);
+            iter_lag(full_c{}, no_c{}, smem + 2 * KV_SLOT, smem + 3 * KV_SLOT, smem + 4 * KV_SLOT, t + 2);
+            iter_lag(full_c{}, no_c{}, smem + 3 * KV_SLOT, smem + 4 * KV_SLOT, smem + 0 * KV_SLOT, t + 3);
+            iter_lag(full_c{}, no_c{}, smem + 4 * KV_SLOT, smem + 0 * KV_SLOT, smem + 1 * KV_SLOT, t + 4);
+        }
+        for (; t < ntiles; ++t) {
+            if (t + 1 < ntiles) iter_lag(std::integral_constant<int, 1>{}, no_c{}, slotp(t - 1), slotp(t), slotp(t + 1), t);
+            else iter_lag(std::integral_constant<int, 2>{}, no_c{}, slotp(t - 1), slotp(t), slotp(t + 1), t);
+        }
+        pv_prev(slotp(ntiles - 1));  // the last tile's P.V
+        t = ntiles;
+    } else if constexpr (NS == 5) {
         for (; t + 6 <= nfull; t += NS) {  // iterations t..t+4 all have a full next tile
             step(full_c{}, smem + 0 * KV_SLOT, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, t);
             step(full_c{}, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, smem + 3 * KV_SLOT, t + 1);
@@ -630,7 +720,7 @@ template <int QB, int ABL, bool WLSE = false>
 static void launch_attn(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, float c_log2, uint16_t* out,
                         int64_t ldo, hipStream_t stream, float* lse = nullptr) {
     constexpr int AQ = 128 * QB;
-    constexpr int lds = ((ABL & 1024) ? 5 : NSLOT) * KV_SLOT;
+    constexpr int lds = ((ABL & (1024 | 4096)) ? 5 : NSLOT) * KV_SLOT;
     static bool attr_set = false;  // per instantiation; idempotent
     if (lds > 64 * 1024 && !attr_set) {
         (void)hipFuncSetAttribute((const void*)attn_fwd_d64_kernel<QB, ABL, WLSE>,
@@ -685,7 +775,7 @@ extern "C" int vc_attention_fwd_ablation(const uint16_t* qkv, int64_t ld, int64_
 #define VC_ABL(QB, N) case 100 * (QB - 1) + N: launch_attn<QB, N>(qkv, ld, B, S, H, c_log2, out, ldo, stream); break;
     switch (abl) {
         VC_ABL(1, 0) VC_ABL(1, 1) VC_ABL(1, 2) VC_ABL(1, 4) VC_ABL(1, 6) VC_ABL(1, 8) VC_ABL(1, 12) VC_ABL(1, 14)
-        VC_ABL(1, 15) VC_ABL(1, 16) VC_ABL(1, 32) VC_ABL(1, 64) VC_ABL(1, 128) VC_ABL(1, 256) VC_ABL(1, 320) VC_ABL(1, 512) VC_ABL(1, 576) VC_ABL(1, 1024) VC_ABL(1, 1088) VC_ABL(1, 1152) VC_ABL(1, 2048)
+        VC_ABL(1, 15) VC_ABL(1, 16) VC_ABL(1, 32) VC_ABL(1, 64) VC_ABL(1, 128) VC_ABL(1, 256) VC_ABL(1, 320) VC_ABL(1, 512) VC_ABL(1, 576) VC_ABL(1, 1024) VC_ABL(1, 1088) VC_ABL(1, 1152) VC_ABL(1, 2048) VC_ABL(1, 4096)
         default: return fail(VC_ERR_INVALID_ARG, "bad ablation");
     }
 #undef VC_ABL
