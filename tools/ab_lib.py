@@ -1,6 +1,6 @@
 """Forward (or train-step) time of one libvclip.so build, for process-level A/B of two builds
 on the same box (tools/ab_build.sh makes ab/<name>/libvclip.so from a git revision):
-  python tools/ab_lib.py <path/to/libvclip.so> [fwd|train] [steps]
+  python tools/ab_lib.py <path/to/libvclip.so> [fwd|train|timesformer|swin] [steps]
 The library is bound before any op runs, so every kernel of the run comes from it."""
 import sys
 import time
@@ -18,10 +18,20 @@ from vclip_amd.vivit import create_model  # noqa: E402
 from vclip_amd.weights import make_synthetic_clips  # noqa: E402
 
 dev = torch.device("cuda", 0)
-B = 8 if mode == "fwd" else 4
-m = create_model(num_frames=32, device=dev)
-pix = torch.from_numpy(make_synthetic_clips(B, 32, 224, seed=1)).to(dev)
-if mode == "fwd":
+B = {"fwd": 8, "timesformer": 16}.get(mode, 4)
+if mode == "timesformer":
+    from vclip_amd.timesformer import create_model as tsf_model
+    m = tsf_model(num_frames=8, device=dev)
+    pix = torch.from_numpy(make_synthetic_clips(B, 8, 224, seed=1)).to(dev)
+elif mode == "swin":
+    from vclip_amd.swin3d import create_model as swin_model
+    from vclip_amd.weights import make_synthetic_video
+    m = swin_model(model_size="tiny", device=dev)
+    pix = torch.from_numpy(make_synthetic_video(B, 32, 224, seed=1)).to(dev)
+else:
+    m = create_model(num_frames=32, device=dev)
+    pix = torch.from_numpy(make_synthetic_clips(B, 32, 224, seed=1)).to(dev)
+if mode != "train":
     step = lambda: m.forward_logits(pix)  # noqa: E731
 else:
     from vclip_amd.optim import AdamW
