@@ -110,6 +110,109 @@ __global__ void __launch_bounds__(256) temporal_attn_kernel(const uint16_t* __re
 }
 
 // ---------------------------------------------------------------------------------
+// Temporal attention, one workgroup per (clip, patch): the patch's T contiguous q|k|v rows
+// (T x 3*H*64 bf16, 36.9 KB at TimeSformer-B T = 8) are copied into LDS with coalesced
+// 16-byte loads (whole rows, so every HBM byte is read once), then two threads per
+// (frame, head) pair each own 32 of the 64 dims: partial QK^T dots joined by one lane
+// exchange, fp32 softmax over the T keys, P.V for the thread's 32 dims, 64-byte stores.
+// The thread-per-query kernel above reads each 128-byte head slice with eight strided
+// 16-byte loads per lane and re-reads K/V rows T times through L1/L2 (1.7 TB/s at B = 16).
+// ---------------------------------------------------------------------------------
+template <int TMAX>
+__global__ void __launch_bounds__(256) temporal_attn_lds_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int P,
+                                                                int T, int H, float c, int exp2_mode,
+                                                                uint16_t* __restrict__ out, int64_t ldo) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int64_t bp = blockIdx.x;  // b*P + p
+    const int64_t b = bp / P, p = bp % P;
+    const int64_t row0 = b * (1 + (int64_t)P * T) + 1 + p * T;
+    const int rw = 3 * H * 8;  // 16-byte pieces per staged row
+    uint4* lds = reinterpret_cast<uint4*>(smem);
+    for (int i = threadIdx.x; i < T * rw; i += 256) {
+        const int t = i / rw, j = i - t * rw;
+        lds[i] = reinterpret_cast<const uint4*>(qkv + (row0 + t) * ld)[j];
+    }
+    __syncthreads();
+    const int hf = threadIdx.x & 1;
+    for (int pair = threadIdx.x >> 1; pair < T * H; pair += 128) {  // uniform trip count per lane pair
+        const int t = pair / H, hh = pair - t * H;
+        const uint4* qp = lds + t * rw + hh * 8 + hf * 4;
+        float q[32];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint4 u = qp[j];
+            const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                q[8 * j + 2 * e] = bf2f((unsigned short)(w[e] & 0xffff)) * c;
+                q[8 * j + 2 * e + 1] = bf2f((unsigned short)(w[e] >> 16)) * c;
+            }
+        }
+        float s[TMAX];
+        float m = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < TMAX; ++k) {
+            if (k < T) {
+                const uint4* kp = lds + k * rw + (H + hh) * 8 + hf * 4;
+                float a = 0.f;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint4 u = kp[j];
+                    const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        a += q[8 * j + 2 * e] * bf2f((unsigned short)(w[e] & 0xffff));
+                        a += q[8 * j + 2 * e + 1] * bf2f((unsigned short)(w[e] >> 16));
+                    }
+                }
+                a += __shfl_xor(a, 1, 64);
+                s[k] = a;
+                m = fmaxf(m, a);
+            }
+        }
+        float l = 0.f;
+#pragma unroll
+        for (int k = 0; k < TMAX; ++k) {
+            if (k < T) {
+                s[k] = exp2_mode ? exp2f(s[k] - m) : __expf(s[k] - m);
+                l += s[k];
+            }
+        }
+        const float inv = 1.0f / l;
+        float o[32];
+#pragma unroll
+        for (int d = 0; d < 32; ++d) o[d] = 0.f;
+#pragma unroll
+        for (int k = 0; k < TMAX; ++k) {
+            if (k < T) {
+                const uint4* vp = lds + k * rw + (2 * H + hh) * 8 + hf * 4;
+                const float pk = s[k] * inv;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint4 u = vp[j];
+                    const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        o[8 * j + 2 * e] += pk * bf2f((unsigned short)(w[e] & 0xffff));
+                        o[8 * j + 2 * e + 1] += pk * bf2f((unsigned short)(w[e] >> 16));
+                    }
+                }
+            }
+        }
+        uint4* op = reinterpret_cast<uint4*>(out + (row0 + t) * ldo + hh * 64 + hf * 32);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint4 u;
+            u.x = pack2bf(o[8 * j + 0], o[8 * j + 1]);
+            u.y = pack2bf(o[8 * j + 2], o[8 * j + 3]);
+            u.z = pack2bf(o[8 * j + 4], o[8 * j + 5]);
+            u.w = pack2bf(o[8 * j + 6], o[8 * j + 7]);
+            op[j] = u;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
 // Residual add + LayerNorm with the clip <-> frame permutes folded in.  One wave per
 // clip-layout row; D % 4 == 0 and D <= 1024 (each lane holds up to 4 float4).
 //   mode 0 (temporal -> spatial):  x[r] += y[r] (patch rows; y bf16 clip layout);
@@ -209,7 +312,14 @@ int vc_temporal_attention(const uint16_t* qkv, int64_t ld, int64_t B, int64_t P,
     const unsigned nb = (unsigned)((nq + 255) / 256);
     // q_prescaled: q already carries scale*log2(e) (folded into the projection) -> exp2
     const float c = q_prescaled ? 1.0f : scale;
-    if (T <= 8)
+    const int64_t lds = T * 3 * H * 64 * 2;  // one patch's q|k|v rows
+    if (T <= 16 && lds <= 64 * 1024 && B * P < (1LL << 31)) {
+        const unsigned nwg = (unsigned)(B * P);
+        if (T <= 8)
+            temporal_attn_lds_kernel<8><<<nwg, 256, lds, stream>>>(qkv, ld, (int)P, (int)T, (int)H, c, q_prescaled, out, ldo);
+        else
+            temporal_attn_lds_kernel<16><<<nwg, 256, lds, stream>>>(qkv, ld, (int)P, (int)T, (int)H, c, q_prescaled, out, ldo);
+    } else if (T <= 8)
         temporal_attn_kernel<8><<<nb, 256, 0, stream>>>(qkv, ld, nq, (int)P, (int)T, (int)H, c, q_prescaled, out, ldo);
     else if (T <= 16)
         temporal_attn_kernel<16><<<nb, 256, 0, stream>>>(qkv, ld, nq, (int)P, (int)T, (int)H, c, q_prescaled, out, ldo);

@@ -45,8 +45,12 @@ def _clip_rows(B, P, T):
 
 
 @pytest.mark.parametrize("B,P,T,H,pre", [(2, 16, 4, 2, False), (3, 196, 8, 12, True), (1, 5, 1, 1, False),
-                                         (2, 7, 16, 2, True)])
+                                         (2, 7, 16, 2, True), (2, 5, 16, 8, False), (2, 5, 12, 10, True),
+                                         (1, 3, 16, 12, True), (2, 3, 32, 2, False)])
 def test_temporal_attention(B, P, T, H, pre):
+    """LDS kernel (one workgroup per patch) when T <= 16 and the patch's q|k|v rows fit 64 KB
+    (T*H <= 128 pairs in one pass, more in a loop); thread-per-query kernel otherwise
+    ((1, 3, 16, 12): 72 KB; T = 32)."""
     g = torch.Generator().manual_seed(B * 1000 + P + T)
     S = 1 + P * T
     rows = B * S + 8
