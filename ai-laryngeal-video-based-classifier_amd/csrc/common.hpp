@@ -72,6 +72,14 @@ __device__ __forceinline__ float gelu_erf(float x) {
     return x * (x >= 0.0f ? 1.0f - h : h);
 }
 
+// sum over aligned groups of L lanes (L a power of two <= 64): every lane gets its group's sum
+template <int L>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+    for (int o = L / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

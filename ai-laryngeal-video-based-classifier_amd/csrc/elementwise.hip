@@ -232,6 +232,80 @@ __global__ void __launch_bounds__(256) layernorm_reg_kernel(const float* __restr
     }
 }
 
+// Narrow-row LayerNorm (Swin's D = 96 / 192 / 384 at 200k / 50k / 12k rows): L lanes per row,
+// 64 / L rows per wave, each lane V float4 (masked past D), single HBM pass, reductions over
+// the L-lane group.  A whole wave per 96-wide row (layernorm_reg_kernel) leaves 40 of 64
+// lanes idle and launches one wave per 384 bytes: 47 us for Swin-T stage 1 at B = 4 (2.5 TB/s).
+template <int L, int V, bool OUTF32>
+__global__ void __launch_bounds__(256) layernorm_grp_kernel(const float* __restrict__ x, int64_t ldx, int64_t M, int D,
+                                                            const float* __restrict__ g, const float* __restrict__ be,
+                                                            float eps, void* __restrict__ y, int64_t ldy) {
+    const int sub = threadIdx.x & (L - 1);
+    const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / L;
+    if (row >= M) return;  // whole L-lane groups exit together
+    const float* xr = x + row * ldx;
+    float4 v[V];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const int n = (i * L + sub) * 4;
+        v[i] = n < D ? *reinterpret_cast<const float4*>(xr + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+        s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    }
+    const float mean = group_sum<L>(s) / (float)D;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        if ((i * L + sub) * 4 < D) {
+            const float a = v[i].x - mean, b = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+            q += (a * a + b * b) + (c * c + d * d);
+        }
+    }
+    const float rstd = rsqrtf(group_sum<L>(q) / (float)D + eps);
+#pragma unroll
+    for (int i = 0; i < V; ++i) {
+        const int n = (i * L + sub) * 4;
+        if (n < D) {
+            const float4 gg = *reinterpret_cast<const float4*>(g + n), bb = *reinterpret_cast<const float4*>(be + n);
+            const float o0 = (v[i].x - mean) * rstd * gg.x + bb.x, o1 = (v[i].y - mean) * rstd * gg.y + bb.y;
+            const float o2 = (v[i].z - mean) * rstd * gg.z + bb.z, o3 = (v[i].w - mean) * rstd * gg.w + bb.w;
+            if constexpr (OUTF32) {
+                *reinterpret_cast<float4*>(reinterpret_cast<float*>(y) + row * ldy + n) = make_float4(o0, o1, o2, o3);
+            } else {
+                uint2 o;
+                o.x = pack2bf(o0, o1);
+                o.y = pack2bf(o2, o3);
+                *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(y) + row * ldy + n) = o;
+            }
+        }
+    }
+}
+
+// lanes per row for a narrow LayerNorm: the smallest L in {8, 16, 32} with D <= L * 3 float4
+// (else L * 4), 0 when D needs the whole-wave kernel
+static inline int grp_lanes(int64_t D, int* V) {
+    for (int L = 8; L <= 32; L *= 2) {
+        if (D <= L * 12) { *V = 3; return L; }
+        if (D <= L * 16) { *V = 4; return L; }
+    }
+    return 0;
+}
+
+template <bool OUTF32>
+static bool launch_ln_grp(const float* x, int64_t ldx, int64_t M, int64_t D, const float* g, const float* be, float eps,
+                          void* y, int64_t ldy, hipStream_t stream) {
+    int V = 0;
+    const int L = grp_lanes(D, &V);
+    if (!L) return false;
+    const unsigned nb = (unsigned)((M * L + 255) / 256);
+#define VC_LN_GRP(LL, VV) layernorm_grp_kernel<LL, VV, OUTF32><<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, g, be, eps, y, ldy)
+    if (L == 8) { if (V == 3) VC_LN_GRP(8, 3); else VC_LN_GRP(8, 4); }
+    else if (L == 16) { if (V == 3) VC_LN_GRP(16, 3); else VC_LN_GRP(16, 4); }
+    else { if (V == 3) VC_LN_GRP(32, 3); else VC_LN_GRP(32, 4); }
+#undef VC_LN_GRP
+    return true;
+}
+
 // Generic-width LayerNorm (any D): one wave per row, three passes over the row (L1/L2-resident).
 // OUTF32: the output is f32 (y is a float*), e.g. Swin's patch_embed.norm feeding the residual stream.
 template <bool OUTF32 = false>
@@ -383,9 +457,10 @@ int vc_layernorm_f32_bf16(const float* x, int64_t ldx, int64_t M, int64_t D, con
         case 1024: layernorm_kernel<4><<<nb, 256, 0, stream>>>(x, ldx, M, gamma, beta, eps, y, ldy); break;
         default:
             if (D <= 0 || D > 65536) return fail(VC_ERR_INVALID_ARG, "vc_layernorm: bad D");
-            if (D <= 1024 && D % 4 == 0 && !(((uintptr_t)x | (uintptr_t)gamma | (uintptr_t)beta) & 15) && !((uintptr_t)y & 7))
+            if (D <= 1024 && D % 4 == 0 && !(((uintptr_t)x | (uintptr_t)gamma | (uintptr_t)beta) & 15) && !((uintptr_t)y & 7)) {
+                if (ldx % 4 == 0 && ldy % 4 == 0 && launch_ln_grp<false>(x, ldx, M, D, gamma, beta, eps, y, ldy, stream)) break;
                 layernorm_reg_kernel<false><<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, gamma, beta, eps, y, ldy);
-            else
+            } else
                 layernorm_any_kernel<false><<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, gamma, beta, eps, y, ldy);
     }
     return check_launch("vc_layernorm_f32_bf16");
@@ -397,9 +472,10 @@ int vc_layernorm_f32(const float* x, int64_t ldx, int64_t M, int64_t D, const fl
     if (D <= 0 || D > 65536 || ldx < D || ldy < D) return fail(VC_ERR_INVALID_ARG, "vc_layernorm_f32: bad D / ld");
     const unsigned nb = (unsigned)((M + 3) / 4);
     if (D <= 1024 && D % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 &&
-        !(((uintptr_t)x | (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)y) & 15))
-        layernorm_reg_kernel<true><<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, gamma, beta, eps, y, ldy);
-    else
+        !(((uintptr_t)x | (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)y) & 15)) {
+        if (!launch_ln_grp<true>(x, ldx, M, D, gamma, beta, eps, y, ldy, stream))
+            layernorm_reg_kernel<true><<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, gamma, beta, eps, y, ldy);
+    } else
         layernorm_any_kernel<true><<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, gamma, beta, eps, y, ldy);
     return check_launch("vc_layernorm_f32");
 }

@@ -363,6 +363,60 @@ __global__ void __launch_bounds__(256) patch_merge_ln_kernel(const float* __rest
     for (int n = lane; n < C4; n += 64) y[row * ldy + n] = f2bf((val(n) - mean) * rstd * g[n] + be[n]);
 }
 
+// Same merge + LayerNorm with float4 loads held in registers: L lanes per merged row (64 / L
+// rows per wave), each lane V float4 of the 4C concatenation, one HBM pass (C % 4 == 0).
+// The scalar kernel above re-reads each value three times and recomputes the quadrant index
+// per element: 78 us for Swin-T stage 1 -> 2 at B = 4 (1.5 TB/s).
+template <int L, int V>
+__global__ void __launch_bounds__(256) patch_merge_ln_grp_kernel(const float* __restrict__ x, int64_t ldx, int64_t B,
+                                                                 int T, int H, int W, int C,
+                                                                 const float* __restrict__ g,
+                                                                 const float* __restrict__ be, float eps,
+                                                                 uint16_t* __restrict__ y, int64_t ldy) {
+    const int sub = threadIdx.x & (L - 1);
+    const int H2 = (H + 1) / 2, W2 = (W + 1) / 2;
+    const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) / L;
+    if (row >= B * T * H2 * W2) return;  // whole L-lane groups exit together
+    const int j = (int)(row % W2);
+    const int i = (int)((row / W2) % H2);
+    const int64_t bt = row / ((int64_t)W2 * H2);
+    const int C4 = 4 * C;
+    float4 v[V];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+        const int n = (k * L + sub) * 4;
+        v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (n < C4) {
+            const int q = n / C, c = n - q * C;  // q: 0 (2i,2j) 1 (2i+1,2j) 2 (2i,2j+1) 3 (2i+1,2j+1)
+            const int hh = 2 * i + (q & 1), ww = 2 * j + (q >> 1);
+            if (hh < H && ww < W) v[k] = *reinterpret_cast<const float4*>(x + ((bt * H + hh) * W + ww) * ldx + c);
+        }
+        s += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+    }
+    const float mean = group_sum<L>(s) / (float)C4;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+        if ((k * L + sub) * 4 < C4) {
+            const float a = v[k].x - mean, b = v[k].y - mean, c = v[k].z - mean, d = v[k].w - mean;
+            q += (a * a + b * b) + (c * c + d * d);
+        }
+    }
+    const float rstd = rsqrtf(group_sum<L>(q) / (float)C4 + eps);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+        const int n = (k * L + sub) * 4;
+        if (n < C4) {
+            const float4 gg = *reinterpret_cast<const float4*>(g + n), bb = *reinterpret_cast<const float4*>(be + n);
+            uint2 o;
+            o.x = pack2bf((v[k].x - mean) * rstd * gg.x + bb.x, (v[k].y - mean) * rstd * gg.y + bb.y);
+            o.y = pack2bf((v[k].z - mean) * rstd * gg.z + bb.z, (v[k].w - mean) * rstd * gg.w + bb.w);
+            *reinterpret_cast<uint2*>(y + row * ldy + n) = o;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------
 // Final LayerNorm over every token, mean over the clip's tokens, classifier GEMV (fp32):
 // logits[b] = W . mean_n LN(x[b, n]) + bias  (torchvision SwinTransformer3d.forward:
@@ -507,6 +561,26 @@ int vc_patch_merge_layernorm(const float* x, int64_t ldx, int64_t B, int64_t T, 
     if (C <= 0 || 4 * C > 4096 || ldx < C || ldy < 4 * C)
         return fail(VC_ERR_INVALID_ARG, "vc_patch_merge_layernorm: bad C / leading dimension");
     const int64_t rows = B * T * ((H + 1) / 2) * ((W + 1) / 2);
+    const int64_t n4 = C;  // float4 pieces per merged row (4C / 4)
+    if (C % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && n4 <= 512 &&
+        !(((uintptr_t)x | (uintptr_t)gamma | (uintptr_t)beta) & 15) && !((uintptr_t)y & 7)) {
+        int L = 64, V = n4 <= 192 ? 3 : n4 <= 256 ? 4 : n4 <= 384 ? 6 : 8;
+        for (int l = 8; l <= 32; l *= 2)
+            if (n4 <= 4 * l) { L = l; V = n4 <= 3 * l ? 3 : 4; break; }
+        const unsigned nb = (unsigned)((rows * L + 255) / 256);
+#define VC_PM_GRP(LL, VV)                                                                                       \
+    patch_merge_ln_grp_kernel<LL, VV><<<nb, 256, 0, stream>>>(x, ldx, B, (int)T, (int)H, (int)W, (int)C, gamma, \
+                                                               beta, eps, y, ldy)
+        if (L == 8) { if (V == 3) VC_PM_GRP(8, 3); else VC_PM_GRP(8, 4); }
+        else if (L == 16) { if (V == 3) VC_PM_GRP(16, 3); else VC_PM_GRP(16, 4); }
+        else if (L == 32) { if (V == 3) VC_PM_GRP(32, 3); else VC_PM_GRP(32, 4); }
+        else if (V == 3) VC_PM_GRP(64, 3);
+        else if (V == 4) VC_PM_GRP(64, 4);
+        else if (V == 6) VC_PM_GRP(64, 6);
+        else VC_PM_GRP(64, 8);
+#undef VC_PM_GRP
+        return check_launch("vc_patch_merge_layernorm");
+    }
     patch_merge_ln_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, stream>>>(x, ldx, B, (int)T, (int)H, (int)W, (int)C,
                                                                         gamma, beta, eps, y, ldy);
     return check_launch("vc_patch_merge_layernorm");

@@ -74,7 +74,7 @@ def test_im2col_bit_exact(B, T, H):
 
 
 # ------------------------------------------------------------------------- layernorm
-@pytest.mark.parametrize("M,D", [(7, 768), (25344, 768), (25097, 768), (8193, 768), (3, 256), (130, 1024), (5, 128), (9, 96), (33, 384)])
+@pytest.mark.parametrize("M,D", [(7, 768), (25344, 768), (25097, 768), (8193, 768), (3, 256), (130, 1024), (5, 128), (9, 96), (33, 384), (1001, 96), (515, 192), (7, 64), (3, 200)])
 def test_layernorm(M, D):
     g = torch.Generator().manual_seed(M)
     x = torch.randn(M, D, generator=g) * 3 + 1

@@ -99,3 +99,40 @@ def test_swin3d_batch_invariance():
     full = m(video).clone()
     one = m(video[1:2].contiguous()).clone()
     assert torch.equal(full[1:2], one)
+
+
+@pytest.mark.parametrize("B,grid,C", [(2, (3, 7, 7), 96), (1, (2, 5, 6), 192), (1, (2, 4, 3), 384), (2, (1, 3, 3), 12),
+                                      (1, (2, 3, 5), 6), (1, (1, 2, 2), 768)])
+def test_patch_merge_layernorm(B, grid, C):
+    """PatchMerging (torchvision swin_transformer.py _patch_merging_pad: 2x2 concat in the order
+    (0,0) (1,0) (0,1) (1,1), zero padding of odd H / W) + LayerNorm(4C) vs torch.  C % 4 == 0 runs
+    the register kernel (L lanes per merged row: C = 12 / 96 / 192 / 384 -> L 8 / 32 / 64 / 64);
+    C = 6 (not a multiple of 4) and C = 768 (> 512 float4 per row) the scalar fallback."""
+    from vclip_amd import ops
+    T, H, W = grid
+    g = torch.Generator().manual_seed(C + H)
+    x = torch.randn(B, T, H, W, C, generator=g) * 2 + 0.5
+    gam = 1 + 0.1 * torch.randn(4 * C, generator=g)
+    bet = 0.1 * torch.randn(4 * C, generator=g)
+    xp = torch.nn.functional.pad(x, (0, 0, 0, W % 2, 0, H % 2))
+    cat = torch.cat([xp[:, :, 0::2, 0::2], xp[:, :, 1::2, 0::2], xp[:, :, 0::2, 1::2], xp[:, :, 1::2, 1::2]], -1)
+    want = torch.nn.functional.layer_norm(cat, (4 * C,), gam, bet, 1e-5).reshape(-1, 4 * C)
+    out = torch.zeros(want.shape[0], 4 * C, dtype=torch.bfloat16, device=DEV)
+    ops.patch_merge_layernorm(x.reshape(-1, C).to(DEV), B, grid, C, gam.to(DEV), bet.to(DEV), 1e-5, out)
+    err = (out.float().cpu() - want).abs().max().item()
+    assert err <= 1e-2 * max(1.0, want.abs().max().item()), err
+
+
+@pytest.mark.parametrize("M,D", [(1001, 96), (77, 192), (130, 384), (9, 768), (33, 40), (17, 1000)])
+def test_layernorm_f32_out(M, D):
+    """f32-output LayerNorm (Swin patch_embed.norm into the residual stream): grouped kernel for
+    D <= 384 (8 / 16 / 32 lanes per row), whole-wave kernel above."""
+    from vclip_amd import ops
+    g = torch.Generator().manual_seed(M + D)
+    x = torch.randn(M, D, generator=g) * 3 + 1
+    gam = 1 + 0.1 * torch.randn(D, generator=g)
+    bet = 0.1 * torch.randn(D, generator=g)
+    y = torch.zeros(M, D, device=DEV)
+    ops.layernorm_f32(x.to(DEV), gam.to(DEV), bet.to(DEV), 1e-5, y)
+    want = torch.nn.functional.layer_norm(x, (D,), gam, bet, 1e-5)
+    np.testing.assert_allclose(y.cpu().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
