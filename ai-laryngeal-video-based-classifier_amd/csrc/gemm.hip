@@ -1037,12 +1037,18 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
 static int pick_cfg(int64_t M, int64_t N, int64_t K, int epi) {
     const bool bf16_out = epi == VC_EPI_BIAS_BF16 || epi == VC_EPI_BIAS_GELU_TANH || epi == VC_EPI_BIAS_GELU_ERF ||
                           epi == VC_EPI_BIAS_RELU_BF16 || epi == VC_EPI_BIAS_GELU_TANH_SAVE;
-    if (bf16_out && M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && K >= 192 && N <= 8192 &&
-        (M / 256) * (N / 256) >= 64)
-        return 4;
     const int64_t t256 = (M / 256) * (N / 256);
-    if (M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && t256 >= 64 && t256 <= 256 && !(N <= 768 && K <= 768))
+    // exact-GELU outputs below ~4 rounds of 256x256 tiles: cfg 5 (Swin-T stages 2-4 fc1,
+    // tools/tune_swin_gemm.py: 28 vs 36 us at 12544x1536x384, 46 vs 55 at 6400x3072x768)
+    if (bf16_out && M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && K >= 192 && N <= 8192 && t256 >= 64 &&
+        !(epi == VC_EPI_BIAS_GELU_ERF && t256 < 1024))
+        return 4;
+    // (t256 >= 128: Swin-T stage 4 fc2, 6400x768x3072 with 75 tiles, runs 51 us on cfg 5 vs 79 on cfg 3)
+    if (M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && t256 >= 128 && t256 <= 256 && !(N <= 768 && K <= 768))
         return 3;
+    // narrow f32-residual outputs (N <= 384): 64x128 tiles, twice the workgroups to hide the
+    // residual round trip (Swin-T proj / fc2: 44 vs 46 us at 200704x128x128, 14 vs 16 at 12544x384x384)
+    if (epi == VC_EPI_BIAS_RESID_F32 && N <= 384 && M % 64 == 0) return 7;
     return 5;
 }
 
