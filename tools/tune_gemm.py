@@ -47,7 +47,7 @@ def main():
         for c in [int(x) for x in a.cfgs.split(",")]:
             # c >= 10: timing ablations of cfg c % 10 (bias epilogue only; wrong results)
             bm, bn = {0: (256, 128), 1: (128, 128), 2: (128, 256), 3: (256, 256), 4: (256, 256),
-                      5: (128, 128), 6: (256, 256)}[c % 10 if c >= 10 else c]
+                      5: (128, 128), 6: (256, 256), 7: (64, 128)}[c % 10 if c >= 10 else c]
             if (c in (4, 6) and "f32" in epi) or (c >= 10 and epi != "bias"):
                 continue
             if M % bm or N % bn:
