@@ -1,6 +1,6 @@
 """Forward (or train-step) time of one libvclip.so build, for process-level A/B of two builds
 on the same box (tools/ab_build.sh makes ab/<name>/libvclip.so from a git revision):
-  python tools/ab_lib.py <path/to/libvclip.so> [fwd|train|timesformer|swin] [steps]
+  python tools/ab_lib.py <path/to/libvclip.so> [fwd|train|timesformer|swin|resnet3d] [steps]
 The library is bound before any op runs, so every kernel of the run comes from it."""
 import sys
 import time
@@ -27,6 +27,11 @@ elif mode == "swin":
     from vclip_amd.swin3d import create_model as swin_model
     from vclip_amd.weights import make_synthetic_video
     m = swin_model(model_size="tiny", device=dev)
+    pix = torch.from_numpy(make_synthetic_video(B, 32, 224, seed=1)).to(dev)
+elif mode == "resnet3d":
+    from vclip_amd.resnet3d import create_model as r3d_model
+    from vclip_amd.weights import make_synthetic_video
+    m = r3d_model(device=dev)
     pix = torch.from_numpy(make_synthetic_video(B, 32, 224, seed=1)).to(dev)
 else:
     m = create_model(num_frames=32, device=dev)
