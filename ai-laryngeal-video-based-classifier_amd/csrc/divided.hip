@@ -241,15 +241,28 @@ __global__ void __launch_bounds__(256) tsf_add_ln_kernel(float* __restrict__ x, 
     const int p = (r - 1) / T, t = (r - 1) % T;  // meaningful for r >= 1
     const int64_t frow = (b * T + t) * (1 + P) + 1 + p;  // frame-layout row of a patch token
     float4 v[4];
+    uint2 yv[4];
     float s = 0.f;
+    // every load of the row (x and, for patch rows, y) is issued before the first add / store
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int n = (i * 64 + lane) * 4;
+        v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        yv[i] = make_uint2(0u, 0u);
+        if (n < D) {
+            v[i] = *reinterpret_cast<const float4*>(x + row * ldx + n);
+            if (r > 0) yv[i] = *reinterpret_cast<const uint2*>(y + (mode == 0 ? row : frow) * ldy + n);
+        }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int n = (i * 64 + lane) * 4;
         if (n < D) {
-            float4 a = *reinterpret_cast<const float4*>(x + row * ldx + n);
+            float4 a = v[i];
             if (r > 0) {
-                const float4 d = ld_bf16x4(y + (mode == 0 ? row : frow) * ldy + n);
-                a.x += d.x; a.y += d.y; a.z += d.z; a.w += d.w;
+                const uint2 u = yv[i];
+                a.x += bf2f((unsigned short)(u.x & 0xffff)); a.y += bf2f((unsigned short)(u.x >> 16));
+                a.z += bf2f((unsigned short)(u.y & 0xffff)); a.w += bf2f((unsigned short)(u.y >> 16));
             } else if (mode == 1) {
                 float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
                 for (int tt = 0; tt < T; ++tt) {
