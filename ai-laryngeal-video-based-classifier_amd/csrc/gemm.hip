@@ -74,6 +74,48 @@ __device__ __forceinline__ void store_tile(const v16f (&acc)[MI][NI], int64_t mb
                                            const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
                                            const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride,
                                            int64_t goff) {
+    // plain bf16 outputs on 16-B aligned rows: lane-pair swap -> one 16-B store per two column
+    // groups (cdna_hip_programming.md T21, as in the persistent kernel's epilogue) instead of
+    // four 8-B stores per 32 columns
+    constexpr bool PLAIN_BF16 = EPI == VC_EPI_BIAS_BF16 || EPI == VC_EPI_BIAS_GELU_TANH ||
+                                EPI == VC_EPI_BIAS_GELU_ERF || EPI == VC_EPI_BIAS_RELU_BF16;
+    if constexpr (PLAIN_BF16) {
+        if ((ldo & 7) == 0 && ((uintptr_t)out & 15) == 0) {
+#pragma unroll
+            for (int i = 0; i < MI; ++i) {
+                uint16_t* orow = reinterpret_cast<uint16_t*>(out) + (mb + i * 32 + r) * ldo;
+#pragma unroll
+                for (int j = 0; j < NI; ++j) {
+                    unsigned pk[4][2];
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const float4 bb = *reinterpret_cast<const float4*>(bias + nb + j * 32 + g * 8 + h * 4);
+                        float v0 = acc[i][j][4 * g + 0] + bb.x, v1 = acc[i][j][4 * g + 1] + bb.y;
+                        float v2 = acc[i][j][4 * g + 2] + bb.z, v3 = acc[i][j][4 * g + 3] + bb.w;
+                        if (EPI == VC_EPI_BIAS_GELU_TANH) {
+                            v0 = gelu_tanh(v0); v1 = gelu_tanh(v1); v2 = gelu_tanh(v2); v3 = gelu_tanh(v3);
+                        } else if (EPI == VC_EPI_BIAS_GELU_ERF) {
+                            v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+                        } else if (EPI == VC_EPI_BIAS_RELU_BF16) {
+                            v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+                        }
+                        pk[g][0] = pack2bf(v0, v1);
+                        pk[g][1] = pack2bf(v2, v3);
+                    }
+#pragma unroll
+                    for (int g = 0; g < 4; g += 2) {
+                        // lower half: cols 8g..8g+7 (own g | upper's g); upper half: 8g+8..8g+15
+                        auto s0 = __builtin_amdgcn_permlane32_swap(pk[g][0], pk[g + 1][0], false, false);
+                        auto s1 = __builtin_amdgcn_permlane32_swap(pk[g][1], pk[g + 1][1], false, false);
+                        uint4 v;
+                        v.x = s0[0]; v.y = s1[0]; v.z = s0[1]; v.w = s1[1];
+                        *reinterpret_cast<uint4*>(orow + nb + j * 32 + g * 8 + h * 8) = v;
+                    }
+                }
+            }
+            return;
+        }
+    }
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
         const int64_t m = mb + i * 32 + r;
