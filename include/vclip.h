@@ -146,6 +146,12 @@ int vc_layernorm_f32_bf16(const float* x, int64_t ldx, int64_t M, int64_t D,
 int vc_attention_fwd(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, int64_t head_dim,
                      float scale, int q_prescaled, uint16_t* out, int64_t ldo, hipStream_t stream);
 
+/* Test build of vc_attention_fwd's deferred running max (q not prescaled): re-bases the max on
+ * EVERY key tile instead of only when a lane's partial row sum exceeds 2^8.  Must agree with
+ * vc_attention_fwd to rounding (tests/test_kernels_gpu.py threshold sweep). */
+int vc_attention_fwd_rebase_always(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, float scale,
+                                   uint16_t* out, int64_t ldo, hipStream_t stream);
+
 /* LayerNorm f32 -> f32 (any D; y may alias nothing of x).  Swin's patch_embed.norm (torchvision
  * PatchEmbed3d, eps 1e-5) whose output is the fp32 residual stream. */
 int vc_layernorm_f32(const float* x, int64_t ldx, int64_t M, int64_t D, const float* gamma, const float* beta,

@@ -288,9 +288,8 @@ def test_attention_score_scales(mag):
 @pytest.mark.parametrize("mag", [4.0, 12.0])
 def test_attention_rebase_threshold_sweep(mag):
     """The shipped partial-sum threshold (re-base only when a lane's row sum exceeds 2^8)
-    and the always-re-base build (ablation 16, threshold 0) must agree to rounding, and
+    and the always-re-base build (vc_attention_fwd_rebase_always, threshold 0) must agree to rounding, and
     both match the fp32 reference (cdna_hip_programming.md rule 26)."""
-    import ctypes
     B, S, H = 2, 777, 2
     g = torch.Generator().manual_seed(int(mag * 10) + 7)
     rows = (B - 1) * S + (S + 63) // 64 * 64 + 64
@@ -304,12 +303,8 @@ def test_attention_rebase_threshold_sweep(mag):
     o_all = torch.zeros_like(o_ship)
     ops().attention(dq, B, S, H, scale, o_ship)
     from vclip_amd import _lib as L
-    lib = L.load()
-    f = lib.vc_attention_fwd_ablation
-    f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_float,
-                  ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
-    assert f(dq.data_ptr(), 3 * H * 64, B, S, H, scale, o_all.data_ptr(), H * 64, 16,
-             torch.cuda.current_stream().cuda_stream) == 0
+    L.call("vc_attention_fwd_rebase_always", dq.data_ptr(), 3 * H * 64, B, S, H, scale, o_all.data_ptr(), H * 64,
+           torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     a, b = o_ship[: B * S].float().cpu(), o_all[: B * S].float().cpu()
     assert torch.isfinite(a).all() and torch.isfinite(b).all()
