@@ -4,33 +4,25 @@
 // softmax(scale * Q K^T) V per (clip, head) over all S = 1 + 16*14*14 = 3137 tokens,
 // without materialising the S x S scores (472 MB fp32 per clip per layer in the eager path).
 //
-// gfx950 structure: an 8-wave PING-PONG workgroup (cdna_hip_programming.md Appendix B
-// "Fused attention prefill"; MI355X_MICROARCH.md "vector-instruction ISSUE cost").
-//   * workgroup = 8 waves = 256 queries of one (clip, head), one workgroup per CU; each wave
-//     owns 32 query rows.  Waves w and w+4 share a SIMD (waves go to SIMDs cyclically), so
-//     every SIMD holds one wave of group A (waves 0-3) and one of group B (waves 4-7);
-//   * per 64-key tile a wave runs two PHASES separated by workgroup barriers:
-//       M(t): the MFMA phase — S'(t+1) = K(t+1).Q'^T - m (8 MFMAs) and O^T += V(t)^T.P(t)^T
-//             (8 MFMAs), operands read from LDS;
-//       V(t): the VALU phase — softmax of tile t+1: 32 exp2 per lane, the row sum, the
-//             overflow check and 16 cvt_pk to bf16 P;
-//     group B runs one phase behind group A, so on every SIMD one wave's 16 MFMAs run while
-//     its partner's ~110 VALU issue into the gaps (an MFMA holds vector issue for 8 of its 32
-//     cycles).  At head_dim 64 the softmax VALU of a tile is ~90 % of its MFMA time, which two
-//     waves in the SAME phase cannot overlap (round 1's 4-wave kernel: MFMA busy 47 %);
-//   * K/V tiles (8 KiB each) arrive by LDS-DMA (global_load_lds_dwordx4, one 1-KiB piece of K
-//     and one of V per wave per tile) into a 4-slot ring, tile j issued 4 phases before its
-//     first use, retired by counted vmcnt waits before the phase barriers; K image
-//     XOR-swizzled for ds_read_b128, V image swizzled for the ds_read_b64_tr_b16 transpose;
-//   * swapped QK^T (S^T = K . Q^T): a query's scores live in ONE lane column;
-//   * the running max enters the QK^T MFMA chain as its initial accumulator (scale*log2 e
-//     folded into Q'), so the common path per score is exp2 + add + cvt: no per-tile max.
-//     Every P >= 0, so a lane's partial row sum <= LIM = 2^8 bounds every P of the tile (an
-//     overflow shows as inf/NaN); only when that fails does the tile recompute S' from the
-//     K tile still in LDS and re-base m on its exact max (defer-max, T13; O already holds
-//     every earlier tile at the old base, and no P is pending, so O and l scale exactly once);
-//   * S'^T accumulators become the B operand of O^T = V^T . P^T after one cvt_pk per pair;
-//     P never touches LDS;
+// gfx950 structure (cdna_hip_programming.md Appendix B "Fused attention prefill"):
+//   * workgroup = 4 waves; each wave owns 32 query rows of one (clip, head); two
+//     workgroups per CU (two waves per SIMD);
+//   * K/V tiles of 64 keys staged by LDS-DMA (global_load_lds, issued from inline asm so
+//     hipcc's LDS wait counts stay exact) into a 4-slot ring; a counted vmcnt retires only
+//     the tile needed next, one raw s_barrier per tile; K image XOR-swizzled for ds_read_b128,
+//     V image swizzled for the ds_read_b64_tr_b16 transpose read;
+//   * swapped QK^T (S^T = K . Q^T): a query's scores live in ONE lane column, so the row
+//     max needs one cross-half exchange and only on the rare re-base path;
+//   * the running row max enters the QK^T MFMA chain as its initial accumulator
+//     (S' = Q'.K^T - m, with scale*log2 e folded into Q'), so the common path per score is
+//     exp2 + a packed add (row sum) + cvt: no per-tile max.  Since every P >= 0, a lane's
+//     partial row sum <= LIM = 2^8 bounds each P of the tile by 2^8 (an overflow shows as
+//     inf/NaN); only when that fails does the tile recompute S' and re-base m on its exact
+//     max (defer-max, cdna_hip_programming.md T13, with the sum as the detector);
+//   * S'^T accumulator registers feed P.V directly as the B operand of O^T = V^T . P^T
+//     (§3 "An accumulator tile as the next MFMA's operand"); P never touches LDS;
+//   * software pipeline inside each wave: the QK^T MFMAs of tile t+1 are issued before
+//     tile t's softmax, so the MFMA pipe runs them while the VALU does exp2/sum/cvt;
 //   * output rows widened to 16-byte stores with v_permlane32_swap (T21).
 #include "common.hpp"
 
@@ -42,16 +34,15 @@ constexpr int AK = 64;                      // keys per tile
 constexpr int KV_TILE_BYTES = AK * 64 * 2;  // 8 KiB (one of K or V)
 constexpr int KV_SLOT = 2 * KV_TILE_BYTES;  // K then V
 constexpr int NSLOT = 4;
-constexpr int AQ = 256;                     // queries per workgroup (8 waves x 32)
 constexpr float LIM = 256.0f;  // partial row-sum bound (P <= 2^8) before the running max is re-based
 
 __device__ __forceinline__ int kswz(int r, int c) { return c ^ ((r >> 1) & 7); }
 __device__ __forceinline__ int vswz(int r, int c) { return c ^ (((r >> 1) & 1) << 2); }
 
-// LDS-DMA of one 16-byte piece per lane: saddr form (64-bit wave-uniform base in SGPRs +
-// 32-bit per-lane offset, so the per-tile address advance is scalar arithmetic).  hipcc never
+// LDS-DMA of one 16-byte piece per lane, saddr form: 64-bit wave-uniform base in SGPRs +
+// 32-bit per-lane offset, so the per-tile address advance is scalar arithmetic.  hipcc never
 // uses m0 in this kernel (checked in the ISA: every m0 access is one of these asm blocks), so
-// m0 is declared clobbered instead of saved / restored.
+// m0 is declared clobbered instead of saved / restored (2 SALU fewer per piece, +0.8 %).
 __device__ __forceinline__ void adma16s(const void* sbase, uint32_t voff, uint32_t lds_addr) {
     asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
                  :
@@ -72,15 +63,24 @@ __device__ __forceinline__ void attn_sync() {
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// REBASE_ALWAYS: the LIM = 0 build of the threshold test (re-base on every tile,
-// cdna_hip_programming.md rule 26: must agree with the shipped build to rounding).
+// One 4-wave workgroup = 128 queries of one (clip, head); each wave owns 32 query rows, two
+// workgroups per CU (two waves per SIMD, 256 VGPRs each).  Measured alternatives (DESIGN.md
+// §5): 64 queries per wave (every K/V fragment feeding two MFMAs) needs ~330 registers and ran
+// 1.3x slower; an 8-wave ping-pong workgroup (MFMA and softmax phases of the two waves of a
+// SIMD offset by a barrier, tools/experiments/attention_pingpong.hip.txt) ran 295-330 us vs
+// 264 us; split-half softmax, K-fragment prefetch, a 5-slot ring and a P.V lag were neutral
+// to 8.5 % slower (round 1).
+// REBASE_ALWAYS: the LIM = 0 build of the threshold test (re-base the running max on every
+// tile, cdna_hip_programming.md rule 26: must agree with the shipped build to rounding).
 // WLSE: also store the base-2 log-sum-exp of each query's scores, lse[(b*H + h)*S + q] =
 // m + log2(l) (running max and row sum), from which the backward kernels recompute P.
-template <bool REBASE_ALWAYS, bool WLSE, int DIAG = 0>
-__global__ void __launch_bounds__(512, 1)
-attn_fwd_pp_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, float c_log2,
-                   uint16_t* __restrict__ out, int64_t ldo, float* __restrict__ lse,
-                   unsigned long long* __restrict__ stamps = nullptr) {
+template <bool REBASE_ALWAYS, bool WLSE>
+__global__ void __launch_bounds__(256, 2)
+attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, float c_log2,
+                    uint16_t* __restrict__ out, int64_t ldo, float* __restrict__ lse) {
+    constexpr int QB = 1;
+    constexpr int AQ = 128;  // query rows per workgroup (4 waves x 32)
+    constexpr int NS = NSLOT;
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     // XCD-aware order: the workgroups of one (clip, head) share its K/V; give every XCD a
@@ -96,98 +96,48 @@ attn_fwd_pp_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, f
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, h = lane >> 5;
-    // Pair the waves by the SIMD they actually run on (HW_ID.SIMD_ID, bits 5:4): of the waves
-    // sharing a SIMD, the lower-numbered leads (group A) and the other trails one phase
-    // (group B).  The wave -> SIMD placement is the dispatcher's; correctness does not depend
-    // on it (every wave runs the same barrier count whichever group it joins), only the overlap.
-    {
-        const int simd = __builtin_amdgcn_s_getreg((1 << 11) | (4 << 6) | 4);
-        if (lane == 0) reinterpret_cast<volatile int*>(smem + 3 * KV_SLOT)[wave] = simd;
-    }
-    __syncthreads();
-    bool lead;
-    {
-        const volatile int* ids = reinterpret_cast<const volatile int*>(smem + 3 * KV_SLOT);
-        const int mine = ids[wave];
-        int before = 0;
-        for (int w = 0; w < wave; ++w) before += ids[w] == mine;
-        lead = (__builtin_amdgcn_readfirstlane(before) & 1) == 0;
-    }
 
     const int64_t tok0 = (int64_t)b * S;
+    const uint16_t* qbase = qkv + hh * 64;
     const uint16_t* kbase = qkv + (int64_t)H * 64 + hh * 64 + tok0 * ld;
     const uint16_t* vbase = qkv + (int64_t)2 * H * 64 + hh * 64 + tok0 * ld;
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem);
 
     // ---- Q'^T fragments (B operand of S^T = K.Q'^T): lane holds Q'[q][d = 16kk + 8h + 0..7]
-    const int q = qblk * AQ + wave * 32 + r;
-    const int qc = q < S ? q : S - 1;
-    v8bf qf[4];
-    {
-        const uint16_t* qrow = qkv + hh * 64 + (tok0 + qc) * ld + 8 * h;
-        v8s raw[4];
+    v8bf qf[QB][4];
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) raw[kk] = *reinterpret_cast<const v8s*>(qrow + 16 * kk);
+    for (int qb = 0; qb < QB; ++qb) {
+        const int q = qblk * AQ + (wave * QB + qb) * 32 + r;
+        const int qc = q < S ? q : S - 1;
+        const uint16_t* qrow = qbase + (tok0 + qc) * ld + 8 * h;
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) qf[kk] = __builtin_bit_cast(v8bf, raw[kk]);  // producer folded the scale
-        if (c_log2 != 1.0f) {
+        for (int kk = 0; kk < 4; ++kk) {
+            const v8s raw = *reinterpret_cast<const v8s*>(qrow + 16 * kk);
+            if (c_log2 == 1.0f) {
+                qf[qb][kk] = __builtin_bit_cast(v8bf, raw);  // producer folded the scale into q
+            } else {
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) qf[kk][j] = (__bf16)(bf2f((unsigned short)raw[kk][j]) * c_log2);
+                for (int j = 0; j < 8; ++j) qf[qb][kk][j] = (__bf16)(bf2f((unsigned short)raw[j]) * c_log2);
+            }
         }
     }
 
-    // staging: wave w fills rows 8w..8w+7 of the K image and of the V image (one 1-KiB piece
-    // each); per-lane byte offsets are loop-invariant, the tile advance goes into the scalar base
-    const int srow = wave * 8 + (lane >> 3), spc = lane & 7;
-    const uint32_t ko = (uint32_t)(srow * ld + kswz(srow, spc) * 8) * 2;
-    const uint32_t vo = (uint32_t)(srow * ld + vswz(srow, spc) * 8) * 2;
-    const int ntiles = (S + AK - 1) / AK;
-    // tiles are staged in order 0, 1, 2, ...: one running scalar source pointer each for K, V
-    const uint16_t* ksrc = kbase;
-    const uint16_t* vsrc = vbase;
-    const int64_t tile_stride = (int64_t)AK * ld;
-    auto stage = [&](int t) __attribute__((always_inline)) {
-        const uint32_t s = lds0 + (t % NSLOT) * KV_SLOT + wave * 8 * 128;
-        adma16s(ksrc, ko, __builtin_amdgcn_readfirstlane(s));
-        adma16s(vsrc, vo, __builtin_amdgcn_readfirstlane(s + KV_TILE_BYTES));
-        ksrc += tile_stride;
-        vsrc += tile_stride;
-    };
-    // Global phase phi (the same for every wave: phases end at workgroup barriers).  A wave
-    // issues its DMA pieces in its MFMA phase, after the MFMAs (the wave is idle while the
-    // matrix pipe drains them): tile j >= 3 at phase 2j - 5 by group A (its M(j-3)) and at
-    // 2j - 4 by group B (its M(j-3)), into the slot of tile j - 4, whose last reader (B's
-    // V(j-5), reading the fragments of its M(j-4)) finished at phase 2j - 7.  Tile j is first
-    // read in phase 2j - 2 (A's V(j-2) reads K(j) for M(j-1)), so before the barrier that
-    // ends phase phi every wave retires its pieces of all tiles j <= (phi + 3) / 2.
-    const int lag = __builtin_amdgcn_readfirstlane(lead ? 5 : 4);
-    auto maybe_stage = [&](int phi) __attribute__((always_inline)) {
-        if (((phi + lag) & 1) == 0) {
-            const int j = (phi + lag) >> 1;
-            if (j < ntiles) stage(j);
-        }
-    };
-    // DIAGNOSTIC stamps (STAMP build only): s_memtime into LDS past the ring, copied out at the end
-    unsigned long long* lstamp = reinterpret_cast<unsigned long long*>(smem + NSLOT * KV_SLOT);
-    auto stamp = [&](int phi, int k) __attribute__((always_inline)) {
-        if constexpr ((DIAG & 1) != 0) {
-            const unsigned long long tt = __builtin_amdgcn_s_memtime();
-            if (lane == 0 && phi >= -1 && phi < 63) lstamp[(wave * 64 + phi + 1) * 4 + k] = tt;
-        }
-    };
-    auto end_phase = [&](int phi) __attribute__((always_inline)) {
-        stamp(phi, 2);
-        const int issued = min(ntiles - 1, max(2, (phi + lag) >> 1));  // tiles 0-2: the prologue
-        const int needed = min(ntiles - 1, (phi + 3) >> 1);
-        const int ahead = issued - needed;  // tiles this wave may leave in flight (2 pieces each)
-        if (ahead >= 2) attn_wait_vm<4>();
-        else if (ahead == 1) attn_wait_vm<2>();
-        else attn_wait_vm<0>();
-        attn_sync();
-        stamp(phi, 3);
+    // staging: 64 key rows of K and V (8 rows x 128 B per wave-instruction), wave w: rows 16w..16w+15;
+    // per-lane byte offsets are loop-invariant, the tile advance goes into the scalar base
+    const int srow = wave * 16 + (lane >> 3), spc = lane & 7;
+    const uint32_t ko0 = (uint32_t)(srow * ld + kswz(srow, spc) * 8) * 2;
+    const uint32_t ko1 = (uint32_t)((srow + 8) * ld + kswz(srow + 8, spc) * 8) * 2;
+    const uint32_t vo0 = (uint32_t)(srow * ld + vswz(srow, spc) * 8) * 2;
+    const uint32_t vo1 = (uint32_t)((srow + 8) * ld + vswz(srow + 8, spc) * 8) * 2;
+    auto stage = [&](int t) {
+        const uint32_t s = lds0 + (t % NS) * KV_SLOT + wave * 16 * 128;
+        const uint16_t* kt = kbase + (int64_t)t * AK * ld;
+        const uint16_t* vt = vbase + (int64_t)t * AK * ld;
+        adma16s(kt, ko0, __builtin_amdgcn_readfirstlane(s));
+        adma16s(kt, ko1, __builtin_amdgcn_readfirstlane(s + 8 * 128));
+        adma16s(vt, vo0, __builtin_amdgcn_readfirstlane(s + KV_TILE_BYTES));
+        adma16s(vt, vo1, __builtin_amdgcn_readfirstlane(s + KV_TILE_BYTES + 8 * 128));
     };
 
     // per-lane constant LDS byte offsets (relative to a ring slot):
@@ -208,55 +158,66 @@ attn_fwd_pp_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, f
         voff[db] = KV_TILE_BYTES + ra * 128 + vswz(ra, col >> 3) * 16 + (col & 7) * 2;
     }
 
-    v16f o[2];      // O^T[d][q], d-blocks 0/1
-    v16f minit;     // -running max of this lane's query, broadcast: initial accumulator of S'
-    float l_run = 0.f;  // this lane's partial row sum (its 32 keys of every tile)
+    v16f o[QB][2];   // O^T[d][q] per query block, d-blocks 0/1
+    v16f minit[QB];  // -running max of this lane's query, broadcast: initial accumulator of S'
+    v2f l_run[QB];   // packed partial row sums
 #pragma unroll
-    for (int e = 0; e < 16; ++e) { o[0][e] = 0.f; o[1][e] = 0.f; minit[e] = 0.f; }
+    for (int qb = 0; qb < QB; ++qb) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) { o[qb][0][e] = 0.f; o[qb][1][e] = 0.f; minit[qb][e] = 0.f; }
+        l_run[qb] = v2f{0.f, 0.f};
+    }
 
-    // ---- S'^T = K . Q'^T - m for the two 32-key blocks of a tile (-m enters as the C operand)
-    auto qk_mfma = [&](const char* slot, v16f (&sc)[2]) __attribute__((always_inline)) {
+    // ---- S'^T = K . Q'^T - m for QB query blocks x two 32-key blocks of tile t; each K
+    //      fragment feeds QB MFMAs (-m enters as the C operand of the first k-step)
+    auto qk_mfma = [&](const char* slot, v16f (&sc)[QB][2]) {
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
             const v8bf k0 = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(slot + koff[kk]));
             const v8bf k1 = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(slot + koff[kk] + 4096));
-            sc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[kk], kk == 0 ? minit : sc[0], 0, 0, 0);
-            sc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[kk], kk == 0 ? minit : sc[1], 0, 0, 0);
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb) {
+                sc[qb][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[qb][kk], kk == 0 ? minit[qb] : sc[qb][0], 0, 0, 0);
+                sc[qb][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[qb][kk], kk == 0 ? minit[qb] : sc[qb][1], 0, 0, 0);
+            }
         }
     };
     //      keys beyond S masked to -inf (last tile only)
-    auto qk = [&](const char* slot, int t, v16f (&sc)[2]) __attribute__((always_inline)) {
+    auto qk = [&](const char* slot, int t, v16f (&sc)[QB][2]) {
         qk_mfma(slot, sc);
         const int kv0 = t * AK;
         if (kv0 + AK > S) {
 #pragma unroll
+            for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int key = (e & 3) + 8 * (e >> 2) + 4 * h;
+                    if (kv0 + key >= S) sc[qb][0][e] = -INFINITY;
+                    if (kv0 + 32 + key >= S) sc[qb][1][e] = -INFINITY;
+                }
+        }
+    };
+    // P = exp2(S') in place; this lane's partial row sums (32 keys) as packed pairs
+    auto expsum = [&](v16f (&sc)[QB][2], v2f (&ps)[QB]) {
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {
+#pragma unroll
             for (int e = 0; e < 16; ++e) {
-                const int key = (e & 3) + 8 * (e >> 2) + 4 * h;
-                if (kv0 + key >= S) sc[0][e] = -INFINITY;
-                if (kv0 + 32 + key >= S) sc[1][e] = -INFINITY;
+                sc[qb][0][e] = __builtin_amdgcn_exp2f(sc[qb][0][e]);
+                sc[qb][1][e] = __builtin_amdgcn_exp2f(sc[qb][1][e]);
             }
+            v2f u[8];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                u[j] = v2f{sc[qb][0][4 * j], sc[qb][0][4 * j + 1]} + v2f{sc[qb][0][4 * j + 2], sc[qb][0][4 * j + 3]};
+                u[4 + j] = v2f{sc[qb][1][4 * j], sc[qb][1][4 * j + 1]} + v2f{sc[qb][1][4 * j + 2], sc[qb][1][4 * j + 3]};
+            }
+            ps[qb] = ((u[0] + u[1]) + (u[2] + u[3])) + ((u[4] + u[5]) + (u[6] + u[7]));
         }
     };
-    // P = exp2(S') in place; this lane's partial row sum (32 keys) by scalar adds (packed f32
-    // adds are an anti-lever beside MFMAs, MI355X_MICROARCH.md "price of one filler")
-    auto expsum = [&](v16f (&sc)[2]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            if constexpr ((DIAG & 4) == 0) {
-                sc[0][e] = __builtin_amdgcn_exp2f(sc[0][e]);
-                sc[1][e] = __builtin_amdgcn_exp2f(sc[1][e]);
-            }
-        }
-        float u[8];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            u[j] = (sc[0][4 * j] + sc[0][4 * j + 1]) + (sc[0][4 * j + 2] + sc[0][4 * j + 3]);
-            u[4 + j] = (sc[1][4 * j] + sc[1][4 * j + 1]) + (sc[1][4 * j + 2] + sc[1][4 * j + 3]);
-        }
-        return ((u[0] + u[1]) + (u[2] + u[3])) + ((u[4] + u[5]) + (u[6] + u[7]));
-    };
-    // exact row max of S (both lane halves)
-    auto rowmax_of = [&](const v16f (&sc)[2]) __attribute__((always_inline)) {
+    // exact row max of S (both lane halves); plain fmaxf, not inline-asm v_max3: the
+    // hazard recognizer must see these reads of fresh MFMA results to pad them
+    auto rowmax_of = [&](const v16f (&sc)[2]) {
         float m0 = fmaxf(sc[0][0], sc[1][0]), m1 = fmaxf(sc[0][1], sc[1][1]);
 #pragma unroll
         for (int e = 2; e < 16; e += 2) {
@@ -266,214 +227,174 @@ attn_fwd_pp_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, f
         const float m = fmaxf(m0, m1);
         return fmaxf(m, __shfl_xor(m, 32, 64));
     };
-    // bf16 P fragments: (key block kb, k-step s2) = regs 8s2..8s2+7 of block kb
-    v8bf pf[2][2];
-    auto to_bf16 = [&](const v16f (&sc)[2]) __attribute__((always_inline)) {
+
+    const int ntiles = (S + AK - 1) / AK;
+    // Static wave priority for one of the two workgroups that share a CU (MI355X_MICROARCH.md
+    // "Two waves per SIMD" item 4: priority outranks age, so one fixed winner instead of the
+    // age-based arbitration flipping between them): initially co-resident blocks are L and
+    // L + 256, so prio 1 by bit 8 of L.  +1.2 % (three interleaved A/Bs at B = 8: 259/263,
+    // 256/259, 258/261 us; priority by block-id bit 3 instead: neutral).
+    if ((L >> 8) & 1) __builtin_amdgcn_s_setprio(1);
+    stage(0);
+    if (ntiles > 1) stage(1);
+    if (ntiles > 2) stage(2);
+    if (ntiles > 2) attn_wait_vm<4>();  // tiles 0 and 1 resident, 2 in flight
+    else attn_wait_vm<0>();
+    attn_sync();
+    // tile 0 establishes the running max m
+    v16f scur[QB][2];
+    qk(smem, 0, scur);
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+        const float m = rowmax_of(scur[qb]);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) { scur[qb][0][e] -= m; scur[qb][1][e] -= m; minit[qb][e] = -m; }
+    }
+
+    // one iteration: S' of tile t+1 is computed (MFMA) while tile t's softmax runs on the
+    // VALU, then O += P_t V_t.  Ring of NSLOT = 4: slot t (V_t), slot t+1 (K_{t+1}) are
+    // read, t+2 lands, t+3 is staged into the slot read one iteration ago.
+    // NEXT: 0 = tile t+1 is a full tile, 1 = tile t+1 may be partial (masked), 2 = t is last.
+    // In the unrolled main loop the slots are compile-time constants, so every LDS address is
+    // a loop-invariant per-lane VGPR plus an immediate offset.
+    auto iter = [&](auto next_c, const char* slot, const char* nslot, int t) {
+        constexpr int NEXT = decltype(next_c)::value;
+        if (t + NS - 1 < ntiles) stage(t + NS - 1);
+        v16f snext[QB][2];
+        if constexpr (NEXT == 0) qk_mfma(nslot, snext);
+        else if constexpr (NEXT == 1) qk(nslot, t + 1, snext);
+
+        // ---- online softmax with a deferred running max: scores are relative to m already.
+        //      Every P is >= 0, so a partial row sum <= LIM bounds every P of the tile by
+        //      LIM (an overflow shows up as inf); only when it fails is tile t recomputed
+        //      against an exact re-based max.
+        v2f ps[QB];
+        expsum(scur, ps);
+        bool grow = false;
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) grow = grow || !(ps[qb][0] + ps[qb][1] <= (REBASE_ALWAYS ? -1.0f : LIM));
+        if (__any(grow)) {
+            qk(slot, t, scur);
+#pragma unroll
+            for (int qb = 0; qb < QB; ++qb) {
+                const float delta = fmaxf(rowmax_of(scur[qb]), 0.f);
+                const float alpha = __builtin_amdgcn_exp2f(-delta);
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    scur[qb][0][e] -= delta;
+                    scur[qb][1][e] -= delta;
+                    o[qb][0][e] *= alpha;
+                    o[qb][1][e] *= alpha;
+                    minit[qb][e] -= delta;
+                }
+                if constexpr (NEXT != 2) {
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) { snext[qb][0][e] -= delta; snext[qb][1][e] -= delta; }
+                }
+                l_run[qb] *= alpha;
+            }
+            expsum(scur, ps);
+        }
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) l_run[qb] += ps[qb];
+
+        // ---- O^T += V^T . P^T: P fragment of (key block kb, k-step s2) = regs 8s2..8s2+7;
+        //      every V^T fragment read from LDS feeds QB MFMAs
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2)
+            for (int s2 = 0; s2 < 2; ++s2) {
+                v8bf pf[QB];
 #pragma unroll
-                for (int jj = 0; jj < 8; ++jj) pf[kb][s2][jj] = (__bf16)sc[kb][8 * s2 + jj];
-        // keep the conversions in the VALU phase (LLVM would sink them to their MFMA uses)
-        asm volatile("" ::"v"(pf[0][0]), "v"(pf[0][1]), "v"(pf[1][0]), "v"(pf[1][1]));
-    };
-    // softmax of a tile whose S' (relative to the running max) sits in sc; kslot / tt = that
-    // tile's ring slot and index, for the rare exact re-base
-    auto softmax = [&](v16f (&sc)[2], const char* kslot, int tt) __attribute__((always_inline)) {
-        float ps = expsum(sc);
-        // the fragment reads issued just before (prefetch) interleave with the exp2 / sum VALU:
-        // one LDS read per two VALU, so neither the LDS queue nor the VALU stalls the wave
+                for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
-        for (int i = 0; i < 24; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-        }
-        if (__any(!(ps <= (REBASE_ALWAYS ? -1.0f : LIM)))) {
-            qk(kslot, tt, sc);
-            const float delta = fmaxf(rowmax_of(sc), 0.f);
-            const float alpha = __builtin_amdgcn_exp2f(-delta);
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                sc[0][e] -= delta;
-                sc[1][e] -= delta;
-                o[0][e] *= alpha;
-                o[1][e] *= alpha;
-                minit[e] -= delta;
-            }
-            l_run *= alpha;
-            ps = expsum(sc);
-        }
-        l_run += ps;
-        to_bf16(sc);
-    };
-    // ---- K and V^T fragments of the next MFMA phase, read from LDS at the START of the VALU
-    //      phase before it (64 VGPRs): they land while the softmax runs, so the MFMA phase
-    //      issues its 16 MFMAs back to back (it is the only MFMA issuer on its SIMD then)
-    v8bf kf[4][2];
-    v8bf vf[2][2][2];
-    auto prefetch = [&](const char* vslot, const char* kslot, auto with_k) __attribute__((always_inline)) {
-        if constexpr ((DIAG & 2) != 0) { asm volatile("" : "+v"(kf[0][0]), "+v"(vf[0][0][0])); return; }
-        if (with_k) {
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {
-                kf[kk][0] = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(kslot + koff[kk]));
-                kf[kk][1] = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(kslot + koff[kk] + 4096));
-            }
-        }
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2)
+                    for (int jj = 0; jj < 8; ++jj) pf[qb][jj] = (__bf16)scur[qb][kb][8 * s2 + jj];
 #pragma unroll
                 for (int db = 0; db < 2; ++db) {
-                    const char* pa = vslot + voff[db] + (kb * 32 + 16 * s2) * 128;
+                    const char* pa = slot + voff[db] + (kb * 32 + 16 * s2) * 128;
                     v4s va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)pa);
                     v4s vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(pa + 8 * 128));
                     v8s vv;
                     vv[0] = va[0]; vv[1] = va[1]; vv[2] = va[2]; vv[3] = va[3];
                     vv[4] = vb[0]; vv[5] = vb[1]; vv[6] = vb[2]; vv[7] = vb[3];
-                    vf[kb][s2][db] = __builtin_bit_cast(v8bf, vv);
-                }
-    };
-
-    // ---- prologue: tiles 0..2 in flight, tiles 0 and 1 resident
-    stage(0);
-    if (ntiles > 1) stage(1);
-    if (ntiles > 2) stage(2);
-    end_phase(-1);
-    int phi = 0;
-    v16f sc[2];
-    // phase 0: both groups form S'(0); A also establishes the running max and P(0).
-    // B does its softmax of tile 0 in phase 1, beside A's first MFMA phase.
-    qk(smem, 0, sc);
-    auto softmax0 = [&]() __attribute__((always_inline)) {
-        prefetch(smem, smem + KV_SLOT, ntiles > 1);
-        __builtin_amdgcn_sched_barrier(0);
-        const float m = rowmax_of(sc);
+                    const v8bf vf = __builtin_bit_cast(v8bf, vv);
 #pragma unroll
-        for (int e = 0; e < 16; ++e) { sc[0][e] -= m; sc[1][e] -= m; minit[e] = -m; }
-        l_run = expsum(sc);
-        to_bf16(sc);
-    };
-    if (lead) softmax0();
-    end_phase(phi++);
-    if (!lead) {
-        softmax0();
-        end_phase(phi++);
-    }
+                    for (int qb = 0; qb < QB; ++qb) {
+                        o[qb][db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[qb], o[qb][db], 0, 0, 0);
+                    }
+                }
+            }
 
-    // M(t): QK^T of tile t+1 (NEXT 0: a full tile, 1: may be partial, 2: none) and P(t).V(t)
-    // from the prefetched fragments
-    auto mphase = [&](auto next_c, int t) __attribute__((always_inline)) {
-        constexpr int NEXT = decltype(next_c)::value;
-        stamp(phi, 0);
-        if constexpr ((DIAG & 8) != 0) {
-            asm volatile("" : "+v"(sc[0]), "+v"(sc[1]), "+v"(o[0]), "+v"(o[1]) : "v"(kf[0][0]), "v"(vf[0][0][0]), "v"(pf[0][0]));
-        } else {
+        // ---- tile t+2 must be resident for the next iteration's K read (t+3 may stay in
+        //      flight); the barrier also retires every wave's reads of slot t before the
+        //      next iteration stages t+4 into it
+        if (t + 2 < ntiles) {
+            if (t + 3 < ntiles) attn_wait_vm<4>();
+            else attn_wait_vm<0>();
+            attn_sync();
+        }
         if constexpr (NEXT != 2) {
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {
-                sc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kk][0], qf[kk], kk == 0 ? minit : sc[0], 0, 0, 0);
-                sc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kk][1], qf[kk], kk == 0 ? minit : sc[1], 0, 0, 0);
-            }
+            for (int qb = 0; qb < QB; ++qb) { scur[qb][0] = snext[qb][0]; scur[qb][1] = snext[qb][1]; }
         }
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-                for (int db = 0; db < 2; ++db)
-                    o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[kb][s2][db], pf[kb][s2], o[db], 0, 0, 0);
-        }
-        stamp(phi, 1);
-        maybe_stage(phi);
-        if constexpr (NEXT == 1) {
-            const int kv0 = (t + 1) * AK;
-            if (kv0 + AK > S) {
-#pragma unroll
-                for (int e = 0; e < 16; ++e) {
-                    const int key = (e & 3) + 8 * (e >> 2) + 4 * h;
-                    if (kv0 + key >= S) sc[0][e] = -INFINITY;
-                    if (kv0 + 32 + key >= S) sc[1][e] = -INFINITY;
-                }
-            }
-        }
-        end_phase(phi++);
-    };
-    // V(t): fragments of M(t+1) (V(t+1), K(t+2) if it exists), then the softmax of tile t+1
-    auto vphase = [&](auto with_k, const char* kslot, const char* k2slot, int t) __attribute__((always_inline)) {
-        stamp(phi, 0);
-        prefetch(kslot, k2slot, with_k);
-        stamp(phi, 1);
-        softmax(sc, kslot, t + 1);
-        end_phase(phi++);
     };
 
     using full_c = std::integral_constant<int, 0>;
     const int nfull = S / AK;  // full tiles
     int t = 0;
-    // unrolled by the ring size so every LDS address is a per-lane VGPR plus an immediate
-    for (; t + 4 < nfull; t += NSLOT) {  // iterations t..t+3 all have a full next tile
-        mphase(full_c{}, t);
-        vphase(std::true_type{}, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, t);
-        mphase(full_c{}, t + 1);
-        vphase(std::true_type{}, smem + 2 * KV_SLOT, smem + 3 * KV_SLOT, t + 1);
-        mphase(full_c{}, t + 2);
-        vphase(std::true_type{}, smem + 3 * KV_SLOT, smem + 0 * KV_SLOT, t + 2);
-        mphase(full_c{}, t + 3);
-        vphase(std::true_type{}, smem + 0 * KV_SLOT, smem + 1 * KV_SLOT, t + 3);
+    for (; t + 5 <= nfull; t += NS) {  // iterations t..t+3 all have a full next tile
+        iter(full_c{}, smem + 0 * KV_SLOT, smem + 1 * KV_SLOT, t);
+        iter(full_c{}, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, t + 1);
+        iter(full_c{}, smem + 2 * KV_SLOT, smem + 3 * KV_SLOT, t + 2);
+        iter(full_c{}, smem + 3 * KV_SLOT, smem + 0 * KV_SLOT, t + 3);
     }
-    for (; t < ntiles; ++t) {  // at most 5 iterations: runtime slots, mask-checked next tile
-        if (t + 1 < ntiles) {
-            mphase(std::integral_constant<int, 1>{}, t);
-            vphase(t + 2 < ntiles, smem + ((t + 1) % NSLOT) * KV_SLOT, smem + ((t + 2) % NSLOT) * KV_SLOT, t);
-        } else {
-            mphase(std::integral_constant<int, 2>{}, t);
-        }
-    }
-    if (lead) end_phase(phi++);  // B's extra (leading) phase: equal barrier counts
-    if constexpr ((DIAG & 1) != 0) {
-        if (wg < 64 && lane == 0) {
-            for (int i = 0; i < 64 * 4; ++i) stamps[(wg * 8 + wave) * 64 * 4 + i] = lstamp[wave * 64 * 4 + i];
-            stamps[64 * 8 * 64 * 4 + wg * 8 + wave] = lead;
-        }
+    for (; t < ntiles; ++t) {  // at most NS + 1 iterations: runtime slot, mask-checked next tile
+        const char* slot = smem + (t % NS) * KV_SLOT;
+        const char* nslot = smem + ((t + 1) % NS) * KV_SLOT;
+        if (t + 1 < ntiles) iter(std::integral_constant<int, 1>{}, slot, nslot, t);
+        else iter(std::integral_constant<int, 2>{}, slot, nslot, t);
     }
 
     // ---- normalise and store O[q][d]: reg 4g+e of block db -> d = 32db + 8g + 4h + e;
     //      lane pairs (h=0/1) swap halves so each lane stores 16 contiguous bytes
-    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-    const float inv = 1.0f / l_tot;
-    if constexpr (WLSE) {
-        if (h == 0 && q < S) lse[(int64_t)bh * S + q] = -minit[0] + __log2f(l_tot);
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb) {
+        const int q = qblk * AQ + (wave * QB + qb) * 32 + r;
+        const int qc = q < S ? q : S - 1;
+        const float l_own = l_run[qb][0] + l_run[qb][1];
+        const float l_tot = l_own + __shfl_xor(l_own, 32, 64);
+        const float inv = 1.0f / l_tot;
+        if constexpr (WLSE) {
+            if (h == 0 && q < S) lse[(int64_t)bh * S + q] = -minit[qb][0] + __log2f(l_tot);
+        }
+        unsigned pk[2][4][2];
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                pk[db][g][0] = pack2bf(o[qb][db][4 * g + 0] * inv, o[qb][db][4 * g + 1] * inv);
+                pk[db][g][1] = pack2bf(o[qb][db][4 * g + 2] * inv, o[qb][db][4 * g + 3] * inv);
+            }
+        uint16_t* orow = out + (tok0 + qc) * ldo + hh * 64;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int g = 0; g < 4; g += 2) {
+                auto x0 = __builtin_amdgcn_permlane32_swap(pk[db][g][0], pk[db][g + 1][0], false, false);
+                auto x1 = __builtin_amdgcn_permlane32_swap(pk[db][g][1], pk[db][g + 1][1], false, false);
+                uint4 v;
+                v.x = x0[0]; v.y = x1[0]; v.z = x0[1]; v.w = x1[1];
+                if (q < S) *reinterpret_cast<uint4*>(orow + db * 32 + g * 8 + h * 8) = v;
+            }
     }
-    unsigned pk[2][4][2];
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            pk[db][g][0] = pack2bf(o[db][4 * g + 0] * inv, o[db][4 * g + 1] * inv);
-            pk[db][g][1] = pack2bf(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv);
-        }
-    uint16_t* orow = out + (tok0 + qc) * ldo + hh * 64;
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-        for (int g = 0; g < 4; g += 2) {
-            auto x0 = __builtin_amdgcn_permlane32_swap(pk[db][g][0], pk[db][g + 1][0], false, false);
-            auto x1 = __builtin_amdgcn_permlane32_swap(pk[db][g][1], pk[db][g + 1][1], false, false);
-            uint4 v;
-            v.x = x0[0]; v.y = x1[0]; v.z = x0[1]; v.w = x1[1];
-            if (q < S) *reinterpret_cast<uint4*>(orow + db * 32 + g * 8 + h * 8) = v;
-        }
 }
 
 template <bool REBASE_ALWAYS, bool WLSE>
 static void launch_attn(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, float c_log2, uint16_t* out,
                         int64_t ldo, hipStream_t stream, float* lse = nullptr) {
-    dim3 grid((unsigned)((S + AQ - 1) / AQ), (unsigned)(B * H));
-    attn_fwd_pp_kernel<REBASE_ALWAYS, WLSE><<<grid, 512, NSLOT * KV_SLOT, stream>>>(qkv, ld, (int)S, (int)H, c_log2,
-                                                                                  out, ldo, lse);
+    dim3 grid((unsigned)((S + 127) / 128), (unsigned)(B * H));
+    attn_fwd_d64_kernel<REBASE_ALWAYS, WLSE><<<grid, 256, NSLOT * KV_SLOT, stream>>>(qkv, ld, (int)S, (int)H, c_log2,
+                                                                                   out, ldo, lse);
 }
 
 }  // namespace vc
@@ -488,8 +409,7 @@ static int attn_checks(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, in
         return fail(VC_ERR_INVALID_ARG, "vc_attention_fwd: bad shape / leading dimension");
     if ((((uintptr_t)qkv) | ((uintptr_t)out)) & 15)
         return fail(VC_ERR_INVALID_ARG, "vc_attention_fwd: pointers must be 16-byte aligned");
-    if (B * H > 65535 || S > (1 << 24) || (int64_t)64 * ld * 2 >= (int64_t)1 << 31)
-        return fail(VC_ERR_INVALID_ARG, "vc_attention_fwd: grid / tile offsets too large");
+    if (B * H > 65535 || S > (1 << 24)) return fail(VC_ERR_INVALID_ARG, "vc_attention_fwd: grid too large");
     return 0;
 }
 
@@ -519,34 +439,4 @@ extern "C" int vc_attention_fwd_rebase_always(const uint16_t* qkv, int64_t ld, i
     if (int rc = attn_checks(qkv, ld, B, S, H, 64, out, ldo)) return rc;
     launch_attn<true, false>(qkv, ld, B, S, H, scale * 1.4426950408889634f, out, ldo, stream);
     return check_launch("vc_attention_fwd_rebase_always");
-}
-
-// DIAGNOSTIC (temporary): per-phase s_memtime stamps of the first 64 workgroups; diag bits
-// 2 / 4 / 8 drop the fragment reads / exp2 / MFMAs (timing only, wrong results).
-template <int D>
-static void launch_diag(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, uint16_t* out, int64_t ldo,
-                        unsigned long long* stamps, hipStream_t stream) {
-    dim3 grid((unsigned)((S + AQ - 1) / AQ), (unsigned)(B * H));
-    const int lds = NSLOT * KV_SLOT + ((D & 1) ? 16384 : 0);
-    (void)hipFuncSetAttribute((const void*)attn_fwd_pp_kernel<false, false, D>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              lds);
-    attn_fwd_pp_kernel<false, false, D><<<grid, 512, lds, stream>>>(qkv, ld, (int)S, (int)H, 1.0f, out, ldo, nullptr,
-                                                                    stamps);
-}
-extern "C" int vc_attention_fwd_diag(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H,
-                                     uint16_t* out, int64_t ldo, unsigned long long* stamps, int diag,
-                                     hipStream_t stream) {
-    if (int rc = attn_checks(qkv, ld, B, S, H, 64, out, ldo)) return rc;
-    switch (diag) {
-        case 0: launch_diag<0>(qkv, ld, B, S, H, out, ldo, stamps, stream); break;
-        case 1: launch_diag<1>(qkv, ld, B, S, H, out, ldo, stamps, stream); break;
-        case 2: launch_diag<2>(qkv, ld, B, S, H, out, ldo, stamps, stream); break;
-        case 4: launch_diag<4>(qkv, ld, B, S, H, out, ldo, stamps, stream); break;
-        case 8: launch_diag<8>(qkv, ld, B, S, H, out, ldo, stamps, stream); break;
-        case 6: launch_diag<6>(qkv, ld, B, S, H, out, ldo, stamps, stream); break;
-        case 12: launch_diag<12>(qkv, ld, B, S, H, out, ldo, stamps, stream); break;
-        case 14: launch_diag<14>(qkv, ld, B, S, H, out, ldo, stamps, stream); break;
-        default: return fail(VC_ERR_INVALID_ARG, "bad diag");
-    }
-    return check_launch("vc_attention_fwd_diag");
 }
