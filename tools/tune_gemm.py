@@ -33,11 +33,17 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--cfgs", default="0,2,3,4")
+    ap.add_argument("--square", type=int, default=0, help="also time an MxNxK = n^3 bias GEMM")
+    ap.add_argument("--no-attn", action="store_true")
     a = ap.parse_args()
+    global M, SHAPES
+    if a.square:
+        SHAPES = [(f"sq{a.square}", a.square, a.square, "bias")] + SHAPES
     dev = "cuda"
     g = torch.Generator(device=dev).manual_seed(0)
     res = {}
     for name, N, K, epi in SHAPES:
+        M = a.square if name.startswith("sq") else 25344
         A = torch.randn(M, K, device=dev, generator=g).bfloat16()
         W = (torch.randn(N, K, device=dev, generator=g) * 0.05).bfloat16()
         b = torch.randn(N, device=dev, generator=g) * 0.1
@@ -68,7 +74,10 @@ def main():
             print(f"{name:7s} N={N:5d} K={K:5d} {k:26s} {med * 1e3:8.1f} us  {fl / med / 1e9:7.1f} TF/s (min {fl / ts[0] / 1e9:7.1f})",
                   flush=True)
             res[(name, k)] = med
+    if a.no_attn:
+        return
     # attention
+    M = 25344
     B, S, H = 8, 3137, 12
     rows = M
     qkv = torch.randn(rows, 3 * H * 64, device=dev, generator=g).bfloat16()
