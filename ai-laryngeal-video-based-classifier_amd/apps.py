@@ -262,7 +262,10 @@ def _device():
     return torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def _batches(fam, split, sampler, args, device, shuffle=False):
+def _batches(fam, split, sampler, args, device, shuffle=False, logger=None):
+    """Batches of (model input, labels).  A clip that cannot be decoded becomes the reference
+    dataset's gray placeholder (127) with a warning (dataset.py:294-381), so one bad video does
+    not end the epoch."""
     paths, labels = split
     order = list(range(len(paths)))
     if shuffle:
@@ -271,8 +274,14 @@ def _batches(fam, split, sampler, args, device, shuffle=False):
         ids = order[s:s + args.batch_size]
         xs = []
         for i in ids:
-            src = video_io.open_video(paths[i])
-            fr = torch.from_numpy(fam.load_clip(src, sampler, paths[i], args.num_frames)).to(device)
+            try:
+                src = video_io.open_video(paths[i])
+                clip = fam.load_clip(src, sampler, paths[i], args.num_frames)
+            except Exception as e:  # noqa: BLE001 - reference: log, placeholder, continue
+                if logger is not None:
+                    logger.warning(f"Failed to load {paths[i]}: {str(e)}; using a placeholder clip")
+                clip = np.full((args.num_frames, 224, 224, 3), 127, np.uint8)
+            fr = torch.from_numpy(clip).to(device)
             xs.append(fam.to_model_input(fr.unsqueeze(0), args.num_frames))
         yield torch.cat(xs), torch.tensor([labels[i] for i in ids], device=device)
 
@@ -289,8 +298,12 @@ def _load_weights(model, path, logger, fam):
 def evaluate(fam, model, split, sampler, args, device, class_names, exp_dir, method, logger):
     model.eval()
     probs, preds, labels = [], [], []
-    for x, y in _batches(fam, split, sampler, args, device):
-        p = torch.softmax(fam.logits(model, x).float(), dim=1)
+    for x, y in _batches(fam, split, sampler, args, device, logger=logger):
+        try:
+            p = torch.softmax(fam.logits(model, x).float(), dim=1)
+        except Exception as e:  # noqa: BLE001 - evaluator.py: log and skip the batch
+            logger.error(f"Error in test batch: {str(e)}")
+            continue
         probs.append(p.cpu().numpy())
         preds += p.argmax(1).tolist()
         labels += y.tolist()
@@ -344,23 +357,31 @@ def run_main(fam_name, argv=None):
         for epoch in range(args.epochs):
             model.train()
             tl, tc, tn = 0.0, 0, 0
-            for x, y in _batches(fam, splits["train"], samplers["train"], args, device, shuffle=True):
-                opt.zero_grad()
-                logits = fam.logits(model, x)
-                loss = crit(logits, y)
-                loss.backward()
-                opt.step()
-                tl += float(loss) * len(y)
-                tc += int((logits.argmax(1) == y).sum())
-                tn += len(y)
+            for x, y in _batches(fam, splits["train"], samplers["train"], args, device, shuffle=True, logger=logger):
+                try:  # trainer.py:133-167: a failing batch is logged and skipped
+                    opt.zero_grad()
+                    logits = fam.logits(model, x)
+                    loss = crit(logits, y)
+                    loss.backward()
+                    opt.step()
+                    tl += float(loss) * len(y)
+                    tc += int((logits.argmax(1) == y).sum())
+                    tn += len(y)
+                except Exception as e:  # noqa: BLE001
+                    logger.error(f"Error in training batch: {str(e)}")
+                    continue
             model.eval()
             vl, vc, vn = 0.0, 0, 0
             with torch.no_grad():
-                for x, y in _batches(fam, splits["val"], samplers["val"], args, device):
-                    logits = fam.logits(model, x)
-                    vl += float(crit(logits, y)) * len(y)
-                    vc += int((logits.argmax(1) == y).sum())
-                    vn += len(y)
+                for x, y in _batches(fam, splits["val"], samplers["val"], args, device, logger=logger):
+                    try:  # trainer.py:192-210
+                        logits = fam.logits(model, x)
+                        vl += float(crit(logits, y)) * len(y)
+                        vc += int((logits.argmax(1) == y).sum())
+                        vn += len(y)
+                    except Exception as e:  # noqa: BLE001
+                        logger.error(f"Error in validation batch: {str(e)}")
+                        continue
             tr_loss, tr_acc = tl / max(tn, 1), tc / max(tn, 1)
             va_loss, va_acc = vl / max(vn, 1), vc / max(vn, 1)
             for k, v in (("train_loss", tr_loss), ("train_acc", tr_acc), ("val_loss", va_loss), ("val_acc", va_acc)):

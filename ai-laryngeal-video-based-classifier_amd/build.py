@@ -42,6 +42,19 @@ def sources():
     return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
 
 
+def source_hash() -> str:
+    """16-hex digest of every source libvclip.so is built from (kernels, headers, the C-ABI):
+    bench.py stamps it on its JSON line and only cites profiles/ summaries of the same build."""
+    import hashlib
+    h = hashlib.sha256()
+    deps = sources() + sorted(glob.glob(os.path.join(CSRC, "*.hpp"))) + sorted(glob.glob(os.path.join(INCLUDE, "*.h")))
+    for d in deps:
+        h.update(os.path.basename(d).encode())
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def needs_build() -> bool:
     if not os.path.exists(LIB_PATH):
         return True

@@ -44,6 +44,11 @@ class AdamW(torch.optim.Optimizer):
         n = p0.untyped_storage().nbytes() // 4
         if g0.untyped_storage().nbytes() // 4 != n:
             return None
+        # the single launch updates the WHOLE flat buffer: only when the parameters cover it
+        # exactly (a subset, e.g. fine-tuning the head only, goes tensor by tensor)
+        offs = {p.storage_offset() for p in params}
+        if len(offs) != len(params) or sum(p.numel() for p in params) != n:
+            return None
         flat_p = torch.empty(0, dtype=torch.float32, device=p0.device).set_(p0.untyped_storage(), 0, (n,))
         flat_g = torch.empty(0, dtype=torch.float32, device=p0.device).set_(g0.untyped_storage(), 0, (n,))
         return flat_p, flat_g
@@ -60,7 +65,9 @@ class AdamW(torch.optim.Optimizer):
             flat = self._flat_view_set(params) if len(self.param_groups) == 1 else None
             if flat is not None:
                 fp, fg = flat
-                key = (fp.data_ptr(), fg.data_ptr(), fp.numel())
+                # keyed by the layout (size, parameter count), not by device pointers, so the moments
+                # survive a state_dict round trip or a re-flattened model of the same layout
+                key = (fp.numel(), len(params))
                 st = self.state.setdefault("flat", {})
                 if st.get("key") != key:
                     st.update(key=key, exp_avg=torch.zeros_like(fp), exp_avg_sq=torch.zeros_like(fp), step=0)

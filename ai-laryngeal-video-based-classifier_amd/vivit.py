@@ -192,11 +192,21 @@ class VivitForVideoClassification(torch.nn.Module):
                 self._gscratch = torch.zeros_like(self._gflat)
             target = self._gscratch
 
+        stages = []
+
         def ready(stage, start, end):
             if not accumulate:
                 for h in self.grad_ready_hooks:
                     h(stage, start, end, target)
+            else:
+                stages.append((stage, start, end))
 
+        if accumulate and self.grad_ready_hooks:
+            g0 = self._gflat.untyped_storage().data_ptr()
+            if any(p.grad is not None and p.grad.untyped_storage().data_ptr() != g0 for p in params):
+                raise RuntimeError("gradient accumulation with grad_ready_hooks (data-parallel all-reduce) needs "
+                                   "every .grad to be the model's own flat-buffer view; zero_grad(set_to_none=True) "
+                                   "or leave .grad as the backward set it")
         eng.backward(dlogits, target, ready)
         lay = self._layout
         if not accumulate:
@@ -209,6 +219,12 @@ class VivitForVideoClassification(torch.nn.Module):
                 p.grad = lay.view(self._gflat, n).copy_(g)
             else:
                 p.grad.add_(g)
+        # accumulated gradients: the hooks (e.g. GradAllReduce) see the summed flat buffer, stage
+        # by stage in backward order once the sum is complete -- as DDP reduces the accumulated
+        # .grad on every backward (the average of (mean + local) is mean + mean)
+        for stage, start, end in stages:
+            for h in self.grad_ready_hooks:
+                h(stage, start, end, self._gflat)
 
     def _weights_version(self):
         from . import vivit_train

@@ -35,44 +35,62 @@ ATTN_IO_BYTES_PER_CLIP = 3137 * 768 * 2 * 4  # q,k,v read + o written once, bf16
 PEAK_BF16_TFLOPS = 2500.0       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 
 
-def _newest(pattern: str):
-    """Newest committed profile matching profiles/<pattern> by round and version number
-    (r01_v10 after r01_v7: a natural sort, not a string sort)."""
+def _build_id():
+    from vclip_amd.build import source_hash
+    return source_hash()
+
+
+def _same_build(pattern: str):
+    """Newest committed profiles/<pattern> summary whose "build" (vclip_amd.build.source_hash of
+    the sources it was measured on) is THIS tree's build, or None: a roofline line never cites
+    counters of another build (tools/collect_profiles.py writes the field)."""
     import glob
     import re
-    fs = glob.glob(os.path.join(ROOT, "profiles", pattern))
-    key = lambda f: [int(x) for x in re.findall(r"\d+", os.path.basename(f))]  # noqa: E731
-    return max(fs, key=key) if fs else None
+    me = _build_id()
+    fs = []
+    for f in glob.glob(os.path.join(ROOT, "profiles", pattern)):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if d.get("build") == me:
+            fs.append((f, d))
+    key = lambda fd: [int(x) for x in re.findall(r"\d+", os.path.basename(fd[0]))]  # noqa: E731
+    return max(fs, key=key) if fs else (None, None)
 
 
 def measured_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/rNN_*traffic.json, written by tools/traffic.sh: rocprofv3 FETCH_SIZE x2 +
-    WRITE_SIZE passes over this same bench command).  None when no summary exists."""
-    f = _newest("r*_traffic.json")
+    """HBM bytes per launch of `kernel` (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes over this bench
+    command, tools/profile_round.sh -> profiles/rNN_*_traffic.json) for this build, else None."""
+    f, d = _same_build("r*_traffic.json")
     if not f:
-        return None, None
-    with open(f) as fh:
-        k = json.load(fh)["kernels"].get(kernel)
+        return None, "no profile of this build under profiles/"
+    k = d["kernels"].get(kernel)
     return (k["hbm_bytes_per_launch"] if k else None), os.path.relpath(f, ROOT)
 
 
-def measured_mfma_busy():
-    """Fraction of SIMD cycles the matrix pipe was busy during the attention kernel, from the
-    newest committed PMC summary (profiles/rNN_*attn_pmc.txt, written by tools/pmc_attn.sh):
-    SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs).  None without one."""
-    f = _newest("r*_attn_pmc.txt")
-    if not f:
-        return None, None
-    c = {}
-    for line in open(f):
-        parts = line.split()
-        if len(parts) >= 2:
-            c[parts[0]] = float(parts[1])
-    if "SQ_VALU_MFMA_BUSY_CYCLES" not in c or "GRBM_GUI_ACTIVE" not in c:
-        return None, None
-    busy = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * c["GRBM_GUI_ACTIVE"] / 8)
-    return round(busy, 4), os.path.relpath(f, ROOT)
+def measured_pmc(kernel: str):
+    """Per-launch PMC averages of `kernel` for this build (profiles/rNN_*_pmc.json), else None."""
+    f, d = _same_build("r*_pmc.json")
+    if not f or kernel not in d.get("kernels", {}):
+        return None, "no profile of this build under profiles/"
+    return d["kernels"][kernel], os.path.relpath(f, ROOT)
+
+
+def _spawn_world(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: re-run this command under torch.distributed.run
+    with N local ranks (one process per GPU, rendezvous on 127.0.0.1).  The parent touches no
+    GPU (the children initialise HIP); it waits and returns the launcher's exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
 
 
 def _dist():
@@ -160,28 +178,64 @@ def kernel_breakdown(model, step, clips, streams, n_steps):
     return out
 
 
-def cpu_baseline(model_cfg, n_clips, gpu_logits_fn):
-    """The fp32 CPU oracle (oracle/vivit_ref.py, a 'port' of the reference's HF ViViT
-    forward) on the host cores: a bounded sample of `n_clips` clips, one at a time
-    (B=1, as the reference's inference CLI runs).  Also returns the logit error of the
-    GPU path on the same clips."""
+def cpu_model() -> str:
+    """The host CPU's model name (/proc/cpuinfo), for the cpu_baseline record."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(model_cfg, n_clips, batch, gpu_logits_fn):
+    """The fp32 CPU oracle (oracle/vivit_ref.py, a 'port' of the reference's HF ViViT forward) on
+    the host cores, on bounded samples of the benchmark workload: `n_clips` clips
+    one at a time (B=1, as the reference's inference CLI runs) and one batch of `batch` clips (the
+    bench's own rank-0 batch, RandomState(1)).  The GPU logit error is measured on that batch, i.e.
+    on exactly the clips the timed region runs."""
     from oracle.vivit_ref import vivit_forward
     from vclip_amd.weights import make_synthetic_clips, make_vivit_weights
 
     sd = {k: torch.from_numpy(v) for k, v in make_vivit_weights(model_cfg, seed=0).items()}
-    pix = make_synthetic_clips(n_clips, model_cfg["num_frames"], model_cfg["image_size"], seed=1)
+    pix = make_synthetic_clips(batch, model_cfg["num_frames"], model_cfg["image_size"], seed=1)
     cores = torch.get_num_threads()
     with torch.no_grad():
         vivit_forward(sd, model_cfg, torch.from_numpy(pix[:1]))  # warm-up
         t0 = time.perf_counter()
-        ref = [vivit_forward(sd, model_cfg, torch.from_numpy(pix[i:i + 1])) for i in range(n_clips)]
-        dt = time.perf_counter() - t0
-    ref = torch.cat(ref).numpy()
+        for i in range(n_clips):
+            vivit_forward(sd, model_cfg, torch.from_numpy(pix[i:i + 1]))
+        dt1 = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        ref = vivit_forward(sd, model_cfg, torch.from_numpy(pix)).numpy()
+        dtb = time.perf_counter() - t0
     got = gpu_logits_fn(pix)
     err = float(np.abs(got - ref).max())
-    return {"value": n_clips / dt, "unit": "clips/s", "cores": cores, "kind": "port",
-            "sample": f"{n_clips} clips ViViT-B/16x2 32x224^2 fp32 forward, B=1 each, oracle/vivit_ref.py "
-                      f"(eager attention), torch CPU {cores} threads"}, err
+    return {"value": n_clips / dt1, "unit": "clips/s", "cores": cores, "kind": "port", "cpu": cpu_model(),
+            "value_b8": round(batch / dtb, 4),
+            "sample": f"ViViT-B/16x2 32x224^2 fp32 forward on the host: {n_clips} clips at B=1 (value) and one "
+                      f"B={batch} batch (value_b8) of the bench's own clips, oracle/vivit_ref.py (eager attention), "
+                      f"torch CPU {cores} threads"}, err
+
+
+def cpu_lstm_cfg1():
+    """BASELINE configs[0]: resnet50-2d-lstm forward, 8x224^2 clip, batch 1, on the CPU (the reference
+    path; resnet50-2d-lstm/src/models/model.py:36-60 restated in oracle/lstm_ref.py, torch's nn.LSTM)."""
+    from oracle.lstm_ref import lstm_forward
+    from vclip_amd.weights import make_resnet50_lstm_weights, make_synthetic_video
+    p = {k: torch.from_numpy(v) for k, v in make_resnet50_lstm_weights(seed=0).items()}
+    x = torch.from_numpy(make_synthetic_video(1, 8, 224, seed=1))
+    with torch.no_grad():
+        lstm_forward(p, x)
+        t0 = time.perf_counter()
+        lstm_forward(p, x)
+        dt = time.perf_counter() - t0
+    return {"value": round(1.0 / dt, 4), "unit": "clips/s", "ms_per_clip": round(dt * 1e3, 1),
+            "gflop_per_clip": 65.44, "cores": torch.get_num_threads(), "cpu": cpu_model(),
+            "workload": "ResNet50-LSTM forward, 8x224x224 clip, batch 1, fp32 (BASELINE configs[0])"}
 
 
 TRAIN_ATTN_GFLOP_PER_CLIP_LAYER = 2 * ATTN_GFLOP_PER_CLIP_LAYER  # dV, dP, dK, dQ (recompute of S not counted)
@@ -382,12 +436,28 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="clips per GPU per step (fwd 8, train 4)")
     ap.add_argument("--cpu-clips", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)  # CPU test of the spawn path
     a = ap.parse_args()
     if a.batch is None:
         a.batch = {"fwd": 8, "train": 4}.get(a.mode) or FAMILIES[a.mode][2]
     if a.cpu_clips is None:
-        a.cpu_clips = {"fwd": 3, "timesformer": 3}.get(a.mode, 1)
+        a.cpu_clips = {"fwd": 2, "timesformer": 3}.get(a.mode, 1)
 
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(_spawn_world(a.gpus))
+    if int(os.environ.get("WORLD_SIZE", "1")) != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={os.environ.get('WORLD_SIZE', '1')} "
+                         "(launch N ranks, or pass --gpus N without a launcher to spawn them)")
+    if a.launch_check:  # tests/test_dist_cpu.py: ranks rendezvous over gloo, no GPU touched
+        import torch.distributed as tdist
+        tdist.init_process_group("gloo")
+        dt = timed_loop(lambda: None, a.steps, a.warmup, tdist)
+        if tdist.get_rank() == 0:
+            print(json.dumps({"n_gpus": tdist.get_world_size(), "world_size_env": int(os.environ["WORLD_SIZE"]),
+                              "steps": a.steps, "seconds": dt}), flush=True)
+        tdist.barrier()
+        tdist.destroy_process_group()
+        return None
     dist, rank, world, local = _dist()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -442,7 +512,12 @@ def main():
         cpu = None
         logit_err = None
         traffic, traffic_src = measured_traffic("attn_fwd_d64_kernel")
-        mfma_busy, mfma_busy_src = measured_mfma_busy()
+        pmc, pmc_src = measured_pmc("attn_fwd_d64_kernel")
+        mfma_busy = valu_per_mfma = None
+        if pmc:
+            # SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs); VALU per MFMA
+            mfma_busy = round(pmc["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * pmc["GRBM_GUI_ACTIVE"] / 8), 4)
+            valu_per_mfma = round(pmc["SQ_INSTS_VALU"] / pmc["SQ_INSTS_MFMA"], 3)  # VALU count includes the MFMAs
         if world == 1 and not a.no_cpu_baseline:
             shape_cfg = dict(cfg.as_shape_cfg(), num_attention_heads=cfg.num_attention_heads,
                              layer_norm_eps=cfg.layer_norm_eps)
@@ -450,7 +525,8 @@ def main():
             def gpu_logits(p):
                 return model.forward_logits(torch.from_numpy(p).to(dev)).cpu().numpy().copy()
 
-            cpu, logit_err = cpu_baseline(shape_cfg, a.cpu_clips, gpu_logits)
+            cpu, logit_err = cpu_baseline(shape_cfg, a.cpu_clips, a.batch, gpu_logits)
+            cpu["lstm_cfg1"] = cpu_lstm_cfg1()
         out = {
             "metric": "clips/sec fwd ViViT-B 32x224^2 bf16",
             "value": round(value, 2),
@@ -473,8 +549,10 @@ def main():
                          "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes": ATTN_IO_BYTES_PER_CLIP * launch_clips, "avg_launch_ms": round(attn_ms, 4),
                          "flop_per_launch": f"{ATTN_GFLOP_PER_CLIP_LAYER:.2f} GF/clip x {launch_clips:g} clips",
-                         "streams": streams, "mfma_busy": mfma_busy, "mfma_busy_source": mfma_busy_src},
+                         "streams": streams, "mfma_busy": mfma_busy, "valu_per_mfma": valu_per_mfma,
+                         "pmc_source": pmc_src},
             "kernel_breakdown": breakdown,
+            "build": _build_id(),
             "model_tflops": round(model_tflops, 1),
             "model_frac_of_peak": round(model_tflops / PEAK_BF16_TFLOPS, 4),
             "cpu_baseline": cpu,

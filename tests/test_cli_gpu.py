@@ -105,3 +105,19 @@ def test_eval_and_inference_clis(dataset, tmp_path, fam, extra):
     res = run_inference(fam, ["--video_path", str(video), "--model_path", str(ck_path), "--log_dir",
                               str(tmp_path / "ilogs")] + extra)
     assert res["predicted_class"] in ("non-referral", "referral") and 0.5 <= res["confidence"] <= 1.0
+
+
+def test_vivit_main_skips_unreadable_clip(dataset, tmp_path):
+    """One undecodable video in the train split: the reference's dataset returns a gray placeholder and
+    its trainer logs a failing batch and continues (dataset.py:371-381, trainer.py:165-167); the run
+    must complete instead of aborting."""
+    import shutil
+    root = tmp_path / "data"
+    shutil.copytree(dataset, root)
+    (root / "train" / "referral" / "zz_broken.npy").write_bytes(b"\x00 not a clip")
+    from vclip_amd.apps import run_main
+    m, history, exp = run_main("vivit", ["--data_dir", str(root), "--log_dir", str(tmp_path / "logs"), "--model_dir",
+                                         str(tmp_path / "models"), "--epochs", "1", "--batch_size", "2"])
+    assert len(history["train_loss"]) == 1 and np.isfinite(history["train_loss"][0])
+    log = "".join(p.read_text() for p in Path(exp).rglob("*.log"))
+    assert "zz_broken.npy" in log

@@ -55,3 +55,22 @@ def test_timed_loop_max_over_ranks_gloo():
     assert abs(dts[0] - dts[1]) < 1e-9  # every rank reports the same (max) time
     assert dts[0] >= 5 * 0.04 * 0.95  # >= the slowest rank's 5 steps
     assert res[0][2] != res[1][2]  # ranks draw different clips
+
+
+def test_bench_gpus_flag_spawns_ranks():
+    """`bench.py --gpus N` without a launcher starts N ranks itself (torch.distributed.run on
+    127.0.0.1); a WORLD_SIZE that disagrees with --gpus is an error, not a silent 1-GPU run."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--launch-check"], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["n_gpus"] == 2 and out["world_size_env"] == 2
+    bad = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--launch-check"],
+                         capture_output=True, text=True, timeout=120, env=dict(env, WORLD_SIZE="1"))
+    assert bad.returncode != 0 and "WORLD_SIZE" in (bad.stderr + bad.stdout)

@@ -46,16 +46,25 @@ def test_ops_reject_cpu_tensors():
         ops.layernorm(x, torch.ones(768), torch.zeros(768), 1e-6, torch.zeros(256, 768, dtype=torch.bfloat16))
 
 
-def test_bench_reads_newest_profile(tmp_path, monkeypatch):
-    """bench.py's roofline traffic / MFMA-busy come from the newest committed PMC summary:
-    r01_v10 must win over r01_v7 (natural, not string, order) and r02 over r01."""
+def test_bench_cites_only_same_build_profiles(tmp_path, monkeypatch):
+    """bench.py's roofline traffic / PMC numbers come from the newest profiles/ summary measured on
+    THIS build (vclip_amd.build.source_hash): r01_v10 beats r01_v7 (natural order), a newer summary
+    of another build is ignored, and with none of this build the line says so instead of citing one."""
+    import json as _json
     import bench
     prof = tmp_path / "profiles"
     prof.mkdir()
+    me = bench._build_id()
+    k = {"kernels": {"attn_fwd_d64_kernel": {"hbm_bytes_per_launch": 1.0}}}
     for n in ("r01_v7_traffic.json", "r01_v10_traffic.json", "r01_v9_traffic.json"):
-        (prof / n).write_text("{}")
+        (prof / n).write_text(_json.dumps(dict(k, build=me)))
+    (prof / "r03_v1_traffic.json").write_text(_json.dumps(dict(k, build="another-build")))
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
-    assert bench._newest("r*_traffic.json").endswith("r01_v10_traffic.json")
-    (prof / "r02_v1_traffic.json").write_text("{}")
-    assert bench._newest("r*_traffic.json").endswith("r02_v1_traffic.json")
-    assert bench._newest("r*_nothing.json") is None
+    assert bench._same_build("r*_traffic.json")[0].endswith("r01_v10_traffic.json")
+    (prof / "r02_v1_traffic.json").write_text(_json.dumps(dict(k, build=me)))
+    assert bench.measured_traffic("attn_fwd_d64_kernel") == (1.0, "profiles/r02_v1_traffic.json")
+    assert bench._same_build("r*_nothing.json") == (None, None)
+    for n in list(prof.iterdir()):
+        if "another" not in n.read_text():
+            n.unlink()
+    assert bench.measured_traffic("attn_fwd_d64_kernel")[0] is None
