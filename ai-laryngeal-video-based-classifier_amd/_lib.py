@@ -51,6 +51,7 @@ SIGNATURES = {
     "vc_lstm_recurrence": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_i64, c_p, c_p], c_int),
     "vc_mlp_head": ([c_p, c_i64, c_i64, c_p, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p], c_int),
     "vc_resample_u8": ([c_p, c_i64, c_i64, c_i64, c_i64, c_int, c_i64, c_p, c_p, c_i64, c_p, c_p], c_int),
+    "vc_resize_linear_u8": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_int, c_p, c_p], c_int),
     "vc_video_transform": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p,
                             c_p, c_int, c_int, c_p, c_p], c_int),
     "vc_divided_add_layernorm": ([c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_int, c_p,

@@ -162,7 +162,7 @@ class Family:
         if isinstance(idx, tuple):
             idx = idx[0]
         if self.name in ("vivit", "timesformer"):
-            fr = video_io.resize_frames_224(src.read(idx))
+            fr = src.read(idx)  # resized to 224x224 on the GPU (to_model_input), as dataset.py:271-277
             if len(fr) < num_frames:  # pad by repeating the last frame (dataset.py:256-265)
                 fr = np.concatenate([fr, np.repeat(fr[-1:], num_frames - len(fr), 0)])
             return fr[:num_frames]
@@ -171,6 +171,8 @@ class Family:
 
     def to_model_input(self, frames_u8: torch.Tensor, num_frames, div255=False):
         from . import preprocess as pp
+        if self.name in ("vivit", "timesformer") and tuple(frames_u8.shape[-3:-1]) != (224, 224):
+            frames_u8 = pp.cv2_resize_u8(frames_u8, (224, 224))  # cv2.resize INTER_LINEAR (dataset.py:271-277)
         if self.name == "vivit":
             return pp.vivit_preprocess(frames_u8)
         if self.name == "timesformer":

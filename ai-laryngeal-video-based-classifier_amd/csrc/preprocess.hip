@@ -11,6 +11,11 @@
 //    align_corners=False: pytorchvideo ShortSideScale), crop (torchvision CenterCrop), per-channel
 //    affine x*scale[c] + shift[c] (Normalize / the /255 of the inference scripts), and the output
 //    layout [B][T][C][h][w] (HF pixel_values) or [B][C][T][h][w] (torchvision video models).
+//  * resize_linear_u8_kernel — OpenCV cv2.resize(frame, (w, h)) INTER_LINEAR on uint8 frames (the
+//    reference's resize of decoded frames to 224x224, vivit dataset.py:271-277, :348,
+//    inference.py:155): 11-bit fixed-point coefficient tables from the host (vclip_amd/resize.py,
+//    OpenCV resizeGeneric_'s float math), the exact horizontal pass, VResizeLinearVec_32s8u's
+//    vertical rounding, and INTER_AREA's 2x2 fast path for an exact 2x downscale.
 #include "common.hpp"
 
 namespace vc {
@@ -106,6 +111,45 @@ __global__ void __launch_bounds__(256) video_transform_kernel(const uint8_t* __r
     }
 }
 
+// One thread per output pixel (all C <= 4 channels).  tab: int32 xofs[w] | xa0[w] | xa1[w] |
+// yofs[h] | yb0[h] | yb1[h]; columns >= xlim copy S[xofs] * 2048 (HResizeLinear's xmax).
+__global__ void __launch_bounds__(256) resize_linear_u8_kernel(const uint8_t* __restrict__ src, int64_t N, int H, int W,
+                                                               int C, int h, int w, const int* __restrict__ tab,
+                                                               int xlim, int area2x, uint8_t* __restrict__ dst) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= N * h * w) return;
+    const int dx = i % w;
+    const int dy = (i / w) % h;
+    const int64_t n = i / ((int64_t)w * h);
+    const uint8_t* img = src + n * (int64_t)H * W * C;
+    uint8_t* o = dst + ((n * h + dy) * (int64_t)w + dx) * C;
+    if (area2x) {
+        const uint8_t* p0 = img + ((int64_t)(2 * dy) * W + 2 * dx) * C;
+        const uint8_t* p1 = p0 + (int64_t)W * C;
+        for (int c = 0; c < C; ++c) o[c] = (uint8_t)(((int)p0[c] + p0[C + c] + p1[c] + p1[C + c] + 2) >> 2);
+        return;
+    }
+    const int sx = tab[dx], a0 = tab[w + dx], a1 = tab[2 * w + dx];
+    const int sy = tab[3 * w + dy], b0 = tab[3 * w + h + dy], b1 = tab[3 * w + 2 * h + dy];
+    const int y0 = sy < 0 ? 0 : (sy > H - 1 ? H - 1 : sy);
+    const int y1 = sy + 1 < 0 ? 0 : (sy + 1 > H - 1 ? H - 1 : sy + 1);
+    const uint8_t* r0 = img + (int64_t)y0 * W * C;
+    const uint8_t* r1 = img + (int64_t)y1 * W * C;
+    for (int c = 0; c < C; ++c) {
+        int h0, h1;
+        if (dx < xlim) {
+            h0 = (int)r0[sx * C + c] * a0 + (int)r0[(sx + 1) * C + c] * a1;
+            h1 = (int)r1[sx * C + c] * a0 + (int)r1[(sx + 1) * C + c] * a1;
+        } else {
+            h0 = (int)r0[sx * C + c] * 2048;
+            h1 = (int)r1[sx * C + c] * 2048;
+        }
+        // VResizeLinearVec_32s8u: int16 lanes of row >> 4, mul_hi by the 11-bit betas, (+2) >> 2
+        int v = ((((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16) + 2) >> 2;
+        o[c] = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+    }
+}
+
 }  // namespace vc
 
 using namespace vc;
@@ -121,6 +165,18 @@ int vc_resample_u8(const uint8_t* src, int64_t N, int64_t H, int64_t W, int64_t 
     resample_u8_kernel<<<(unsigned)((total + 255) / 256), 256, 0, stream>>>(src, N, (int)H, (int)W, (int)C, axis,
                                                                            (int)out_size, bounds, coeffs, (int)ksize, dst);
     return check_launch("vc_resample_u8");
+}
+
+int vc_resize_linear_u8(const uint8_t* src, int64_t N, int64_t H, int64_t W, int64_t C, int64_t h, int64_t w,
+                        const int* tables, int64_t xlim, int area2x, uint8_t* dst, hipStream_t stream) {
+    if (!src || !dst || (!tables && !area2x)) return fail(VC_ERR_INVALID_ARG, "vc_resize_linear_u8: null pointer");
+    if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || C > 4 || h <= 0 || w <= 0 || xlim < 0 || xlim > w ||
+        (area2x && (H != 2 * h || W != 2 * w)))
+        return fail(VC_ERR_INVALID_ARG, "vc_resize_linear_u8: bad shape");
+    const int64_t total = N * h * w;
+    resize_linear_u8_kernel<<<(unsigned)((total + 255) / 256), 256, 0, stream>>>(src, N, (int)H, (int)W, (int)C, (int)h,
+                                                                                (int)w, tables, (int)xlim, area2x, dst);
+    return check_launch("vc_resize_linear_u8");
 }
 
 int vc_video_transform(const uint8_t* frames, int64_t nclips, int64_t F, int64_t H, int64_t W, const int64_t* idx,

@@ -98,6 +98,33 @@ def pil_resize_u8(frames: torch.Tensor, out_hw) -> torch.Tensor:
     return x
 
 
+_CV_TABLES = {}
+
+
+def cv2_resize_u8(frames: torch.Tensor, size) -> torch.Tensor:
+    """cv2.resize(frame, size) INTER_LINEAR on device uint8 frames [..., H, W, C]; size = (w, h) as
+    cv2 takes it (vc_resize_linear_u8; tables from vclip_amd.resize, the host restatement)."""
+    from . import resize as R
+    w, h = int(size[0]), int(size[1])
+    _need(frames.dtype == torch.uint8 and frames.is_cuda and frames.dim() >= 3, "cv2_resize_u8: cuda uint8 [..., H, W, C]")
+    x = frames.contiguous()
+    H, W, C = x.shape[-3:]
+    if (H, W) == (h, w):
+        return x.clone()
+    N = x.numel() // (H * W * C)
+    y = torch.empty(*x.shape[:-3], h, w, C, dtype=torch.uint8, device=x.device)
+    area = int(R.is_area_fast_2x((H, W), (h, w)))
+    key = (H, W, h, w, x.device)
+    if key not in _CV_TABLES:
+        xo, xa0, xa1, xlim = R.linear_tables(W, w, clamp=True)
+        yo, yb0, yb1, _ = R.linear_tables(H, h, clamp=False)
+        tab = np.concatenate([xo, xa0, xa1, yo, yb0, yb1]).astype(np.int32)
+        _CV_TABLES[key] = (torch.from_numpy(tab).to(x.device), xlim)
+    tab, xlim = _CV_TABLES[key]
+    _lib.call("vc_resize_linear_u8", _p(x), N, H, W, C, h, w, _p(tab), xlim, area, _p(y), _stream(x))
+    return y
+
+
 def _transform(frames, idx, T, resize_hw, crop, scale3, shift3, layout, out_bf16=False):
     B, F, H, W, C = frames.shape
     _need(C == 3 and frames.dtype == torch.uint8 and frames.is_contiguous(), "frames: u8 [B, F, H, W, 3]")

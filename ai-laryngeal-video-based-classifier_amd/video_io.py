@@ -138,14 +138,5 @@ def list_videos(class_dir) -> list:
     return out
 
 
-def resize_frames_224(frames: np.ndarray) -> np.ndarray:
-    """dataset.py:271-277 resizes decoded frames to 224x224 when they are not (cv2 INTER_LINEAR).
-    cv2 is absent here: Pillow bilinear is used (parity unpinned for non-224 sources)."""
-    if frames.shape[1:3] == (224, 224):
-        return frames
-    from PIL import Image
-    return np.stack([np.asarray(Image.fromarray(f).resize((224, 224), Image.BILINEAR)) for f in frames])
-
-
 def exists(path) -> bool:
     return os.path.exists(path)

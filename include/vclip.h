@@ -185,6 +185,17 @@ int vc_resample_u8(const uint8_t* src, int64_t N, int64_t H, int64_t W, int64_t 
                    const int* bounds, const int* coeffs, int64_t ksize, uint8_t* dst, hipStream_t stream);
 
 /*
+ * OpenCV cv2.resize(frame, (w, h)) with INTER_LINEAR on N uint8 frames [N][H][W][C] -> [N][h][w][C]
+ * (C <= 4): the reference's resize of decoded frames to 224x224 (vivit_transformer/vivit_classifier/
+ * data_config/dataset.py:271-277, :348; vivit_transformer/inference.py:155).  tables: int32
+ * xofs[w] | xa0[w] | xa1[w] | yofs[h] | yb0[h] | yb1[h] (11-bit coefficients, vclip_amd/resize.py
+ * linear_tables); columns >= xlim copy the last source column.  area2x != 0: an exact 2x
+ * downscale, INTER_AREA's fast 2x2 average (tables may be null).
+ */
+int vc_resize_linear_u8(const uint8_t* src, int64_t N, int64_t H, int64_t W, int64_t C, int64_t h, int64_t w,
+                        const int* tables, int64_t xlim, int area2x, uint8_t* dst, hipStream_t stream);
+
+/*
  * frames u8 [nclips][F][H][W][3] -> out[clip][t] = affine(crop(resize(frames[clip][idx[clip][t]]))):
  * idx int64 [nclips][T] (clamped to [0, F-1]); resize to (resize_h, resize_w) with torch
  * F.interpolate bilinear, align_corners=False semantics (skipped when equal to (H, W)); crop

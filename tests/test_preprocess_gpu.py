@@ -60,3 +60,20 @@ def test_video_eval_transform(F, H, W, T, div255):
     want = (x - 0.45) / 0.225
     tol = 1e-4 * (1.0 if div255 else 255.0)
     assert got.shape == want.shape and (got - want).abs().max().item() < tol
+
+
+@pytest.mark.parametrize("shape", [(48, 64, 224, 224), (240, 320, 224, 224), (448, 448, 224, 224), (100, 90, 224, 224),
+                                   (17, 23, 11, 7), (7, 5, 10, 13)])
+def test_cv2_resize_gpu_bit_exact(shape):
+    """vc_resize_linear_u8 == the host restatement of cv2.resize INTER_LINEAR (vclip_amd/resize.py), which
+    tests/test_video_dataset.py pins to the loop oracle (oracle/cv2_resize_ref.py); parity with cv2 itself
+    is unpinned (cv2 absent from the image).  448 -> 224 is the exact-2x INTER_AREA path."""
+    from vclip_amd import preprocess
+    from vclip_amd.resize import resize_linear_u8
+    H, W, h, w = shape
+    x = np.random.RandomState(H + W).randint(0, 256, (3, H, W, 3)).astype(np.uint8)
+    got = preprocess.cv2_resize_u8(torch.from_numpy(x).cuda(), (w, h)).cpu().numpy()
+    np.testing.assert_array_equal(got, resize_linear_u8(x, (w, h)))
+    if H * W * h * w < 2e6:
+        from oracle.cv2_resize_ref import resize_linear_u8 as ref
+        np.testing.assert_array_equal(got[0], np.array(ref(x[0].tolist(), w, h), dtype=np.uint8))
