@@ -344,9 +344,9 @@ def run_main(fam_name, argv=None):
         _load_weights(model, args.checkpoint_path, logger, fam)
     history = {"train_loss": [], "train_acc": [], "val_loss": [], "val_acc": []}
     if not args.skip_train:
-        if fam.name != "vivit":
-            raise NotImplementedError(f"{fam.name}: only the ViViT train step has GPU backward kernels in libvclip "
-                                      "(SURVEY.md §8 a16); evaluate a trained checkpoint with --skip_train "
+        if fam.name not in ("vivit", "timesformer"):
+            raise NotImplementedError(f"{fam.name}: only the ViViT and TimeSformer train steps have GPU backward "
+                                      "kernels in libvclip; evaluate a trained checkpoint with --skip_train "
                                       "--checkpoint_path")
         from .optim import AdamW
         opt = AdamW(model.parameters(), lr=args.learning_rate, weight_decay=args.weight_decay)

@@ -1,0 +1,227 @@
+"""torch.autograd Functions over the libvclip kernels, for the train steps composed in Python
+(TimeSformer: vclip_amd/timesformer.py `_forward_train`).
+
+Every arithmetic op here is a HIP kernel of libvclip.so, forward and backward:
+  linear      bf16 MFMA GEMM + bias (vc_gemm_bf16) / dgrad GEMM on the packed W^T / split-K wgrad
+              (vc_wgrad_bf16) / bias column sums (vc_colsum); an optional row block of the weight is
+              pre-scaled (the q rows: scale * log2 e folded as in the inference path, with the chain
+              rule applied to the fp32 master weight and bias);
+  layer_norm  vc_layernorm_f32_bf16 / vc_layernorm_f32, backward vc_layernorm_bwd;
+  attention   flash forward with the base-2 log-sum-exp (vc_attention_fwd_lse) / flash backward
+              (vc_attention_bwd) — joint or spatial (TimeSformer B*T sequences of 1 + P tokens);
+  temporal_attention  vc_temporal_attention / vc_temporal_attention_bwd (clip layout, T <= 32);
+  gelu_erf    vc_gelu_erf / vc_gelu_erf_bwd;
+  cls_head    vc_cls_head / vc_cls_head_bwd (final LayerNorm on the CLS rows + classifier).
+The tensors between them (residual adds, the clip <-> frame permutes, the CLS frame mean) are
+ordinary torch tensor ops: layout glue, autograd's bookkeeping.  Rows are padded internally to the
+kernels' tile multiples; the returned tensors have exactly the caller's rows.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib, ops
+from .ops import _p, _stream
+
+
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+def _padded(x: torch.Tensor, rows: int, dtype=None) -> torch.Tensor:
+    """Contiguous copy of x (converted to dtype) with zero rows up to `rows`."""
+    dtype = dtype or x.dtype
+    out = torch.zeros((rows,) + tuple(x.shape[1:]), dtype=dtype, device=x.device)
+    out[: x.shape[0]].copy_(x)
+    return out
+
+
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, out_f32: bool, qrows: int, qscale: float):
+        M, K = x.shape
+        N = w.shape[0]
+        Mp = _round_up(M, 256)
+        xp = _padded(x, Mp, torch.bfloat16)
+        wc = w.detach().contiguous().float()
+        wb = torch.empty(N, K, dtype=torch.bfloat16, device=x.device)
+        wt = torch.empty(K, N, dtype=torch.bfloat16, device=x.device)
+        ops.pack_weight(wc, wb, wt, nscaled=qrows, scale=qscale)
+        bb = b.detach().float().clone()
+        if qrows:
+            bb[:qrows] *= qscale
+        out = torch.empty(Mp, N, dtype=torch.float32 if out_f32 else torch.bfloat16, device=x.device)
+        ops.gemm(xp, wb, bb, "bias_f32" if out_f32 else "bias", out)
+        ctx.save_for_backward(xp, wt)
+        ctx.M, ctx.qrows, ctx.qscale, ctx.xdtype = M, qrows, qscale, x.dtype
+        return out[:M]
+
+    @staticmethod
+    def backward(ctx, dy):
+        xp, wt = ctx.saved_tensors
+        Mp, K = xp.shape
+        N = wt.shape[1]
+        dyp = _padded(dy, Mp, torch.bfloat16)
+        dx = torch.empty(Mp, K, dtype=torch.bfloat16, device=dy.device)
+        ops.gemm(dyp, wt, torch.zeros(K, dtype=torch.float32, device=dy.device), "bias", dx)
+        dw = torch.empty(N, K, dtype=torch.float32, device=dy.device)
+        work = torch.empty(2 * N * K, dtype=torch.float32, device=dy.device)
+        ops.wgrad(dyp, xp, dw, work, nscaled=ctx.qrows, scale=ctx.qscale)
+        db = torch.empty(N, dtype=torch.float32, device=dy.device)
+        ops.colsum(dyp, db, nscaled=ctx.qrows, scale=ctx.qscale)
+        return dx[: ctx.M].to(ctx.xdtype), dw, db, None, None, None
+
+
+def linear(x, w, b, out_f32=False, qrows=0, qscale=1.0):
+    """y = x @ w.T + b with bf16 operands (x bf16 [M, K], w / b fp32 masters), fp32 accumulation;
+    rows < qrows of w and b act multiplied by qscale."""
+    return _Linear.apply(x, w, b, out_f32, qrows, qscale)
+
+
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g, b, eps: float, out_bf16: bool):
+        x = x.contiguous().float()
+        M, D = x.shape
+        y = torch.empty(M, D, dtype=torch.bfloat16 if out_bf16 else torch.float32, device=x.device)
+        gc, bc = g.detach().float().contiguous(), b.detach().float().contiguous()
+        if out_bf16:
+            ops.layernorm(x, gc, bc, eps, y)
+        else:
+            ops.layernorm_f32(x, gc, bc, eps, y)
+        ctx.save_for_backward(x, gc)
+        ctx.eps = eps
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, g = ctx.saved_tensors
+        M, D = x.shape
+        dyf = dy.float().contiguous()
+        dx = torch.zeros(M, D, dtype=torch.float32, device=x.device)
+        dxb = torch.empty(M, D, dtype=torch.bfloat16, device=x.device)
+        dg = torch.empty(D, dtype=torch.float32, device=x.device)
+        dbeta = torch.empty(D, dtype=torch.float32, device=x.device)
+        nb = min(512, (M + 3) // 4)
+        work = torch.empty((nb + (nb + 31) // 32) * 4 * D, dtype=torch.float32, device=x.device)
+        ops.layernorm_bwd(dyf, x, g, ctx.eps, dx, dxb, dg, dbeta, work)
+        return dx, dg, dbeta, None, None
+
+
+def layer_norm(x, g, b, eps, out_bf16=True):
+    """Row LayerNorm of f32 x [M, D] -> bf16 (out_bf16) or f32."""
+    return _LayerNorm.apply(x, g, b, eps, out_bf16)
+
+
+class _Attention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, B: int, S: int, H: int):
+        rows = (B - 1) * S + _round_up(S, 64) + 64
+        qp = _padded(qkv, max(rows, qkv.shape[0]))
+        out = torch.zeros(qp.shape[0], H * 64, dtype=torch.bfloat16, device=qkv.device)
+        lse = torch.empty(B * H * S, dtype=torch.float32, device=qkv.device)
+        ops.attention_fwd_lse(qp, B, S, H, out, lse)
+        ctx.save_for_backward(qp, out, lse)
+        ctx.dims = (B, S, H, qkv.shape[0])
+        return out[: qkv.shape[0]]
+
+    @staticmethod
+    def backward(ctx, dout):
+        qp, out, lse = ctx.saved_tensors
+        B, S, H, M = ctx.dims
+        dp = _padded(dout, qp.shape[0], torch.bfloat16)
+        delta = torch.empty(B * H * S, dtype=torch.float32, device=dout.device)
+        dqkv = torch.zeros_like(qp)
+        ops.attention_bwd(qp, out, dp, lse, delta, B, S, H, dqkv)
+        return dqkv[:M], None, None, None
+
+
+def attention(qkv, B, S, H):
+    """softmax(q' k^T) v per (sequence, head) for B sequences of S rows of q'|k|v (q' prescaled by
+    scale * log2 e), bf16 [B*S, 3*H*64] -> bf16 [B*S, H*64]."""
+    return _Attention.apply(qkv, B, S, H)
+
+
+class _TemporalAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, B: int, P: int, T: int, H: int):
+        qkv = qkv.contiguous()
+        out = torch.zeros(qkv.shape[0], H * 64, dtype=torch.bfloat16, device=qkv.device)
+        ops.temporal_attention(qkv, B, P, T, H, 1.0, out, q_prescaled=True)
+        ctx.save_for_backward(qkv)
+        ctx.dims = (B, P, T, H)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (qkv,) = ctx.saved_tensors
+        B, P, T, H = ctx.dims
+        d = dout.to(torch.bfloat16).contiguous()
+        dqkv = torch.zeros_like(qkv)
+        _lib.call("vc_temporal_attention_bwd", _p(qkv), qkv.stride(0), _p(d), d.stride(0), B, P, T, H, 64, _p(dqkv),
+                  dqkv.stride(0), _stream(qkv))
+        return dqkv, None, None, None, None
+
+
+def temporal_attention(qkv, B, P, T, H):
+    """TimeSformer temporal attention on the clip layout (rows b*(1+P*T) + 1 + p*T + t; CLS rows of
+    the output are zero and get no gradient), q' prescaled."""
+    return _TemporalAttention.apply(qkv, B, P, T, H)
+
+
+class _GeluErf(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        M, N = x.shape
+        y = torch.empty_like(x)
+        _lib.call("vc_gelu_erf", _p(x), x.stride(0), M, N, _p(y), y.stride(0), _stream(x))
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        M, N = x.shape
+        dy = dy.contiguous()
+        if dy.dtype not in (torch.bfloat16, torch.float32):
+            dy = dy.float()
+        dx = torch.empty_like(x)
+        _lib.call("vc_gelu_erf_bwd", _p(dy), int(dy.dtype == torch.bfloat16), dy.stride(0), _p(x), x.stride(0), M, N,
+                  _p(dx), dx.stride(0), _stream(x))
+        return dx
+
+
+def gelu_erf(x):
+    """Exact GELU of bf16 [M, N]."""
+    return _GeluErf.apply(x)
+
+
+class _ClsHead(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g, b, wc, bc, B: int, S: int, eps: float):
+        x = x.contiguous().float()
+        gc, bcn, wcc, bcc = (t.detach().float().contiguous() for t in (g, b, wc, bc))
+        logits = ops.cls_head(x, B, S, gc, bcn, eps, wcc, bcc)
+        ctx.save_for_backward(x, gc, bcn, wcc)
+        ctx.dims = (B, S, eps)
+        return logits.clone()
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        x, g, b, wc = ctx.saved_tensors
+        B, S, eps = ctx.dims
+        D = g.numel()
+        dx = torch.zeros_like(x)
+        dxb = torch.zeros(x.shape, dtype=torch.bfloat16, device=x.device)
+        dwc = torch.empty_like(wc)
+        dbc = torch.empty(wc.shape[0], dtype=torch.float32, device=x.device)
+        dg = torch.empty(D, dtype=torch.float32, device=x.device)
+        db = torch.empty(D, dtype=torch.float32, device=x.device)
+        ops.cls_head_bwd(x, B, S, g, b, eps, wc, dlogits.float().contiguous(), dx, dxb, dwc, dbc, dg, db)
+        return dx, dg, db, dwc, dbc, None, None, None
+
+
+def cls_head(x, g, b, wc, bc, B, S, eps):
+    """logits = classifier(LayerNorm(x[b*S])) over the CLS rows of f32 x [B*S, D]."""
+    return _ClsHead.apply(x, g, b, wc, bc, B, S, eps)

@@ -192,16 +192,12 @@ __device__ __forceinline__ void store_tile(const v16f (&acc)[MI][NI], int64_t mb
 
 // ST: LDS ring depth in tiles (prefetch distance ST - 1).  ST = 2 at 128x128 needs 64 KiB of
 // LDS, so two workgroups share a CU and one's epilogue overlaps the other's main loop.
-// PRE (f32 residual epilogue only): load this wave's residual elements into registers before
-// the K loop, so their latency overlaps the main loop instead of opening the epilogue
-// (+20 VGPRs at 128x128).  Bit-identical; ViViT-B B=8 forward 9.224 vs 9.265 ms/step with
-// every residual GEMM on cfg 5 vs cfg 8 (= cfg 5 without it), interleaved, tools/ab_rpre.py:
-// +0.4 %, inside the noise band; isolated o_proj / fc2 within 1-2 % either way.
-// PRIO: static s_setprio 1 for one of two co-resident workgroups (bit 8 of the block id; cfg 9).
-// Measured slower (o_proj 67.0 vs 64.4 us, fc2 152.6 vs 151.0, model 9.792 vs 9.755 ms/step,
-// tools/ab_rpre.py 5,9): unlike the attention kernel's, the GEMM's two workgroups per CU gain
-// nothing from a fixed arbitration winner; cfg 5 ships without it.
-template <int BM, int BN, int WM, int WN, int EPI, int ST = 3, bool PRE = true, bool PRIO = false>
+// f32 residual epilogue: this wave's residual elements are loaded into registers before the K
+// loop, so their latency overlaps the main loop instead of opening the epilogue (+20 VGPRs at
+// 128x128; +0.4 % on the ViViT-B forward in an interleaved A/B, round 1).
+// (A static s_setprio for one of two co-resident workgroups measured slower here, unlike in
+// the attention kernel: o_proj 67.0 vs 64.4 us, fc2 152.6 vs 151.0; round 1.)
+template <int BM, int BN, int WM, int WN, int EPI, int ST = 3>
 __global__ void __launch_bounds__(512, ST == 2 ? 2 : 1)
 gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
                  int nbm, int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
@@ -221,9 +217,6 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
     const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
     const int tm = wgid / nbn, tn = wgid % nbn;
     const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-    if constexpr (PRIO) {
-        if ((bid >> 8) & 1) __builtin_amdgcn_s_setprio(1);
-    }
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -265,7 +258,7 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
 
     const int nk = K / GBK;
     stage(0, 0);
-    constexpr bool RPRE = PRE && EPI == VC_EPI_BIAS_RESID_F32;
+    constexpr bool RPRE = EPI == VC_EPI_BIAS_RESID_F32;
     float4 xres[RPRE ? MI : 1][RPRE ? NI : 1][4];
     if constexpr (RPRE) {
 #pragma unroll
@@ -353,7 +346,7 @@ __device__ __forceinline__ v8bf lds_frag64(const char* tile, int row, int chunk)
     return __builtin_bit_cast(v8bf, v);
 }
 
-template <int EPI, int ABL = 0>  // ABL: ablation bits for timing studies (1: no loop loads, 2: no MFMA)
+template <int EPI>
 __global__ void __launch_bounds__(512, 1)
 gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
                      int nbm, int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
@@ -407,19 +400,6 @@ gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
     const int nk = K / BKH;
     // fragments of one 16-deep k-step (kk) of half-tile t
     auto read_frags = [&](int t, int kk, v8bf (&fa)[MI], v8bf (&fw)[NI]) {
-        if constexpr (ABL & 8) {  // timing ablation: no LDS fragment reads
-#pragma unroll
-            for (int i = 0; i < MI; ++i) {
-                v8s z = {(short)t, (short)kk, 0, 0, 0, 0, 0, (short)i};
-                fa[i] = __builtin_bit_cast(v8bf, z);
-            }
-#pragma unroll
-            for (int j = 0; j < NI; ++j) {
-                v8s z = {(short)kk, (short)t, 0, 0, 0, 0, 0, (short)j};
-                fw[j] = __builtin_bit_cast(v8bf, z);
-            }
-            return;
-        }
         const char* At = smem + (t % NS) * SLOT;
         const char* Wt = At + BM * 64;
         const int ch = kk * 2 + h;
@@ -429,24 +409,14 @@ gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
         for (int j = 0; j < NI; ++j) fw[j] = lds_frag64(Wt, wn * TN + j * 32 + r, ch);
     };
     auto mfmas = [&](const v8bf (&fa)[MI], const v8bf (&fw)[NI]) {
-        if constexpr (ABL & 2) {
-#pragma unroll
-            for (int i = 0; i < MI; ++i) asm volatile("" ::"v"(fa[i]));
-#pragma unroll
-            for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(fw[j]));
-            return;
-        }
-        if constexpr (ABL & 16) __builtin_amdgcn_s_setprio(1);  // T5: keep the cluster between barriers
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int j = 0; j < NI; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[j], fa[i], acc[i][j], 0, 0, 0);
-        if constexpr (ABL & 16) __builtin_amdgcn_s_setprio(0);
     };
     // 6 fragment reads ride between 8 MFMAs
     auto interleave = [&]() {
-        if constexpr (ABL & 32) return;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -472,7 +442,7 @@ gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
     // (the last half-tile is peeled so the loop body has no join in front of its MFMAs:
     // a join makes hipcc's wait-count merge fall back to lgkmcnt(0))
     for (int t = 0; t < nk - 1; ++t) {
-        if (!(ABL & 1) && t + 3 < nk) stage(t + 3);
+        if (t + 3 < nk) stage(t + 3);
         read_frags(t, 1, fa1, fw1);
         mfmas(fa0, fw0);
         interleave();
@@ -487,13 +457,6 @@ gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
     read_frags(nk - 1, 1, fa1, fw1);
     mfmas(fa0, fw0);
     mfmas(fa1, fw1);
-    if constexpr (ABL & 4) {  // timing ablation: no epilogue
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(acc[i][j]));
-        return;
-    }
     store_tile<EPI, MI, NI>(acc, m0 + wm * TM, n0 + wn * TN, r, h, bias, out, ldo, aux, ldaux, G, gstride, goff);
 }
 
@@ -507,7 +470,7 @@ gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
 // ---------------------------------------------------------------------------------
 // Epilogue of the 256x256 persistent kernels: + bias (LDS), activation, bf16, lane-pair
 // swap -> 16-B row stores (MI*NI*2 stores per wave, twice that with the saved pre-activation).
-template <int EPI, int MI, int NI, int TM, int TN, bool NOSTORE>
+template <int EPI, int MI, int NI, int TM, int TN>
 __device__ __forceinline__ void epi256(const v16f (&acc)[MI][NI], int64_t m0, int64_t n0, int wm, int wn, int r, int h,
                                        const float* bias_lds, uint16_t* __restrict__ out, int64_t ldo,
                                        uint16_t* __restrict__ pre_out, int64_t ldpre) {
@@ -551,8 +514,7 @@ __device__ __forceinline__ void epi256(const v16f (&acc)[MI][NI], int64_t m0, in
                 const int64_t col = n0 + wn * TN + j * 32 + g * 8 + h * 8;
                 uint4 v;
                 v.x = s0[0]; v.y = s1[0]; v.z = s0[1]; v.w = s1[1];
-                if constexpr (NOSTORE) asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w), "v"(orow + col));
-                else *reinterpret_cast<uint4*>(orow + col) = v;
+                *reinterpret_cast<uint4*>(orow + col) = v;
                 if constexpr (SAVE) {
                     auto q0 = __builtin_amdgcn_permlane32_swap(pp[g][0], pp[g + 1][0], false, false);
                     auto q1 = __builtin_amdgcn_permlane32_swap(pp[g][1], pp[g + 1][1], false, false);
@@ -565,7 +527,7 @@ __device__ __forceinline__ void epi256(const v16f (&acc)[MI][NI], int64_t m0, in
     }
 }
 
-template <int EPI, int ABL = 0>  // ABL: timing ablations (1 no loop loads, 2 no MFMA, 4 no stores, 8 no LDS reads)
+template <int EPI>
 __global__ void __launch_bounds__(512, 1)
 gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
                          int nbm, int nbn, int K, int N, const float* __restrict__ bias, uint16_t* __restrict__ out,
@@ -600,9 +562,6 @@ gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint
     const int acol1 = swz64(arow + 16, lane & 3) * 8;
 
     auto stage = [&](int64_t m0, int64_t n0, int t, int slotidx) {
-        if constexpr (ABL & 1) {
-            if (t >= 3) return;
-        }
         const uint32_t s = lds0 + (slotidx % NS) * SLOT;
         const int64_t k0 = (int64_t)t * BKH;
         glds16(A + (m0 + arow) * lda + k0 + acol0, __builtin_amdgcn_readfirstlane(s + (wave * 32) * 64));
@@ -612,19 +571,6 @@ gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint
                __builtin_amdgcn_readfirstlane(s + BM * 64 + (wave * 32 + 16) * 64));
     };
     auto read_frags = [&](int slotidx, int kk, v8bf (&fa)[MI], v8bf (&fw)[NI]) {
-        if constexpr (ABL & 8) {
-#pragma unroll
-            for (int i = 0; i < MI; ++i) {
-                v8s z = {(short)slotidx, (short)kk, 0, 0, 0, 0, 0, (short)i};
-                fa[i] = __builtin_bit_cast(v8bf, z);
-            }
-#pragma unroll
-            for (int j = 0; j < NI; ++j) {
-                v8s z = {(short)kk, (short)slotidx, 0, 0, 0, 0, 0, (short)j};
-                fw[j] = __builtin_bit_cast(v8bf, z);
-            }
-            return;
-        }
         const char* At = smem + (slotidx % NS) * SLOT;
         const char* Wt = At + BM * 64;
         const int ch = kk * 2 + h;
@@ -635,23 +581,13 @@ gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint
     };
     v16f acc[MI][NI];
     auto mfmas = [&](const v8bf (&fa)[MI], const v8bf (&fw)[NI]) {
-        if constexpr (ABL & 2) {
-#pragma unroll
-            for (int i = 0; i < MI; ++i) asm volatile("" ::"v"(fa[i]));
-#pragma unroll
-            for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(fw[j]));
-            return;
-        }
-        if constexpr (ABL & 16) __builtin_amdgcn_s_setprio(1);  // T5: keep the cluster between barriers
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int j = 0; j < NI; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[j], fa[i], acc[i][j], 0, 0, 0);
-        if constexpr (ABL & 16) __builtin_amdgcn_s_setprio(0);
     };
     auto interleave = [&]() {
-        if constexpr (ABL & 32) return;
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -730,7 +666,7 @@ gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint
             stage(nm0, nn0, 2, nbase + 2);
         }
 
-        epi256<EPI, MI, NI, TM, TN, (ABL & 4) != 0>(acc, m0, n0, wm, wn, r, h, bias_lds, out, ldo, pre_out, ldpre);
+        epi256<EPI, MI, NI, TM, TN>(acc, m0, n0, wm, wn, r, h, bias_lds, out, ldo, pre_out, ldpre);
         if (!more) break;
         first = false;
         m0 = nm0;
@@ -743,214 +679,46 @@ gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint
     }
 }
 
-// ---------------------------------------------------------------------------------
-// Ping-pong persistent 256x256 kernel (cfg 6): same tiles, LDS ring, staging and
-// epilogue as gemm_bf16_persist_kernel, different schedule (cdna_hip_programming.md §5,
-// the 256^2 template's staggered wave groups).  Every 32-deep half-tile is two
-// barrier-separated sections per wave:
-//   L: issue the LDS-DMA of half-tile u+3, read all fragments of half-tile u, retire
-//      half-tile u+1 with a counted vmcnt, lgkmcnt(0);
-//   M: 16 MFMAs (+ the tile's epilogue after its last half-tile).
-// The wave group wm = 1 starts one barrier late, so on every SIMD (one wave of each
-// group) one wave's M section runs against the other's L section and the MFMA pipe
-// does not idle while fragments and DMAs are issued.  The staging cursor runs three
-// half-tiles ahead across tile boundaries (the next tile's prologue is part of the
-// stream), so the per-tile pipeline fill of the plain kernel disappears.
-// Ordering (u = flat half-tile index of this workgroup):
-//   RAW  half-tile u is retired by every wave in its L_{u-1}, and both groups pass a
-//        barrier after that before any wave reads u (group 0 in L_u, group 1 one
-//        section later);
-//   WAR  slot (u+3)%4 = slot of u-1, whose readers finished L_{u-1} with lgkmcnt(0)
-//        before the barrier that precedes the earliest L_u of either group.
-// vmcnt counts the epilogue stores too (issued in M after the DMA being retired), so
-// the count adds NST when one of the two preceding M sections stored a tile.
-// ---------------------------------------------------------------------------------
-template <int EPI, int ABL = 0>
-__global__ void __launch_bounds__(512, 1)
-gemm_bf16_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
-                    int nbm, int nbn, int K, int N, const float* __restrict__ bias, uint16_t* __restrict__ out,
-                    int64_t ldo, uint16_t* __restrict__ pre_out, int64_t ldpre) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int BM = 256, BN = 256, BKH = 32, NS = 4;
-    constexpr int SLOT = (BM + BN) * 64;
-    constexpr int TM = 128, TN = 64, MI = 4, NI = 2;
-    constexpr bool SAVE = EPI == VC_EPI_BIAS_GELU_TANH_SAVE;
-    constexpr int NST = MI * NI * 2 * (SAVE ? 2 : 1);
-    float* bias_lds = reinterpret_cast<float*>(smem + NS * SLOT);
-
-    const int ntiles = nbm * nbn;
-    const int G = gridDim.x;
-    const int b = blockIdx.x;
-    const int lane_slot = (b & 7) * (G >> 3) + (b >> 3);
-    if (lane_slot >= ntiles) return;  // whole workgroup, before any barrier
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 2, wn = wave & 3;
-    const int r = lane & 31, h = lane >> 5;
-
-    for (int n = tid * 4; n < N; n += 512 * 4)
-        *reinterpret_cast<float4*>(bias_lds + n) = *reinterpret_cast<const float4*>(bias + n);
-    __syncthreads();
-
-    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
-    const int nk = K / BKH;
-    const int own = (ntiles - lane_slot + G - 1) / G;  // tiles lane_slot, lane_slot + G, ...
-    const int U = own * nk;
-    const int arow = wave * 32 + (lane >> 2);
-    const int acol0 = swz64(arow, lane & 3) * 8;
-    const int acol1 = swz64(arow + 16, lane & 3) * 8;
-
-    auto origin = [&](int it, int64_t& m0, int64_t& n0) {
-        const int tile = it * G + lane_slot;
-        const int tm = tile / nbn;
-        m0 = (int64_t)tm * BM;
-        n0 = (int64_t)(tile - tm * nbn) * BN;
-    };
-    // staging cursor (three half-tiles ahead of the compute cursor)
-    int s_it = 0, s_t = 0;
-    int64_t s_m0, s_n0;
-    origin(0, s_m0, s_n0);
-    auto stage_next = [&](int u) {
-        const uint32_t s = lds0 + (u % NS) * SLOT;
-        const int64_t k0 = (int64_t)s_t * BKH;
-        if (!((ABL & 1) && u >= 3)) {
-            glds16(A + (s_m0 + arow) * lda + k0 + acol0, __builtin_amdgcn_readfirstlane(s + (wave * 32) * 64));
-            glds16(A + (s_m0 + arow + 16) * lda + k0 + acol1, __builtin_amdgcn_readfirstlane(s + (wave * 32 + 16) * 64));
-            glds16(W + (s_n0 + arow) * ldw + k0 + acol0, __builtin_amdgcn_readfirstlane(s + BM * 64 + (wave * 32) * 64));
-            glds16(W + (s_n0 + arow + 16) * ldw + k0 + acol1,
-                   __builtin_amdgcn_readfirstlane(s + BM * 64 + (wave * 32 + 16) * 64));
-        }
-        if (++s_t == nk) {
-            s_t = 0;
-            if (++s_it < own) origin(s_it, s_m0, s_n0);
-        }
-    };
-    auto read_frags = [&](int u, int kk, v8bf (&fa)[MI], v8bf (&fw)[NI]) {
-        const char* At = smem + (u % NS) * SLOT;
-        const char* Wt = At + BM * 64;
-        const int ch = kk * 2 + h;
-#pragma unroll
-        for (int i = 0; i < MI; ++i) fa[i] = lds_frag64(At, wm * TM + i * 32 + r, ch);
-#pragma unroll
-        for (int j = 0; j < NI; ++j) fw[j] = lds_frag64(Wt, wn * TN + j * 32 + r, ch);
-    };
-    v16f acc[MI][NI];
-    auto mfmas = [&](const v8bf (&fa)[MI], const v8bf (&fw)[NI]) {
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int j = 0; j < NI; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[j], fa[i], acc[i][j], 0, 0, 0);
-    };
-    auto raw_barrier = [&]() {
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-    };
-
-    stage_next(0);
-    stage_next(1);
-    stage_next(2);
-    wait_vm<8>();
-    block_sync_lds();
-    if (wm == 1) raw_barrier();  // the stagger
-
-    int c_t = 0, c_it = 0;
-    int64_t m0, n0;
-    origin(0, m0, n0);
-    bool ep1 = false, ep2 = false;  // did M_{u-1} / M_{u-2} store a tile
-    v8bf fa0[MI], fw0[NI], fa1[MI], fw1[NI];
-    for (int u = 0; u < U; ++u) {
-        // ---------------- L section
-        if (u + 3 < U) stage_next(u + 3);
-        read_frags(u, 0, fa0, fw0);
-        read_frags(u, 1, fa1, fw1);
-        if (u + 1 < U) {
-            const int y = (u + 2 < U ? 1 : 0) + (u + 3 < U ? 1 : 0);
-            if (ep1 || ep2) {
-                if (y == 2) wait_vm<8 + NST>();
-                else if (y == 1) wait_vm<4 + NST>();
-                else wait_vm<NST>();
-            } else {
-                if (y == 2) wait_vm<8>();
-                else if (y == 1) wait_vm<4>();
-                else wait_vm<0>();
-            }
-        }
-        block_sync_lds();
-        // ---------------- M section
-        if (c_t == 0) {
-#pragma unroll
-            for (int i = 0; i < MI; ++i)
-#pragma unroll
-                for (int j = 0; j < NI; ++j)
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-        }
-        if constexpr (ABL & 2) {
-#pragma unroll
-            for (int i = 0; i < MI; ++i) asm volatile("" ::"v"(fa0[i]), "v"(fa1[i]));
-#pragma unroll
-            for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(fw0[j]), "v"(fw1[j]));
-        } else {
-            mfmas(fa0, fw0);
-            mfmas(fa1, fw1);
-        }
-        ep2 = ep1;
-        ep1 = false;
-        if (++c_t == nk) {
-            epi256<EPI, MI, NI, TM, TN, (ABL & 4) != 0>(acc, m0, n0, wm, wn, r, h, bias_lds, out, ldo, pre_out, ldpre);
-            ep1 = true;
-            c_t = 0;
-            if (++c_it < own) origin(c_it, m0, n0);
-        }
-        raw_barrier();
-    }
-    if (wm == 0) raw_barrier();  // same barrier count in both groups
-    wait_vm<0>();
-}
-
-// Tile configurations (BM, BN, WM, WN).
+// Tile configurations (BM, BN); cfg 6 (a ping-pong schedule of the persistent kernel, 23 %
+// slower in round 1) is retired, and with it every timing-only ablation build.
 struct GemmCfg {
     int bm, bn;
 };
-static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}, {128, 128}, {256, 256},
-                                 {64, 128}, {128, 128}, {128, 128}};  // 8: cfg 5 without the residual prefetch,
-constexpr int kNumCfgs = 10;                                          // 9: cfg 5 + static priority (A/Bs)
+static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}, {128, 128}, {0, 0},
+                                 {64, 128}};
+constexpr int kNumCfgs = 8;
 
-template <int BM, int BN, int WM, int WN, int E, int ST = 3, bool PRE = true, bool PRIO = false>
+template <int BM, int BN, int WM, int WN, int E, int ST = 3>
 static int launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
                       const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
                       int64_t gs, int64_t go, hipStream_t stream) {
     constexpr int lds = ST * (BM + BN) * 128;
     static bool attr_set = false;  // per instantiation; benign race (idempotent)
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, WM, WN, E, ST, PRE, PRIO>,
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, WM, WN, E, ST>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
         attr_set = true;
     }
-    gemm_bf16_kernel<BM, BN, WM, WN, E, ST, PRE, PRIO><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(
+    gemm_bf16_kernel<BM, BN, WM, WN, E, ST><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(
         A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go);
     return check_launch("vc_gemm_bf16");
 }
 
-template <int E, int ABL = 0>
+template <int E>
 static int launch_big(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
                       const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
                       int64_t gs, int64_t go, hipStream_t stream) {
     constexpr int lds = 4 * 512 * 64;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_big_kernel<E, ABL>,
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_big_kernel<E>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
         attr_set = true;
     }
-    gemm_bf16_big_kernel<E, ABL><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo,
-                                                                          aux, ldaux, G, gs, go);
+    gemm_bf16_big_kernel<E><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo,
+                                                                     aux, ldaux, G, gs, go);
     return check_launch("vc_gemm_bf16");
 }
 
@@ -966,14 +734,14 @@ static int num_cus() {
     return n;
 }
 
-template <int E, int ABL = 0>
+template <int E>
 static int launch_persist(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
                           int N, const float* bias, void* out, int64_t ldo, hipStream_t stream,
                           const float* aux = nullptr, int64_t ldaux = 0) {
     const int lds = 4 * 512 * 64 + N * 4;
     static int attr_set = 0;
     if (attr_set < lds) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_persist_kernel<E, ABL>,
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_persist_kernel<E>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
         attr_set = 160 * 1024;
@@ -981,30 +749,9 @@ static int launch_persist(const uint16_t* A, int64_t lda, const uint16_t* W, int
     const int ntiles = nbm * nbn;
     int grid = num_cus() / 8 * 8;
     if (grid > (ntiles + 7) / 8 * 8) grid = (ntiles + 7) / 8 * 8;
-    gemm_bf16_persist_kernel<E, ABL><<<(unsigned)grid, 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, N, bias,
-                                                                      (uint16_t*)out, ldo,
-                                                                      (uint16_t*)const_cast<float*>(aux), ldaux);
-    return check_launch("vc_gemm_bf16");
-}
-
-template <int E, int ABL = 0>
-static int launch_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K, int N,
-                     const float* bias, void* out, int64_t ldo, hipStream_t stream, const float* aux = nullptr,
-                     int64_t ldaux = 0) {
-    const int lds = 4 * 512 * 64 + N * 4;
-    static int attr_set = 0;
-    if (attr_set < lds) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_pp_kernel<E, ABL>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
-        attr_set = 160 * 1024;
-    }
-    const int ntiles = nbm * nbn;
-    int grid = num_cus() / 8 * 8;
-    if (grid > (ntiles + 7) / 8 * 8) grid = (ntiles + 7) / 8 * 8;
-    gemm_bf16_pp_kernel<E, ABL><<<(unsigned)grid, 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, N, bias,
-                                                                 (uint16_t*)out, ldo,
-                                                                 (uint16_t*)const_cast<float*>(aux), ldaux);
+    gemm_bf16_persist_kernel<E><<<(unsigned)grid, 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, N, bias,
+                                                                  (uint16_t*)out, ldo,
+                                                                  (uint16_t*)const_cast<float*>(aux), ldaux);
     return check_launch("vc_gemm_bf16");
 }
 
@@ -1012,39 +759,7 @@ template <int E>
 static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int64_t M, int64_t N,
                       int K, const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
                       int64_t gs, int64_t go, hipStream_t s) {
-    const int bm = kCfgs[cfg >= 10 ? 3 : cfg].bm, bn = kCfgs[cfg >= 10 ? 3 : cfg].bn;  // x3/x4/x6 ablations: 256x256
-    const int nbm = (int)(M / bm), nbn = (int)(N / bn);
-    if constexpr (E == VC_EPI_BIAS_BF16) {  // timing ablations / schedule variants: bias epilogue only
-        switch (cfg) {
-            case 16: return launch_pp<E, 1>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
-            case 26: return launch_pp<E, 2>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
-            case 46: return launch_pp<E, 4>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
-            case 14: return launch_persist<E, 1>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
-            case 24: return launch_persist<E, 2>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
-            case 44: return launch_persist<E, 4>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
-            case 84: return launch_persist<E, 8>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
-            case 64: return launch_persist<E, 6>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
-            case 74: return launch_persist<E, 7>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
-            case 154: return launch_persist<E, 15>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
-            case 13: return launch_big<E, 1>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-            case 23: return launch_big<E, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-            case 33: return launch_big<E, 3>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-            case 43: return launch_big<E, 4>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-            case 73: return launch_big<E, 7>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-            case 83: return launch_big<E, 8>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-            case 153: return launch_big<E, 15>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-            // scheduling variants (correct results; tools/ab_gemm_sched.py): 16 s_setprio around each MFMA
-            // cluster (cdna_hip_programming.md T5) measured 4-15 % SLOWER on every ViViT shape, 32 without the
-            // sched_group_barrier interleave within +-1 %: neither ships
-            case 163: return launch_big<E, 16>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-            case 323: return launch_big<E, 32>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-            case 483: return launch_big<E, 48>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-            case 164: return launch_persist<E, 16>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
-            case 324: return launch_persist<E, 32>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
-            case 484: return launch_persist<E, 48>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
-            default: break;
-        }
-    }
+    const int nbm = (int)(M / kCfgs[cfg].bm), nbn = (int)(N / kCfgs[cfg].bn);
     switch (cfg) {
         case 0: return launch_cfg<256, 128, 4, 2, E>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 1: return launch_cfg<128, 128, 2, 4, E>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
@@ -1052,18 +767,11 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
         case 3: return launch_big<E>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 5: return launch_cfg<128, 128, 2, 4, E, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 7: return launch_cfg<64, 128, 2, 4, E, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-        case 8: return launch_cfg<128, 128, 2, 4, E, 2, false>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-        case 9: return launch_cfg<128, 128, 2, 4, E, 2, true, true>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 4:
             if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
                           E == VC_EPI_BIAS_RELU_BF16 || E == VC_EPI_BIAS_GELU_TANH_SAVE)
                 return launch_persist<E>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s, aux, ldaux);
             return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 4 supports bf16-output epilogues only");
-        case 6:
-            if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
-                          E == VC_EPI_BIAS_RELU_BF16 || E == VC_EPI_BIAS_GELU_TANH_SAVE)
-                return launch_pp<E>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s, aux, ldaux);
-            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 6 supports bf16-output epilogues only");
     }
     return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad config");
 }
@@ -1125,21 +833,14 @@ extern "C" int vc_gemm_bf16_cfg(const uint16_t* A, int64_t lda, const uint16_t* 
         cfg = pick_cfg(M, N, K, epilogue);
         if (cfg == 4 && !st16_ok) cfg = 5;
     }
-    const int ablation = cfg >= 10 ? cfg : -1;  // x3 / x4 / x6: timing-only ablations of cfg 3 / 4 / 6 (wrong results)
-    if (ablation > 0) cfg = ablation % 10;
-    if (ablation > 0 && cfg != 3 && cfg != 4 && cfg != 6) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad config");
-    if (cfg < 0 || cfg >= kNumCfgs || M % kCfgs[cfg].bm || N % kCfgs[cfg].bn)
+    if (cfg < 0 || cfg >= kNumCfgs || kCfgs[cfg].bm == 0 || M % kCfgs[cfg].bm || N % kCfgs[cfg].bn)
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: no tile config divides M x N");
     if ((M / kCfgs[cfg].bm) * (N / kCfgs[cfg].bn) > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: grid too large");
     const int k = (int)K;
-    if ((cfg == 4 || cfg == 6) && (K % 32 || K / 32 < 6 || N > 8192 || !st16_ok ||
+    if (cfg == 4 && (K % 32 || K / 32 < 6 || N > 8192 || !st16_ok ||
                      (epilogue > VC_EPI_BIAS_GELU_ERF && epilogue != VC_EPI_BIAS_RELU_BF16 &&
                       epilogue != VC_EPI_BIAS_GELU_TANH_SAVE)))
-        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 4/6 need K%32==0, K>=192, N<=8192, ldo%8==0, bf16 epilogue");
-    if (ablation > 0) {
-        if (epilogue != VC_EPI_BIAS_BF16) return fail(VC_ERR_INVALID_ARG, "ablation: bias epilogue only");
-        return launch_epi<VC_EPI_BIAS_BF16>(ablation, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
-    }
+        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 4 needs K%32==0, K>=192, N<=8192, ldo%8==0, bf16 epilogue");
     switch (epilogue) {
         case VC_EPI_BIAS_BF16:
             return launch_epi<VC_EPI_BIAS_BF16>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);

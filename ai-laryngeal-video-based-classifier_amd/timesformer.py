@@ -99,7 +99,7 @@ class TimesformerForVideoClassification(torch.nn.Module):
         self._names = list(shapes.keys())
         self.kernel_events = None  # list: HIP events around each spatial-attention launch (bench.py)
         for name, shape in shapes.items():
-            self.params[name.replace(".", "__")] = torch.nn.Parameter(torch.zeros(shape), requires_grad=False)
+            self.params[name.replace(".", "__")] = torch.nn.Parameter(torch.zeros(shape))
         self._packed = None
         self._ws = {}
 
@@ -125,15 +125,20 @@ class TimesformerForVideoClassification(torch.nn.Module):
     def P(self, name):
         return self.params[name.replace(".", "__")]
 
+    def _weights_version(self):
+        from . import vivit_train
+        return (vivit_train.MASTER_EPOCH[0], sum(p._version for p in self.params.values()))
+
     def _pack(self, device):
-        if self._packed is not None and self._packed["device"] == device:
+        ver = self._weights_version()  # the fused AdamW updates in place without bumping _version
+        if self._packed is not None and self._packed["device"] == device and self._packed["version"] == ver:
             return self._packed
         c = self.config
         bf, f32 = torch.bfloat16, torch.float32
         P = lambda n: self.P(n).detach().to(device=device, dtype=f32)  # noqa: E731
         D, T = c.hidden_size, c.num_frames
         e = "timesformer.embeddings."
-        pk = {"device": device}
+        pk = {"device": device, "version": ver}
         pk["w_emb"] = P(e + "patch_embeddings.projection.weight").reshape(D, -1).to(bf).contiguous()
         pk["b_emb"] = P(e + "patch_embeddings.projection.bias").contiguous()
         pos = P(e + "position_embeddings").reshape(-1, D)
@@ -203,14 +208,20 @@ class TimesformerForVideoClassification(torch.nn.Module):
         self._ws = {key: ws}
         return ws
 
-    @torch.no_grad()
     def forward(self, pixel_values: torch.Tensor = None, labels: torch.Tensor = None, **kw):
+        """HF call convention.  In training mode with autograd enabled (the reference's train loop,
+        timesformer/timesformer_classifier/trainers/trainer.py:165-174) the logits carry the graph of
+        the HIP train step (_forward_train); otherwise the fused inference path runs."""
         if pixel_values is None:
             raise ValueError("pixel_values required")
         if pixel_values.device.type != "cuda":
             raise RuntimeError("TimesformerForVideoClassification (vclip_amd) runs on the GPU only")
         x = pixel_values.contiguous().float() if pixel_values.dtype != torch.float32 else pixel_values.contiguous()
-        logits = self.forward_logits(x)
+        if self.training and torch.is_grad_enabled():
+            logits = self._forward_train(x)
+        else:
+            with torch.no_grad():
+                logits = self.forward_logits(x)
         loss = None
         if labels is not None:
             loss = torch.nn.functional.cross_entropy(logits, labels.to(logits.device))
@@ -258,6 +269,67 @@ class TimesformerForVideoClassification(torch.nn.Module):
             ops.gemm(Hc, L["w_1"], L["b_1"], act, Hd)
             ops.gemm(Hd, L["w_2"], L["b_2"], "bias_resid_f32", X)
         return ops.cls_head(X, B, S, pk["lnf_g"], pk["lnf_b"], eps, pk["w_cls"], pk["b_cls"], out=ws["logits"])
+
+
+    def _forward_train(self, pix: torch.Tensor) -> torch.Tensor:
+        """The TimeSformer forward (TF5/models/timesformer/modeling_timesformer.py:67-145, 332-398,
+        oracle/timesformer_ref.py) as autograd ops over the HIP kernels (vclip_amd/autograd_ops.py):
+        bf16 MFMA GEMMs with fp32 accumulation on the fp32 master weights, fp32 residual stream,
+        exact GELU, flash spatial attention, VALU temporal attention; layout glue in torch."""
+        from . import autograd_ops as A
+        c = self.config
+        B, T, C, H, W = pix.shape
+        if T != c.num_frames or H != c.image_size or W != c.image_size or C != c.num_channels:
+            raise ValueError(f"pixel_values {tuple(pix.shape)} do not match config")
+        if c.hidden_act != "gelu":
+            raise NotImplementedError("train step: hidden_act 'gelu' (TimeSformer's) only")
+        D, Hn, eps, pc = c.hidden_size, c.num_attention_heads, c.layer_norm_eps, c.patch_size
+        P = (c.image_size // pc) ** 2
+        S = 1 + P * T
+        e = "timesformer.embeddings."
+        M = B * P * T
+        a_emb = torch.zeros(_round_up(M, 128), C * pc * pc, dtype=torch.bfloat16, device=pix.device)
+        ops.tubelet_im2col(pix, (1, pc, pc), a_emb, order="patch_major")  # rows (b, p, t)
+        emb = A.linear(a_emb[:M], self.P(e + "patch_embeddings.projection.weight").reshape(D, -1),
+                       self.P(e + "patch_embeddings.projection.bias"), out_f32=True)
+        pos = self.P(e + "position_embeddings").reshape(-1, D)
+        tim = self.P(e + "time_embeddings").reshape(-1, D)[:T]
+        emb = emb.reshape(B, P, T, D) + pos[1:].reshape(1, P, 1, D) + tim.reshape(1, 1, T, D)
+        cls = (self.P(e + "cls_token").reshape(1, 1, D) + pos[0].reshape(1, 1, D)).expand(B, 1, D)
+        x = torch.cat([cls, emb.reshape(B, P * T, D)], 1)  # [B, S, D] patch-major, time-minor
+        qs = (D // Hn) ** -0.5 * ops.LOG2E
+        for i in range(c.num_hidden_layers):
+            p = f"timesformer.encoder.layer.{i}."
+            W_ = lambda n: self.P(p + n)  # noqa: E731
+            # temporal branch on the clip layout (CLS rows computed and discarded, as inference)
+            h = A.layer_norm(x.reshape(B * S, D), W_("temporal_layernorm.weight"), W_("temporal_layernorm.bias"), eps)
+            qkv = A.linear(h, W_("temporal_attention.attention.qkv.weight"), W_("temporal_attention.attention.qkv.bias"),
+                           qrows=D, qscale=qs)
+            o = A.temporal_attention(qkv, B, P, T, Hn)
+            a = A.linear(o, W_("temporal_attention.output.dense.weight"), W_("temporal_attention.output.dense.bias"))
+            rt = A.linear(a, W_("temporal_dense.weight"), W_("temporal_dense.bias"), out_f32=True).reshape(B, S, D)
+            te = x[:, 1:] + rt[:, 1:]
+            # spatial branch: B*T sequences of CLS + P patches
+            init_cls = x[:, :1]
+            sp = te.reshape(B, P, T, D).permute(0, 2, 1, 3).reshape(B * T, P, D)
+            sp = torch.cat([init_cls.expand(B, T, D).reshape(B * T, 1, D), sp], 1)
+            h = A.layer_norm(sp.reshape(B * T * (1 + P), D), W_("layernorm_before.weight"), W_("layernorm_before.bias"),
+                             eps)
+            qkv = A.linear(h, W_("attention.attention.qkv.weight"), W_("attention.attention.qkv.bias"), qrows=D,
+                           qscale=qs)
+            o = A.attention(qkv, B * T, 1 + P, Hn)
+            y = A.linear(o, W_("attention.output.dense.weight"), W_("attention.output.dense.bias"),
+                         out_f32=True).reshape(B * T, 1 + P, D)
+            cls_res = y[:, 0].reshape(B, T, D).mean(1, keepdim=True)
+            res = y[:, 1:].reshape(B, T, P, D).permute(0, 2, 1, 3).reshape(B, P * T, D)
+            x = torch.cat([init_cls + cls_res, te + res], 1)
+            # MLP
+            h = A.layer_norm(x.reshape(B * S, D), W_("layernorm_after.weight"), W_("layernorm_after.bias"), eps)
+            g = A.gelu_erf(A.linear(h, W_("intermediate.dense.weight"), W_("intermediate.dense.bias")))
+            x = x + A.linear(g, W_("output.dense.weight"), W_("output.dense.bias"), out_f32=True).reshape(B, S, D)
+        return A.cls_head(x.reshape(B * S, D), self.P("timesformer.layernorm.weight"),
+                          self.P("timesformer.layernorm.bias"), self.P("classifier.weight"), self.P("classifier.bias"),
+                          B, S, eps)
 
 
 def create_model(model_name="facebook/timesformer-base-finetuned-k400", num_classes=2, class_labels=None,

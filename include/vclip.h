@@ -115,7 +115,7 @@ int vc_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
  * Same as vc_gemm_bf16 with an explicit block-tile configuration (tuning hook):
  *   cfg 0: 256x128, cfg 1: 128x128, cfg 2: 128x256, cfg 3: 256x256, cfg 4: 256x256 persistent
  *   (bf16-output epilogues 0/1/2/6 only), cfg 5: 128x128 with a 2-tile LDS ring (two workgroups
- *   per CU); -1 = automatic (measured choice, gemm.hip pick_cfg).
+ *   per CU), cfg 7: 64x128 (two workgroups per CU); -1 = automatic (measured choice, gemm.hip pick_cfg).
  */
 int vc_gemm_bf16_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
                      int64_t M, int64_t N, int64_t K, const float* bias, int epilogue,
@@ -398,6 +398,26 @@ int vc_cls_head_bwd(const float* x, int64_t ldx, int64_t B, int64_t S, int64_t D
  */
 int vc_embed_bwd(const float* dx, int64_t lddx, int64_t B, int64_t S, int64_t D, float* dpos, float* dcls,
                  uint16_t* demb, int64_t ldde, hipStream_t stream);
+
+/* ---- TimeSformer train step (timesformer/.../trainers/trainer.py:139-174) ---- */
+
+/*
+ * Temporal self-attention backward (TimesformerSelfAttention over the T frames of a patch,
+ * TF5/models/timesformer/modeling_timesformer.py:148-180, 332-349), on the clip layout of
+ * vc_temporal_attention: rows b*(1 + P*T) + 1 + p*T + t of qkv (q' = q * scale * log2 e | k | v,
+ * head h at column h*64 of each third), dout (dL/dO) and dqkv (written: dL/dq' | dL/dk | dL/dv;
+ * CLS rows untouched).  T <= 32.  Deterministic.
+ */
+int vc_temporal_attention_bwd(const uint16_t* qkv, int64_t ld, const uint16_t* dout, int64_t lddo, int64_t B, int64_t P,
+                              int64_t T, int64_t H, int64_t head_dim, uint16_t* dqkv, int64_t lddq, hipStream_t stream);
+
+/* Exact GELU x * Phi(x) on bf16 rows [M][N] (N % 8 == 0): TimeSformer / Swin hidden_act "gelu". */
+int vc_gelu_erf(const uint16_t* x, int64_t ldx, int64_t M, int64_t N, uint16_t* y, int64_t ldy, hipStream_t stream);
+
+/* Its backward: dx = dy * (Phi(x) + x phi(x)), x = the bf16 pre-activation, dy f32 (dy_bf16 = 0) or
+ * bf16 (dy_bf16 = 1), dx bf16. */
+int vc_gelu_erf_bwd(const void* dy, int dy_bf16, int64_t lddy, const uint16_t* x, int64_t ldx, int64_t M, int64_t N,
+                    uint16_t* dx, int64_t lddx, hipStream_t stream);
 
 /*
  * torch.optim.AdamW step (decoupled weight decay, bias-corrected) over flat f32 buffers, with the

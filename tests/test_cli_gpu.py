@@ -98,9 +98,10 @@ def test_eval_and_inference_clis(dataset, tmp_path, fam, extra):
                                str(tmp_path / "models"), "--skip_train", "--checkpoint_path", str(ck_path),
                                "--batch_size", "2"] + extra)
     assert (exp / "test_metrics_uniform.json").exists() and 0.0 <= m["accuracy"] <= 1.0
-    with pytest.raises(NotImplementedError):
-        run_main(fam, ["--data_dir", str(dataset), "--log_dir", str(tmp_path / "l2"), "--model_dir",
-                       str(tmp_path / "m2"), "--epochs", "1"] + extra)
+    if fam != "timesformer":  # the TimeSformer train step exists (test_timesformer_main_trains)
+        with pytest.raises(NotImplementedError):
+            run_main(fam, ["--data_dir", str(dataset), "--log_dir", str(tmp_path / "l2"), "--model_dir",
+                           str(tmp_path / "m2"), "--epochs", "1"] + extra)
     video = sorted((dataset / "test" / "referral").iterdir())[0]
     res = run_inference(fam, ["--video_path", str(video), "--model_path", str(ck_path), "--log_dir",
                               str(tmp_path / "ilogs")] + extra)
@@ -121,3 +122,16 @@ def test_vivit_main_skips_unreadable_clip(dataset, tmp_path):
     assert len(history["train_loss"]) == 1 and np.isfinite(history["train_loss"][0])
     log = "".join(p.read_text() for p in Path(exp).rglob("*.log"))
     assert "zz_broken.npy" in log
+
+
+def test_timesformer_main_trains(dataset, tmp_path):
+    """timesformer/main.py's default invocation trains (trainer.py:139-174): one epoch of the reference
+    loop on the HIP TimeSformer train step, best checkpoint in the reference dict schema, test metrics."""
+    from vclip_amd.apps import run_main
+    m, history, exp = run_main("timesformer", ["--data_dir", str(dataset), "--log_dir", str(tmp_path / "logs"),
+                                               "--model_dir", str(tmp_path / "models"), "--epochs", "1",
+                                               "--batch_size", "2", "--num_frames", "8"])
+    assert len(history["train_loss"]) == 1 and np.isfinite(history["train_loss"][0])
+    assert (exp / "test_metrics_uniform.json").exists()
+    ck = torch.load(tmp_path / "models" / "best_model_uniform.pth", weights_only=True)
+    assert "model_state_dict" in ck and "optimizer_state_dict" in ck and ck["num_frames"] == 8

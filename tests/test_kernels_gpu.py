@@ -108,7 +108,7 @@ def test_gemm_bias_bf16(M, N, K):
     assert err < 8e-3, err
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 7])
 @pytest.mark.parametrize("epi", ["bias", "bias_gelu_tanh"])
 def test_gemm_every_tile_config(cfg, epi):
     """Every block-tile configuration on a shape with more tiles than CUs (the persistent
@@ -126,20 +126,19 @@ def test_gemm_every_tile_config(cfg, epi):
 @pytest.mark.parametrize("M,N,K", [(768, 768, 192), (256, 256, 768), (2304, 768, 3072), (25344, 3072, 768),
                                    (4096, 2304, 256), (12800, 768, 768)])
 @pytest.mark.parametrize("epi", ["bias", "bias_gelu_erf", "bias_relu"])
-def test_gemm_pingpong_matches_persistent(M, N, K, epi):
-    """cfg 6 (staggered ping-pong schedule, staging cursor running across tiles) computes the
-    same MFMAs in the same k order as cfg 4: bit-identical outputs, at shapes with one tile
-    per workgroup, tile counts not a multiple of 8, the minimum K (6 half-tiles) and long K."""
+def test_gemm_persistent_edge_shapes(M, N, K, epi):
+    """cfg 4 (the persistent 256x256 kernel: next tile's loads in flight across the epilogue) at one
+    tile per workgroup, tile counts not a multiple of 8, the minimum K (6 half-tiles) and long K,
+    against fp32 math of the bf16 operands with the epilogue applied in torch."""
     a, w, bias, ref = _gemm_case(M, N, K, M + 7 * N + K)
-    ad, wd, bd = a.to(DEV), w.to(DEV), bias.to(DEV)
-    o4 = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
-    o6 = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
-    ops().gemm(ad, wd, bd, epi, o4, cfg=4)
-    ops().gemm(ad, wd, bd, epi, o6, cfg=6)
-    assert torch.equal(o4, o6)
-    if epi == "bias":
-        err = ((o6.float().cpu() - ref).abs() / (ref.abs() + 1.0)).max().item()
-        assert err < 8e-3, err
+    out = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+    ops().gemm(a.to(DEV), w.to(DEV), bias.to(DEV), epi, out, cfg=4)
+    if epi == "bias_gelu_erf":
+        ref = torch.nn.functional.gelu(ref)
+    elif epi == "bias_relu":
+        ref = torch.relu(ref)
+    err = ((out.float().cpu() - ref).abs() / (ref.abs() + 1.0)).max().item()
+    assert err < 8e-3, err
 
 
 @pytest.mark.parametrize("M,N,K,epi,main_cfg,tail_cfg", [
@@ -189,20 +188,16 @@ def test_gemm_gelu(act):
     assert err < 8e-3, err
 
 
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 5, 7, 8])
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 5, 7])
 def test_gemm_resid_f32(cfg):
-    """f32 residual epilogue on every 128/64-row config: cfgs 0-2, 5, 7 prefetch the residual
-    into registers before the K loop, cfg 8 reads it in the epilogue (bit-identical to 5)."""
+    """f32 residual epilogue on every 128/64-row config (each prefetches the residual into
+    registers before the K loop)."""
     M, N, K = 512, 768, 3072
     a, w, bias, ref = _gemm_case(M, N, K, 12)
     x0 = torch.randn(M, N)
     x = x0.clone().to(DEV)
     ops().gemm(a.to(DEV), w.to(DEV), bias.to(DEV), "bias_resid_f32", x, cfg=cfg)
     np.testing.assert_allclose(x.cpu().numpy(), (x0 + ref).numpy(), rtol=1e-4, atol=1e-4)
-    if cfg == 5:
-        x8 = x0.clone().to(DEV)
-        ops().gemm(a.to(DEV), w.to(DEV), bias.to(DEV), "bias_resid_f32", x8, cfg=8)
-        assert torch.equal(x, x8)
 
 
 def test_gemm_embed_remap():

@@ -51,10 +51,9 @@ def main():
         fl = 2.0 * M * N * K
         cands = {}
         for c in [int(x) for x in a.cfgs.split(",")]:
-            # c >= 10: timing ablations of cfg c % 10 (bias epilogue only; wrong results)
             bm, bn = {0: (256, 128), 1: (128, 128), 2: (128, 256), 3: (256, 256), 4: (256, 256),
-                      5: (128, 128), 6: (256, 256), 7: (64, 128)}[c % 10 if c >= 10 else c]
-            if (c in (4, 6) and "f32" in epi) or (c >= 10 and epi != "bias"):
+                      5: (128, 128), 7: (64, 128)}[c]
+            if c == 4 and "f32" in epi:
                 continue
             if M % bm or N % bn:
                 continue
