@@ -37,6 +37,12 @@ SIGNATURES = {
     "vc_layernorm_f32_bf16": ([c_p, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_p, c_i64, c_p], c_int),
     "vc_attention_fwd": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_int, c_p, c_i64, c_p], c_int),
     "vc_attention_fwd_rebase_always": ([c_p, c_i64, c_i64, c_i64, c_i64, c_f, c_p, c_i64, c_p], c_int),
+    "vc_patch_im2col_h16": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_int, c_int, c_int, c_p,
+                             c_i64, c_p], c_int),
+    "vc_gemm_h16": ([c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_int, c_p, c_i64, c_p, c_i64,
+                     c_i64, c_i64, c_i64, c_int, c_int, c_p], c_int),
+    "vc_layernorm_f32_h16": ([c_p, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_int, c_p, c_i64, c_p], c_int),
+    "vc_attention_fwd_h16": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_int, c_int, c_p, c_i64, c_p], c_int),
     "vc_cls_init": ([c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p], c_int),
     "vc_cls_head": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_p, c_p, c_i64, c_p, c_p], c_int),
     "vc_temporal_attention": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_int, c_p, c_i64, c_p], c_int),

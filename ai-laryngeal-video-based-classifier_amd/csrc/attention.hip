@@ -74,7 +74,8 @@ __device__ __forceinline__ void attn_sync() {
 // tile, cdna_hip_programming.md rule 26: must agree with the shipped build to rounding).
 // WLSE: also store the base-2 log-sum-exp of each query's scores, lse[(b*H + h)*S + q] =
 // m + log2(l) (running max and row sum), from which the backward kernels recompute P.
-template <bool REBASE_ALWAYS, bool WLSE>
+// ET: 16-bit operand type of q|k|v, P and out (VC_ELEM_BF16 / VC_ELEM_F16).
+template <bool REBASE_ALWAYS, bool WLSE, int ET = VC_ELEM_BF16>
 __global__ void __launch_bounds__(256, 2)
 attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, float c_log2,
                     uint16_t* __restrict__ out, int64_t ldo, float* __restrict__ lse) {
@@ -105,7 +106,7 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
         (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem);
 
     // ---- Q'^T fragments (B operand of S^T = K.Q'^T): lane holds Q'[q][d = 16kk + 8h + 0..7]
-    v8bf qf[QB][4];
+    v8s qf[QB][4];
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb) {
         const int q = qblk * AQ + (wave * QB + qb) * 32 + r;
@@ -115,10 +116,10 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
         for (int kk = 0; kk < 4; ++kk) {
             const v8s raw = *reinterpret_cast<const v8s*>(qrow + 16 * kk);
             if (c_log2 == 1.0f) {
-                qf[qb][kk] = __builtin_bit_cast(v8bf, raw);  // producer folded the scale into q
+                qf[qb][kk] = raw;  // producer folded the scale into q
             } else {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) qf[qb][kk][j] = (__bf16)(bf2f((unsigned short)raw[j]) * c_log2);
+                for (int j = 0; j < 8; ++j) qf[qb][kk][j] = (short)to16<ET>(from16<ET>((unsigned short)raw[j]) * c_log2);
             }
         }
     }
@@ -173,12 +174,12 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
     auto qk_mfma = [&](const char* slot, v16f (&sc)[QB][2]) {
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
-            const v8bf k0 = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(slot + koff[kk]));
-            const v8bf k1 = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(slot + koff[kk] + 4096));
+            const v8s k0 = *reinterpret_cast<const v8s*>(slot + koff[kk]);
+            const v8s k1 = *reinterpret_cast<const v8s*>(slot + koff[kk] + 4096);
 #pragma unroll
             for (int qb = 0; qb < QB; ++qb) {
-                sc[qb][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[qb][kk], kk == 0 ? minit[qb] : sc[qb][0], 0, 0, 0);
-                sc[qb][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[qb][kk], kk == 0 ? minit[qb] : sc[qb][1], 0, 0, 0);
+                sc[qb][0] = mfma32x16<ET>(k0, qf[qb][kk], kk == 0 ? minit[qb] : sc[qb][0]);
+                sc[qb][1] = mfma32x16<ET>(k1, qf[qb][kk], kk == 0 ? minit[qb] : sc[qb][1]);
             }
         }
     };
@@ -304,11 +305,15 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
-                v8bf pf[QB];
+                v8s pf[QB];
 #pragma unroll
-                for (int qb = 0; qb < QB; ++qb)
+                for (int qb = 0; qb < QB; ++qb) {
+                    v4u pu;
 #pragma unroll
-                    for (int jj = 0; jj < 8; ++jj) pf[qb][jj] = (__bf16)scur[qb][kb][8 * s2 + jj];
+                    for (int jj = 0; jj < 4; ++jj)
+                        pu[jj] = pack2<ET>(scur[qb][kb][8 * s2 + 2 * jj], scur[qb][kb][8 * s2 + 2 * jj + 1]);
+                    pf[qb] = __builtin_bit_cast(v8s, pu);
+                }
 #pragma unroll
                 for (int db = 0; db < 2; ++db) {
                     const char* pa = slot + voff[db] + (kb * 32 + 16 * s2) * 128;
@@ -317,11 +322,8 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
                     v8s vv;
                     vv[0] = va[0]; vv[1] = va[1]; vv[2] = va[2]; vv[3] = va[3];
                     vv[4] = vb[0]; vv[5] = vb[1]; vv[6] = vb[2]; vv[7] = vb[3];
-                    const v8bf vf = __builtin_bit_cast(v8bf, vv);
 #pragma unroll
-                    for (int qb = 0; qb < QB; ++qb) {
-                        o[qb][db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[qb], o[qb][db], 0, 0, 0);
-                    }
+                    for (int qb = 0; qb < QB; ++qb) o[qb][db] = mfma32x16<ET>(vv, pf[qb], o[qb][db]);
                 }
             }
 
@@ -372,8 +374,8 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
         for (int db = 0; db < 2; ++db)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                pk[db][g][0] = pack2bf(o[qb][db][4 * g + 0] * inv, o[qb][db][4 * g + 1] * inv);
-                pk[db][g][1] = pack2bf(o[qb][db][4 * g + 2] * inv, o[qb][db][4 * g + 3] * inv);
+                pk[db][g][0] = pack2<ET>(o[qb][db][4 * g + 0] * inv, o[qb][db][4 * g + 1] * inv);
+                pk[db][g][1] = pack2<ET>(o[qb][db][4 * g + 2] * inv, o[qb][db][4 * g + 3] * inv);
             }
         uint16_t* orow = out + (tok0 + qc) * ldo + hh * 64;
 #pragma unroll
@@ -389,11 +391,11 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
     }
 }
 
-template <bool REBASE_ALWAYS, bool WLSE>
+template <bool REBASE_ALWAYS, bool WLSE, int ET = VC_ELEM_BF16>
 static void launch_attn(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, float c_log2, uint16_t* out,
                         int64_t ldo, hipStream_t stream, float* lse = nullptr) {
     dim3 grid((unsigned)((S + 127) / 128), (unsigned)(B * H));
-    attn_fwd_d64_kernel<REBASE_ALWAYS, WLSE><<<grid, 256, NSLOT * KV_SLOT, stream>>>(qkv, ld, (int)S, (int)H, c_log2,
+    attn_fwd_d64_kernel<REBASE_ALWAYS, WLSE, ET><<<grid, 256, NSLOT * KV_SLOT, stream>>>(qkv, ld, (int)S, (int)H, c_log2,
                                                                                    out, ldo, lse);
 }
 
@@ -419,6 +421,19 @@ extern "C" int vc_attention_fwd(const uint16_t* qkv, int64_t ld, int64_t B, int6
     const float c_log2 = q_prescaled ? 1.0f : scale * 1.4426950408889634f;
     launch_attn<false, false>(qkv, ld, B, S, H, c_log2, out, ldo, stream);
     return check_launch("vc_attention_fwd");
+}
+
+// vc_attention_fwd with the 16-bit operand type as an argument (fp16: the inference forward's
+// higher-precision build, same kernel and MFMA rate).
+extern "C" int vc_attention_fwd_h16(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H,
+                                    int64_t head_dim, float scale, int q_prescaled, int elem, uint16_t* out,
+                                    int64_t ldo, hipStream_t stream) {
+    if (int rc = attn_checks(qkv, ld, B, S, H, head_dim, out, ldo)) return rc;
+    const float c_log2 = q_prescaled ? 1.0f : scale * 1.4426950408889634f;
+    if (elem == VC_ELEM_F16) launch_attn<false, false, VC_ELEM_F16>(qkv, ld, B, S, H, c_log2, out, ldo, stream);
+    else if (elem == VC_ELEM_BF16) launch_attn<false, false>(qkv, ld, B, S, H, c_log2, out, ldo, stream);
+    else return fail(VC_ERR_INVALID_ARG, "vc_attention_fwd_h16: bad elem");
+    return check_launch("vc_attention_fwd_h16");
 }
 
 // Training forward: vc_attention_fwd plus the base-2 log-sum-exp per (clip, head, query).

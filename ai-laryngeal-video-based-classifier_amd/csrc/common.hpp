@@ -40,6 +40,47 @@ __device__ __forceinline__ float bf2f(unsigned short u) {
     return __builtin_bit_cast(float, ((unsigned int)u) << 16);
 }
 
+// ---- 16-bit operand type of the inference forward (VC_ELEM_BF16 / VC_ELEM_F16).  Both run
+// the same 32x32x16 MFMA rate; fp16 trades exponent range for 3 more mantissa bits (the
+// ViViT-B logits move from ~4e-3 to ~7e-4 of the fp32 reference).  Kernels
+// templated on ET keep their operands as raw 16-bit lanes (v8s) and go through these.
+typedef _Float16 v2h __attribute__((ext_vector_type(2)));
+typedef _Float16 v8h __attribute__((ext_vector_type(8)));
+// two f32 -> one packed 16-bit pair (v_cvt_pk_bf16_f32 / v_cvt_pk_f16_f32, RNE)
+template <int ET>
+__device__ __forceinline__ unsigned int pack2(float lo, float hi) {
+    const v2f x = {lo, hi};
+    if constexpr (ET == VC_ELEM_F16) return __builtin_bit_cast(unsigned int, __builtin_convertvector(x, v2h));
+    else return __builtin_bit_cast(unsigned int, __builtin_convertvector(x, v2bf));
+}
+template <int ET>
+__device__ __forceinline__ unsigned short to16(float x) {
+    if constexpr (ET == VC_ELEM_F16) return __builtin_bit_cast(unsigned short, (_Float16)x);
+    else return f2bf(x);
+}
+template <int ET>
+__device__ __forceinline__ float from16(unsigned short u) {
+    if constexpr (ET == VC_ELEM_F16) return (float)__builtin_bit_cast(_Float16, u);
+    else return bf2f(u);
+}
+// D = A.B + C over one 32x32x16 block, operands as raw 16-bit lanes
+template <int ET>
+__device__ __forceinline__ v16f mfma32x16(v8s a, v8s b, v16f c) {
+    if constexpr (ET == VC_ELEM_F16)
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(v8h, a), __builtin_bit_cast(v8h, b), c, 0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf, a), __builtin_bit_cast(v8bf, b), c, 0, 0, 0);
+}
+// D = A.B + C over one 16x16x32 block: lane l holds A[l & 15][8(l >> 4) .. +7], B likewise,
+// and D[4(l >> 4) + e][l & 15] in c[e]
+template <int ET>
+__device__ __forceinline__ v4f mfma16x32(v8s a, v8s b, v4f c) {
+    if constexpr (ET == VC_ELEM_F16)
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(v8h, a), __builtin_bit_cast(v8h, b), c, 0, 0, 0);
+    else
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v8bf, a), __builtin_bit_cast(v8bf, b), c, 0, 0, 0);
+}
+
 __device__ __forceinline__ float gelu_tanh(float x) {
     // gelu_fast: 0.5x(1+tanh(u)), u = 0.7978845608 x (1 + 0.044715 x^2)  (TF5/activations.py)
     // evaluated as x * sigmoid(2u) = x / (1 + 2^(-2u log2 e)): one v_exp_f32 + one v_rcp_f32

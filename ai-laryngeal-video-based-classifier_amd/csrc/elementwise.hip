@@ -106,7 +106,7 @@ __global__ void __launch_bounds__(256) gather_norm_kernel(const uint8_t* __restr
 // the TimeSformer token order).  One thread converts VEC consecutive pixels of one image
 // row (VEC = 8, or 4 for 4-wide patches such as Swin's 2x4x4).
 // ---------------------------------------------------------------------------------
-template <int VEC>
+template <int VEC, int ET = VC_ELEM_BF16>
 __global__ void __launch_bounds__(256) im2col_kernel(const float* __restrict__ pix, int64_t totalv, int T, int C,
                                                      int H, int W, int kt, int kh, int kw, int order, int layout,
                                                      uint16_t* __restrict__ A, int64_t lda) {
@@ -133,15 +133,15 @@ __global__ void __launch_bounds__(256) im2col_kernel(const float* __restrict__ p
     if constexpr (VEC == 8) {
         const float4 v = s[1];
         uint4 o;
-        o.x = pack2bf(u.x, u.y);
-        o.y = pack2bf(u.z, u.w);
-        o.z = pack2bf(v.x, v.y);
-        o.w = pack2bf(v.z, v.w);
+        o.x = pack2<ET>(u.x, u.y);
+        o.y = pack2<ET>(u.z, u.w);
+        o.z = pack2<ET>(v.x, v.y);
+        o.w = pack2<ET>(v.z, v.w);
         *reinterpret_cast<uint4*>(A + m * lda + k) = o;
     } else {
         uint2 o;
-        o.x = pack2bf(u.x, u.y);
-        o.y = pack2bf(u.z, u.w);
+        o.x = pack2<ET>(u.x, u.y);
+        o.y = pack2<ET>(u.z, u.w);
         *reinterpret_cast<uint2*>(A + m * lda + k) = o;
     }
 }
@@ -149,7 +149,7 @@ __global__ void __launch_bounds__(256) im2col_kernel(const float* __restrict__ p
 // ---------------------------------------------------------------------------------
 // LayerNorm f32 -> bf16, one wave per row, D = 64*V*4 (V float4 per lane).
 // ---------------------------------------------------------------------------------
-template <int V>
+template <int V, int ET = VC_ELEM_BF16>
 __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict__ x, int64_t ldx, int64_t M,
                                                         const float* __restrict__ g, const float* __restrict__ be,
                                                         float eps, uint16_t* __restrict__ y, int64_t ldy) {
@@ -179,15 +179,15 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
     for (int i = 0; i < V; ++i) {
         const float4 gg = g4[i * 64 + lane], bb = b4[i * 64 + lane];
         uint2 o;
-        o.x = pack2bf((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y);
-        o.y = pack2bf((v[i].z - mean) * rstd * gg.z + bb.z, (v[i].w - mean) * rstd * gg.w + bb.w);
+        o.x = pack2<ET>((v[i].x - mean) * rstd * gg.x + bb.x, (v[i].y - mean) * rstd * gg.y + bb.y);
+        o.y = pack2<ET>((v[i].z - mean) * rstd * gg.z + bb.z, (v[i].w - mean) * rstd * gg.w + bb.w);
         *reinterpret_cast<uint2*>(y + row * ldy + (i * 64 + lane) * 4) = o;
     }
 }
 
 // LayerNorm for any D % 4 == 0, D <= 1024 (Swin's 96/192/384, TimeSformer-tiny 128 ...):
 // one wave per row held in registers (up to 4 float4 per lane, masked), single HBM pass.
-template <bool OUTF32>
+template <bool OUTF32, int ET = VC_ELEM_BF16>
 __global__ void __launch_bounds__(256) layernorm_reg_kernel(const float* __restrict__ x, int64_t ldx, int64_t M, int D,
                                                             const float* __restrict__ g, const float* __restrict__ be,
                                                             float eps, void* __restrict__ y, int64_t ldy) {
@@ -224,8 +224,8 @@ __global__ void __launch_bounds__(256) layernorm_reg_kernel(const float* __restr
                 *reinterpret_cast<float4*>(reinterpret_cast<float*>(y) + row * ldy + n) = make_float4(o0, o1, o2, o3);
             } else {
                 uint2 o;
-                o.x = pack2bf(o0, o1);
-                o.y = pack2bf(o2, o3);
+                o.x = pack2<ET>(o0, o1);
+                o.y = pack2<ET>(o2, o3);
                 *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(y) + row * ldy + n) = o;
             }
         }
@@ -236,7 +236,7 @@ __global__ void __launch_bounds__(256) layernorm_reg_kernel(const float* __restr
 // 64 / L rows per wave, each lane V float4 (masked past D), single HBM pass, reductions over
 // the L-lane group.  A whole wave per 96-wide row (layernorm_reg_kernel) leaves 40 of 64
 // lanes idle and launches one wave per 384 bytes: 47 us for Swin-T stage 1 at B = 4 (2.5 TB/s).
-template <int L, int V, bool OUTF32>
+template <int L, int V, bool OUTF32, int ET = VC_ELEM_BF16>
 __global__ void __launch_bounds__(256) layernorm_grp_kernel(const float* __restrict__ x, int64_t ldx, int64_t M, int D,
                                                             const float* __restrict__ g, const float* __restrict__ be,
                                                             float eps, void* __restrict__ y, int64_t ldy) {
@@ -273,8 +273,8 @@ __global__ void __launch_bounds__(256) layernorm_grp_kernel(const float* __restr
                 *reinterpret_cast<float4*>(reinterpret_cast<float*>(y) + row * ldy + n) = make_float4(o0, o1, o2, o3);
             } else {
                 uint2 o;
-                o.x = pack2bf(o0, o1);
-                o.y = pack2bf(o2, o3);
+                o.x = pack2<ET>(o0, o1);
+                o.y = pack2<ET>(o2, o3);
                 *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(y) + row * ldy + n) = o;
             }
         }
@@ -291,14 +291,14 @@ static inline int grp_lanes(int64_t D, int* V) {
     return 0;
 }
 
-template <bool OUTF32>
+template <bool OUTF32, int ET = VC_ELEM_BF16>
 static bool launch_ln_grp(const float* x, int64_t ldx, int64_t M, int64_t D, const float* g, const float* be, float eps,
                           void* y, int64_t ldy, hipStream_t stream) {
     int V = 0;
     const int L = grp_lanes(D, &V);
     if (!L) return false;
     const unsigned nb = (unsigned)((M * L + 255) / 256);
-#define VC_LN_GRP(LL, VV) layernorm_grp_kernel<LL, VV, OUTF32><<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, g, be, eps, y, ldy)
+#define VC_LN_GRP(LL, VV) layernorm_grp_kernel<LL, VV, OUTF32, ET><<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, g, be, eps, y, ldy)
     if (L == 8) { if (V == 3) VC_LN_GRP(8, 3); else VC_LN_GRP(8, 4); }
     else if (L == 16) { if (V == 3) VC_LN_GRP(16, 3); else VC_LN_GRP(16, 4); }
     else { if (V == 3) VC_LN_GRP(32, 3); else VC_LN_GRP(32, 4); }
@@ -308,7 +308,7 @@ static bool launch_ln_grp(const float* x, int64_t ldx, int64_t M, int64_t D, con
 
 // Generic-width LayerNorm (any D): one wave per row, three passes over the row (L1/L2-resident).
 // OUTF32: the output is f32 (y is a float*), e.g. Swin's patch_embed.norm feeding the residual stream.
-template <bool OUTF32 = false>
+template <bool OUTF32 = false, int ET = VC_ELEM_BF16>
 __global__ void __launch_bounds__(256) layernorm_any_kernel(const float* __restrict__ x, int64_t ldx, int64_t M,
                                                             int D, const float* __restrict__ g,
                                                             const float* __restrict__ be, float eps,
@@ -331,7 +331,7 @@ __global__ void __launch_bounds__(256) layernorm_any_kernel(const float* __restr
         if constexpr (OUTF32)
             reinterpret_cast<float*>(y)[row * ldy + n] = v;
         else
-            reinterpret_cast<uint16_t*>(y)[row * ldy + n] = f2bf(v);
+            reinterpret_cast<uint16_t*>(y)[row * ldy + n] = to16<ET>(v);
     }
 }
 
@@ -419,8 +419,10 @@ int vc_frame_gather(const uint8_t* frames, int64_t nclips, int64_t F, int64_t H,
     return check_launch("vc_frame_gather");
 }
 
-int vc_patch_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C, int64_t H, int64_t W, int kt, int kh,
-                    int kw, int token_order, int layout, uint16_t* A, int64_t lda, hipStream_t stream) {
+int vc_patch_im2col_h16(const float* pixel_values, int64_t B, int64_t T, int64_t C, int64_t H, int64_t W, int kt,
+                        int kh, int kw, int token_order, int layout, int elem, uint16_t* A, int64_t lda,
+                        hipStream_t stream) {
+    if (elem != VC_ELEM_BF16 && elem != VC_ELEM_F16) return fail(VC_ERR_INVALID_ARG, "vc_patch_im2col: bad elem");
     if (!pixel_values || !A) return fail(VC_ERR_INVALID_ARG, "vc_patch_im2col: null pointer");
     if (kt <= 0 || kh <= 0 || kw <= 0 || T % kt || H % kh || W % kw || kw % 4 || W % 4 || lda % 4 ||
         lda < C * kt * kh * kw || ((uintptr_t)pixel_values & 15) || ((uintptr_t)A & 7))
@@ -430,14 +432,30 @@ int vc_patch_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C, 
     if (layout != VC_VIDEO_BTCHW && layout != VC_VIDEO_BCTHW) return fail(VC_ERR_INVALID_ARG, "vc_patch_im2col: bad layout");
     if (kw % 8 == 0 && lda % 8 == 0 && !((uintptr_t)A & 15)) {
         const int64_t totalv = B * T * C * H * (W / 8);
-        im2col_kernel<8><<<(unsigned)((totalv + 255) / 256), 256, 0, stream>>>(
-            pixel_values, totalv, (int)T, (int)C, (int)H, (int)W, kt, kh, kw, token_order, layout, A, lda);
+        const unsigned nb = (unsigned)((totalv + 255) / 256);
+        if (elem == VC_ELEM_F16)
+            im2col_kernel<8, VC_ELEM_F16><<<nb, 256, 0, stream>>>(pixel_values, totalv, (int)T, (int)C, (int)H, (int)W,
+                                                                 kt, kh, kw, token_order, layout, A, lda);
+        else
+            im2col_kernel<8><<<nb, 256, 0, stream>>>(pixel_values, totalv, (int)T, (int)C, (int)H, (int)W, kt, kh, kw,
+                                                    token_order, layout, A, lda);
     } else {
         const int64_t totalv = B * T * C * H * (W / 4);
-        im2col_kernel<4><<<(unsigned)((totalv + 255) / 256), 256, 0, stream>>>(
-            pixel_values, totalv, (int)T, (int)C, (int)H, (int)W, kt, kh, kw, token_order, layout, A, lda);
+        const unsigned nb = (unsigned)((totalv + 255) / 256);
+        if (elem == VC_ELEM_F16)
+            im2col_kernel<4, VC_ELEM_F16><<<nb, 256, 0, stream>>>(pixel_values, totalv, (int)T, (int)C, (int)H, (int)W,
+                                                                 kt, kh, kw, token_order, layout, A, lda);
+        else
+            im2col_kernel<4><<<nb, 256, 0, stream>>>(pixel_values, totalv, (int)T, (int)C, (int)H, (int)W, kt, kh, kw,
+                                                    token_order, layout, A, lda);
     }
     return check_launch("vc_patch_im2col");
+}
+
+int vc_patch_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C, int64_t H, int64_t W, int kt, int kh,
+                    int kw, int token_order, int layout, uint16_t* A, int64_t lda, hipStream_t stream) {
+    return vc_patch_im2col_h16(pixel_values, B, T, C, H, W, kt, kh, kw, token_order, layout, VC_ELEM_BF16, A, lda,
+                               stream);
 }
 
 int vc_tubelet_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C, int64_t H, int64_t W, int kt,
@@ -445,25 +463,40 @@ int vc_tubelet_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C
     return vc_patch_im2col(pixel_values, B, T, C, H, W, kt, kh, kw, VC_TOKENS_TIME_MAJOR, VC_VIDEO_BTCHW, A, lda, stream);
 }
 
-int vc_layernorm_f32_bf16(const float* x, int64_t ldx, int64_t M, int64_t D, const float* gamma, const float* beta,
-                          float eps, uint16_t* y, int64_t ldy, hipStream_t stream) {
+// Row LayerNorm f32 -> 16-bit (ET) for any D: register kernels for the ViViT widths, the
+// grouped / register / three-pass kernels for the rest.
+extern "C++" template <int ET>
+static int layernorm16(const float* x, int64_t ldx, int64_t M, int64_t D, const float* gamma, const float* beta,
+                       float eps, uint16_t* y, int64_t ldy, hipStream_t stream) {
     if (!x || !gamma || !beta || !y) return fail(VC_ERR_INVALID_ARG, "vc_layernorm: null pointer");
     if (ldx % 4 || ldy % 4) return fail(VC_ERR_INVALID_ARG, "vc_layernorm: ld must be a multiple of 4");
     const unsigned nb = (unsigned)((M + 3) / 4);
     switch (D) {
-        case 256: layernorm_kernel<1><<<nb, 256, 0, stream>>>(x, ldx, M, gamma, beta, eps, y, ldy); break;
-        case 512: layernorm_kernel<2><<<nb, 256, 0, stream>>>(x, ldx, M, gamma, beta, eps, y, ldy); break;
-        case 768: layernorm_kernel<3><<<nb, 256, 0, stream>>>(x, ldx, M, gamma, beta, eps, y, ldy); break;
-        case 1024: layernorm_kernel<4><<<nb, 256, 0, stream>>>(x, ldx, M, gamma, beta, eps, y, ldy); break;
+        case 256: layernorm_kernel<1, ET><<<nb, 256, 0, stream>>>(x, ldx, M, gamma, beta, eps, y, ldy); break;
+        case 512: layernorm_kernel<2, ET><<<nb, 256, 0, stream>>>(x, ldx, M, gamma, beta, eps, y, ldy); break;
+        case 768: layernorm_kernel<3, ET><<<nb, 256, 0, stream>>>(x, ldx, M, gamma, beta, eps, y, ldy); break;
+        case 1024: layernorm_kernel<4, ET><<<nb, 256, 0, stream>>>(x, ldx, M, gamma, beta, eps, y, ldy); break;
         default:
             if (D <= 0 || D > 65536) return fail(VC_ERR_INVALID_ARG, "vc_layernorm: bad D");
             if (D <= 1024 && D % 4 == 0 && !(((uintptr_t)x | (uintptr_t)gamma | (uintptr_t)beta) & 15) && !((uintptr_t)y & 7)) {
-                if (ldx % 4 == 0 && ldy % 4 == 0 && launch_ln_grp<false>(x, ldx, M, D, gamma, beta, eps, y, ldy, stream)) break;
-                layernorm_reg_kernel<false><<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, gamma, beta, eps, y, ldy);
+                if (launch_ln_grp<false, ET>(x, ldx, M, D, gamma, beta, eps, y, ldy, stream)) break;
+                layernorm_reg_kernel<false, ET><<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, gamma, beta, eps, y, ldy);
             } else
-                layernorm_any_kernel<false><<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, gamma, beta, eps, y, ldy);
+                layernorm_any_kernel<false, ET><<<nb, 256, 0, stream>>>(x, ldx, M, (int)D, gamma, beta, eps, y, ldy);
     }
-    return check_launch("vc_layernorm_f32_bf16");
+    return check_launch("vc_layernorm_f32_h16");
+}
+
+int vc_layernorm_f32_h16(const float* x, int64_t ldx, int64_t M, int64_t D, const float* gamma, const float* beta,
+                         float eps, int elem, uint16_t* y, int64_t ldy, hipStream_t stream) {
+    if (elem == VC_ELEM_F16) return layernorm16<VC_ELEM_F16>(x, ldx, M, D, gamma, beta, eps, y, ldy, stream);
+    if (elem == VC_ELEM_BF16) return layernorm16<VC_ELEM_BF16>(x, ldx, M, D, gamma, beta, eps, y, ldy, stream);
+    return fail(VC_ERR_INVALID_ARG, "vc_layernorm: bad elem");
+}
+
+int vc_layernorm_f32_bf16(const float* x, int64_t ldx, int64_t M, int64_t D, const float* gamma, const float* beta,
+                          float eps, uint16_t* y, int64_t ldy, hipStream_t stream) {
+    return layernorm16<VC_ELEM_BF16>(x, ldx, M, D, gamma, beta, eps, y, ldy, stream);
 }
 
 int vc_layernorm_f32(const float* x, int64_t ldx, int64_t M, int64_t D, const float* gamma, const float* beta,

@@ -20,6 +20,7 @@
 #include "common.hpp"
 
 #include <cmath>
+#include <type_traits>
 
 namespace vc {
 
@@ -47,9 +48,8 @@ __device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
-__device__ __forceinline__ v8bf lds_frag(const char* tile, int row, int chunk) {
-    const v8s v = *reinterpret_cast<const v8s*>(tile + row * 128 + swz(row, chunk) * 16);
-    return __builtin_bit_cast(v8bf, v);
+__device__ __forceinline__ v8s lds_frag(const char* tile, int row, int chunk) {
+    return *reinterpret_cast<const v8s*>(tile + row * 128 + swz(row, chunk) * 16);
 }
 
 // s_waitcnt through the builtin (not inline asm) so the compiler's own wait-count
@@ -67,9 +67,74 @@ __device__ __forceinline__ void block_sync_lds() {
     __builtin_amdgcn_sched_barrier(0);
 }
 
+// One lane's 4 consecutive output columns n..n+3 of row m (bias already added): the epilogue
+// body shared by the 32x32 and 16x16 block layouts.
+template <int EPI, int ET>
+__device__ __forceinline__ void store4(int64_t m, int64_t n, float v0, float v1, float v2, float v3,
+                                       void* __restrict__ out, int64_t ldo, const float* __restrict__ aux,
+                                       int64_t ldaux, int64_t G, int64_t gstride, int64_t goff) {
+    if (EPI == VC_EPI_BIAS_GELU_TANH_SAVE || EPI == VC_EPI_DGELU_TANH) {
+        uint2* ap = reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(const_cast<float*>(aux)) + m * ldaux + n);
+        if (EPI == VC_EPI_BIAS_GELU_TANH_SAVE) {
+            // keep the bf16 pre-activation for the backward's gelu'
+            uint2 pre;
+            pre.x = pack2bf(v0, v1);
+            pre.y = pack2bf(v2, v3);
+            *ap = pre;
+            v0 = gelu_tanh(v0); v1 = gelu_tanh(v1); v2 = gelu_tanh(v2); v3 = gelu_tanh(v3);
+        } else {
+            const uint2 pre = *ap;
+            v0 *= dgelu_tanh(bf2f((unsigned short)(pre.x & 0xffff)));
+            v1 *= dgelu_tanh(bf2f((unsigned short)(pre.x >> 16)));
+            v2 *= dgelu_tanh(bf2f((unsigned short)(pre.y & 0xffff)));
+            v3 *= dgelu_tanh(bf2f((unsigned short)(pre.y >> 16)));
+        }
+        uint2 p;
+        p.x = pack2bf(v0, v1);
+        p.y = pack2bf(v2, v3);
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + m * ldo + n) = p;
+    } else if (EPI == VC_EPI_BIAS_ADD_F32) {
+        const float4 a = *reinterpret_cast<const float4*>(aux + m * ldaux + n);
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + m * ldo + n) =
+            make_float4(a.x + v0, a.y + v1, a.z + v2, a.w + v3);
+    } else if (EPI == VC_EPI_BIAS_BF16 || EPI == VC_EPI_BIAS_GELU_TANH || EPI == VC_EPI_BIAS_GELU_ERF ||
+        EPI == VC_EPI_BIAS_RELU_BF16 || EPI == VC_EPI_BIAS_RESID_RELU_BF16) {
+        if (EPI == VC_EPI_BIAS_GELU_TANH) {
+            v0 = gelu_tanh(v0); v1 = gelu_tanh(v1); v2 = gelu_tanh(v2); v3 = gelu_tanh(v3);
+        } else if (EPI == VC_EPI_BIAS_GELU_ERF) {
+            v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+        } else if (EPI == VC_EPI_BIAS_RELU_BF16 || EPI == VC_EPI_BIAS_RESID_RELU_BF16) {
+            if (EPI == VC_EPI_BIAS_RESID_RELU_BF16) {
+                const uint2 rr = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(aux) + m * ldaux + n);
+                v0 += bf2f((unsigned short)(rr.x & 0xffff)); v1 += bf2f((unsigned short)(rr.x >> 16));
+                v2 += bf2f((unsigned short)(rr.y & 0xffff)); v3 += bf2f((unsigned short)(rr.y >> 16));
+            }
+            v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+        }
+        uint2 p;
+        p.x = pack2<ET>(v0, v1);
+        p.y = pack2<ET>(v2, v3);
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + m * ldo + n) = p;
+    } else if (EPI == VC_EPI_BIAS_RESID_F32) {
+        float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + m * ldo + n);
+        float4 x = *o;
+        x.x += v0; x.y += v1; x.z += v2; x.w += v3;
+        *o = x;
+    } else if (EPI == VC_EPI_BIAS_F32) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + m * ldo + n) = make_float4(v0, v1, v2, v3);
+    } else {  // VC_EPI_EMBED_F32
+        const int64_t gi = m / G, gr = m - gi * G;
+        const float4 a = *reinterpret_cast<const float4*>(aux + gr * ldaux + n);
+        float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(out) +
+                                              (gi * gstride + goff + gr) * ldo + n);
+        *o = make_float4(v0 + a.x, v1 + a.y, v2 + a.z, v3 + a.w);
+    }
+}
+
 // Epilogue shared by the GEMM kernels.  acc[i][j] holds D[n][m] of a 32x32 block:
 // lane -> m = mb + 32i + r; reg 4g+e -> n = nb + 32j + 8g + 4h + e (4 consecutive columns).
-template <int EPI, int MI, int NI>
+// ET: 16-bit type of the plain 16-bit outputs (epilogues 0-2; the others are bf16-only)
+template <int EPI, int MI, int NI, int ET = VC_ELEM_BF16>
 __device__ __forceinline__ void store_tile(const v16f (&acc)[MI][NI], int64_t mb, int64_t nb, int r, int h,
                                            const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
                                            const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride,
@@ -99,8 +164,8 @@ __device__ __forceinline__ void store_tile(const v16f (&acc)[MI][NI], int64_t mb
                         } else if (EPI == VC_EPI_BIAS_RELU_BF16) {
                             v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
                         }
-                        pk[g][0] = pack2bf(v0, v1);
-                        pk[g][1] = pack2bf(v2, v3);
+                        pk[g][0] = pack2<ET>(v0, v1);
+                        pk[g][1] = pack2<ET>(v2, v3);
                     }
 #pragma unroll
                     for (int g = 0; g < 4; g += 2) {
@@ -125,69 +190,66 @@ __device__ __forceinline__ void store_tile(const v16f (&acc)[MI][NI], int64_t mb
             for (int g = 0; g < 4; ++g) {
                 const int64_t n = nb + j * 32 + g * 8 + h * 4;
                 const float4 bb = *reinterpret_cast<const float4*>(bias + n);
-                float v0 = acc[i][j][4 * g + 0] + bb.x;
-                float v1 = acc[i][j][4 * g + 1] + bb.y;
-                float v2 = acc[i][j][4 * g + 2] + bb.z;
-                float v3 = acc[i][j][4 * g + 3] + bb.w;
-                if (EPI == VC_EPI_BIAS_GELU_TANH_SAVE || EPI == VC_EPI_DGELU_TANH) {
-                    uint2* ap = reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(const_cast<float*>(aux)) + m * ldaux + n);
-                    if (EPI == VC_EPI_BIAS_GELU_TANH_SAVE) {
-                        // keep the bf16 pre-activation for the backward's gelu'
-                        uint2 pre;
-                        pre.x = pack2bf(v0, v1);
-                        pre.y = pack2bf(v2, v3);
-                        *ap = pre;
-                        v0 = gelu_tanh(v0); v1 = gelu_tanh(v1); v2 = gelu_tanh(v2); v3 = gelu_tanh(v3);
-                    } else {
-                        const uint2 pre = *ap;
-                        v0 *= dgelu_tanh(bf2f((unsigned short)(pre.x & 0xffff)));
-                        v1 *= dgelu_tanh(bf2f((unsigned short)(pre.x >> 16)));
-                        v2 *= dgelu_tanh(bf2f((unsigned short)(pre.y & 0xffff)));
-                        v3 *= dgelu_tanh(bf2f((unsigned short)(pre.y >> 16)));
-                    }
-                    uint2 p;
-                    p.x = pack2bf(v0, v1);
-                    p.y = pack2bf(v2, v3);
-                    *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + m * ldo + n) = p;
-                } else if (EPI == VC_EPI_BIAS_ADD_F32) {
-                    const float4 a = *reinterpret_cast<const float4*>(aux + m * ldaux + n);
-                    *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + m * ldo + n) =
-                        make_float4(a.x + v0, a.y + v1, a.z + v2, a.w + v3);
-                } else if (EPI == VC_EPI_BIAS_BF16 || EPI == VC_EPI_BIAS_GELU_TANH || EPI == VC_EPI_BIAS_GELU_ERF ||
-                    EPI == VC_EPI_BIAS_RELU_BF16 || EPI == VC_EPI_BIAS_RESID_RELU_BF16) {
-                    if (EPI == VC_EPI_BIAS_GELU_TANH) {
-                        v0 = gelu_tanh(v0); v1 = gelu_tanh(v1); v2 = gelu_tanh(v2); v3 = gelu_tanh(v3);
-                    } else if (EPI == VC_EPI_BIAS_GELU_ERF) {
-                        v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
-                    } else if (EPI == VC_EPI_BIAS_RELU_BF16 || EPI == VC_EPI_BIAS_RESID_RELU_BF16) {
-                        if (EPI == VC_EPI_BIAS_RESID_RELU_BF16) {
-                            const uint2 rr = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(aux) + m * ldaux + n);
-                            v0 += bf2f((unsigned short)(rr.x & 0xffff)); v1 += bf2f((unsigned short)(rr.x >> 16));
-                            v2 += bf2f((unsigned short)(rr.y & 0xffff)); v3 += bf2f((unsigned short)(rr.y >> 16));
-                        }
-                        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
-                    }
-                    uint2 p;
-                    p.x = pack2bf(v0, v1);
-                    p.y = pack2bf(v2, v3);
-                    *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + m * ldo + n) = p;
-                } else if (EPI == VC_EPI_BIAS_RESID_F32) {
-                    float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + m * ldo + n);
-                    float4 x = *o;
-                    x.x += v0; x.y += v1; x.z += v2; x.w += v3;
-                    *o = x;
-                } else if (EPI == VC_EPI_BIAS_F32) {
-                    *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + m * ldo + n) = make_float4(v0, v1, v2, v3);
-                } else {  // VC_EPI_EMBED_F32
-                    const int64_t gi = m / G, gr = m - gi * G;
-                    const float4 a = *reinterpret_cast<const float4*>(aux + gr * ldaux + n);
-                    float4* o = reinterpret_cast<float4*>(reinterpret_cast<float*>(out) +
-                                                          (gi * gstride + goff + gr) * ldo + n);
-                    *o = make_float4(v0 + a.x, v1 + a.y, v2 + a.z, v3 + a.w);
-                }
+                store4<EPI, ET>(m, n, acc[i][j][4 * g + 0] + bb.x, acc[i][j][4 * g + 1] + bb.y, acc[i][j][4 * g + 2] + bb.z,
+                                acc[i][j][4 * g + 3] + bb.w, out, ldo, aux, ldaux, G, gstride, goff);
             }
         }
     }
+}
+
+// Epilogue of the 16x16x32 kernels: acc[i][j] holds D[n][m] of a 16x16 block, lane (c16, q) ->
+// m = mb + 16i + c16, reg e -> n = nb + 16j + 4q + e.  Plain 16-bit outputs pair blocks j, j+1
+// with v_permlane16_swap so each lane stores 8 consecutive columns (16 B).
+template <int EPI, int MI, int NI, int ET = VC_ELEM_BF16>
+__device__ __forceinline__ void store_tile16(const v4f (&acc)[MI][NI], int64_t mb, int64_t nb, int c16, int q,
+                                             const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
+                                             const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride,
+                                             int64_t goff) {
+    constexpr bool PLAIN16 = EPI == VC_EPI_BIAS_BF16 || EPI == VC_EPI_BIAS_GELU_TANH || EPI == VC_EPI_BIAS_GELU_ERF ||
+                             EPI == VC_EPI_BIAS_RELU_BF16;
+    if constexpr (PLAIN16 && NI % 2 == 0) {
+        if ((ldo & 7) == 0 && ((uintptr_t)out & 15) == 0) {
+#pragma unroll
+            for (int i = 0; i < MI; ++i) {
+                uint16_t* orow = reinterpret_cast<uint16_t*>(out) + (mb + i * 16 + c16) * ldo;
+#pragma unroll
+                for (int jp = 0; jp < NI / 2; ++jp) {
+                    unsigned pk[2][2];
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const float4 bb = *reinterpret_cast<const float4*>(bias + nb + (2 * jp + s) * 16 + 4 * q);
+                        float v0 = acc[i][2 * jp + s][0] + bb.x, v1 = acc[i][2 * jp + s][1] + bb.y;
+                        float v2 = acc[i][2 * jp + s][2] + bb.z, v3 = acc[i][2 * jp + s][3] + bb.w;
+                        if (EPI == VC_EPI_BIAS_GELU_TANH) {
+                            v0 = gelu_tanh(v0); v1 = gelu_tanh(v1); v2 = gelu_tanh(v2); v3 = gelu_tanh(v3);
+                        } else if (EPI == VC_EPI_BIAS_GELU_ERF) {
+                            v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+                        } else if (EPI == VC_EPI_BIAS_RELU_BF16) {
+                            v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+                        }
+                        pk[s][0] = pack2<ET>(v0, v1);
+                        pk[s][1] = pack2<ET>(v2, v3);
+                    }
+                    // even q: block 2jp, columns 4q .. 4q+7; odd q: block 2jp+1, columns 4(q-1) .. 4(q-1)+7
+                    auto s0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+                    auto s1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+                    uint4 v;
+                    v.x = s0[0]; v.y = s1[0]; v.z = s0[1]; v.w = s1[1];
+                    *reinterpret_cast<uint4*>(orow + nb + (2 * jp + (q & 1)) * 16 + 4 * (q & 2)) = v;
+                }
+            }
+            return;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+            const int64_t m = mb + i * 16 + c16, n = nb + j * 16 + 4 * q;
+            const float4 bb = *reinterpret_cast<const float4*>(bias + n);
+            store4<EPI, ET>(m, n, acc[i][j][0] + bb.x, acc[i][j][1] + bb.y, acc[i][j][2] + bb.z, acc[i][j][3] + bb.w,
+                            out, ldo, aux, ldaux, G, gstride, goff);
+        }
 }
 
 // ST: LDS ring depth in tiles (prefetch distance ST - 1).  ST = 2 at 128x128 needs 64 KiB of
@@ -197,7 +259,10 @@ __device__ __forceinline__ void store_tile(const v16f (&acc)[MI][NI], int64_t mb
 // 128x128; +0.4 % on the ViViT-B forward in an interleaved A/B, round 1).
 // (A static s_setprio for one of two co-resident workgroups measured slower here, unlike in
 // the attention kernel: o_proj 67.0 vs 64.4 us, fc2 152.6 vs 151.0; round 1.)
-template <int BM, int BN, int WM, int WN, int EPI, int ST = 3>
+// The wave tile is built from 16x16 blocks of v_mfma_f32_16x16x32, two 32-deep k-steps per
+// 64-deep tile (the shape sustains more FLOP/s than 32x32x16 under the power-limited clock; see
+// the persistent kernel below): ViViT-B B=8 o_proj 552 vs 516 TF/s, fc2 864 vs 784 at 128x128.
+template <int BM, int BN, int WM, int WN, int EPI, int ST = 3, int ET = VC_ELEM_BF16>
 __global__ void __launch_bounds__(512, ST == 2 ? 2 : 1)
 gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
                  int nbm, int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
@@ -206,22 +271,22 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
     static_assert(ST == 2 || ST == 3, "ring depth");
     constexpr int SLOT = (BM + BN) * 128;       // bytes per ring slot (A then W, 128-B rows)
     constexpr int TM = BM / WM, TN = BN / WN;   // wave tile
-    constexpr int MI = TM / 32, NI = TN / 32;
+    constexpr int MI = TM / 16, NI = TN / 16;
     constexpr int AL = BM / 64, BL = BN / 64;   // glds per thread per tile (8 rows per wave-instr, 8 waves)
     constexpr int LPT = AL + BL;
     static_assert(WM * WN == 8 && TM % 32 == 0 && TN % 32 == 0, "8 waves, 32-multiple wave tiles");
 
     const int nwg = nbm * nbn;
     const int bid = blockIdx.x;
-    const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
-    const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+    const int xcd = bid & 7, xq = nwg >> 3, rr = nwg & 7;
+    const int wgid = (xcd < rr ? xcd * (xq + 1) : rr * (xq + 1) + (xcd - rr) * xq) + (bid >> 3);
     const int tm = wgid / nbn, tn = wgid % nbn;
     const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave % WN;
-    const int r = lane & 31, h = lane >> 5;
+    const int c16 = lane & 15, q = lane >> 4;
 
     // per-lane staging sources (k offset added per tile)
     const uint16_t* asrc[AL];
@@ -248,27 +313,25 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
             glds16(bsrc[i] + k0, __builtin_amdgcn_readfirstlane(s + BM * 128 + (wave * (BN / 8) + i * 8) * 128));
     };
 
-    v16f acc[MI][NI];
+    v4f acc[MI][NI];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < NI; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+        for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
     const int nk = K / GBK;
     stage(0, 0);
+    // lane (c16, q) holds output row m0 + wm*TM + 16i + c16, columns n0 + wn*TN + 16j + 4q .. +3
     constexpr bool RPRE = EPI == VC_EPI_BIAS_RESID_F32;
-    float4 xres[RPRE ? MI : 1][RPRE ? NI : 1][4];
+    float4 xres[RPRE ? MI : 1][RPRE ? NI : 1];
     if constexpr (RPRE) {
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int j = 0; j < NI; ++j)
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    xres[i][j][g] = *reinterpret_cast<const float4*>(
-                        reinterpret_cast<const float*>(out) + (m0 + wm * TM + i * 32 + r) * ldo + n0 + wn * TN + j * 32 + g * 8 + h * 4);
+                xres[i][j] = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(out) +
+                                                              (m0 + wm * TM + i * 16 + c16) * ldo + n0 + wn * TN +
+                                                              j * 16 + 4 * q);
     }
     if (ST == 3 && nk > 1) {
         stage(1, 1);
@@ -284,26 +347,25 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
         const char* At = smem + slot * SLOT;
         const char* Wt = At + BM * 128;
 
-        v8bf af[2][MI], wf[2][NI];
+        v8s af[2][MI], wf[2][NI];
+        {
+            // two 32-deep k-steps: lane (c16, q) reads row 16i + c16, 16-B chunk 4kk + q (the 16
+            // rows of a ds_read_b128 lane group land on 16 distinct bank slots under swz)
 #pragma unroll
-        for (int i = 0; i < MI; ++i) af[0][i] = lds_frag(At, wm * TM + i * 32 + r, h);
+            for (int i = 0; i < MI; ++i) af[0][i] = lds_frag(At, wm * TM + i * 16 + c16, q);
 #pragma unroll
-        for (int j = 0; j < NI; ++j) wf[0][j] = lds_frag(Wt, wn * TN + j * 32 + r, h);
+            for (int j = 0; j < NI; ++j) wf[0][j] = lds_frag(Wt, wn * TN + j * 16 + c16, q);
 #pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-            const int cb = kk & 1, nb = cb ^ 1;
-            if (kk < 3) {
-                const int ch = (kk + 1) * 2 + h;
+            for (int i = 0; i < MI; ++i) af[1][i] = lds_frag(At, wm * TM + i * 16 + c16, 4 + q);
 #pragma unroll
-                for (int i = 0; i < MI; ++i) af[nb][i] = lds_frag(At, wm * TM + i * 32 + r, ch);
+            for (int j = 0; j < NI; ++j) wf[1][j] = lds_frag(Wt, wn * TN + j * 16 + c16, 4 + q);
 #pragma unroll
-                for (int j = 0; j < NI; ++j) wf[nb][j] = lds_frag(Wt, wn * TN + j * 32 + r, ch);
-            }
+            for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-            for (int i = 0; i < MI; ++i)
+                for (int i = 0; i < MI; ++i)
 #pragma unroll
-                for (int j = 0; j < NI; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[cb][j], af[cb][i], acc[i][j], 0, 0, 0);
+                    for (int j = 0; j < NI; ++j)
+                        acc[i][j] = mfma16x32<ET>(wf[kk][j], af[kk][i], acc[i][j]);
         }
         // retire tile t+1 (with ST = 3, tile t+2 may stay in flight), then all waves pass the barrier
         if (ST == 3 && t + 2 < nk) wait_vm<LPT>();
@@ -316,19 +378,19 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
         for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int j = 0; j < NI; ++j)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const int64_t m = m0 + wm * TM + i * 32 + r, n = n0 + wn * TN + j * 32 + g * 8 + h * 4;
-                    const float4 bb = *reinterpret_cast<const float4*>(bias + n);
-                    float4 x = xres[i][j][g];
-                    x.x += acc[i][j][4 * g + 0] + bb.x;
-                    x.y += acc[i][j][4 * g + 1] + bb.y;
-                    x.z += acc[i][j][4 * g + 2] + bb.z;
-                    x.w += acc[i][j][4 * g + 3] + bb.w;
-                    *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + m * ldo + n) = x;
-                }
+            {
+                const int64_t m = m0 + wm * TM + i * 16 + c16, n = n0 + wn * TN + j * 16 + 4 * q;
+                const float4 bb = *reinterpret_cast<const float4*>(bias + n);
+                float4 x = xres[i][j];
+                x.x += acc[i][j][0] + bb.x;
+                x.y += acc[i][j][1] + bb.y;
+                x.z += acc[i][j][2] + bb.z;
+                x.w += acc[i][j][3] + bb.w;
+                *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + m * ldo + n) = x;
+            }
     } else {
-        store_tile<EPI, MI, NI>(acc, m0 + wm * TM, n0 + wn * TN, r, h, bias, out, ldo, aux, ldaux, G, gstride, goff);
+        store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bias, out, ldo, aux, ldaux, G, gstride,
+                                      goff);
     }
 }
 
@@ -341,12 +403,11 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
 // ---------------------------------------------------------------------------------
 __device__ __forceinline__ int swz64(int r, int c) { return c ^ ((r >> 2) & 3); }
 
-__device__ __forceinline__ v8bf lds_frag64(const char* tile, int row, int chunk) {
-    const v8s v = *reinterpret_cast<const v8s*>(tile + row * 64 + swz64(row, chunk) * 16);
-    return __builtin_bit_cast(v8bf, v);
+__device__ __forceinline__ v8s lds_frag64(const char* tile, int row, int chunk) {
+    return *reinterpret_cast<const v8s*>(tile + row * 64 + swz64(row, chunk) * 16);
 }
 
-template <int EPI>
+template <int EPI, int ET = VC_ELEM_BF16>
 __global__ void __launch_bounds__(512, 1)
 gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
                      int nbm, int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
@@ -399,7 +460,7 @@ gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
 
     const int nk = K / BKH;
     // fragments of one 16-deep k-step (kk) of half-tile t
-    auto read_frags = [&](int t, int kk, v8bf (&fa)[MI], v8bf (&fw)[NI]) {
+    auto read_frags = [&](int t, int kk, v8s (&fa)[MI], v8s (&fw)[NI]) {
         const char* At = smem + (t % NS) * SLOT;
         const char* Wt = At + BM * 64;
         const int ch = kk * 2 + h;
@@ -408,12 +469,12 @@ gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
 #pragma unroll
         for (int j = 0; j < NI; ++j) fw[j] = lds_frag64(Wt, wn * TN + j * 32 + r, ch);
     };
-    auto mfmas = [&](const v8bf (&fa)[MI], const v8bf (&fw)[NI]) {
+    auto mfmas = [&](const v8s (&fa)[MI], const v8s (&fw)[NI]) {
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int j = 0; j < NI; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[j], fa[i], acc[i][j], 0, 0, 0);
+                acc[i][j] = mfma32x16<ET>(fw[j], fa[i], acc[i][j]);
     };
     // 6 fragment reads ride between 8 MFMAs
     auto interleave = [&]() {
@@ -426,7 +487,7 @@ gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
     };
 
     // prologue: half-tiles 0..2 in flight; wait for 0, read its first k-step
-    v8bf fa0[MI], fw0[NI], fa1[MI], fw1[NI];
+    v8s fa0[MI], fw0[NI], fa1[MI], fw1[NI];
     stage(0);
     if (nk > 1) stage(1);
     if (nk > 2) stage(2);
@@ -457,111 +518,58 @@ gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
     read_frags(nk - 1, 1, fa1, fw1);
     mfmas(fa0, fw0);
     mfmas(fa1, fw1);
-    store_tile<EPI, MI, NI>(acc, m0 + wm * TM, n0 + wn * TN, r, h, bias, out, ldo, aux, ldaux, G, gstride, goff);
+    store_tile<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, r, h, bias, out, ldo, aux, ldaux, G, gstride, goff);
 }
 
 // ---------------------------------------------------------------------------------
-// Persistent variant of the 256x256 kernel for the bf16-output epilogues (q|k|v, fc1):
-// one workgroup per CU walks its tiles; the next tile's first three half-tiles are put in
-// flight BEFORE the current tile's epilogue, so the epilogue stores (and the prologue
-// latency) hide behind the next tile's loads.  The bias lives in LDS (no VMEM in the
-// epilogue, so the counted vmcnt stays exact), and each lane's 4+4 columns are merged
-// with v_permlane32_swap into 16-byte stores (cdna_hip_programming.md T21).
+// Persistent 256x256 kernel for the 16-bit-output epilogues (q|k|v, fc1; cfg 4): one workgroup
+// per CU walks its tiles; the next tile's first three half-tiles (BK = 32, 4-slot LDS ring,
+// counted vmcnt, one barrier per half-tile) go in flight BEFORE the current tile's epilogue,
+// so the epilogue stores and the prologue latency hide behind the next tile's loads.  The bias
+// lives in LDS (no VMEM in the epilogue, so the counted vmcnt stays exact).  Wave tile 128 x 64
+// = 8 x 4 blocks of v_mfma_f32_16x16x32, one MFMA per block per half-tile.  Under the power-limited clocks of a dense
+// MFMA loop the 16x16x32 shape sustains more FLOP/s than 32x32x16 at equal cycles per FLOP
+// (MI355X_MICROARCH.md DVFS item 7: 1.12-1.14x with LDS-fed operands; measured here, same
+// schedule on 32x32x16: 4096^3 1279 vs 1139 TF/s, ViViT-B q|k|v 1007 vs 911, fc1 964 vs 928).  Per half-tile a wave
+// runs two 16-MFMA groups over output rows 0-63 / 64-127 of its tile: the row-64..127 A
+// fragments are read under the first group, the next half-tile's row-0..63 A and all W
+// fragments (second register set) under the second, after the barrier that publishes it.
+// Epilogue: lane (c = l & 15, q = l >> 4) holds 4 consecutive columns of row c per block;
+// v_permlane16_swap pairs blocks j, j+1 so each lane stores 8 consecutive columns (16 B).
 // ---------------------------------------------------------------------------------
-// Epilogue of the 256x256 persistent kernels: + bias (LDS), activation, bf16, lane-pair
-// swap -> 16-B row stores (MI*NI*2 stores per wave, twice that with the saved pre-activation).
-template <int EPI, int MI, int NI, int TM, int TN>
-__device__ __forceinline__ void epi256(const v16f (&acc)[MI][NI], int64_t m0, int64_t n0, int wm, int wn, int r, int h,
-                                       const float* bias_lds, uint16_t* __restrict__ out, int64_t ldo,
-                                       uint16_t* __restrict__ pre_out, int64_t ldpre) {
-    constexpr bool SAVE = EPI == VC_EPI_BIAS_GELU_TANH_SAVE;
-    // epilogue: + bias (LDS), activation, bf16, lane-pair swap -> 16-B row stores
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-        const int64_t m = m0 + wm * TM + i * 32 + r;
-        uint16_t* orow = out + m * ldo;
-        uint16_t* prow = SAVE ? pre_out + m * ldpre : nullptr;
-#pragma unroll
-        for (int j = 0; j < NI; ++j) {
-            unsigned pk[4][2], pp[4][2];
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int nl = (int)n0 + wn * TN + j * 32 + g * 8 + h * 4;
-                const float4 bb = *reinterpret_cast<const float4*>(bias_lds + nl);
-                float v0 = acc[i][j][4 * g + 0] + bb.x;
-                float v1 = acc[i][j][4 * g + 1] + bb.y;
-                float v2 = acc[i][j][4 * g + 2] + bb.z;
-                float v3 = acc[i][j][4 * g + 3] + bb.w;
-                if constexpr (SAVE) {
-                    pp[g][0] = pack2bf(v0, v1);
-                    pp[g][1] = pack2bf(v2, v3);
-                }
-                if (EPI == VC_EPI_BIAS_GELU_TANH || SAVE) {
-                    v0 = gelu_tanh(v0); v1 = gelu_tanh(v1); v2 = gelu_tanh(v2); v3 = gelu_tanh(v3);
-                } else if (EPI == VC_EPI_BIAS_GELU_ERF) {
-                    v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
-                } else if (EPI == VC_EPI_BIAS_RELU_BF16) {
-                    v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
-                }
-                pk[g][0] = pack2bf(v0, v1);
-                pk[g][1] = pack2bf(v2, v3);
-            }
-#pragma unroll
-            for (int g = 0; g < 4; g += 2) {
-                // lower half: cols 8g..8g+7 (own g | upper's g); upper half: 8g+8..8g+15
-                auto s0 = __builtin_amdgcn_permlane32_swap(pk[g][0], pk[g + 1][0], false, false);
-                auto s1 = __builtin_amdgcn_permlane32_swap(pk[g][1], pk[g + 1][1], false, false);
-                const int64_t col = n0 + wn * TN + j * 32 + g * 8 + h * 8;
-                uint4 v;
-                v.x = s0[0]; v.y = s1[0]; v.z = s0[1]; v.w = s1[1];
-                *reinterpret_cast<uint4*>(orow + col) = v;
-                if constexpr (SAVE) {
-                    auto q0 = __builtin_amdgcn_permlane32_swap(pp[g][0], pp[g + 1][0], false, false);
-                    auto q1 = __builtin_amdgcn_permlane32_swap(pp[g][1], pp[g + 1][1], false, false);
-                    uint4 u;
-                    u.x = q0[0]; u.y = q1[0]; u.z = q0[1]; u.w = q1[1];
-                    *reinterpret_cast<uint4*>(prow + col) = u;
-                }
-            }
-        }
-    }
-}
-
-template <int EPI>
+template <int EPI, int ET = VC_ELEM_BF16>
 __global__ void __launch_bounds__(512, 1)
 gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
-                         int nbm, int nbn, int K, int N, const float* __restrict__ bias, uint16_t* __restrict__ out,
-                         int64_t ldo, uint16_t* __restrict__ pre_out, int64_t ldpre) {
+                      int nbm, int nbn, int K, int N, const float* __restrict__ bias, uint16_t* __restrict__ out,
+                      int64_t ldo, uint16_t* __restrict__ pre_out, int64_t ldpre) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int BM = 256, BN = 256, BKH = 32, NS = 4;
-    constexpr int SLOT = (BM + BN) * 64;   // 32 KiB
-    constexpr int TM = 128, TN = 64, MI = 4, NI = 2;
-    constexpr bool SAVE = EPI == VC_EPI_BIAS_GELU_TANH_SAVE;  // + bf16 pre-activation to pre_out
-    constexpr int NST = MI * NI * 2 * (SAVE ? 2 : 1);          // 16-B stores per wave per tile epilogue
+    constexpr int SLOT = (BM + BN) * 64;  // 32 KiB
+    constexpr int TM = 128, TN = 64, MI = 8, NI = 4, MH = MI / 2;
+    constexpr bool SAVE = EPI == VC_EPI_BIAS_GELU_TANH_SAVE;
+    constexpr int NST = MI * (NI / 2) * (SAVE ? 2 : 1);  // 16-B stores per wave per tile epilogue
     float* bias_lds = reinterpret_cast<float*>(smem + NS * SLOT);
 
     const int ntiles = nbm * nbn;
-    const int G = gridDim.x;               // multiple of 8 (host guarantees)
+    const int G = gridDim.x;
     const int b = blockIdx.x;
-    const int lane_slot = (b & 7) * (G >> 3) + (b >> 3);  // XCD-contiguous slot of this WG in a round
+    const int lane_slot = (b & 7) * (G >> 3) + (b >> 3);
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
-    const int r = lane & 31, h = lane >> 5;
+    const int c16 = lane & 15, q = lane >> 4;
 
-    // bias -> LDS once
     for (int n = tid * 4; n < N; n += 512 * 4)
         *reinterpret_cast<float4*>(bias_lds + n) = *reinterpret_cast<const float4*>(bias + n);
     __syncthreads();
 
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
     const int nk = K / BKH;
-    const int arow = wave * 32 + (lane >> 2);           // staging row (+16 for the second piece)
+    const int arow = wave * 32 + (lane >> 2);
     const int acol0 = swz64(arow, lane & 3) * 8;
     const int acol1 = swz64(arow + 16, lane & 3) * 8;
-
-    auto stage = [&](int64_t m0, int64_t n0, int t, int slotidx) {
+    auto stage = [&](int64_t m0, int64_t n0, int t, int slotidx) __attribute__((always_inline)) {
         const uint32_t s = lds0 + (slotidx % NS) * SLOT;
         const int64_t k0 = (int64_t)t * BKH;
         glds16(A + (m0 + arow) * lda + k0 + acol0, __builtin_amdgcn_readfirstlane(s + (wave * 32) * 64));
@@ -570,32 +578,42 @@ gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint
         glds16(W + (n0 + arow + 16) * ldw + k0 + acol1,
                __builtin_amdgcn_readfirstlane(s + BM * 64 + (wave * 32 + 16) * 64));
     };
-    auto read_frags = [&](int slotidx, int kk, v8bf (&fa)[MI], v8bf (&fw)[NI]) {
+    // fragments of a half-tile (ring slot): A rows wm*TM + 16i + c16 for i in [i0, i0 + 4) and W rows
+    // wn*TN + 16j + c16 for j in [j0, j0 + 2), k-chunk q
+    auto read_a = [&](int slotidx, int i0, v8s (&fa)[4]) __attribute__((always_inline)) {
         const char* At = smem + (slotidx % NS) * SLOT;
-        const char* Wt = At + BM * 64;
-        const int ch = kk * 2 + h;
 #pragma unroll
-        for (int i = 0; i < MI; ++i) fa[i] = lds_frag64(At, wm * TM + i * 32 + r, ch);
-#pragma unroll
-        for (int j = 0; j < NI; ++j) fw[j] = lds_frag64(Wt, wn * TN + j * 32 + r, ch);
+        for (int i = 0; i < 4; ++i) fa[i] = lds_frag64(At, wm * TM + (i0 + i) * 16 + c16, q);
     };
-    v16f acc[MI][NI];
-    auto mfmas = [&](const v8bf (&fa)[MI], const v8bf (&fw)[NI]) {
+    auto read_w = [&](int slotidx, int j0, v8s (&fw)[2]) __attribute__((always_inline)) {
+        const char* Wt = smem + (slotidx % NS) * SLOT + BM * 64;
 #pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int j = 0; j < NI; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[j], fa[i], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) fw[j] = lds_frag64(Wt, wn * TN + (j0 + j) * 16 + c16, q);
     };
-    auto interleave = [&]() {
+    v4f acc[MI][NI];
+    // one output quadrant (4 x 2 blocks) of the wave tile: 8 MFMAs
+    auto quad = [&](auto I0, auto J0, const v8s (&fa)[4], const v8s (&fw)[2]) __attribute__((always_inline)) {
+        constexpr int i0 = decltype(I0)::value, j0 = decltype(J0)::value;
 #pragma unroll
-        for (int i = 0; i < 6; ++i) {
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i0 + i][j0 + j] = mfma16x32<ET>(fw[j], fa[i], acc[i0 + i][j0 + j]);
+    };
+    // NR fragment reads ride between a quadrant's 8 MFMAs
+    auto interleave = [&](auto NR) __attribute__((always_inline)) {
+        constexpr int nr = decltype(NR)::value;
+#pragma unroll
+        for (int i = 0; i < nr; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 8 - nr, 0);
     };
-    auto tile_origin = [&](int it, int64_t& m0, int64_t& n0) {
+    using C0 = std::integral_constant<int, 0>;
+    using C2 = std::integral_constant<int, 2>;
+    using C4 = std::integral_constant<int, 4>;
+    using C6 = std::integral_constant<int, 6>;
+    auto tile_origin = [&](int it, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
         const int tile = it * G + lane_slot;
         const int tm = tile / nbn, tn = tile - (tile / nbn) * nbn;
         m0 = (int64_t)tm * BM;
@@ -606,55 +624,90 @@ gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint
     if (it * G + lane_slot >= ntiles) return;
     int64_t m0, n0;
     tile_origin(0, m0, n0);
-    int sbase = 0;  // ring slot of this tile's half-tile 0
+    int sbase = 0;
     stage(m0, n0, 0, sbase + 0);
     stage(m0, n0, 1, sbase + 1);
     stage(m0, n0, 2, sbase + 2);
     wait_vm<8>();
     block_sync_lds();
-    v8bf fa0[MI], fw0[NI], fa1[MI], fw1[NI];
-    read_frags(sbase, 0, fa0, fw0);
+    // two register sets for the fragments that cross a half-tile boundary (A rows 0-63, W
+    // columns 0-31 and 32-63); A rows 64-127 are read and consumed inside one half-tile
+    v8s aloA[4], w01A[2], w23A[2], aloB[4], w01B[2], w23B[2], ahi[4];
+    auto read_head = [&](int slotidx) __attribute__((always_inline)) {
+        read_a(slotidx, 0, aloA);
+        read_w(slotidx, 0, w01A);
+        read_w(slotidx, 2, w23A);
+    };
+    read_head(sbase);
     bool first = true;
+
+    // half-tile t (t < nk - 1), quadrants (lo, 01) (lo, 23) | barrier | (hi, 23) (hi, 01):
+    // rows 64-127 of t are read under the first quadrant, t + 1's lo / 01 / 23 fragments under the
+    // last two, after the barrier that publishes t + 1.  PH (compile time, so the steady-state
+    // body is one branch-free block): 0 head (t = 0, 1: stage t + 3; the previous epilogue's NST
+    // stores are younger than half-tile t + 1), 1 main (stage t + 3, retire t + 1 with t + 2,
+    // t + 3 in flight), 2 (t = nk - 3: retire t + 1 with t + 2 in flight), 3 (t = nk - 2: drain).
+    auto step = [&](auto PH, int t, v8s (&alo)[4], v8s (&w01)[2], v8s (&w23)[2], v8s (&alo2)[4],
+                    v8s (&w012)[2], v8s (&w232)[2]) __attribute__((always_inline)) {
+        constexpr int ph = decltype(PH)::value;
+        if constexpr (ph <= 1) stage(m0, n0, t + 3, sbase + t + 3);
+        read_a(sbase + t, 4, ahi);
+        quad(C0{}, C0{}, alo, w01);
+        interleave(C4{});
+        quad(C0{}, C2{}, alo, w23);
+        if constexpr (ph == 0) {
+            if (first) wait_vm<8>();
+            else wait_vm<8 + NST>();
+        } else if constexpr (ph == 1) {
+            wait_vm<8>();
+        } else if constexpr (ph == 2) {
+            wait_vm<4>();
+        } else {
+            wait_vm<0>();
+        }
+        block_sync_lds();
+        read_a(sbase + t + 1, 0, alo2);
+        read_w(sbase + t + 1, 0, w012);
+        quad(C4{}, C2{}, ahi, w23);
+        interleave(C6{});
+        read_w(sbase + t + 1, 2, w232);
+        quad(C4{}, C0{}, ahi, w01);
+        interleave(C2{});
+    };
+    auto last = [&](int t, v8s (&alo)[4], v8s (&w01)[2], v8s (&w23)[2]) __attribute__((always_inline)) {
+        __builtin_amdgcn_sched_barrier(0);  // keeps the scheduler from overlapping two half-tiles' fragments
+        read_a(sbase + t, 4, ahi);
+        quad(C0{}, C0{}, alo, w01);
+        quad(C0{}, C2{}, alo, w23);
+        quad(C4{}, C2{}, ahi, w23);
+        quad(C4{}, C0{}, ahi, w01);
+    };
+    using Head = std::integral_constant<int, 0>;
+    using Main = std::integral_constant<int, 1>;
+    using Tail4 = std::integral_constant<int, 2>;
+    using Tail0 = std::integral_constant<int, 3>;
 
     while (true) {
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
-            for (int j = 0; j < NI; ++j)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-        // half-tiles 0 and 1: the previous epilogue's NST stores are younger than t+1
-        for (int t = 0; t < 2; ++t) {
-            stage(m0, n0, t + 3, sbase + t + 3);
-            read_frags(sbase + t, 1, fa1, fw1);
-            mfmas(fa0, fw0);
-            interleave();
-            if (first) wait_vm<8>();
-            else wait_vm<8 + NST>();
-            block_sync_lds();
-            read_frags(sbase + t + 1, 0, fa0, fw0);
-            mfmas(fa1, fw1);
-            interleave();
+            for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+        step(Head{}, 0, aloA, w01A, w23A, aloB, w01B, w23B);
+        step(Head{}, 1, aloB, w01B, w23B, aloA, w01A, w23A);
+        // nk = K / 32 is even (K % 64 == 0): main pairs t = 2 .. nk - 5, one more main step, the
+        // tail nk - 3, nk - 2 and the last half-tile nk - 1 -- one straight-line path, so each
+        // accumulator stays in its registers (a parity-dependent two-way tail made hipcc rename
+        // the accumulators across the join and spill ~300 VGPRs)
+        int t = 2;
+        for (; t < nk - 4; t += 2) {
+            step(Main{}, t, aloA, w01A, w23A, aloB, w01B, w23B);
+            step(Main{}, t + 1, aloB, w01B, w23B, aloA, w01A, w23A);
         }
-        for (int t = 2; t < nk - 1; ++t) {
-            if (t + 3 < nk) stage(m0, n0, t + 3, sbase + t + 3);
-            read_frags(sbase + t, 1, fa1, fw1);
-            mfmas(fa0, fw0);
-            interleave();
-            if (t + 3 < nk) wait_vm<8>();
-            else if (t + 2 < nk) wait_vm<4>();
-            else wait_vm<0>();
-            block_sync_lds();
-            read_frags(sbase + t + 1, 0, fa0, fw0);
-            mfmas(fa1, fw1);
-            interleave();
-        }
-        read_frags(sbase + nk - 1, 1, fa1, fw1);
-        mfmas(fa0, fw0);
-        mfmas(fa1, fw1);
+        step(Main{}, t, aloA, w01A, w23A, aloB, w01B, w23B);
+        step(Tail4{}, t + 1, aloB, w01B, w23B, aloA, w01A, w23A);
+        step(Tail0{}, t + 2, aloA, w01A, w23A, aloB, w01B, w23B);
+        last(t + 3, aloB, w01B, w23B);
 
-        // next tile's first three half-tiles go in flight before this tile's epilogue
         ++it;
         const bool more = it * G + lane_slot < ntiles;
         int64_t nm0 = 0, nn0 = 0;
@@ -666,16 +719,59 @@ gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint
             stage(nm0, nn0, 2, nbase + 2);
         }
 
-        epi256<EPI, MI, NI, TM, TN>(acc, m0, n0, wm, wn, r, h, bias_lds, out, ldo, pre_out, ldpre);
+        // epilogue: + bias (LDS), activation, 16-bit, permlane16 pairs -> 16-B row stores
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            const int64_t m = m0 + wm * TM + i * 16 + c16;
+            uint16_t* orow = out + m * ldo;
+            uint16_t* prow = SAVE ? pre_out + m * ldpre : nullptr;
+#pragma unroll
+            for (int jp = 0; jp < NI / 2; ++jp) {
+                unsigned pk[2][2], pp[2][2];
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const int nl = (int)n0 + wn * TN + (2 * jp + s) * 16 + 4 * q;
+                    const float4 bb = *reinterpret_cast<const float4*>(bias_lds + nl);
+                    float v0 = acc[i][2 * jp + s][0] + bb.x, v1 = acc[i][2 * jp + s][1] + bb.y;
+                    float v2 = acc[i][2 * jp + s][2] + bb.z, v3 = acc[i][2 * jp + s][3] + bb.w;
+                    if constexpr (SAVE) {
+                        pp[s][0] = pack2bf(v0, v1);
+                        pp[s][1] = pack2bf(v2, v3);
+                    }
+                    if (EPI == VC_EPI_BIAS_GELU_TANH || SAVE) {
+                        v0 = gelu_tanh(v0); v1 = gelu_tanh(v1); v2 = gelu_tanh(v2); v3 = gelu_tanh(v3);
+                    } else if (EPI == VC_EPI_BIAS_GELU_ERF) {
+                        v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+                    } else if (EPI == VC_EPI_BIAS_RELU_BF16) {
+                        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+                    }
+                    pk[s][0] = pack2<ET>(v0, v1);
+                    pk[s][1] = pack2<ET>(v2, v3);
+                }
+                // even q: block 2jp, columns 4q .. 4q+7; odd q: block 2jp+1, columns 4(q-1) .. 4(q-1)+7
+                const int64_t col = n0 + wn * TN + (2 * jp + (q & 1)) * 16 + 4 * (q & 2);
+                auto s0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+                auto s1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+                uint4 v;
+                v.x = s0[0]; v.y = s1[0]; v.z = s0[1]; v.w = s1[1];
+                *reinterpret_cast<uint4*>(orow + col) = v;
+                if constexpr (SAVE) {
+                    auto u0 = __builtin_amdgcn_permlane16_swap(pp[0][0], pp[1][0], false, false);
+                    auto u1 = __builtin_amdgcn_permlane16_swap(pp[0][1], pp[1][1], false, false);
+                    uint4 u;
+                    u.x = u0[0]; u.y = u1[0]; u.z = u0[1]; u.w = u1[1];
+                    *reinterpret_cast<uint4*>(prow + col) = u;
+                }
+            }
+        }
         if (!more) break;
         first = false;
         m0 = nm0;
         n0 = nn0;
         sbase = nbase;
-        // half-tile 0 of the new tile (older than its half-tiles 1, 2 and the NST stores)
         wait_vm<8 + NST>();
         block_sync_lds();
-        read_frags(sbase, 0, fa0, fw0);
+        read_head(sbase);
     }
 }
 
@@ -688,36 +784,36 @@ static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, 
                                  {64, 128}};
 constexpr int kNumCfgs = 8;
 
-template <int BM, int BN, int WM, int WN, int E, int ST = 3>
+template <int BM, int BN, int WM, int WN, int E, int ST = 3, int ET = VC_ELEM_BF16>
 static int launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
                       const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
                       int64_t gs, int64_t go, hipStream_t stream) {
     constexpr int lds = ST * (BM + BN) * 128;
     static bool attr_set = false;  // per instantiation; benign race (idempotent)
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, WM, WN, E, ST>,
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_kernel<BM, BN, WM, WN, E, ST, ET>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
         attr_set = true;
     }
-    gemm_bf16_kernel<BM, BN, WM, WN, E, ST><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(
+    gemm_bf16_kernel<BM, BN, WM, WN, E, ST, ET><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(
         A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go);
     return check_launch("vc_gemm_bf16");
 }
 
-template <int E>
+template <int E, int ET>
 static int launch_big(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
                       const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
                       int64_t gs, int64_t go, hipStream_t stream) {
     constexpr int lds = 4 * 512 * 64;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_big_kernel<E>,
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_big_kernel<E, ET>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
         attr_set = true;
     }
-    gemm_bf16_big_kernel<E><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo,
+    gemm_bf16_big_kernel<E, ET><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo,
                                                                      aux, ldaux, G, gs, go);
     return check_launch("vc_gemm_bf16");
 }
@@ -734,43 +830,43 @@ static int num_cus() {
     return n;
 }
 
-template <int E>
+template <int E, int ET>
 static int launch_persist(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
-                          int N, const float* bias, void* out, int64_t ldo, hipStream_t stream,
-                          const float* aux = nullptr, int64_t ldaux = 0) {
+                            int N, const float* bias, void* out, int64_t ldo, hipStream_t stream,
+                            const float* aux = nullptr, int64_t ldaux = 0) {
     const int lds = 4 * 512 * 64 + N * 4;
-    static int attr_set = 0;
-    if (attr_set < lds) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_persist_kernel<E>,
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_bf16_persist_kernel<E, ET>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
-        attr_set = 160 * 1024;
+        attr_set = true;
     }
     const int ntiles = nbm * nbn;
     int grid = num_cus() / 8 * 8;
     if (grid > (ntiles + 7) / 8 * 8) grid = (ntiles + 7) / 8 * 8;
-    gemm_bf16_persist_kernel<E><<<(unsigned)grid, 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, N, bias,
-                                                                  (uint16_t*)out, ldo,
-                                                                  (uint16_t*)const_cast<float*>(aux), ldaux);
+    gemm_bf16_persist_kernel<E, ET><<<(unsigned)grid, 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, N, bias,
+                                                                         (uint16_t*)out, ldo,
+                                                                         (uint16_t*)const_cast<float*>(aux), ldaux);
     return check_launch("vc_gemm_bf16");
 }
 
-template <int E>
+template <int E, int ET>
 static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int64_t M, int64_t N,
                       int K, const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
                       int64_t gs, int64_t go, hipStream_t s) {
     const int nbm = (int)(M / kCfgs[cfg].bm), nbn = (int)(N / kCfgs[cfg].bn);
     switch (cfg) {
-        case 0: return launch_cfg<256, 128, 4, 2, E>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-        case 1: return launch_cfg<128, 128, 2, 4, E>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-        case 2: return launch_cfg<128, 256, 2, 4, E>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-        case 3: return launch_big<E>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-        case 5: return launch_cfg<128, 128, 2, 4, E, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-        case 7: return launch_cfg<64, 128, 2, 4, E, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 0: return launch_cfg<256, 128, 4, 2, E, 3, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 1: return launch_cfg<128, 128, 2, 4, E, 3, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 2: return launch_cfg<128, 256, 2, 4, E, 3, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 3: return launch_big<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 5: return launch_cfg<128, 128, 2, 4, E, 2, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 7: return launch_cfg<64, 128, 2, 4, E, 2, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 4:
             if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
                           E == VC_EPI_BIAS_RELU_BF16 || E == VC_EPI_BIAS_GELU_TANH_SAVE)
-                return launch_persist<E>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s, aux, ldaux);
+                return launch_persist<E, ET>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s, aux, ldaux);
             return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 4 supports bf16-output epilogues only");
     }
     return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad config");
@@ -806,10 +902,14 @@ static int pick_cfg(int64_t M, int64_t N, int64_t K, int epi) {
 
 using namespace vc;
 
-extern "C" int vc_gemm_bf16_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int64_t M, int64_t N,
-                                int64_t K, const float* bias, int epilogue, void* out, int64_t ldo, const float* aux,
-                                int64_t ldaux, int64_t G, int64_t group_stride, int64_t group_offset, int cfg,
-                                hipStream_t stream) {
+// elem = VC_ELEM_F16: the fp16 operand build of the inference epilogues 0-4 (bf16 for the rest)
+extern "C" int vc_gemm_h16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int64_t M, int64_t N,
+                           int64_t K, const float* bias, int epilogue, void* out, int64_t ldo, const float* aux,
+                           int64_t ldaux, int64_t G, int64_t group_stride, int64_t group_offset, int elem, int cfg,
+                           hipStream_t stream) {
+    if (elem != VC_ELEM_BF16 && elem != VC_ELEM_F16) return fail(VC_ERR_INVALID_ARG, "vc_gemm: bad elem");
+    if (elem == VC_ELEM_F16 && epilogue > VC_EPI_EMBED_F32)
+        return fail(VC_ERR_UNSUPPORTED, "vc_gemm: fp16 operands support epilogues 0-4 (the inference forward) only");
     if (!A || !W || !bias || !out) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: null pointer");
     if (M <= 0 || N <= 0 || K <= 0 || M % 128 || N % 128 || K % GBK)
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: need M%128==0, N%128==0, K%64==0 (got M=" +
@@ -837,35 +937,40 @@ extern "C" int vc_gemm_bf16_cfg(const uint16_t* A, int64_t lda, const uint16_t* 
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: no tile config divides M x N");
     if ((M / kCfgs[cfg].bm) * (N / kCfgs[cfg].bn) > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: grid too large");
     const int k = (int)K;
-    if (cfg == 4 && (K % 32 || K / 32 < 6 || N > 8192 || !st16_ok ||
+    if (cfg == 4 && (K / 32 < 6 || N > 8192 || !st16_ok ||
                      (epilogue > VC_EPI_BIAS_GELU_ERF && epilogue != VC_EPI_BIAS_RELU_BF16 &&
                       epilogue != VC_EPI_BIAS_GELU_TANH_SAVE)))
-        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 4 needs K%32==0, K>=192, N<=8192, ldo%8==0, bf16 epilogue");
+        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 4 needs K>=192, N<=8192, ldo%8==0, a 16-bit-output epilogue");
+#define VC_GEMM_CASE(E)                                                                                         \
+    case E:                                                                                                     \
+        return elem == VC_ELEM_F16 ? launch_epi<(E) <= VC_EPI_EMBED_F32 ? (E) : 0, VC_ELEM_F16>(                  \
+                                         cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, \
+                                         group_offset, stream)                                                  \
+                                   : launch_epi<E, VC_ELEM_BF16>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, \
+                                                                 ldaux, G, group_stride, group_offset, stream);
     switch (epilogue) {
-        case VC_EPI_BIAS_BF16:
-            return launch_epi<VC_EPI_BIAS_BF16>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
-        case VC_EPI_BIAS_GELU_TANH:
-            return launch_epi<VC_EPI_BIAS_GELU_TANH>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
-        case VC_EPI_BIAS_GELU_ERF:
-            return launch_epi<VC_EPI_BIAS_GELU_ERF>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
-        case VC_EPI_BIAS_RESID_F32:
-            return launch_epi<VC_EPI_BIAS_RESID_F32>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
-        case VC_EPI_EMBED_F32:
-            return launch_epi<VC_EPI_EMBED_F32>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
-        case VC_EPI_BIAS_F32:
-            return launch_epi<VC_EPI_BIAS_F32>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
-        case VC_EPI_BIAS_RELU_BF16:
-            return launch_epi<VC_EPI_BIAS_RELU_BF16>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
-        case VC_EPI_BIAS_RESID_RELU_BF16:
-            return launch_epi<VC_EPI_BIAS_RESID_RELU_BF16>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
-        case VC_EPI_BIAS_ADD_F32:
-            return launch_epi<VC_EPI_BIAS_ADD_F32>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
-        case VC_EPI_BIAS_GELU_TANH_SAVE:
-            return launch_epi<VC_EPI_BIAS_GELU_TANH_SAVE>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
-        case VC_EPI_DGELU_TANH:
-            return launch_epi<VC_EPI_DGELU_TANH>(cfg, A, lda, W, ldw, M, N, k, bias, out, ldo, aux, ldaux, G, group_stride, group_offset, stream);
+        VC_GEMM_CASE(VC_EPI_BIAS_BF16)
+        VC_GEMM_CASE(VC_EPI_BIAS_GELU_TANH)
+        VC_GEMM_CASE(VC_EPI_BIAS_GELU_ERF)
+        VC_GEMM_CASE(VC_EPI_BIAS_RESID_F32)
+        VC_GEMM_CASE(VC_EPI_EMBED_F32)
+        VC_GEMM_CASE(VC_EPI_BIAS_F32)
+        VC_GEMM_CASE(VC_EPI_BIAS_RELU_BF16)
+        VC_GEMM_CASE(VC_EPI_BIAS_RESID_RELU_BF16)
+        VC_GEMM_CASE(VC_EPI_BIAS_ADD_F32)
+        VC_GEMM_CASE(VC_EPI_BIAS_GELU_TANH_SAVE)
+        VC_GEMM_CASE(VC_EPI_DGELU_TANH)
     }
+#undef VC_GEMM_CASE
     return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad epilogue");
+}
+
+extern "C" int vc_gemm_bf16_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int64_t M, int64_t N,
+                                int64_t K, const float* bias, int epilogue, void* out, int64_t ldo, const float* aux,
+                                int64_t ldaux, int64_t G, int64_t group_stride, int64_t group_offset, int cfg,
+                                hipStream_t stream) {
+    return vc_gemm_h16(A, lda, W, ldw, M, N, K, bias, epilogue, out, ldo, aux, ldaux, G, group_stride, group_offset,
+                       VC_ELEM_BF16, cfg, stream);
 }
 
 extern "C" int vc_gemm_bf16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int64_t M, int64_t N,

@@ -58,6 +58,9 @@ def frame_gather(frames: torch.Tensor, idx: torch.Tensor, kind: str = "f32", sca
 
 TOKEN_ORDER = {"time_major": 0, "patch_major": 1}
 VIDEO_LAYOUT = {"btchw": 0, "bcthw": 1}
+# 16-bit operand types (include/vclip.h VC_ELEM_*): bf16 everywhere; fp16 for the inference forward
+H16 = (torch.bfloat16, torch.float16)
+ELEM_F16 = 1
 
 
 def tubelet_im2col(pix: torch.Tensor, tubelet, out: torch.Tensor, order: str = "time_major",
@@ -73,28 +76,35 @@ def tubelet_im2col(pix: torch.Tensor, tubelet, out: torch.Tensor, order: str = "
         B, C, T, H, W = pix.shape
     kt, kh, kw = tubelet
     ntok = B * (T // kt) * (H // kh) * (W // kw)
-    _need(out.dtype == torch.bfloat16 and out.dim() == 2 and out.shape[0] >= ntok and out.shape[1] >= C * kt * kh * kw
-          and out.stride(1) == 1, "im2col out: bf16 [rows, >= C*kt*kh*kw]")
+    _need(out.dtype in H16 and out.dim() == 2 and out.shape[0] >= ntok and out.shape[1] >= C * kt * kh * kw
+          and out.stride(1) == 1, "im2col out: bf16 / fp16 [rows, >= C*kt*kh*kw]")
     _need(H % kh == 0 and W % kw == 0 and T % kt == 0 and kw % 4 == 0, "im2col: shape not divisible by the patch")
-    _lib.call("vc_patch_im2col", _p(pix), B, T, C, H, W, kt, kh, kw, TOKEN_ORDER[order], VIDEO_LAYOUT[layout], _p(out),
-              out.stride(0), _stream(pix))
+    if out.dtype == torch.float16:
+        _lib.call("vc_patch_im2col_h16", _p(pix), B, T, C, H, W, kt, kh, kw, TOKEN_ORDER[order], VIDEO_LAYOUT[layout],
+                  ELEM_F16, _p(out), out.stride(0), _stream(pix))
+    else:
+        _lib.call("vc_patch_im2col", _p(pix), B, T, C, H, W, kt, kh, kw, TOKEN_ORDER[order], VIDEO_LAYOUT[layout],
+                  _p(out), out.stride(0), _stream(pix))
     return out
 
 
 def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: str, out: torch.Tensor,
          aux: torch.Tensor | None = None, group: int = 0, group_stride: int = 0, group_offset: int = 0,
          m: int | None = None, cfg: int = -1) -> torch.Tensor:
-    """out (+)= epilogue(a[:m] @ w.T + bias).  a bf16 [M,K], w bf16 [N,K], bias f32 [N]."""
+    """out (+)= epilogue(a[:m] @ w.T + bias).  a bf16 [M,K], w bf16 [N,K], bias f32 [N]; or a, w (and the
+    16-bit out) fp16 for the inference epilogues (bias / gelu / resid_f32 / embed_f32)."""
     _dev(a, w, bias, out)
     M = a.shape[0] if m is None else m
     K = a.shape[1]
     N = w.shape[0]
-    _need(a.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and bias.dtype == torch.float32, "gemm dtypes")
+    _need(a.dtype in H16 and w.dtype == a.dtype and bias.dtype == torch.float32, "gemm dtypes (a, w: bf16 or fp16)")
+    f16 = a.dtype == torch.float16
     _need(a.stride(1) == 1 and w.stride(1) == 1 and out.stride(-1) == 1 and w.shape[1] == K, "gemm layout")
     _need(bias.numel() == N and bias.is_contiguous(), "gemm bias")
     e = EPI[epilogue]
+    _need(not f16 or e <= 4, "gemm: fp16 operands support the inference epilogues only")
     if e in (0, 1, 2, 6, 7, 9, 10):
-        _need(out.dtype == torch.bfloat16, "gemm out must be bf16 for this epilogue")
+        _need(out.dtype == a.dtype, "gemm out must have the operand type for this epilogue")
     else:
         _need(out.dtype == torch.float32, "gemm out must be f32 for this epilogue")
     if e in (7, 9, 10):
@@ -111,8 +121,12 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: str, ou
     _need(a.shape[0] >= M, "gemm a rows")
     aux_p = _p(aux) if aux is not None else None
     ldaux = aux.stride(0) if aux is not None else 0
-    _lib.call("vc_gemm_bf16_cfg", _p(a), a.stride(0), _p(w), w.stride(0), M, N, K, _p(bias), e, _p(out),
-              out.stride(0), aux_p, ldaux, group, group_stride, group_offset, cfg, _stream(a))
+    if f16:
+        _lib.call("vc_gemm_h16", _p(a), a.stride(0), _p(w), w.stride(0), M, N, K, _p(bias), e, _p(out),
+                  out.stride(0), aux_p, ldaux, group, group_stride, group_offset, ELEM_F16, cfg, _stream(a))
+    else:
+        _lib.call("vc_gemm_bf16_cfg", _p(a), a.stride(0), _p(w), w.stride(0), M, N, K, _p(bias), e, _p(out),
+                  out.stride(0), aux_p, ldaux, group, group_stride, group_offset, cfg, _stream(a))
     return out
 
 
@@ -159,16 +173,20 @@ def gemm_rounds(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: 
 
 def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, out: torch.Tensor,
               m: int | None = None) -> torch.Tensor:
-    """LayerNorm of the first gamma.numel() columns of each row (x f32 -> out bf16)."""
+    """LayerNorm of the first gamma.numel() columns of each row (x f32 -> out bf16 or fp16)."""
     _dev(x, gamma, beta, out)
     M = x.shape[0] if m is None else m
     D = gamma.numel()
-    _need(x.dtype == torch.float32 and out.dtype == torch.bfloat16 and x.stride(1) == 1 and out.stride(1) == 1,
-          "layernorm: x f32, out bf16, unit column stride")
+    _need(x.dtype == torch.float32 and out.dtype in H16 and x.stride(1) == 1 and out.stride(1) == 1,
+          "layernorm: x f32, out bf16 / fp16, unit column stride")
     _need(beta.numel() == D and x.shape[1] >= D and out.shape[1] >= D and out.shape[0] >= M and x.shape[0] >= M,
           "layernorm shapes")
-    _lib.call("vc_layernorm_f32_bf16", _p(x), x.stride(0), M, D, _p(gamma), _p(beta), eps, _p(out), out.stride(0),
-              _stream(x))
+    if out.dtype == torch.float16:
+        _lib.call("vc_layernorm_f32_h16", _p(x), x.stride(0), M, D, _p(gamma), _p(beta), eps, ELEM_F16, _p(out),
+                  out.stride(0), _stream(x))
+    else:
+        _lib.call("vc_layernorm_f32_bf16", _p(x), x.stride(0), M, D, _p(gamma), _p(beta), eps, _p(out), out.stride(0),
+                  _stream(x))
     return out
 
 
@@ -191,17 +209,21 @@ LOG2E = 1.4426950408889634
 
 def attention(qkv: torch.Tensor, B: int, S: int, H: int, scale: float, out: torch.Tensor,
               q_prescaled: bool = False) -> torch.Tensor:
-    """qkv bf16 [rows, 3*H*64] (q|k|v per token row b*S+s) -> out bf16 [rows, H*64].
+    """qkv bf16 [rows, 3*H*64] (q|k|v per token row b*S+s) -> out bf16 [rows, H*64] (or fp16 -> fp16).
     q_prescaled: q already holds q * scale * log2(e) (folded into the projection)."""
     _dev(qkv, out)
-    _need(qkv.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and qkv.stride(1) == 1 and out.stride(1) == 1,
+    _need(qkv.dtype in H16 and out.dtype == qkv.dtype and qkv.stride(1) == 1 and out.stride(1) == 1,
           "attention dtypes/layout")
     _need(qkv.shape[1] >= 3 * H * 64 and out.shape[1] >= H * 64, "attention columns")
     # the kernel reads K/V rows up to (B-1)*S + roundup(S,64) - 1
     _need(qkv.shape[0] >= (B - 1) * S + (S + 63) // 64 * 64, "attention: qkv needs row padding to a 64-key tile")
     _need(out.shape[0] >= B * S, "attention out rows")
-    _lib.call("vc_attention_fwd", _p(qkv), qkv.stride(0), B, S, H, 64, scale, int(bool(q_prescaled)), _p(out),
-              out.stride(0), _stream(qkv))
+    if qkv.dtype == torch.float16:
+        _lib.call("vc_attention_fwd_h16", _p(qkv), qkv.stride(0), B, S, H, 64, scale, int(bool(q_prescaled)), ELEM_F16,
+                  _p(out), out.stride(0), _stream(qkv))
+    else:
+        _lib.call("vc_attention_fwd", _p(qkv), qkv.stride(0), B, S, H, 64, scale, int(bool(q_prescaled)), _p(out),
+                  out.stride(0), _stream(qkv))
     return out
 
 

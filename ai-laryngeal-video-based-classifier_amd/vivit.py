@@ -120,6 +120,10 @@ class VivitForVideoClassification(torch.nn.Module):
         # faster per GEMM in isolation but 0.6 % SLOWER in the model (tools/ab_model.py
         # round_split, interleaved, B = 8: 9.340 vs 9.285 ms/step), so off by default
         self.round_split = False
+        # 16-bit operand type of the inference forward: bf16 (the benchmarked configuration) or
+        # torch.float16 (same kernels and MFMA rate, logits ~6x closer to the fp32 reference;
+        # DESIGN.md §6).  The train step (vivit_train.py) is bf16 either way.
+        self.compute_dtype = torch.bfloat16
 
     # ---- state dict in HF naming ---------------------------------------------------
     def hf_state_dict(self):
@@ -233,15 +237,18 @@ class VivitForVideoClassification(torch.nn.Module):
     # ---- device packing ----------------------------------------------------------
     def _pack(self, device):
         ver = self._weights_version()
-        if self._packed is not None and self._packed["device"] == device and self._packed["version"] == ver:
+        bf = self.compute_dtype
+        if bf not in (torch.bfloat16, torch.float16):
+            raise ValueError(f"compute_dtype must be torch.bfloat16 or torch.float16, not {bf}")
+        if (self._packed is not None and self._packed["device"] == device and self._packed["version"] == ver
+                and self._packed["dtype"] == bf):
             return self._packed
         c = self.config
-        bf = torch.bfloat16
         f32 = torch.float32
         P = lambda n: self.P(n).detach().to(device)  # noqa: E731
         D = c.hidden_size
         kt, kh, kw = c.tubelet_size
-        pk = {"device": device, "version": ver}
+        pk = {"device": device, "version": ver, "dtype": bf}
         pk["w_emb"] = P("vivit.embeddings.patch_embeddings.projection.weight").reshape(D, -1).to(bf).contiguous()
         pk["b_emb"] = P("vivit.embeddings.patch_embeddings.projection.bias").to(f32).contiguous()
         pk["pos"] = P("vivit.embeddings.position_embeddings").reshape(-1, D).to(f32).contiguous()
@@ -286,7 +293,7 @@ class VivitForVideoClassification(torch.nn.Module):
         return npatch, S, Mpad, Memb
 
     def _workspace(self, B, device, part: int = 0):
-        key = (B, str(device), part)
+        key = (B, str(device), part, self.compute_dtype)
         if key in self._ws:
             return self._ws[key]
         if len(self._ws) >= 4:
@@ -295,7 +302,7 @@ class VivitForVideoClassification(torch.nn.Module):
         D, I = c.hidden_size, c.intermediate_size
         kt, kh, kw = c.tubelet_size
         npatch, S, Mpad, Memb = self.geometry(B)
-        bf = torch.bfloat16
+        bf = self.compute_dtype
         z = lambda *s, dt=bf: torch.zeros(s, dtype=dt, device=device)  # noqa: E731
         ws = dict(A_emb=z(Memb, c.num_channels * kt * kh * kw), X=z(Mpad, D, dt=torch.float32), Y=z(Mpad, D),
                   QKV=z(Mpad, 3 * D), O=z(Mpad, D), Hd=z(Mpad, I), logits=z(B, c.num_labels, dt=torch.float32))

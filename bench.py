@@ -191,12 +191,13 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(model_cfg, n_clips, batch, gpu_logits_fn):
+def cpu_baseline(model_cfg, n_clips, batch, gpu_logits_fns):
     """The fp32 CPU oracle (oracle/vivit_ref.py, a 'port' of the reference's HF ViViT forward) on
     the host cores, on bounded samples of the benchmark workload: `n_clips` clips
     one at a time (B=1, as the reference's inference CLI runs) and one batch of `batch` clips (the
-    bench's own rank-0 batch, RandomState(1)).  The GPU logit error is measured on that batch, i.e.
-    on exactly the clips the timed region runs."""
+    bench's own rank-0 batch, RandomState(1)).  The GPU logit errors (one per entry of
+    `gpu_logits_fns`: the bf16 headline build and the fp16-operand build) are measured on that
+    batch, i.e. on exactly the clips the timed region runs."""
     from oracle.vivit_ref import vivit_forward
     from vclip_amd.weights import make_synthetic_clips, make_vivit_weights
 
@@ -212,8 +213,7 @@ def cpu_baseline(model_cfg, n_clips, batch, gpu_logits_fn):
         t0 = time.perf_counter()
         ref = vivit_forward(sd, model_cfg, torch.from_numpy(pix)).numpy()
         dtb = time.perf_counter() - t0
-    got = gpu_logits_fn(pix)
-    err = float(np.abs(got - ref).max())
+    err = {k: float(np.abs(fn(pix) - ref).max()) for k, fn in gpu_logits_fns.items()}
     return {"value": n_clips / dt1, "unit": "clips/s", "cores": cores, "kind": "port", "cpu": cpu_model(),
             "value_b8": round(batch / dtb, 4),
             "sample": f"ViViT-B/16x2 32x224^2 fp32 forward on the host: {n_clips} clips at B=1 (value) and one "
@@ -496,6 +496,19 @@ def main():
     streams = model.last_streams
     attn_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
 
+    # the fp16-operand build of the same forward (VC_ELEM_F16: same kernels, same MFMA rate,
+    # logits within 1e-3), timed the same way after the bf16 headline; reported beside it
+    model.compute_dtype = torch.float16
+    evs16 = []
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    model.kernel_events = evs16
+    dt16 = timed_loop(step, a.steps, 0, dist, torch.cuda.synchronize)
+    model.kernel_events = None
+    attn_ms16 = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs16]))
+    model.compute_dtype = torch.bfloat16
+
     breakdown = kernel_breakdown(model, step, a.batch // streams, streams, 3)
 
     clips = a.batch * a.steps * world
@@ -510,7 +523,7 @@ def main():
     out = None
     if rank == 0:
         cpu = None
-        logit_err = None
+        logit_err = logit_err16 = None
         traffic, traffic_src = measured_traffic("attn_fwd_d64_kernel")
         pmc, pmc_src = measured_pmc("attn_fwd_d64_kernel")
         mfma_busy = valu_per_mfma = None
@@ -522,10 +535,17 @@ def main():
             shape_cfg = dict(cfg.as_shape_cfg(), num_attention_heads=cfg.num_attention_heads,
                              layer_norm_eps=cfg.layer_norm_eps)
 
-            def gpu_logits(p):
-                return model.forward_logits(torch.from_numpy(p).to(dev)).cpu().numpy().copy()
+            def gpu_logits(dtype):
+                def fn(p):
+                    model.compute_dtype = dtype
+                    lg = model.forward_logits(torch.from_numpy(p).to(dev)).cpu().numpy().copy()
+                    model.compute_dtype = torch.bfloat16
+                    return lg
+                return fn
 
-            cpu, logit_err = cpu_baseline(shape_cfg, a.cpu_clips, a.batch, gpu_logits)
+            cpu, errs = cpu_baseline(shape_cfg, a.cpu_clips, a.batch,
+                                     {"bf16": gpu_logits(torch.bfloat16), "fp16": gpu_logits(torch.float16)})
+            logit_err, logit_err16 = errs["bf16"], errs["fp16"]
             cpu["lstm_cfg1"] = cpu_lstm_cfg1()
         out = {
             "metric": "clips/sec fwd ViViT-B 32x224^2 bf16",
@@ -555,6 +575,11 @@ def main():
             "build": _build_id(),
             "model_tflops": round(model_tflops, 1),
             "model_frac_of_peak": round(model_tflops / PEAK_BF16_TFLOPS, 4),
+            "fp16": {"value": round(clips / dt16, 2), "ms_per_step": round(dt16 / a.steps * 1e3, 3),
+                     "logit_max_abs_err": logit_err16, "attn_avg_launch_ms": round(attn_ms16, 4),
+                     "attn_frac": round(ATTN_GFLOP_PER_CLIP_LAYER * launch_clips / (attn_ms16 * 1e-3) / 1e3
+                                        / PEAK_BF16_TFLOPS, 4),
+                     "note": "same forward with fp16 MFMA operands (VC_ELEM_F16; fp16 dense peak = bf16's)"},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

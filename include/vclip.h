@@ -152,6 +152,37 @@ int vc_attention_fwd(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int6
 int vc_attention_fwd_rebase_always(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, float scale,
                                    uint16_t* out, int64_t ldo, hipStream_t stream);
 
+/*
+ * 16-bit operand type of the inference forward (`elem` of the *_h16 entry points below).
+ * VC_ELEM_BF16 is the benchmarked configuration (north_star: "ViViT-B ... forward bf16");
+ * VC_ELEM_F16 runs the same kernels at the same MFMA rate with fp16 operands — 3 more
+ * mantissa bits, 5 fewer exponent bits — for logits within 1e-3 of the fp32 reference
+ * (DESIGN.md §6).  Accumulation, softmax statistics, LayerNorm statistics and the residual
+ * stream stay fp32 in both.
+ */
+#define VC_ELEM_BF16 0
+#define VC_ELEM_F16  1
+
+/* vc_patch_im2col with the output element type as an argument. */
+int vc_patch_im2col_h16(const float* pixel_values, int64_t B, int64_t T, int64_t C, int64_t H, int64_t W,
+                        int kt, int kh, int kw, int token_order, int layout, int elem, uint16_t* A, int64_t lda,
+                        hipStream_t stream);
+
+/* vc_gemm_bf16_cfg with the operand type as an argument: A, W and the 16-bit outputs are `elem`;
+ * fp16 supports epilogues 0-4 (the inference forward's), bf16 all of them. */
+int vc_gemm_h16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
+                int64_t M, int64_t N, int64_t K, const float* bias, int epilogue,
+                void* out, int64_t ldo, const float* aux, int64_t ldaux,
+                int64_t G, int64_t group_stride, int64_t group_offset, int elem, int cfg, hipStream_t stream);
+
+/* vc_layernorm_f32_bf16 with the output type as an argument (same widths and kernels). */
+int vc_layernorm_f32_h16(const float* x, int64_t ldx, int64_t M, int64_t D, const float* gamma, const float* beta,
+                         float eps, int elem, uint16_t* y, int64_t ldy, hipStream_t stream);
+
+/* vc_attention_fwd with the operand type of q|k|v, P and out as an argument. */
+int vc_attention_fwd_h16(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, int64_t head_dim,
+                         float scale, int q_prescaled, int elem, uint16_t* out, int64_t ldo, hipStream_t stream);
+
 /* LayerNorm f32 -> f32 (any D; y may alias nothing of x).  Swin's patch_embed.norm (torchvision
  * PatchEmbed3d, eps 1e-5) whose output is the fp32 residual stream. */
 int vc_layernorm_f32(const float* x, int64_t ldx, int64_t M, int64_t D, const float* gamma, const float* beta,

@@ -207,9 +207,9 @@ def test_gemm_training_epilogues():
     np.testing.assert_allclose(dh.cpu().float().numpy(), ref.numpy(), rtol=1e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("cfg", [4, 5, 6, -1])
+@pytest.mark.parametrize("cfg", [4, 5, -1])
 def test_gemm_gelu_save_configs(cfg):
-    """GELU_SAVE on the persistent 256x256 kernel (cfg 4, two bf16 outputs per tile) vs cfg 5:
+    """GELU_SAVE on the persistent 256x256 kernel (cfg 4, two bf16 outputs per tile) and cfg 5:
     identical bits (same fp32 accumulation order per output is not guaranteed, so compare to the
     double reference), at a shape with several tiles per workgroup."""
     O = ops()

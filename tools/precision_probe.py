@@ -75,6 +75,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--clips", type=int, default=2)
     ap.add_argument("--layers", type=int, default=12)
+    ap.add_argument("--fp16-ablate", action="store_true", help="all fp16, one point at a time back to fp32")
     a = ap.parse_args()
     torch.set_num_threads(os.cpu_count())
     cfg = dict(hidden_size=768, intermediate_size=3072, tubelet_size=[2, 16, 16], num_channels=3, num_frames=32,
@@ -86,6 +87,15 @@ def main():
         ref = forward(sd, cfg, pix, {k: None for k in POINTS})
         print("fp32 logits", ref.numpy().round(4).tolist(), flush=True)
         shipped = {k: bf for k in POINTS}
+        if a.fp16_ablate:
+            half = {k: hf for k in POINTS}
+            runs = [("all fp16", half)] + [(f"all fp16 except {k} fp32", dict(half, **{k: None})) for k in POINTS]
+            runs += [("all fp16 except w+ln fp32", dict(half, w=None, ln=None)),
+                     ("all fp16 except p+o fp32", dict(half, p=None, o=None))]
+            for name, rp in runs:
+                got = forward(sd, cfg, pix, rp)
+                print(f"{name:40s} max|err| {float((got - ref).abs().max()):.3e}", flush=True)
+            return
         runs = [("all bf16 (shipped rounding points)", shipped)]
         for k in POINTS:
             runs.append((f"all bf16 except {k} fp32", dict(shipped, **{k: None})))

@@ -18,7 +18,21 @@ SHAPES = [("qkv", 2304, 768, "bias"), ("o_proj", 768, 768, "bias_resid_f32"), ("
           ("fc2", 768, 3072, "bias_resid_f32")]
 
 
+COLD = None
+
+
 def timeit(fn, iters):
+    if COLD is not None:  # the inputs as the model sees them: not resident in L2 / MALL
+        ts = []
+        for _ in range(iters):
+            COLD.add_(1.0)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        return sum(ts) / len(ts)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(iters):
@@ -35,8 +49,12 @@ def main():
     ap.add_argument("--cfgs", default="0,2,3,4")
     ap.add_argument("--square", type=int, default=0, help="also time an MxNxK = n^3 bias GEMM")
     ap.add_argument("--no-attn", action="store_true")
+    ap.add_argument("--cold", action="store_true",
+                    help="stream 1 GiB through the caches before every timed launch (each launch timed alone)")
     a = ap.parse_args()
-    global M, SHAPES
+    global M, SHAPES, COLD
+    if a.cold:
+        COLD = torch.zeros(256 << 20, device="cuda")
     if a.square:
         SHAPES = [(f"sq{a.square}", a.square, a.square, "bias")] + SHAPES
     dev = "cuda"
