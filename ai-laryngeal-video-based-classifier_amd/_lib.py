@@ -60,6 +60,8 @@ SIGNATURES = {
     "vc_resize_linear_u8": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_int, c_p, c_p], c_int),
     "vc_video_transform": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p,
                             c_p, c_int, c_int, c_p, c_p], c_int),
+    "vc_video_transform_clips": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_p, c_p, c_int,
+                                  c_int, c_p, c_p], c_int),
     "vc_divided_add_layernorm": ([c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_int, c_p,
                                   c_i64, c_p], c_int),
     # train step

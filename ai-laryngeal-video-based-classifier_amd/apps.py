@@ -169,7 +169,9 @@ class Family:
         lo, hi = int(min(idx)), int(max(idx))
         return src.read(list(range(lo, hi + 1)))
 
-    def to_model_input(self, frames_u8: torch.Tensor, num_frames, div255=False):
+    def to_model_input(self, frames_u8: torch.Tensor, num_frames, div255=False, train=False):
+        """train: the Swin / ResNet3D train chain (RandomShortSideScale, RandomCrop, RandomHorizontalFlip;
+        dataset.py:151-163 / :176-182) instead of the eval chain; ViViT / TimeSformer have one chain."""
         from . import preprocess as pp
         if self.name in ("vivit", "timesformer") and tuple(frames_u8.shape[-3:-1]) != (224, 224):
             frames_u8 = pp.cv2_resize_u8(frames_u8, (224, 224))  # cv2.resize INTER_LINEAR (dataset.py:271-277)
@@ -177,6 +179,8 @@ class Family:
             return pp.vivit_preprocess(frames_u8)
         if self.name == "timesformer":
             return pp.timesformer_preprocess(frames_u8)
+        if train:
+            return pp.video_train_transform(frames_u8, num_frames, div255=div255)[0]
         return pp.video_eval_transform(frames_u8, num_frames, div255=div255)
 
     def create_model(self, args, class_labels, device, logger):
@@ -265,7 +269,8 @@ def _device():
 
 
 def _batches(fam, split, sampler, args, device, shuffle=False, logger=None):
-    """Batches of (model input, labels).  A clip that cannot be decoded becomes the reference
+    """Batches of (model input, labels); shuffle = the train split (shuffled order, train-time
+    transforms).  A clip that cannot be decoded becomes the reference
     dataset's gray placeholder (127) with a warning (dataset.py:294-381), so one bad video does
     not end the epoch."""
     paths, labels = split
@@ -284,7 +289,7 @@ def _batches(fam, split, sampler, args, device, shuffle=False, logger=None):
                     logger.warning(f"Failed to load {paths[i]}: {str(e)}; using a placeholder clip")
                 clip = np.full((args.num_frames, 224, 224, 3), 127, np.uint8)
             fr = torch.from_numpy(clip).to(device)
-            xs.append(fam.to_model_input(fr.unsqueeze(0), args.num_frames))
+            xs.append(fam.to_model_input(fr.unsqueeze(0), args.num_frames, train=shuffle))
         yield torch.cat(xs), torch.tensor([labels[i] for i in ids], device=device)
 
 

@@ -64,9 +64,12 @@ struct VideoXform {
     int bf16;
 };
 
+// clip_p (optional, train-time transforms): per clip int32 {resize h, resize w, crop top, crop
+// left, horizontal flip} (pytorchvideo RandomShortSideScale, torchvision RandomCrop /
+// RandomHorizontalFlip with their parameters drawn on the host); overrides p's resize / crop.
 __global__ void __launch_bounds__(256) video_transform_kernel(const uint8_t* __restrict__ frames,
                                                               const int64_t* __restrict__ idx, int64_t nclip, VideoXform p,
-                                                              void* __restrict__ out) {
+                                                              const int* __restrict__ clip_p, void* __restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t per_frame = (int64_t)p.ch * p.cw;
     if (i >= nclip * p.T * per_frame) return;
@@ -77,7 +80,13 @@ __global__ void __launch_bounds__(256) video_transform_kernel(const uint8_t* __r
     int64_t f = idx[b * p.T + t];
     f = f < 0 ? 0 : (f >= p.F ? p.F - 1 : f);
     const uint8_t* fr = frames + (b * p.F + f) * (int64_t)p.H * p.W * 3;
-    const int y = r + p.top, x = j + p.left;
+    int jj = j;
+    if (clip_p) {
+        const int* cp = clip_p + b * 5;
+        p.Hr = cp[0]; p.Wr = cp[1]; p.top = cp[2]; p.left = cp[3];
+        if (cp[4]) jj = p.cw - 1 - j;  // F.hflip of the cropped clip
+    }
+    const int y = r + p.top, x = jj + p.left;
     float v[3];
     if (p.Hr == p.H && p.Wr == p.W) {
 #pragma unroll
@@ -195,8 +204,28 @@ int vc_video_transform(const uint8_t* frames, int64_t nclips, int64_t F, int64_t
     p.layout = layout;
     p.bf16 = out_bf16 ? 1 : 0;
     const int64_t total = nclips * T * crop_h * crop_w;
-    video_transform_kernel<<<(unsigned)((total + 255) / 256), 256, 0, stream>>>(frames, idx, nclips, p, out);
+    video_transform_kernel<<<(unsigned)((total + 255) / 256), 256, 0, stream>>>(frames, idx, nclips, p, nullptr, out);
     return check_launch("vc_video_transform");
+}
+
+int vc_video_transform_clips(const uint8_t* frames, int64_t nclips, int64_t F, int64_t H, int64_t W, const int64_t* idx,
+                             int64_t T, const int* clip_params, int64_t crop_h, int64_t crop_w, const float* scale3,
+                             const float* shift3, int layout, int out_bf16, void* out, hipStream_t stream) {
+    if (!frames || !idx || !clip_params || !scale3 || !shift3 || !out)
+        return fail(VC_ERR_INVALID_ARG, "vc_video_transform_clips: null pointer");
+    if (nclips <= 0 || F <= 0 || H <= 0 || W <= 0 || T <= 0 || crop_h <= 0 || crop_w <= 0 || (layout != 0 && layout != 1))
+        return fail(VC_ERR_INVALID_ARG, "vc_video_transform_clips: bad geometry");
+    // the per-clip crop windows are validated by the caller on the host (they live in device memory here)
+    VideoXform p;
+    p.F = (int)F; p.H = (int)H; p.W = (int)W; p.T = (int)T;
+    p.Hr = (int)H; p.Wr = (int)W;
+    p.top = 0; p.left = 0; p.ch = (int)crop_h; p.cw = (int)crop_w;
+    for (int c = 0; c < 3; ++c) { p.sc[c] = scale3[c]; p.sh[c] = shift3[c]; }
+    p.layout = layout;
+    p.bf16 = out_bf16 ? 1 : 0;
+    const int64_t total = nclips * T * crop_h * crop_w;
+    video_transform_kernel<<<(unsigned)((total + 255) / 256), 256, 0, stream>>>(frames, idx, nclips, p, clip_params, out);
+    return check_launch("vc_video_transform_clips");
 }
 
 }  // extern "C"

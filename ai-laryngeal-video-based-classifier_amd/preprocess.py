@@ -183,6 +183,61 @@ def video_eval_transform(frames: torch.Tensor, num_frames: int, short_side: int 
                       layout=1 if layout == "bcthw" else 0)
 
 
+def train_transform_params(n_clips: int, H: int, W: int, min_size: int = 256, max_size: int = 320, crop: int = 224,
+                           flip_p: float = 0.5, generator: torch.Generator | None = None):
+    """Host draw of the train chain's random parameters, per clip in the reference's order
+    (videoswintransformer/swin_video_classifier/data_config/dataset.py:151-163, one clip per
+    __getitem__): pytorchvideo RandomShortSideScale `torch.randint(min, max + 1, (1,))`; torchvision
+    RandomCrop.get_params `torch.randint(0, h - th + 1, (1,))` then the same for w (no draw when
+    the frame already is crop x crop); RandomHorizontalFlip `torch.rand(1) < p`.  torch's default
+    generator unless one is given (the reference's DataLoader with num_workers = 0 draws from it).
+    Returns int32 [n_clips, 5] {resize_h, resize_w, top, left, flip}."""
+    out = []
+    for _ in range(n_clips):
+        size = int(torch.randint(min_size, max_size + 1, (1,), generator=generator).item())
+        rh, rw = short_side_size(H, W, size)
+        if rh < crop or rw < crop:
+            raise ValueError(f"RandomCrop: required crop {crop} larger than the scaled frame {rh}x{rw}")
+        if rh == crop and rw == crop:
+            top = left = 0
+        else:
+            top = int(torch.randint(0, rh - crop + 1, size=(1,), generator=generator).item())
+            left = int(torch.randint(0, rw - crop + 1, size=(1,), generator=generator).item())
+        flip = int(bool(torch.rand(1, generator=generator) < flip_p))
+        out.append((rh, rw, top, left, flip))
+    return torch.tensor(out, dtype=torch.int32)
+
+
+def video_train_transform(frames: torch.Tensor, num_frames: int, min_size: int = 256, max_size: int = 320,
+                          crop: int = 224, mean=(0.45, 0.45, 0.45), std=(0.225, 0.225, 0.225), div255: bool = False,
+                          layout: str = "bcthw", generator: torch.Generator | None = None, params=None):
+    """Train-time chain of the Swin / ResNet3D datasets: frames u8 [B, F, H, W, 3] (device) ->
+    f32 [B, 3, T, crop, crop]; UniformTemporalSubsample, RandomShortSideScale(min, max) (torch
+    bilinear), RandomCrop(crop), RandomHorizontalFlip, Normalize -- one fused kernel
+    (vc_video_transform_clips) with the random parameters drawn on the host
+    (`train_transform_params`, or `params` as returned by it).  Returns (clip, params)."""
+    _dev(frames)
+    B, F, H, W, C = frames.shape
+    _need(C == 3 and frames.dtype == torch.uint8 and frames.is_contiguous(), "frames: u8 [B, F, H, W, 3]")
+    if params is None:
+        params = train_transform_params(B, H, W, min_size, max_size, crop, generator=generator)
+    params = params.to(torch.int32).contiguous()
+    _need(tuple(params.shape) == (B, 5), "params: int32 [B, 5]")
+    for rh, rw, top, left, _ in params.tolist():
+        _need(0 <= top and top + crop <= rh and 0 <= left and left + crop <= rw, "crop window outside the frame")
+    idx = uniform_temporal_subsample_indices(F, num_frames).to(frames.device).repeat(B, 1).contiguous()
+    k = 255.0 if div255 else 1.0
+    sc = (ctypes.c_float * 3)(*(1.0 / (k * s) for s in std))
+    sh = (ctypes.c_float * 3)(*(-m / s for m, s in zip(mean, std)))
+    lay = 1 if layout == "bcthw" else 0
+    shape = (B, num_frames, 3, crop, crop) if lay == 0 else (B, 3, num_frames, crop, crop)
+    out = torch.empty(shape, dtype=torch.float32, device=frames.device)
+    pd = params.to(frames.device)
+    _lib.call("vc_video_transform_clips", _p(frames), B, F, H, W, _p(idx), num_frames, _p(pd), crop, crop,
+              ctypes.addressof(sc), ctypes.addressof(sh), lay, 0, _p(out), _stream(frames))
+    return out, params
+
+
 def timesformer_preprocess(frames: torch.Tensor, mean=(0.45, 0.45, 0.45), std=(0.225, 0.225, 0.225)) -> torch.Tensor:
     """frames u8 [B, T, 224, 224, 3] -> pixel_values f32 [B, T, 3, 224, 224] = (x/255 - mean)/std."""
     _dev(frames)

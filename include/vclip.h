@@ -242,6 +242,19 @@ int vc_video_transform(const uint8_t* frames, int64_t nclips, int64_t F, int64_t
                        int64_t crop_w, const float* scale3, const float* shift3, int layout, int out_bf16, void* out,
                        hipStream_t stream);
 
+/*
+ * Train-time variant (videoswintransformer/.../data_config/dataset.py:151-163 train chain:
+ * UniformTemporalSubsample -> RandomShortSideScale(256, 320) -> RandomCrop(224) ->
+ * RandomHorizontalFlip(0.5) -> Normalize): clip_params = device int32 [nclips][5]
+ * {resize_h, resize_w, top, left, flip} drawn on the host (vclip_amd/preprocess.py
+ * video_train_transform, torch's RNG in the reference's draw order); each clip is resized, cropped
+ * to crop_h x crop_w at (top, left), mirrored when flip != 0, and normalised.  The caller keeps
+ * every crop window inside its resized frame.
+ */
+int vc_video_transform_clips(const uint8_t* frames, int64_t nclips, int64_t F, int64_t H, int64_t W, const int64_t* idx,
+                             int64_t T, const int* clip_params, int64_t crop_h, int64_t crop_w, const float* scale3,
+                             const float* shift3, int layout, int out_bf16, void* out, hipStream_t stream);
+
 /* ---- TimeSformer divided space-time attention ------------------------
  * Clip layout: rows b*S + r, S = 1 + P*T, r = 0 (CLS) or 1 + p*T + t (patch-major, time-minor).
  * Frame layout: rows (b*T + t)*(1 + P) + j, j = 0 (CLS copy) or 1 + p (the spatial sequences). */

@@ -31,3 +31,19 @@ def test_short_side_size():
     assert short_side_size(480, 640, 256) == (256, 341)
     assert short_side_size(640, 480, 256) == (341, 256)
     assert short_side_size(224, 224, 256) == (256, 256)
+
+
+@pytest.mark.parametrize("H,W", [(240, 320), (320, 240), (256, 256), (224, 224)])
+def test_train_transform_params_draw_order(H, W):
+    """The host draw of the train chain's parameters consumes torch's RNG exactly as the
+    restated pytorchvideo / torchvision transforms do (oracle/video_transforms_ref.py), clip
+    after clip, and yields the same sizes, crop windows and flips."""
+    from oracle.video_transforms_ref import train_transform
+    from vclip_amd.preprocess import train_transform_params
+    clip = torch.zeros(4, H, W, 3, dtype=torch.uint8)
+    g1, g2 = torch.Generator().manual_seed(123), torch.Generator().manual_seed(123)
+    got = train_transform_params(6, H, W, generator=g1).tolist()
+    want = [list(train_transform(clip, 2, generator=g2)[1]) for _ in range(6)]
+    assert got == want
+    assert torch.rand(1, generator=g1).item() == torch.rand(1, generator=g2).item()  # same RNG position after
+    assert all(r[0] >= 224 and r[1] >= 224 for r in got)

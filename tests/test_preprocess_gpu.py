@@ -77,3 +77,20 @@ def test_cv2_resize_gpu_bit_exact(shape):
     if H * W * h * w < 2e6:
         from oracle.cv2_resize_ref import resize_linear_u8 as ref
         np.testing.assert_array_equal(got[0], np.array(ref(x[0].tolist(), w, h), dtype=np.uint8))
+
+
+@pytest.mark.parametrize("F,H,W,T", [(40, 240, 320, 16), (12, 224, 224, 8), (9, 300, 256, 8)])
+def test_video_train_transform(F, H, W, T):
+    """RandomShortSideScale -> RandomCrop -> RandomHorizontalFlip -> Normalize on the GPU (parameters
+    drawn on the host) vs the CPU restatement of the pytorchvideo / torchvision chain with the same
+    generator seed (oracle/video_transforms_ref.py; parity unpinned: neither library is installed)."""
+    from oracle.video_transforms_ref import train_transform
+    from vclip_amd.preprocess import video_train_transform
+    rng = np.random.RandomState(F + H)
+    frames = rng.randint(0, 256, (3, F, H, W, 3)).astype(np.uint8)
+    got, params = video_train_transform(torch.from_numpy(frames).to(DEV), T, generator=torch.Generator().manual_seed(7))
+    g = torch.Generator().manual_seed(7)
+    for b in range(3):
+        want, p = train_transform(torch.from_numpy(frames[b]), T, generator=g)
+        assert list(p) == params[b].tolist()
+        assert (got[b].cpu() - want).abs().max().item() < 1e-4 * 255.0

@@ -117,7 +117,7 @@ def _model(cfg):
     c = TimesformerConfig(**cfg, id2label={0: "non-referral", 1: "referral"})
     m = TimesformerForVideoClassification(c)
     m.load_state_dict(make_timesformer_weights(cfg, seed=0))
-    return m.cuda()
+    return m.cuda().eval()  # constructed models start in train mode, as HF's (forward would then train)
 
 
 def test_timesformer_tiny_logits():

@@ -23,9 +23,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short_name(k: str) -> str:
-    k = re.sub(r"\(.*", "", k)
+    """Kernel name with its template arguments (they tell the bf16 / fp16 builds and the GEMM
+    epilogues apart), without the namespace and the parameter list."""
     k = re.sub(r"^void ", "", k)
-    return k.split("<")[0].split("::")[-1] if "<" in k else k.split("::")[-1]
+    k = k.split("(")[0]
+    return re.sub(r"^vc::", "", k).strip()
 
 
 def per_kernel(d):
