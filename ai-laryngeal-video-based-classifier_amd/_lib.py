@@ -48,8 +48,16 @@ SIGNATURES = {
     "vc_temporal_attention": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_int, c_p, c_i64, c_p], c_int),
     "vc_window_attention3d": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_int, c_int,
                                c_int, c_p, c_i64, c_p, c_i64, c_p], c_int),
+    "vc_window_attention3d_lse": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_int,
+                                   c_int, c_int, c_p, c_i64, c_p, c_i64, c_p, c_p], c_int),
+    "vc_window_attention3d_bwd": ([c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64,
+                                   c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_p, c_p, c_i64,
+                                   c_p, c_p], c_int),
     "vc_patch_merge_layernorm": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_p, c_i64, c_p], c_int),
     "vc_pool_head": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_p, c_p, c_i64, c_p, c_p, c_p], c_int),
+    "vc_pool_head_pooled": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_p, c_p, c_i64, c_p, c_p, c_p, c_p],
+                            c_int),
+    "vc_pool_head_bwd": ([c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f, c_p, c_p, c_p, c_p], c_int),
     "vc_conv3d_im2col": ([c_p, c_i64, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p], c_int),
     "vc_maxpool3d": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p], c_int),
     "vc_avgpool_head": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_i64, c_p, c_p, c_p], c_int),

@@ -349,9 +349,9 @@ def run_main(fam_name, argv=None):
         _load_weights(model, args.checkpoint_path, logger, fam)
     history = {"train_loss": [], "train_acc": [], "val_loss": [], "val_acc": []}
     if not args.skip_train:
-        if fam.name not in ("vivit", "timesformer"):
-            raise NotImplementedError(f"{fam.name}: only the ViViT and TimeSformer train steps have GPU backward "
-                                      "kernels in libvclip; evaluate a trained checkpoint with --skip_train "
+        if fam.name not in ("vivit", "timesformer", "swin"):
+            raise NotImplementedError(f"{fam.name}: only the ViViT, TimeSformer and Swin3D train steps have GPU "
+                                      "backward kernels in libvclip; evaluate a trained checkpoint with --skip_train "
                                       "--checkpoint_path")
         from .optim import AdamW
         opt = AdamW(model.parameters(), lr=args.learning_rate, weight_decay=args.weight_decay)
@@ -371,7 +371,7 @@ def run_main(fam_name, argv=None):
                     loss = crit(logits, y)
                     loss.backward()
                     opt.step()
-                    tl += float(loss) * len(y)
+                    tl += loss.item() * len(y)
                     tc += int((logits.argmax(1) == y).sum())
                     tn += len(y)
                 except Exception as e:  # noqa: BLE001
@@ -397,12 +397,15 @@ def run_main(fam_name, argv=None):
                         f"val loss {va_loss:.4f} acc {va_acc:.4f}")
 
             def save(path, epoch=epoch, va_loss=va_loss, va_acc=va_acc):
-                torch.save({"epoch": epoch, "model_state_dict": model.state_dict(),
-                            "optimizer_state_dict": opt.state_dict(), "val_loss": va_loss, "val_acc": va_acc,
-                            "history": history, "config": model.config.to_dict(), "id2label": model.config.id2label,
-                            "label2id": model.config.label2id, "num_frames": args.num_frames,
-                            "train_sampling": args.train_sampling, "val_sampling": args.val_sampling,
-                            "test_sampling": args.test_sampling}, path)
+                ck = {"epoch": epoch, "model_state_dict": model.state_dict(), "optimizer_state_dict": opt.state_dict(),
+                      "val_loss": va_loss, "val_acc": va_acc, "history": history}
+                if hasattr(model, "config"):  # HF families: vivit trainer.py:291-305 (and TimeSformer's)
+                    ck.update({"config": model.config.to_dict(), "id2label": model.config.id2label,
+                               "label2id": model.config.label2id, "num_frames": args.num_frames,
+                               "train_sampling": args.train_sampling, "val_sampling": args.val_sampling,
+                               "test_sampling": args.test_sampling})
+                # (Swin3D: videoswintransformer/.../trainers/trainer.py:191-198 saves the six keys above)
+                torch.save(ck, path)
 
             if va_loss < best_val:  # trainer.py:231-236 + _save_best_model
                 best_val = va_loss
@@ -445,6 +448,7 @@ def run_inference(fam_name, argv=None):
     else:
         model = fam.create_model(args, class_labels, device, logger)
     model.load_state_dict(sd)
+    model.eval()  # the reference inference scripts' model.eval()
     src = video_io.open_video(args.video_path)
     if fam.name in ("vivit", "timesformer"):
         sampler = sampling.VivitSampler(args.num_frames, args.sampling_method, logger)

@@ -1,5 +1,5 @@
 """torch.autograd Functions over the libvclip kernels, for the train steps composed in Python
-(TimeSformer: vclip_amd/timesformer.py `_forward_train`).
+(TimeSformer: vclip_amd/timesformer.py `_forward_train`; Swin3D: vclip_amd/swin3d.py `_forward_train`).
 
 Every arithmetic op here is a HIP kernel of libvclip.so, forward and backward:
   linear      bf16 MFMA GEMM + bias (vc_gemm_bf16) / dgrad GEMM on the packed W^T / split-K wgrad
@@ -11,7 +11,11 @@ Every arithmetic op here is a HIP kernel of libvclip.so, forward and backward:
               (vc_attention_bwd) — joint or spatial (TimeSformer B*T sequences of 1 + P tokens);
   temporal_attention  vc_temporal_attention / vc_temporal_attention_bwd (clip layout, T <= 32);
   gelu_erf    vc_gelu_erf / vc_gelu_erf_bwd;
-  cls_head    vc_cls_head / vc_cls_head_bwd (final LayerNorm on the CLS rows + classifier).
+  cls_head    vc_cls_head / vc_cls_head_bwd (final LayerNorm on the CLS rows + classifier);
+  window_attention  vc_window_attention3d_lse / vc_window_attention3d_bwd (Swin3D, head_dim 32, the
+              relative-position bias table differentiable) + vc_colsum of its per-window partials;
+  pool_head   vc_pool_head_pooled / vc_pool_head_bwd + vc_layernorm_bwd (Swin3D's final LayerNorm,
+              token mean and classifier).
 The tensors between them (residual adds, the clip <-> frame permutes, the CLS frame mean) are
 ordinary torch tensor ops: layout glue, autograd's bookkeeping.  Rows are padded internally to the
 kernels' tile multiples; the returned tensors have exactly the caller's rows.
@@ -41,40 +45,57 @@ class _Linear(torch.autograd.Function):
     def forward(ctx, x, w, b, out_f32: bool, qrows: int, qscale: float):
         M, K = x.shape
         N = w.shape[0]
-        Mp = _round_up(M, 256)
-        xp = _padded(x, Mp, torch.bfloat16)
-        wc = w.detach().contiguous().float()
-        wb = torch.empty(N, K, dtype=torch.bfloat16, device=x.device)
-        wt = torch.empty(K, N, dtype=torch.bfloat16, device=x.device)
+        # the GEMM tiles need M % 256 (rows), N and K % 128 (both also serve as the dgrad / wgrad
+        # GEMMs' output widths): zero rows / columns, exactly 0 through every product
+        Mp, Np, Kp = _round_up(M, 256), _round_up(N, 128), _round_up(K, 128)
+        xp = torch.zeros(Mp, Kp, dtype=torch.bfloat16, device=x.device)
+        xp[:M, :K].copy_(x)
+        wc = w.detach().float()
+        if (Np, Kp) != (N, K):
+            wc = torch.zeros(Np, Kp, dtype=torch.float32, device=x.device)
+            wc[:N, :K].copy_(w.detach())
+        wc = wc.contiguous()
+        wb = torch.empty(Np, Kp, dtype=torch.bfloat16, device=x.device)
+        wt = torch.empty(Kp, Np, dtype=torch.bfloat16, device=x.device)
         ops.pack_weight(wc, wb, wt, nscaled=qrows, scale=qscale)
-        bb = b.detach().float().clone()
-        if qrows:
-            bb[:qrows] *= qscale
-        out = torch.empty(Mp, N, dtype=torch.float32 if out_f32 else torch.bfloat16, device=x.device)
+        bb = torch.zeros(Np, dtype=torch.float32, device=x.device)
+        if b is not None:
+            bb[:N].copy_(b.detach())
+            if qrows:
+                bb[:qrows] *= qscale
+        out = torch.empty(Mp, Np, dtype=torch.float32 if out_f32 else torch.bfloat16, device=x.device)
         ops.gemm(xp, wb, bb, "bias_f32" if out_f32 else "bias", out)
         ctx.save_for_backward(xp, wt)
-        ctx.M, ctx.qrows, ctx.qscale, ctx.xdtype = M, qrows, qscale, x.dtype
-        return out[:M]
+        ctx.M, ctx.N, ctx.K, ctx.qrows, ctx.qscale, ctx.xdtype = M, N, K, qrows, qscale, x.dtype
+        ctx.has_bias = b is not None
+        return out[:M, :N] if Np != N else out[:M]
 
     @staticmethod
     def backward(ctx, dy):
         xp, wt = ctx.saved_tensors
-        Mp, K = xp.shape
-        N = wt.shape[1]
-        dyp = _padded(dy, Mp, torch.bfloat16)
-        dx = torch.empty(Mp, K, dtype=torch.bfloat16, device=dy.device)
-        ops.gemm(dyp, wt, torch.zeros(K, dtype=torch.float32, device=dy.device), "bias", dx)
-        dw = torch.empty(N, K, dtype=torch.float32, device=dy.device)
-        work = torch.empty(2 * N * K, dtype=torch.float32, device=dy.device)
+        Mp, Kp = xp.shape
+        Np = wt.shape[1]
+        M, N, K = ctx.M, ctx.N, ctx.K
+        dyp = torch.zeros(Mp, Np, dtype=torch.bfloat16, device=dy.device)
+        dyp[:M, :N].copy_(dy)
+        dx = torch.empty(Mp, Kp, dtype=torch.bfloat16, device=dy.device)
+        ops.gemm(dyp, wt, torch.zeros(Kp, dtype=torch.float32, device=dy.device), "bias", dx)
+        dw = torch.empty(Np, Kp, dtype=torch.float32, device=dy.device)
+        work = torch.empty(2 * Np * Kp, dtype=torch.float32, device=dy.device)
         ops.wgrad(dyp, xp, dw, work, nscaled=ctx.qrows, scale=ctx.qscale)
-        db = torch.empty(N, dtype=torch.float32, device=dy.device)
-        ops.colsum(dyp, db, nscaled=ctx.qrows, scale=ctx.qscale)
-        return dx[: ctx.M].to(ctx.xdtype), dw, db, None, None, None
+        db = None
+        if ctx.has_bias:
+            db = torch.empty(Np, dtype=torch.float32, device=dy.device)
+            ops.colsum(dyp, db, nscaled=ctx.qrows, scale=ctx.qscale)
+            db = db[:N]
+        dx = dx[:M, :K] if Kp != K else dx[:M]
+        dw = dw[:N, :K] if (Np, Kp) != (N, K) else dw
+        return dx.to(ctx.xdtype), dw, db, None, None, None
 
 
 def linear(x, w, b, out_f32=False, qrows=0, qscale=1.0):
-    """y = x @ w.T + b with bf16 operands (x bf16 [M, K], w / b fp32 masters), fp32 accumulation;
-    rows < qrows of w and b act multiplied by qscale."""
+    """y = x @ w.T + b with bf16 operands (x bf16 [M, K], w / b fp32 masters, b may be None), fp32
+    accumulation; rows < qrows of w and b act multiplied by qscale.  Any M, N, K (padded inside)."""
     return _Linear.apply(x, w, b, out_f32, qrows, qscale)
 
 
@@ -225,3 +246,86 @@ class _ClsHead(torch.autograd.Function):
 def cls_head(x, g, b, wc, bc, B, S, eps):
     """logits = classifier(LayerNorm(x[b*S])) over the CLS rows of f32 x [B*S, D]."""
     return _ClsHead.apply(x, g, b, wc, bc, B, S, eps)
+
+
+class _WindowAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, table, B: int, grid, heads: int, window, shift, full_window):
+        from .swin3d import expand_bias
+        T, H, W = grid
+        rows = B * T * H * W
+        biasT = expand_bias(table.detach(), full_window, window, qkv.device)
+        out = torch.empty(rows, heads * 32, dtype=torch.bfloat16, device=qkv.device)
+        lse = torch.empty(rows * heads, dtype=torch.float32, device=qkv.device)
+        ops.window_attention3d(qkv, B, grid, heads, window, shift, biasT, out, lse=lse)
+        ctx.save_for_backward(qkv, out, lse, table)
+        ctx.dims = (B, tuple(grid), heads, tuple(window), tuple(shift), tuple(full_window))
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse, table = ctx.saved_tensors
+        B, grid, heads, window, shift, full_window = ctx.dims
+        T, H, W = grid
+        ft, fh, fw = full_window
+        ntab = (2 * ft - 1) * (2 * fh - 1) * (2 * fw - 1)
+        nwin = B * (T // window[0]) * (H // window[1]) * (W // window[2])
+        d = dout.to(torch.bfloat16).contiguous()
+        dqkv = torch.empty(qkv.shape[0], 3 * heads * 32, dtype=torch.bfloat16, device=qkv.device)
+        part = torch.empty(nwin, heads * ntab, dtype=torch.float32, device=qkv.device)
+        tab = table.detach().float().contiguous()
+        ops.window_attention3d_bwd(qkv, out, d, lse, B, grid, heads, window, shift, full_window, tab, dqkv, part)
+        dtab = torch.empty(heads * ntab, dtype=torch.float32, device=qkv.device)
+        ops.colsum(part, dtab)  # sum of the per-(window, head) partials, fixed order
+        return dqkv, dtab.view(heads, ntab).t(), None, None, None, None, None, None
+
+
+def window_attention(qkv, table, B, grid, heads, window, shift, full_window):
+    """Swin 3D shifted-window attention (head_dim 32) with the relative-position bias table
+    [ntab, heads] as a differentiable input; qkv bf16 [B*T*H*W rows, 3*heads*32] (q' prescaled)."""
+    return _WindowAttention.apply(qkv, table, B, tuple(grid), heads, tuple(window), tuple(shift), tuple(full_window))
+
+
+class _PoolHead(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g, b, wc, bc, B: int, ntok: int, eps: float):
+        x = x.contiguous().float()
+        D = g.numel()
+        gc, bcn, wcc, bcc = (t.detach().float().contiguous() for t in (g, b, wc, bc))
+        nl = wcc.shape[0]
+        logits = torch.empty(B, nl, dtype=torch.float32, device=x.device)
+        pooled = torch.empty(B, D, dtype=torch.float32, device=x.device)
+        work = torch.empty(B * 64 * D, dtype=torch.float32, device=x.device)
+        _lib.call("vc_pool_head_pooled", _p(x), x.stride(0), B, ntok, D, _p(gc), _p(bcn), eps, _p(wcc), _p(bcc), nl,
+                  _p(logits), _p(work), _p(pooled), _stream(x))
+        ctx.save_for_backward(x, gc, wcc, pooled)
+        ctx.dims = (B, ntok, eps)
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        x, g, wc, pooled = ctx.saved_tensors
+        B, ntok, eps = ctx.dims
+        D, nl = g.numel(), wc.shape[0]
+        dl = dlogits.float().contiguous()
+        dpooled = torch.empty(B, D, dtype=torch.float32, device=x.device)
+        dwc = torch.empty(nl, D, dtype=torch.float32, device=x.device)
+        dbc = torch.empty(nl, dtype=torch.float32, device=x.device)
+        _lib.call("vc_pool_head_bwd", _p(pooled), _p(dl), _p(wc), B, D, nl, 1.0 / ntok, _p(dpooled), _p(dwc), _p(dbc),
+                  _stream(x))
+        dy = dpooled.repeat_interleave(ntok, 0)  # the mean's backward: every token of clip b gets dpooled[b]
+        M = x.shape[0]
+        dx = torch.zeros(M, D, dtype=torch.float32, device=x.device)
+        dxb = torch.empty(M, D, dtype=torch.bfloat16, device=x.device)
+        dg = torch.empty(D, dtype=torch.float32, device=x.device)
+        db = torch.empty(D, dtype=torch.float32, device=x.device)
+        nb = min(512, (M + 3) // 4)
+        work = torch.empty((nb + (nb + 31) // 32) * 4 * D, dtype=torch.float32, device=x.device)
+        ops.layernorm_bwd(dy, x, g, eps, dx, dxb, dg, db, work)
+        return dx, dg, db, dwc, dbc, None, None, None
+
+
+def pool_head(x, g, b, wc, bc, B, ntok, eps):
+    """torchvision SwinTransformer3d head: logits = Linear(mean over each clip's ntok tokens of
+    LayerNorm(x)) for f32 x [B*ntok, D]."""
+    return _PoolHead.apply(x, g, b, wc, bc, B, ntok, eps)

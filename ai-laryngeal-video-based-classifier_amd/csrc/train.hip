@@ -23,15 +23,18 @@ namespace trn {
 // ---------------------------------------------------------------------------------
 // SUMS: also the column sums of dx before and after the update (the bias gradients of the
 // Linear layers whose outputs these residual gradients are) -> part[block][4][D].
-template <int V, bool SUMS>
+// MASK: a width D <= 256 V that is any multiple of 4 (Swin's 96 / 192 / 384 / 1536): lanes past D
+// load zeros and store nothing; otherwise D = 256 V exactly.
+template <int V, bool SUMS, bool MASK = false>
 __global__ void __launch_bounds__(256) ln_bwd_kernel(const float* __restrict__ dy, int64_t lddy,
                                                      const float* __restrict__ x, int64_t ldx,
                                                      const float* __restrict__ gamma, float eps, int64_t M,
                                                      float* __restrict__ dx, int64_t lddx, uint16_t* __restrict__ dxb,
-                                                     int64_t lddxb, float* __restrict__ part) {
-    constexpr int D = V * 256;
+                                                     int64_t lddxb, float* __restrict__ part, int Drt = V * 256) {
+    constexpr int DV = V * 256;
+    const int D = MASK ? Drt : DV;
     constexpr int NP = SUMS ? 4 : 2;
-    __shared__ float red[4][NP * D];
+    __shared__ float red[4][NP * DV];
     float4 so[SUMS ? V : 1], sn[SUMS ? V : 1];
     if constexpr (SUMS) {
 #pragma unroll
@@ -43,8 +46,10 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const float* __restrict__ d
     for (int i = 0; i < V; ++i) {
         pg[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         pb[i] = pg[i];
-        g4[i] = reinterpret_cast<const float4*>(gamma)[i * 64 + lane];
+        g4[i] = (!MASK || (i * 64 + lane) * 4 < D) ? reinterpret_cast<const float4*>(gamma)[i * 64 + lane]
+                                                    : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    auto in_row = [&](int i) { return !MASK || (i * 64 + lane) * 4 < D; };
     for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < M; row += (int64_t)gridDim.x * 4) {
         const float4* xr = reinterpret_cast<const float4*>(x + row * ldx);
         const float4* dr = reinterpret_cast<const float4*>(dy + row * lddy);
@@ -52,18 +57,20 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const float* __restrict__ d
         float s = 0.f;
 #pragma unroll
         for (int i = 0; i < V; ++i) {
-            xv[i] = xr[i * 64 + lane];
-            dv[i] = dr[i * 64 + lane];
+            xv[i] = in_row(i) ? xr[i * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+            dv[i] = in_row(i) ? dr[i * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
             s += (xv[i].x + xv[i].y) + (xv[i].z + xv[i].w);
         }
-        const float mean = wave_sum(s) * (1.0f / D);
+        const float invD = MASK ? 1.0f / (float)D : 1.0f / DV;
+        const float mean = wave_sum(s) * invD;
         float q = 0.f;
 #pragma unroll
         for (int i = 0; i < V; ++i) {
+            if (!in_row(i)) continue;
             const float a = xv[i].x - mean, b = xv[i].y - mean, c = xv[i].z - mean, d = xv[i].w - mean;
             q += (a * a + b * b) + (c * c + d * d);
         }
-        const float rstd = rsqrtf(wave_sum(q) * (1.0f / D) + eps);
+        const float rstd = rsqrtf(wave_sum(q) * invD + eps);
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int i = 0; i < V; ++i) {
@@ -76,10 +83,11 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const float* __restrict__ d
             pg[i].z += dv[i].z * xv[i].z; pg[i].w += dv[i].w * xv[i].w;
             pb[i].x += dv[i].x; pb[i].y += dv[i].y; pb[i].z += dv[i].z; pb[i].w += dv[i].w;
         }
-        const float c1 = wave_sum(s1) * (1.0f / D), c2 = wave_sum(s2) * (1.0f / D);
+        const float c1 = wave_sum(s1) * invD, c2 = wave_sum(s2) * invD;
         float4* dxr = reinterpret_cast<float4*>(dx + row * lddx);
 #pragma unroll
         for (int i = 0; i < V; ++i) {
+            if (!in_row(i)) continue;
             float4 o = dxr[i * 64 + lane];
             if constexpr (SUMS) { so[i].x += o.x; so[i].y += o.y; so[i].z += o.z; so[i].w += o.w; }
             o.x += rstd * (dv[i].x * g4[i].x - c1 - xv[i].x * c2);
@@ -96,6 +104,7 @@ __global__ void __launch_bounds__(256) ln_bwd_kernel(const float* __restrict__ d
     }
 #pragma unroll
     for (int i = 0; i < V; ++i) {
+        if (!in_row(i)) continue;
         reinterpret_cast<float4*>(red[w])[i * 64 + lane] = pg[i];
         reinterpret_cast<float4*>(red[w] + D)[i * 64 + lane] = pb[i];
         if constexpr (SUMS) {
@@ -684,8 +693,8 @@ int vc_layernorm_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx,
                      hipStream_t stream) {
     if (!dy || !x || !gamma || !dx || !dxb || !dgamma || !dbeta || !work)
         return fail(VC_ERR_INVALID_ARG, "vc_layernorm_bwd: null pointer");
-    if (D != 256 && D != 512 && D != 768 && D != 1024)
-        return fail(VC_ERR_UNSUPPORTED, "vc_layernorm_bwd: D must be 256, 512, 768 or 1024");
+    if (D <= 0 || D % 4 || D > 1536)
+        return fail(VC_ERR_UNSUPPORTED, "vc_layernorm_bwd: D must be a multiple of 4, at most 1536");
     if (lddy % 4 || ldx % 4 || lddx % 4 || lddxb % 4 || M <= 0)
         return fail(VC_ERR_INVALID_ARG, "vc_layernorm_bwd: leading dimensions must be multiples of 4");
     if ((dsum_in == nullptr) != (dsum_out == nullptr))
@@ -702,13 +711,25 @@ int vc_layernorm_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx,
                                                                       lddxb, work), 0)                             \
           : (ln_bwd_kernel<V, false><<<(unsigned)nb, 256, 0, stream>>>(dy, lddy, x, ldx, gamma, eps, M, dx, lddx, dxb, \
                                                                        lddxb, work), 0))
+#define VC_LNBM(V)                                                                                                  \
+    (sums ? (ln_bwd_kernel<V, true, true><<<(unsigned)nb, 256, 0, stream>>>(dy, lddy, x, ldx, gamma, eps, M, dx, lddx,  \
+                                                                            dxb, lddxb, work, (int)D), 0)              \
+          : (ln_bwd_kernel<V, false, true><<<(unsigned)nb, 256, 0, stream>>>(dy, lddy, x, ldx, gamma, eps, M, dx, lddx, \
+                                                                             dxb, lddxb, work, (int)D), 0))
     switch (D) {
         case 256: VC_LNB(1); break;
         case 512: VC_LNB(2); break;
         case 768: VC_LNB(3); break;
-        default: VC_LNB(4); break;
+        case 1024: VC_LNB(4); break;
+        default:
+            if (D <= 256) VC_LNBM(1);
+            else if (D <= 512) VC_LNBM(2);
+            else if (D <= 768) VC_LNBM(3);
+            else if (D <= 1024) VC_LNBM(4);
+            else VC_LNBM(6);
     }
 #undef VC_LNB
+#undef VC_LNBM
     // partials [nb][np*D] -> [nsp][np*D] (32 rows per block) -> the np outputs
     float* tmp = work + nb * np * D;
     colsum_kernel<float><<<dim3((unsigned)((np * D + 255) / 256), (unsigned)nsp), 256, 0, stream>>>(

@@ -18,7 +18,7 @@
 // are one contiguous 64-B read, prefetched a tile ahead), the shift-region mask as -inf
 // (torchvision adds -100: exp(-100) ~ 4e-44 is below fp32 resolution of the row sum, so the
 // results agree), online softmax in exp2, O^T += V^T.P^T with V^T from ds_read_b64_tr_b16.
-#include "common.hpp"
+#include "window_common.hpp"
 
 #include <cstdlib>
 
@@ -26,42 +26,24 @@ namespace vc {
 
 constexpr int WNP_MAX = 448;  // max padded window volume (8*7*7 = 392 -> 448)
 
-__device__ __forceinline__ int kchunk_swz(int r, int c) { return c ^ ((r >> 2) & 3); }
-
-struct WinGeom {
-    int T, H, W;      // token grid (multiples of the window)
-    int wt, wh, ww;   // window
-    int st, sh, sw;   // shift (0 where none)
-    int nwt, nwh, nww;
-};
-
-// Shift-region label of one dimension for a rolled coordinate c (torchvision's t/h/w
-// slices: 0 below P-w, 1 in [P-w, P-s), 2 from P-s; with s == 0 the slices are (0,-w),
-// (-w,0) = empty and (0,None) = all, so every position gets 2).  Inside ONE window a
-// dimension takes at most two of these values ({0} or {1,2} or {2}), so "label == 2" is
-// one bit and the 3-bit code (t,h,w) compares equal exactly when the labels do.
-__device__ __forceinline__ int region_bit(int c, int P, int w, int s) {
-    if (s == 0) return 1;
-    return c >= P - s ? 1 : 0;
-}
-
-// DEFER (default): the ViViT kernel's deferred running max (attention.hip) — scores are taken
-// relative to a running max m fixed by the first key tile; per tile only exp2, the row sum and
-// the convert run; a lane's partial row sum <= LIM bounds every P of the tile, and only when
-// that fails is m re-based on the tile's exact max (O and l scaled by 2^-delta).  DEFER = false
-// is the online-softmax form with a per-tile max (and its rescale of O and l).  Swin-T B=4
-// (tools/swin_attn_stages.py, VCLIP_WINDOW_VARIANT A/B on one box): DEFER 1-5 % faster per
-// launch.  Where the rest goes: the fragment-order f32 bias stream (784 KB per (window, head)
-// workgroup, one tile of prefetch) costs 15-20 % (variant 2: no bias loads, timing only); the
+// Softmax with the ViViT kernel's deferred running max (attention.hip): scores are taken relative
+// to a running max m fixed by the first key tile; per tile only exp2, the row sum and the convert
+// run; a lane's partial row sum <= LIM bounds every P of the tile, and only when that fails is m
+// re-based on the tile's exact max (O and l scaled by 2^-delta).  Measured (Swin-T B=4, round 1):
+// 1-5 % faster per launch than a per-tile max.  Where the rest goes: the fragment-order f32 bias
+// stream (784 KB per (window, head) workgroup, one tile of prefetch) costs 15-20 %; the
 // shift-region mask +15-25 % on the shifted blocks; stages 3-4 fill only 384 / 192 of the 512
-// workgroup slots; 13 query blocks over 4 waves leave one wave a block longer than the rest.
+// workgroup slots (splitting a pair's query blocks over more workgroups measured slower: each
+// re-stages the window's K/V); 13 query blocks over 4 waves leave one wave a block longer.
+// WLSE (train step): also store each query's base-2 log-sum-exp lse[row * heads + head] = m +
+// log2(l) (row = global token row), from which window_bwd.hip recomputes P.
 constexpr float WLIM = 256.0f;
 
-template <bool DEFER, int ABL = 0>  // ABL 1: no bias loads (timing only, wrong results)
+template <bool WLSE>
 __global__ void __launch_bounds__(256, 2)
 window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, int heads, int vol, int NP,
                        const float* __restrict__ biasF, int masked, uint16_t* __restrict__ out, int64_t ldo,
-                       int qsplit) {
+                       float* __restrict__ lse) {
     __shared__ __attribute__((aligned(16))) char kv[2 * WNP_MAX * 64];
     __shared__ unsigned lab4[WNP_MAX / 8];  // 4-bit region code per window token (15: padding)
 
@@ -73,21 +55,9 @@ window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, 
     r -= wi_t * g.nwh * g.nww;
     const int wi_h = r / g.nww, wi_w = r - (r / g.nww) * g.nww;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int hw = g.wh * g.ww;
     const int C = heads * 32;
 
-    auto token_row = [&](int n, int* label) -> int64_t {
-        const int i = n / hw, j = (n / g.ww) % g.wh, k = n % g.ww;
-        const int tr = wi_t * g.wt + i, hr = wi_h * g.wh + j, wr = wi_w * g.ww + k;
-        if (label)
-            *label = 4 * region_bit(tr, g.T, g.wt, g.st) + 2 * region_bit(hr, g.H, g.wh, g.sh) +
-                     region_bit(wr, g.W, g.ww, g.sw);
-        int t = tr + g.st, hh = hr + g.sh, w = wr + g.sw;
-        t -= t >= g.T ? g.T : 0;
-        hh -= hh >= g.H ? g.H : 0;
-        w -= w >= g.W ? g.W : 0;
-        return (((int64_t)b * g.T + t) * g.H + hh) * g.W + w;
-    };
+    auto token_row = [&](int n, int* label) -> int64_t { return win_token_row(g, b, wi_t, wi_h, wi_w, n, label); };
 
     // ---- stage K (swizzled 16-B chunks) and V (plain 64-B rows) of this window/head in LDS
     char* Ks = kv;
@@ -132,13 +102,6 @@ window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, 
     // bias fragments: biasF[head][qb][t][kb][lane][16] f32 = this lane's 16 C-operand values
     const float* bh = biasF + (int64_t)head * (NP / 32) * ntile * 2 * 64 * 16 + lane * 16;
     auto load_bias = [&](int qb, int t, v16f (&c)[2]) {
-        if constexpr (ABL & 1) {
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) c[kb][e] = (float)(t + kb);
-            return;
-        }
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
             const float4* bp = reinterpret_cast<const float4*>(bh + (((int64_t)qb * ntile + t) * 2 + kb) * 64 * 16);
@@ -150,8 +113,8 @@ window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, 
         }
     };
 
-    // query blocks of this (window, head) are dealt over qsplit workgroups (blockIdx.z) x 4 waves
-    for (int qb = blockIdx.z + qsplit * wave; qb < nqb; qb += 4 * qsplit) {
+    // query blocks of this (window, head) are dealt over the 4 waves
+    for (int qb = wave; qb < nqb; qb += 4) {
         const int qn = qb * 32 + rr;  // this lane's query (window-local)
         const int qc = qn < vol ? qn : vol - 1;
         int qlab = 0;
@@ -164,89 +127,10 @@ window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, 
         float m_run = -1e30f, l_run = 0.f;
         v16f bnext[2];
         load_bias(qb, 0, bnext);
-        if constexpr (DEFER) {
-            // (bias fragments two tiles ahead instead of one: 238 VGPRs, 2 % slower per forward)
-            v2f l2 = {0.f, 0.f};
-            for (int t = 0; t < ntile; ++t) {
-                v16f sc[2] = {bnext[0], bnext[1]};
-                if (t + 1 < ntile) load_bias(qb, t + 1, bnext);
-#pragma unroll
-                for (int kk = 0; kk < 2; ++kk) {
-#pragma unroll
-                    for (int kb = 0; kb < 2; ++kb) {
-                        const v8bf kf = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(Ks + (t * 64 + kb * 32) * 64 + koff[kk]));
-                        sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kk], sc[kb], 0, 0, 0);
-                    }
-                }
-                if (masked) {
-#pragma unroll
-                    for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-                        for (int g4 = 0; g4 < 4; ++g4) {
-                            const int k0 = t * 64 + kb * 32 + 8 * g4 + 4 * h;
-                            const unsigned wv = lab4[k0 >> 3] >> (4 * (k0 & 7));
-#pragma unroll
-                            for (int e = 0; e < 4; ++e)
-                                if ((int)((wv >> (4 * e)) & 15) != qlab) sc[kb][4 * g4 + e] = -INFINITY;
-                        }
-                    }
-                }
-                auto rowmax = [&]() {
-                    float a = fmaxf(sc[0][0], sc[1][0]), c = fmaxf(sc[0][1], sc[1][1]);
-#pragma unroll
-                    for (int e = 2; e < 16; e += 2) {
-                        a = fmaxf(a, fmaxf(sc[0][e], sc[1][e]));
-                        c = fmaxf(c, fmaxf(sc[0][e + 1], sc[1][e + 1]));
-                    }
-                    const float x = fmaxf(a, c);
-                    return fmaxf(x, __shfl_xor(x, 32, 64));
-                };
-                if (t == 0) m_run = fmaxf(rowmax(), -1e30f);  // first tile fixes m (fully masked rows: -1e30)
-                v16f p[2];
-                auto expsum = [&]() {
-#pragma unroll
-                    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                        for (int e = 0; e < 16; ++e) p[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e] - m_run);
-                    v2f u[8];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        u[j] = v2f{p[0][4 * j], p[0][4 * j + 1]} + v2f{p[0][4 * j + 2], p[0][4 * j + 3]};
-                        u[4 + j] = v2f{p[1][4 * j], p[1][4 * j + 1]} + v2f{p[1][4 * j + 2], p[1][4 * j + 3]};
-                    }
-                    return ((u[0] + u[1]) + (u[2] + u[3])) + ((u[4] + u[5]) + (u[6] + u[7]));
-                };
-                v2f ps = expsum();
-                if (__any(!(ps[0] + ps[1] <= WLIM))) {  // rare: re-base m on this tile's exact max
-                    const float delta = fmaxf(rowmax() - m_run, 0.f);
-                    const float alpha = __builtin_amdgcn_exp2f(-delta);
-                    m_run += delta;
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) o[e] *= alpha;
-                    l2 *= alpha;
-                    ps = expsum();
-                }
-                l2 += ps;
-#pragma unroll
-                for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2) {
-                        v8bf pf;
-#pragma unroll
-                        for (int jj = 0; jj < 8; ++jj) pf[jj] = (__bf16)p[kb][8 * s2 + jj];
-                        const char* pa = Vs + (t * 64 + kb * 32 + 16 * s2) * 64 + voff;
-                        const v4s va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)pa);
-                        const v4s vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(pa + 8 * 64));
-                        v8s vv;
-                        vv[0] = va[0]; vv[1] = va[1]; vv[2] = va[2]; vv[3] = va[3];
-                        vv[4] = vb[0]; vv[5] = vb[1]; vv[6] = vb[2]; vv[7] = vb[3];
-                        o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf, vv), pf, o, 0, 0, 0);
-                    }
-            }
-            l_run = l2[0] + l2[1];
-        } else
+        // (bias fragments two tiles ahead instead of one: 238 VGPRs, 2 % slower per forward)
+        v2f l2 = {0.f, 0.f};
         for (int t = 0; t < ntile; ++t) {
-            v16f sc[2] = {bnext[0], bnext[1]};  // C = bias tile (prefetched one tile ahead)
+            v16f sc[2] = {bnext[0], bnext[1]};
             if (t + 1 < ntile) load_bias(qb, t + 1, bnext);
 #pragma unroll
             for (int kk = 0; kk < 2; ++kk) {
@@ -261,7 +145,6 @@ window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, 
                 for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
                     for (int g4 = 0; g4 < 4; ++g4) {
-                        // keys t*64 + kb*32 + 8*g4 + 4h + 0..3: one 16-bit run of the nibble table
                         const int k0 = t * 64 + kb * 32 + 8 * g4 + 4 * h;
                         const unsigned wv = lab4[k0 >> 3] >> (4 * (k0 & 7));
 #pragma unroll
@@ -270,32 +153,49 @@ window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, 
                     }
                 }
             }
-            float mx = m_run;
+            auto rowmax = [&]() {
+                float a = fmaxf(sc[0][0], sc[1][0]), c = fmaxf(sc[0][1], sc[1][1]);
 #pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) mx = fmaxf(mx, sc[kb][e]);
-            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-            const float alpha = __builtin_amdgcn_exp2f(m_run - mx);
-            m_run = mx;
-            float ls = 0.f;
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) {
-                    sc[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e] - mx);
-                    ls += sc[kb][e];
+                for (int e = 2; e < 16; e += 2) {
+                    a = fmaxf(a, fmaxf(sc[0][e], sc[1][e]));
+                    c = fmaxf(c, fmaxf(sc[0][e + 1], sc[1][e + 1]));
                 }
-            l_run = l_run * alpha + ls;
+                const float x = fmaxf(a, c);
+                return fmaxf(x, __shfl_xor(x, 32, 64));
+            };
+            if (t == 0) m_run = fmaxf(rowmax(), -1e30f);  // first tile fixes m (fully masked rows: -1e30)
+            v16f p[2];
+            auto expsum = [&]() {
 #pragma unroll
-            for (int e = 0; e < 16; ++e) o[e] *= alpha;
+                for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) p[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e] - m_run);
+                v2f u[8];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    u[j] = v2f{p[0][4 * j], p[0][4 * j + 1]} + v2f{p[0][4 * j + 2], p[0][4 * j + 3]};
+                    u[4 + j] = v2f{p[1][4 * j], p[1][4 * j + 1]} + v2f{p[1][4 * j + 2], p[1][4 * j + 3]};
+                }
+                return ((u[0] + u[1]) + (u[2] + u[3])) + ((u[4] + u[5]) + (u[6] + u[7]));
+            };
+            v2f ps = expsum();
+            if (__any(!(ps[0] + ps[1] <= WLIM))) {  // rare: re-base m on this tile's exact max
+                const float delta = fmaxf(rowmax() - m_run, 0.f);
+                const float alpha = __builtin_amdgcn_exp2f(-delta);
+                m_run += delta;
+#pragma unroll
+                for (int e = 0; e < 16; ++e) o[e] *= alpha;
+                l2 *= alpha;
+                ps = expsum();
+            }
+            l2 += ps;
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) {
                     v8bf pf;
 #pragma unroll
-                    for (int jj = 0; jj < 8; ++jj) pf[jj] = (__bf16)sc[kb][8 * s2 + jj];
+                    for (int jj = 0; jj < 8; ++jj) pf[jj] = (__bf16)p[kb][8 * s2 + jj];
                     const char* pa = Vs + (t * 64 + kb * 32 + 16 * s2) * 64 + voff;
                     const v4s va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)pa);
                     const v4s vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(pa + 8 * 64));
@@ -305,9 +205,14 @@ window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, 
                     o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf, vv), pf, o, 0, 0, 0);
                 }
         }
+        l_run = l2[0] + l2[1];
+
         // ---- O^T[d][q]: reg 4g+e -> d = 8g + 4h + e; lane pairs swap halves -> 16-B stores
         const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
         const float inv = 1.0f / l_tot;
+        if constexpr (WLSE) {
+            if (h == 0 && qn < vol) lse[qrow * heads + head] = m_run + __log2f(l_tot);
+        }
         unsigned pk[4][2];
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
@@ -479,9 +384,10 @@ __global__ void __launch_bounds__(256) pool_partial_kernel(const float* __restri
         work[((int64_t)b * POOL_CHUNKS + ch) * D + n] = (red[0][n] + red[1][n]) + (red[2][n] + red[3][n]);
 }
 
+// pooled (optional, train step): the pooled features [B][D] the head saw, for its backward
 __global__ void __launch_bounds__(256) pool_final_kernel(const float* __restrict__ work, int64_t ntok, int D,
                                                          const float* __restrict__ Wc, const float* __restrict__ bc,
-                                                         int nl, float* __restrict__ logits) {
+                                                         int nl, float* __restrict__ logits, float* __restrict__ pooled_out) {
     __shared__ float pooled[1024];
     const int b = blockIdx.x;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -489,6 +395,7 @@ __global__ void __launch_bounds__(256) pool_final_kernel(const float* __restrict
         float s = 0.f;
         for (int c = 0; c < POOL_CHUNKS; ++c) s += work[((int64_t)b * POOL_CHUNKS + c) * D + n];
         pooled[n] = s / (float)ntok;
+        if (pooled_out) pooled_out[(int64_t)b * D + n] = pooled[n];
     }
     __syncthreads();
     for (int c = w; c < nl; c += 4) {
@@ -505,9 +412,9 @@ using namespace vc;
 
 extern "C" {
 
-int vc_window_attention3d(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T, int64_t H, int64_t W, int64_t heads,
-                          int64_t head_dim, int wt, int wh, int ww, int st, int sh, int sw, const float* biasF,
-                          int64_t np, uint16_t* out, int64_t ldo, hipStream_t stream) {
+static int window_fwd(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T, int64_t H, int64_t W, int64_t heads,
+                      int64_t head_dim, int wt, int wh, int ww, int st, int sh, int sw, const float* biasF, int64_t np,
+                      uint16_t* out, int64_t ldo, float* lse, hipStream_t stream) {
     if (!qkv || !biasF || !out) return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d: null pointer");
     if (head_dim != 32) return fail(VC_ERR_UNSUPPORTED, "vc_window_attention3d: head_dim must be 32");
     if (wt <= 0 || wh <= 0 || ww <= 0 || T % wt || H % wh || W % ww)
@@ -524,34 +431,27 @@ int vc_window_attention3d(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T,
     if (nwin > 0x7fffffff || heads > 65535) return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d: grid too large");
     dim3 grid((unsigned)nwin, (unsigned)heads);
     if ((uintptr_t)biasF & 15) return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d: biasF must be 16-B aligned");
-    static const int variant = [] {  // VCLIP_WINDOW_VARIANT (A/B only): 0 per-tile max, 1 no query split
-        const char* v = getenv("VCLIP_WINDOW_VARIANT");
-        return v ? atoi(v) : 1;
-    }();
-    // Variant 3 (A/B only): later Swin stages have few (window, head) pairs (Swin-T B=4: 384 and
-    // 192 workgroups for 512 slots); split each pair's query blocks over qsplit workgroups (each
-    // stages the window's K/V itself) until the grid holds >= 3 rounds of two workgroups per CU.
-    // Measured SLOWER (stage 4: 41.6 vs 36.4 us): those launches are bound by each workgroup's
-    // staging and single-wave latency, not by the empty slots, so the default keeps qsplit = 1.
-    static const int slots = [] {
-        int dev = 0, n = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-        return 2 * n;
-    }();
-    int qsplit = 1;
-    const int nqb = (vol + 31) / 32;
-    if (variant == 3)
-        while (qsplit < 8 && 2 * qsplit <= nqb && nwin * heads * qsplit < 3LL * slots) qsplit *= 2;
-    grid.z = (unsigned)qsplit;
     const int mk = (st | sh | sw) ? 1 : 0;
-    if (variant == 2)  // timing-only ablation: no bias loads
-        window_attn_d32_kernel<true, 1><<<grid, 256, 0, stream>>>(qkv, ld, g, (int)heads, vol, (int)np, biasF, mk, out, ldo, qsplit);
-    else if (variant == 0)
-        window_attn_d32_kernel<false><<<grid, 256, 0, stream>>>(qkv, ld, g, (int)heads, vol, (int)np, biasF, mk, out, ldo, qsplit);
+    if (lse)
+        window_attn_d32_kernel<true><<<grid, 256, 0, stream>>>(qkv, ld, g, (int)heads, vol, (int)np, biasF, mk, out, ldo, lse);
     else
-        window_attn_d32_kernel<true><<<grid, 256, 0, stream>>>(qkv, ld, g, (int)heads, vol, (int)np, biasF, mk, out, ldo, qsplit);
+        window_attn_d32_kernel<false><<<grid, 256, 0, stream>>>(qkv, ld, g, (int)heads, vol, (int)np, biasF, mk, out, ldo,
+                                                                nullptr);
     return check_launch("vc_window_attention3d");
+}
+
+int vc_window_attention3d(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T, int64_t H, int64_t W, int64_t heads,
+                          int64_t head_dim, int wt, int wh, int ww, int st, int sh, int sw, const float* biasF,
+                          int64_t np, uint16_t* out, int64_t ldo, hipStream_t stream) {
+    return window_fwd(qkv, ld, B, T, H, W, heads, head_dim, wt, wh, ww, st, sh, sw, biasF, np, out, ldo, nullptr, stream);
+}
+
+int vc_window_attention3d_lse(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T, int64_t H, int64_t W,
+                              int64_t heads, int64_t head_dim, int wt, int wh, int ww, int st, int sh, int sw,
+                              const float* biasF, int64_t np, uint16_t* out, int64_t ldo, float* lse,
+                              hipStream_t stream) {
+    if (!lse) return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d_lse: null lse");
+    return window_fwd(qkv, ld, B, T, H, W, heads, head_dim, wt, wh, ww, st, sh, sw, biasF, np, out, ldo, lse, stream);
 }
 
 int vc_patch_merge_layernorm(const float* x, int64_t ldx, int64_t B, int64_t T, int64_t H, int64_t W, int64_t C,
@@ -586,16 +486,60 @@ int vc_patch_merge_layernorm(const float* x, int64_t ldx, int64_t B, int64_t T, 
     return check_launch("vc_patch_merge_layernorm");
 }
 
-int vc_pool_head(const float* x, int64_t ldx, int64_t B, int64_t ntok, int64_t D, const float* gamma,
-                 const float* beta, float eps, const float* Wc, const float* bc, int64_t num_labels, float* logits,
-                 float* work, hipStream_t stream) {
+int vc_pool_head_pooled(const float* x, int64_t ldx, int64_t B, int64_t ntok, int64_t D, const float* gamma,
+                        const float* beta, float eps, const float* Wc, const float* bc, int64_t num_labels, float* logits,
+                        float* work, float* pooled, hipStream_t stream) {
     if (!x || !gamma || !beta || !Wc || !bc || !logits || !work)
         return fail(VC_ERR_INVALID_ARG, "vc_pool_head: null pointer");
     if (D <= 0 || D > 1024 || D % 4 || ldx % 4 || ntok <= 0 || ((uintptr_t)x & 15))
         return fail(VC_ERR_UNSUPPORTED, "vc_pool_head: D % 4 == 0, D <= 1024, 16-B aligned rows, ntok > 0");
     pool_partial_kernel<<<dim3((unsigned)B, POOL_CHUNKS), 256, 0, stream>>>(x, ldx, ntok, (int)D, gamma, beta, eps, work);
-    pool_final_kernel<<<(unsigned)B, 256, 0, stream>>>(work, ntok, (int)D, Wc, bc, (int)num_labels, logits);
+    pool_final_kernel<<<(unsigned)B, 256, 0, stream>>>(work, ntok, (int)D, Wc, bc, (int)num_labels, logits, pooled);
     return check_launch("vc_pool_head");
+}
+
+int vc_pool_head(const float* x, int64_t ldx, int64_t B, int64_t ntok, int64_t D, const float* gamma,
+                 const float* beta, float eps, const float* Wc, const float* bc, int64_t num_labels, float* logits,
+                 float* work, hipStream_t stream) {
+    return vc_pool_head_pooled(x, ldx, B, ntok, D, gamma, beta, eps, Wc, bc, num_labels, logits, work, nullptr, stream);
+}
+
+// Backward of the classifier GEMV of vc_pool_head_pooled (fp32): dpooled[b] = scale * dlogits[b] . Wc,
+// dWc[c] = sum_b dlogits[b][c] pooled[b], dbc[c] = sum_b dlogits[b][c] (fixed summation order)
+__global__ void __launch_bounds__(256) head_bwd_kernel(const float* __restrict__ pooled, const float* __restrict__ dlog,
+                                                       const float* __restrict__ Wc, int B, int D, int nl, float scale,
+                                                       float* __restrict__ dpooled, float* __restrict__ dWc,
+                                                       float* __restrict__ dbc) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < (int64_t)B * D + (int64_t)nl * D + nl;
+         i += (int64_t)gridDim.x * 256) {
+        if (i < (int64_t)B * D) {
+            const int b = (int)(i / D), n = (int)(i % D);
+            float s = 0.f;
+            for (int c = 0; c < nl; ++c) s += dlog[b * nl + c] * Wc[(int64_t)c * D + n];
+            dpooled[i] = s * scale;
+        } else if (i < (int64_t)B * D + (int64_t)nl * D) {
+            const int64_t j = i - (int64_t)B * D;
+            const int c = (int)(j / D), n = (int)(j % D);
+            float s = 0.f;
+            for (int b = 0; b < B; ++b) s += dlog[b * nl + c] * pooled[(int64_t)b * D + n];
+            dWc[j] = s;
+        } else {
+            const int c = (int)(i - (int64_t)B * D - (int64_t)nl * D);
+            float s = 0.f;
+            for (int b = 0; b < B; ++b) s += dlog[b * nl + c];
+            dbc[c] = s;
+        }
+    }
+}
+
+int vc_pool_head_bwd(const float* pooled, const float* dlogits, const float* Wc, int64_t B, int64_t D, int64_t num_labels,
+                     float scale, float* dpooled, float* dWc, float* dbc, hipStream_t stream) {
+    if (!pooled || !dlogits || !Wc || !dpooled || !dWc || !dbc) return fail(VC_ERR_INVALID_ARG, "vc_pool_head_bwd: null pointer");
+    if (B <= 0 || D <= 0 || num_labels <= 0) return fail(VC_ERR_INVALID_ARG, "vc_pool_head_bwd: bad shape");
+    const int64_t n = B * D + num_labels * D + num_labels;
+    head_bwd_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(pooled, dlogits, Wc, (int)B, (int)D, (int)num_labels,
+                                                                    scale, dpooled, dWc, dbc);
+    return check_launch("vc_pool_head_bwd");
 }
 
 }  // extern "C"

@@ -285,7 +285,7 @@ def divided_add_layernorm(x: torch.Tensor, y: torch.Tensor, B: int, P: int, T: i
 
 
 def window_attention3d(qkv: torch.Tensor, B: int, grid, heads: int, window, shift, biasT: torch.Tensor,
-                       out: torch.Tensor) -> torch.Tensor:
+                       out: torch.Tensor, lse: torch.Tensor | None = None) -> torch.Tensor:
     """Swin 3D shifted-window attention (head_dim 32) on the token layout [B][T][H][W]:
     qkv bf16 [>= B*T*H*W, >= 3*heads*32] (q pre-scaled by d^-1/2 * log2 e), biasT the f32
     fragment-order bias of swin3d.expand_bias (see include/vclip.h) -> out bf16 [rows, >= heads*32]."""
@@ -302,9 +302,40 @@ def window_attention3d(qkv: torch.Tensor, B: int, grid, heads: int, window, shif
     _need(qkv.shape[0] >= B * T * H * W and out.shape[0] >= B * T * H * W, "window_attention3d rows")
     _need(qkv.shape[1] >= 3 * heads * 32 and out.shape[1] >= heads * 32, "window_attention3d columns")
     _need(T % wt == 0 and H % wh == 0 and W % ww == 0, "window_attention3d: grid must be whole windows")
+    if lse is not None:  # train step: + base-2 log-sum-exp per (token row, head)
+        _dev(lse)
+        _need(lse.dtype == torch.float32 and lse.is_contiguous() and lse.numel() >= B * T * H * W * heads,
+              "window_attention3d lse: f32 [rows * heads]")
+        _lib.call("vc_window_attention3d_lse", _p(qkv), qkv.stride(0), B, T, H, W, heads, 32, wt, wh, ww, st, sh, sw,
+                  _p(biasT), np_, _p(out), out.stride(0), _p(lse), _stream(qkv))
+        return out
     _lib.call("vc_window_attention3d", _p(qkv), qkv.stride(0), B, T, H, W, heads, 32, wt, wh, ww, st, sh, sw, _p(biasT),
               np_, _p(out), out.stride(0), _stream(qkv))
     return out
+
+
+def window_attention3d_bwd(qkv: torch.Tensor, out: torch.Tensor, dout: torch.Tensor, lse: torch.Tensor, B: int, grid,
+                           heads: int, window, shift, full_window, table: torch.Tensor, dqkv: torch.Tensor,
+                           dtable_part: torch.Tensor) -> torch.Tensor:
+    """Backward of window_attention3d: dqkv (bf16 rows, d q' | dk | dv) and the per-(window, head)
+    bias-table gradient partials dtable_part f32 [B * nwindows, heads, ntab] (sum over dim 0)."""
+    _dev(qkv, out, dout, lse, table, dqkv, dtable_part)
+    T, H, W = grid
+    wt, wh, ww = window
+    st, sh, sw = shift
+    ft, fh, fw = full_window
+    ntab = (2 * ft - 1) * (2 * fh - 1) * (2 * fw - 1)
+    nwin = B * (T // wt) * (H // wh) * (W // ww)
+    for nm, t in (("qkv", qkv), ("out", out), ("dout", dout), ("dqkv", dqkv)):
+        _need(t.dtype == torch.bfloat16 and t.stride(1) == 1 and t.shape[0] >= B * T * H * W, f"window bwd {nm}")
+    _need(table.dtype == torch.float32 and table.is_contiguous() and tuple(table.shape) == (ntab, heads),
+          "window bwd table: f32 [ntab, heads]")
+    _need(dtable_part.dtype == torch.float32 and dtable_part.is_contiguous() and dtable_part.numel() >= nwin * heads * ntab,
+          "window bwd dtable_part: f32 [B * nwindows * heads * ntab]")
+    _lib.call("vc_window_attention3d_bwd", _p(qkv), qkv.stride(0), _p(out), out.stride(0), _p(dout), dout.stride(0),
+              _p(lse), B, T, H, W, heads, 32, wt, wh, ww, st, sh, sw, ft, fh, fw, _p(table), _p(dqkv), dqkv.stride(0),
+              _p(dtable_part), _stream(qkv))
+    return dqkv
 
 
 def patch_merge_layernorm(x: torch.Tensor, B: int, grid, C: int, gamma, beta, eps: float,

@@ -34,12 +34,13 @@ from .weights import swin3d_param_shapes
 LOG2E = ops.LOG2E
 
 SWIN3D_CONFIGS = {
+    # stochastic_depth_prob: torchvision swin3d_t / _s / _b (train-time only)
     "tiny": dict(patch_size=(2, 4, 4), embed_dim=96, depths=(2, 2, 6, 2), num_heads=(3, 6, 12, 24),
-                 window_size=(8, 7, 7), mlp_ratio=4.0, layer_norm_eps=1e-5),
+                 window_size=(8, 7, 7), mlp_ratio=4.0, layer_norm_eps=1e-5, stochastic_depth_prob=0.1),
     "small": dict(patch_size=(2, 4, 4), embed_dim=96, depths=(2, 2, 18, 2), num_heads=(3, 6, 12, 24),
-                  window_size=(8, 7, 7), mlp_ratio=4.0, layer_norm_eps=1e-5),
+                  window_size=(8, 7, 7), mlp_ratio=4.0, layer_norm_eps=1e-5, stochastic_depth_prob=0.2),
     "base": dict(patch_size=(2, 4, 4), embed_dim=128, depths=(2, 2, 18, 2), num_heads=(4, 8, 16, 32),
-                 window_size=(8, 7, 7), mlp_ratio=4.0, layer_norm_eps=1e-5),
+                 window_size=(8, 7, 7), mlp_ratio=4.0, layer_norm_eps=1e-5, stochastic_depth_prob=0.1),
 }
 SWIN3D_CONFIGS["base_in22k"] = SWIN3D_CONFIGS["base"]
 
@@ -109,11 +110,12 @@ class Swin3d(torch.nn.Module):
         self._names = list(shapes.keys())
         self.params = torch.nn.ParameterDict()
         for n, s in shapes.items():
-            self.params[n.replace(".", "__")] = torch.nn.Parameter(torch.zeros(s), requires_grad=False)
+            self.params[n.replace(".", "__")] = torch.nn.Parameter(torch.zeros(s))
         self._packed = None
         self._bias_cache = {}
         self._ws = {}
         self.kernel_events = None  # list: HIP events around each window-attention launch (bench.py)
+        self.stochastic_depth = True  # train step: torchvision's StochasticDepth on the residual branches
 
     def state_dict(self, *a, **k):
         return OrderedDict((n, self.params[n.replace(".", "__")].detach()) for n in self._names)
@@ -137,9 +139,18 @@ class Swin3d(torch.nn.Module):
         return missing, unexpected
 
     # ---- packing -------------------------------------------------------------------
+    def P(self, name):
+        return self.params[name.replace(".", "__")]
+
+    def _weights_version(self):
+        from . import vivit_train
+        return (vivit_train.MASTER_EPOCH[0], sum(p._version for p in self.params.values()))
+
     def _pack(self, device):
-        if self._packed is not None and self._packed["device"] == device:
+        ver = self._weights_version()  # the fused AdamW updates in place without bumping _version
+        if self._packed is not None and self._packed["device"] == device and self._packed["version"] == ver:
             return self._packed
+        self._bias_cache = {}
         c = self.cfg
         bf, f32 = torch.bfloat16, torch.float32
         P = lambda n: self.params[n.replace(".", "__")].detach().to(device=device, dtype=f32)  # noqa: E731
@@ -155,7 +166,7 @@ class Swin3d(torch.nn.Module):
                 out[:b.numel()] = b
             return out
 
-        pk = {"device": device}
+        pk = {"device": device, "version": ver}
         C0 = c["embed_dim"]
         pt, ph, pw = c["patch_size"]
         K0 = 3 * pt * ph * pw
@@ -243,12 +254,84 @@ class Swin3d(torch.nn.Module):
         return ws
 
     # ---- forward -------------------------------------------------------------------
-    @torch.no_grad()
     def forward(self, video: torch.Tensor) -> torch.Tensor:
+        """`model(clips)` -> logits.  In training mode with autograd enabled (the reference's train
+        loop, videoswintransformer/swin_video_classifier/trainers/trainer.py:105-122) the logits carry
+        the graph of the HIP train step (_forward_train); otherwise the fused inference path runs."""
         if video.device.type != "cuda":
             raise RuntimeError("Swin3d (vclip_amd) runs on the GPU only: move the clip batch to cuda")
         x = video.contiguous().float() if video.dtype != torch.float32 else video.contiguous()
-        return self.forward_logits(x)
+        if self.training and torch.is_grad_enabled():
+            return self._forward_train(x)
+        with torch.no_grad():
+            return self.forward_logits(x).clone()  # the workspace buffer is reused by the next call
+
+    def _forward_train(self, video: torch.Tensor) -> torch.Tensor:
+        """torchvision's SwinTransformer3d forward (oracle/swin3d_ref.py) as autograd ops over the HIP
+        kernels (vclip_amd/autograd_ops.py): bf16 MFMA GEMMs with fp32 accumulation on the fp32
+        master weights, fp32 residual stream, exact GELU, the shifted-window attention with its
+        relative-position bias table differentiable, the fused pool head; the token layout
+        [B][T][H][W] rows throughout, PatchMerging's neighbour gather and the residual adds as torch
+        layout glue.  Stochastic depth as torchvision's StochasticDepth(p_k, "row") on both residual
+        branches of block k (p_k = stochastic_depth_prob * k / (blocks - 1); a per-clip keep mask
+        from torch's RNG, scaled by 1 / (1 - p_k)); `self.stochastic_depth = False` turns it off."""
+        from . import autograd_ops as A
+        c = self.cfg
+        B, Cin, T, H, W = video.shape
+        if Cin != 3:
+            raise ValueError("video must be [B, 3, T, H, W]")
+        eps = c["layer_norm_eps"]
+        pt, ph, pw = c["patch_size"]
+        grids = self.geometry(B, T, H, W)
+        t0, h0, w0 = grids[0]
+        C0 = c["embed_dim"]
+        M0 = B * t0 * h0 * w0
+        K0 = 3 * pt * ph * pw
+        a_emb = torch.zeros(_ru(M0, 256), _ru(K0, 64), dtype=torch.bfloat16, device=video.device)
+        ops.tubelet_im2col(video, (pt, ph, pw), a_emb, layout="bcthw")
+        e = A.linear(a_emb[:M0, :K0], self.P("patch_embed.proj.weight").reshape(C0, K0), self.P("patch_embed.proj.bias"),
+                     out_f32=True)
+        x = A.layer_norm(e, self.P("patch_embed.norm.weight"), self.P("patch_embed.norm.bias"), eps, out_bf16=False)
+        full = tuple(c["window_size"])
+        nblocks, k = sum(c["depths"]), 0
+        sd = c.get("stochastic_depth_prob", 0.0) if self.stochastic_depth else 0.0
+
+        def drop_path(y, prob):  # torchvision StochasticDepth(prob, "row") on a [B * ntok, C] branch output
+            if prob <= 0.0:
+                return y
+            keep = torch.empty(B, 1, 1, device=y.device).bernoulli_(1.0 - prob).div_(1.0 - prob)
+            return (y.reshape(B, -1, y.shape[-1]) * keep).reshape(y.shape)
+
+        for s, depth in enumerate(c["depths"]):
+            t, h, w = grids[s]
+            C = C0 * 2 ** s
+            heads = c["num_heads"][s]
+            qs = 32 ** -0.5 * LOG2E
+            for i in range(depth):
+                p = f"features.{2 * s}.{i}."
+                shift_full = [0 if i % 2 == 0 else wk // 2 for wk in full]
+                window, shift = window_and_shift((t, h, w), full, shift_full)
+                pk_ = sd * k / (nblocks - 1) if nblocks > 1 else 0.0
+                k += 1
+                y = A.layer_norm(x, self.P(p + "norm1.weight"), self.P(p + "norm1.bias"), eps)
+                qkv = A.linear(y, self.P(p + "attn.qkv.weight"), self.P(p + "attn.qkv.bias"), qrows=C, qscale=qs)
+                o = A.window_attention(qkv, self.P(p + "attn.relative_position_bias_table"), B, (t, h, w), heads,
+                                       window, shift, full)
+                x = x + drop_path(A.linear(o, self.P(p + "attn.proj.weight"), self.P(p + "attn.proj.bias"), out_f32=True),
+                                  pk_)
+                y = A.layer_norm(x, self.P(p + "norm2.weight"), self.P(p + "norm2.bias"), eps)
+                hd = A.gelu_erf(A.linear(y, self.P(p + "mlp.0.weight"), self.P(p + "mlp.0.bias")))
+                x = x + drop_path(A.linear(hd, self.P(p + "mlp.3.weight"), self.P(p + "mlp.3.bias"), out_f32=True), pk_)
+            if s < len(c["depths"]) - 1:
+                p = f"features.{2 * s + 1}."
+                xv = x.reshape(B, t, h, w, C)
+                xv = torch.nn.functional.pad(xv, (0, 0, 0, w % 2, 0, h % 2))  # torchvision _patch_merging_pad
+                xm = torch.cat([xv[:, :, 0::2, 0::2], xv[:, :, 1::2, 0::2], xv[:, :, 0::2, 1::2], xv[:, :, 1::2, 1::2]], -1)
+                y = A.layer_norm(xm.reshape(-1, 4 * C), self.P(p + "norm.weight"), self.P(p + "norm.bias"), eps)
+                x = A.linear(y, self.P(p + "reduction.weight"), None, out_f32=True)
+        t, h, w = grids[-1]
+        return A.pool_head(x, self.P("norm.weight"), self.P("norm.bias"), self.P("head.weight"), self.P("head.bias"), B,
+                           t * h * w, eps)
 
     def forward_logits(self, video: torch.Tensor) -> torch.Tensor:
         c = self.cfg

@@ -355,6 +355,28 @@ int vc_window_attention3d(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T,
                           int64_t head_dim, int wt, int wh, int ww, int st, int sh, int sw, const float* biasF,
                           int64_t np, uint16_t* out, int64_t ldo, hipStream_t stream);
 
+/* Train-step forward: vc_window_attention3d plus lse[row * heads + head] = base-2 log-sum-exp of
+ * each query's scores (row = its global token row), kept for the backward. */
+int vc_window_attention3d_lse(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T, int64_t H, int64_t W,
+                              int64_t heads, int64_t head_dim, int wt, int wh, int ww, int st, int sh, int sw,
+                              const float* biasF, int64_t np, uint16_t* out, int64_t ldo, float* lse,
+                              hipStream_t stream);
+
+/*
+ * Backward of vc_window_attention3d (the Swin3D train step; autograd of torchvision
+ * shifted_window_attention_3d as videoswintransformer/.../trainers/trainer.py:105-122 runs it):
+ * dqkv rows (d q', dk, dv, bf16; every row of the token grid written once) from q|k|v, the
+ * forward output `out`, its gradient `dout` and lse; full_t/h/w = the model's window_size, on
+ * which the relative-position index is defined; table = the f32 bias table [(2ft-1)(2fh-1)(2fw-1)]
+ * [heads] (torchvision layout, natural units).  dtable_part = f32 [B * nwindows][heads][ntab]:
+ * each (window, head)'s bias-table gradient, to be summed over windows by the caller (vc_colsum).
+ */
+int vc_window_attention3d_bwd(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ldo,
+                              const uint16_t* dout, int64_t lddo, const float* lse, int64_t B, int64_t T,
+                              int64_t H, int64_t W, int64_t heads, int64_t head_dim, int wt, int wh, int ww,
+                              int st, int sh, int sw, int full_t, int full_h, int full_w, const float* table,
+                              uint16_t* dqkv, int64_t lddq, float* dtable_part, hipStream_t stream);
+
 /*
  * PatchMerging gather + LayerNorm(4C): y[(b,t,i,j)] = LN(cat(x[2i,2j], x[2i+1,2j], x[2i,2j+1],
  * x[2i+1,2j+1])) in bf16 (zero rows past an odd edge); the Linear(4C, 2C) follows as a GEMM.
@@ -372,6 +394,17 @@ int vc_patch_merge_layernorm(const float* x, int64_t ldx, int64_t B, int64_t T, 
 int vc_pool_head(const float* x, int64_t ldx, int64_t B, int64_t ntok, int64_t D, const float* gamma,
                  const float* beta, float eps, const float* Wc, const float* bc, int64_t num_labels, float* logits,
                  float* work, hipStream_t stream);
+
+/* vc_pool_head that also stores the pooled features pooled[B][D] (train step: the head's input). */
+int vc_pool_head_pooled(const float* x, int64_t ldx, int64_t B, int64_t ntok, int64_t D, const float* gamma,
+                        const float* beta, float eps, const float* Wc, const float* bc, int64_t num_labels, float* logits,
+                        float* work, float* pooled, hipStream_t stream);
+
+/* Backward of vc_pool_head's classifier (fp32): dpooled = scale * dlogits . Wc (scale = 1/ntok folds
+ * the mean's backward), dWc = dlogits^T . pooled, dbc = column sums of dlogits.  The LayerNorm
+ * backward of the pooled tokens is vc_layernorm_bwd. */
+int vc_pool_head_bwd(const float* pooled, const float* dlogits, const float* Wc, int64_t B, int64_t D, int64_t num_labels,
+                     float scale, float* dpooled, float* dWc, float* dbc, hipStream_t stream);
 
 /* ---- ViViT train step: trainers/trainer.py:140-146 — forward, CE loss,
  * loss.backward(), AdamW.step() — and its data-parallel gradient all-reduce (§8e) ----------- */

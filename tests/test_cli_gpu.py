@@ -98,7 +98,7 @@ def test_eval_and_inference_clis(dataset, tmp_path, fam, extra):
                                str(tmp_path / "models"), "--skip_train", "--checkpoint_path", str(ck_path),
                                "--batch_size", "2"] + extra)
     assert (exp / "test_metrics_uniform.json").exists() and 0.0 <= m["accuracy"] <= 1.0
-    if fam != "timesformer":  # the TimeSformer train step exists (test_timesformer_main_trains)
+    if fam == "resnet3d":  # the TimeSformer / Swin3D train steps exist (test_*_main_trains)
         with pytest.raises(NotImplementedError):
             run_main(fam, ["--data_dir", str(dataset), "--log_dir", str(tmp_path / "l2"), "--model_dir",
                            str(tmp_path / "m2"), "--epochs", "1"] + extra)
@@ -135,3 +135,17 @@ def test_timesformer_main_trains(dataset, tmp_path):
     assert (exp / "test_metrics_uniform.json").exists()
     ck = torch.load(tmp_path / "models" / "best_model_uniform.pth", weights_only=True)
     assert "model_state_dict" in ck and "optimizer_state_dict" in ck and ck["num_frames"] == 8
+
+
+def test_swin_main_trains(dataset, tmp_path):
+    """videoswintransformer/main.py trains by default (trainer.py:105-122): one epoch of the reference
+    loop on the HIP Swin3D train step with the train-time transforms, the Swin checkpoint schema."""
+    from vclip_amd.apps import run_main
+    m, history, exp = run_main("swin", ["--data_dir", str(dataset), "--log_dir", str(tmp_path / "logs"),
+                                        "--model_dir", str(tmp_path / "models"), "--epochs", "1", "--batch_size", "2",
+                                        "--num_frames", "8", "--model_size", "tiny"])
+    assert len(history["train_loss"]) == 1 and np.isfinite(history["train_loss"][0])
+    assert (exp / "test_metrics_uniform.json").exists()
+    ck = torch.load(tmp_path / "models" / "best_model_uniform.pth", weights_only=True)
+    assert {"epoch", "model_state_dict", "optimizer_state_dict", "val_loss", "val_acc", "history"} <= set(ck)
+

@@ -68,7 +68,7 @@ def _model(cfg, seed=0):
     from vclip_amd.swin3d import Swin3d
     m = Swin3d({k: v for k, v in cfg.items() if k != "num_classes"}, num_classes=cfg["num_classes"])
     m.load_state_dict(make_swin3d_weights(cfg, seed=seed))
-    return m.to(DEV)
+    return m.to(DEV).eval()  # constructed models start in train mode (torchvision), whose forward trains
 
 
 def _oracle(cfg, video, seed=0):
