@@ -61,6 +61,16 @@ SIGNATURES = {
     "vc_conv3d_im2col": ([c_p, c_i64, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p], c_int),
     "vc_maxpool3d": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p], c_int),
     "vc_avgpool_head": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_i64, c_p, c_p, c_p], c_int),
+    "vc_col2im_cl": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p], c_int),
+    "vc_maxpool3d_bwd": ([c_p, c_i64, c_p, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64,
+                          c_p], c_int),
+    "vc_batchnorm_train_fwd": ([c_p, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_f, c_p, c_p, c_p, c_int, c_i64, c_int, c_p,
+                                c_i64, c_p, c_p, c_i64, c_p], c_int),
+    "vc_batchnorm_train_bwd": ([c_p, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_i64, c_p, c_i64, c_int, c_p, c_i64, c_p,
+                                c_i64, c_p, c_p, c_p, c_i64, c_p], c_int),
+    "vc_resnet_head_train": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_p, c_p, c_p, c_i64, c_p, c_p, c_p],
+                             c_int),
+    "vc_resnet_head_train_bwd": ([c_p, c_i64, c_i64, c_i64, c_i64, c_int, c_p, c_p, c_i64, c_p], c_int),
     "vc_global_avgpool": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p], c_int),
     "vc_lstm_recurrence": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_i64, c_p, c_p], c_int),
     "vc_mlp_head": ([c_p, c_i64, c_i64, c_p, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p], c_int),

@@ -349,12 +349,11 @@ def run_main(fam_name, argv=None):
         _load_weights(model, args.checkpoint_path, logger, fam)
     history = {"train_loss": [], "train_acc": [], "val_loss": [], "val_acc": []}
     if not args.skip_train:
-        if fam.name not in ("vivit", "timesformer", "swin"):
-            raise NotImplementedError(f"{fam.name}: only the ViViT, TimeSformer and Swin3D train steps have GPU "
-                                      "backward kernels in libvclip; evaluate a trained checkpoint with --skip_train "
-                                      "--checkpoint_path")
         from .optim import AdamW
-        opt = AdamW(model.parameters(), lr=args.learning_rate, weight_decay=args.weight_decay)
+        # ResNet3D: torch.optim.Adam(model.parameters(), lr) (resnet50-3d-video/main.py:153) = AdamW with
+        # weight decay 0; its BatchNorm running statistics carry no gradient and are skipped
+        opt = AdamW([q for q in model.parameters() if q.requires_grad], lr=args.learning_rate,
+                    weight_decay=getattr(args, "weight_decay", 0.0))
         crit = torch.nn.CrossEntropyLoss()
         model_dir = Path(args.model_dir)
         model_dir.mkdir(parents=True, exist_ok=True)

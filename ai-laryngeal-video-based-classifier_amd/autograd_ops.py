@@ -15,12 +15,18 @@ Every arithmetic op here is a HIP kernel of libvclip.so, forward and backward:
   window_attention  vc_window_attention3d_lse / vc_window_attention3d_bwd (Swin3D, head_dim 32, the
               relative-position bias table differentiable) + vc_colsum of its per-window partials;
   pool_head   vc_pool_head_pooled / vc_pool_head_bwd + vc_layernorm_bwd (Swin3D's final LayerNorm,
-              token mean and classifier).
+              token mean and classifier);
+  im2col_cl / batchnorm / maxpool / resnet_head   the ResNet3D train step (conv3d_bwd.hip):
+              vc_conv3d_im2col / vc_col2im_cl, BatchNorm3d with batch statistics (+ residual, ReLU)
+              vc_batchnorm_train_fwd / _bwd, vc_maxpool3d / vc_maxpool3d_bwd, the head with its
+              dropout vc_resnet_head_train / vc_pool_head_bwd / vc_resnet_head_train_bwd.
 The tensors between them (residual adds, the clip <-> frame permutes, the CLS frame mean) are
 ordinary torch tensor ops: layout glue, autograd's bookkeeping.  Rows are padded internally to the
 kernels' tile multiples; the returned tensors have exactly the caller's rows.
 """
 from __future__ import annotations
+
+import ctypes
 
 import torch
 
@@ -329,3 +335,153 @@ def pool_head(x, g, b, wc, bc, B, ntok, eps):
     """torchvision SwinTransformer3d head: logits = Linear(mean over each clip's ntok tokens of
     LayerNorm(x)) for f32 x [B*ntok, D]."""
     return _PoolHead.apply(x, g, b, wc, bc, B, ntok, eps)
+
+
+def _i3(v):
+    return (ctypes.c_int * 3)(*[int(x) for x in v])
+
+
+class _Im2colCL(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, B: int, grid, C: int, kernel, stride, pad):
+        To, Ho, Wo = ops.conv_out_size(grid, kernel, stride, pad)
+        M = B * To * Ho * Wo
+        a = torch.empty(M, kernel[0] * kernel[1] * kernel[2] * C, dtype=torch.bfloat16, device=x.device)
+        ops.conv3d_im2col(x, "cl_bf16", B, grid, C, kernel, stride, pad, a)
+        ctx.dims = (B, tuple(grid), C, tuple(kernel), tuple(stride), tuple(pad), x.shape[0])
+        return a
+
+    @staticmethod
+    def backward(ctx, da):
+        B, grid, C, kernel, stride, pad, rows = ctx.dims
+        da = da.to(torch.bfloat16)
+        if da.stride(1) != 1:
+            da = da.contiguous()
+        dx = torch.empty(rows, C, dtype=torch.float32, device=da.device)
+        T, H, W = grid
+        _lib.call("vc_col2im_cl", _p(da), da.stride(0), B, T, H, W, C, ctypes.addressof(k := _i3(kernel)),
+                  ctypes.addressof(s_ := _i3(stride)), ctypes.addressof(p_ := _i3(pad)), _p(dx), C, _stream(da))
+        return dx, None, None, None, None, None, None
+
+
+def im2col_cl(x, B, grid, C, kernel, stride, pad):
+    """Conv3d patches of channels-last bf16 rows [B*T*H*W, C] -> bf16 [B*To*Ho*Wo, kt*kh*kw*C]
+    (columns (kt, kh, kw, c)), differentiable w.r.t. x (col2im)."""
+    return _Im2colCL.apply(x, B, tuple(grid), C, tuple(kernel), tuple(stride), tuple(pad))
+
+
+def _bn_work(M, C, device):
+    splits = min(1024, max(1, (M + 2047) // 2048))
+    return torch.empty(splits * 2 * C, dtype=torch.float32, device=device)
+
+
+class _BatchNormTrain(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y, gamma, beta, res, running_mean, running_var, relu: bool, eps: float, momentum: float):
+        y = y.contiguous().float()
+        M, C = y.shape
+        g, b = gamma.detach().float().contiguous(), beta.detach().float().contiguous()
+        z = torch.empty(M, C, dtype=torch.bfloat16, device=y.device)
+        stat = torch.empty(2, C, dtype=torch.float32, device=y.device)
+        work = _bn_work(M, C, y.device)
+        if res is not None:
+            res = res.to(torch.bfloat16)
+            if res.stride(1) != 1:
+                res = res.contiguous()
+        rm = running_mean.detach() if running_mean is not None else None
+        rv = running_var.detach() if running_var is not None else None
+        _lib.call("vc_batchnorm_train_fwd", _p(y), y.stride(0), M, C, _p(g), _p(b), eps, momentum,
+                  _p(rm) if rm is not None else None, _p(rv) if rv is not None else None,
+                  _p(res) if res is not None else None, 1, res.stride(0) if res is not None else 0, int(relu), _p(z),
+                  C, _p(stat), _p(work), work.numel(), _stream(y))
+        ctx.save_for_backward(y, stat, g, z)
+        ctx.relu, ctx.has_res = relu, res is not None
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        y, stat, g, z = ctx.saved_tensors
+        M, C = y.shape
+        dz = dz.float().contiguous()
+        dy = torch.empty(M, C, dtype=torch.float32, device=y.device)
+        dres = torch.empty(M, C, dtype=torch.float32, device=y.device) if ctx.has_res else None
+        dg = torch.empty(C, dtype=torch.float32, device=y.device)
+        db = torch.empty(C, dtype=torch.float32, device=y.device)
+        work = _bn_work(M, C, y.device)
+        _lib.call("vc_batchnorm_train_bwd", _p(y), C, M, C, _p(stat), _p(g), _p(dz), C, _p(z), C, int(ctx.relu), _p(dy), C,
+                  _p(dres) if dres is not None else None, C, _p(dg), _p(db), _p(work), work.numel(), _stream(y))
+        return dy, dg, db, dres, None, None, None, None, None
+
+
+def batchnorm(y, gamma, beta, running_mean=None, running_var=None, res=None, relu=False, eps=1e-5, momentum=0.1):
+    """nn.BatchNorm3d in training mode on channels-last f32 rows [M, C] (batch statistics; the
+    running statistics updated in place) -> bf16 relu?(BN(y) + res)."""
+    return _BatchNormTrain.apply(y, gamma, beta, res, running_mean, running_var, relu, eps, momentum)
+
+
+class _MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, B: int, grid, C: int, kernel, stride, pad):
+        x = x.contiguous()
+        To, Ho, Wo = ops.conv_out_size(grid, kernel, stride, pad)
+        y = torch.empty(B * To * Ho * Wo, C, dtype=torch.bfloat16, device=x.device)
+        ops.maxpool3d(x, B, grid, C, kernel, stride, pad, y)
+        ctx.save_for_backward(x)
+        ctx.dims = (B, tuple(grid), C, tuple(kernel), tuple(stride), tuple(pad))
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        B, grid, C, kernel, stride, pad = ctx.dims
+        dyf = dy.float().contiguous()
+        dx = torch.empty(x.shape[0], C, dtype=torch.float32, device=x.device)
+        T, H, W = grid
+        _lib.call("vc_maxpool3d_bwd", _p(x), x.stride(0), _p(dyf), 0, C, B, T, H, W, C,
+                  ctypes.addressof(k := _i3(kernel)), ctypes.addressof(s_ := _i3(stride)),
+                  ctypes.addressof(p_ := _i3(pad)), _p(dx), C, _stream(x))
+        return dx, None, None, None, None, None, None
+
+
+def maxpool(x, B, grid, C, kernel, stride, pad):
+    """MaxPool3d on channels-last bf16 rows, differentiable (gradient to each window's first max)."""
+    return _MaxPool.apply(x, B, tuple(grid), C, tuple(kernel), tuple(stride), tuple(pad))
+
+
+class _ResnetHead(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, wc, bc, keep, B: int, T: int, HW: int, pool_t: int):
+        x = x.contiguous()
+        C = x.shape[1]
+        wcc, bcc = wc.detach().float().contiguous(), bc.detach().float().contiguous()
+        nl = wcc.shape[0]
+        u = torch.empty(B, C, dtype=torch.float32, device=x.device)
+        logits = torch.empty(B, nl, dtype=torch.float32, device=x.device)
+        keep = keep.float().contiguous()
+        _lib.call("vc_resnet_head_train", _p(x), x.stride(0), B, T, HW, C, pool_t, _p(keep), _p(wcc), _p(bcc), nl, _p(u),
+                  _p(logits), _stream(x))
+        ctx.save_for_backward(u, wcc, keep)
+        ctx.dims = (B, T, HW, C, pool_t, x.shape[0])
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        u, wc, keep = ctx.saved_tensors
+        B, T, HW, C, pool_t, rows = ctx.dims
+        nl = wc.shape[0]
+        dl = dlogits.float().contiguous()
+        du = torch.empty(B, C, dtype=torch.float32, device=u.device)
+        dwc = torch.empty(nl, C, dtype=torch.float32, device=u.device)
+        dbc = torch.empty(nl, dtype=torch.float32, device=u.device)
+        _lib.call("vc_pool_head_bwd", _p(u), _p(dl), _p(wc), B, C, nl, 1.0, _p(du), _p(dwc), _p(dbc), _stream(u))
+        dx = torch.empty(rows, C, dtype=torch.float32, device=u.device)
+        _lib.call("vc_resnet_head_train_bwd", _p(du), B, T, HW, C, pool_t, _p(keep), _p(dx), C, _stream(u))
+        return dx, dwc, dbc, None, None, None, None, None
+
+
+def resnet_head(x, wc, bc, keep, B, T, HW, pool_t):
+    """pytorchvideo ResNetBasicHead (AvgPool3d((pool_t, H, W), stride 1) -> Dropout -> Linear ->
+    AdaptiveAvgPool3d(1)) on the final channels-last map [B*T*HW, C]; keep = the dropout scale
+    per (clip, pooled position, channel)."""
+    return _ResnetHead.apply(x, wc, bc, keep, B, T, HW, pool_t)
+

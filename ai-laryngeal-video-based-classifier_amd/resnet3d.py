@@ -43,9 +43,12 @@ class ResNet3d(torch.nn.Module):
         self._names = list(shapes.keys())
         self.params = torch.nn.ParameterDict()
         for n, s in shapes.items():
-            self.params[n.replace(".", "__")] = torch.nn.Parameter(torch.zeros(s), requires_grad=False)
+            # BatchNorm running statistics are buffers in pytorchvideo: no gradient, updated by the train step
+            stat = n.endswith("running_mean") or n.endswith("running_var")
+            self.params[n.replace(".", "__")] = torch.nn.Parameter(torch.zeros(s), requires_grad=not stat)
         self._packed = None
         self._ws = {}
+        self.head_dropout = True  # train step: the head's Dropout(0.5) (pytorchvideo create_resnet dropout_rate)
 
     def state_dict(self, *a, **k):
         return OrderedDict((n, self.params[n.replace(".", "__")].detach()) for n in self._names)
@@ -68,8 +71,16 @@ class ResNet3d(torch.nn.Module):
         return missing, unexpected
 
     # ---- packing: BN folded, weights [N_pad, K] bf16 in the im2col column order --------
+    def P(self, name):
+        return self.params[name.replace(".", "__")]
+
+    def _weights_version(self):
+        from . import vivit_train
+        return (vivit_train.MASTER_EPOCH[0], sum(p._version for p in self.params.values()))
+
     def _pack(self, device):
-        if self._packed is not None and self._packed["device"] == device:
+        ver = self._weights_version()  # the fused AdamW updates in place without bumping _version
+        if self._packed is not None and self._packed["device"] == device and self._packed["version"] == ver:
             return self._packed
         c = self.cfg
         eps = c["bn_eps"]
@@ -89,7 +100,7 @@ class ResNet3d(torch.nn.Module):
             B[:b.numel()] = b
             return W.to(torch.bfloat16).contiguous(), B.float().contiguous()
 
-        pk = {"device": device}
+        pk = {"device": device, "version": ver}
         sk = c.get("stem_kernel", (3, 7, 7))
         pk["stem"] = fold("blocks.0.conv", "blocks.0.norm", channels_last=False, k_pad=_ru(3 * sk[0] * sk[1] * sk[2], 64))
         stages = []
@@ -159,12 +170,90 @@ class ResNet3d(torch.nn.Module):
         return ws
 
     # ---- forward -----------------------------------------------------------------------
-    @torch.no_grad()
     def forward(self, video: torch.Tensor) -> torch.Tensor:
+        """`model(clips)` -> logits.  In training mode with autograd enabled (the reference's train loop,
+        resnet50-3d-video/video_classifier/trainers/trainer.py:106-123) the logits carry the graph of the
+        HIP train step (_forward_train: BatchNorm with batch statistics, the head's dropout); otherwise
+        the fused inference path (BatchNorm folded) runs."""
         if video.device.type != "cuda":
             raise RuntimeError("ResNet3d (vclip_amd) runs on the GPU only: move the clip batch to cuda")
         x = video.contiguous().float() if video.dtype != torch.float32 else video.contiguous()
-        return self.forward_logits(x)
+        if self.training and torch.is_grad_enabled():
+            return self._forward_train(x)
+        with torch.no_grad():
+            return self.forward_logits(x).clone()  # the workspace buffer is reused by the next call
+
+    def _forward_train(self, video: torch.Tensor) -> torch.Tensor:
+        """pytorchvideo create_resnet in training mode (oracle/resnet3d_ref.py with batch-statistic
+        BatchNorm) as autograd ops over the HIP kernels (vclip_amd/autograd_ops.py): every Conv3d is
+        an im2col (differentiable: col2im) + bf16 MFMA GEMM with fp32 accumulation on the fp32 master
+        weights, BatchNorm3d with batch statistics (fp32, running statistics updated with momentum
+        0.1) fused with the residual add and ReLU, MaxPool3d with its first-max gradient, and the head
+        (AvgPool3d, Dropout(0.5) from torch's RNG unless `head_dropout = False`, Linear, global
+        average); channels-last rows throughout."""
+        from . import autograd_ops as A
+        c = self.cfg
+        B, Cin, T, H, W = video.shape
+        if Cin != 3:
+            raise ValueError("video must be [B, 3, T, H, W]")
+        eps = c["bn_eps"]
+        stem, grids = self.geometry(T, H, W)
+        sk, sp = c.get("stem_kernel", (3, 7, 7)), c.get("stem_pad", (1, 3, 3))
+        P = self.P
+
+        def bn(y, name, relu, res=None):
+            return A.batchnorm(y, P(name + ".weight"), P(name + ".bias"), P(name + ".running_mean"),
+                               P(name + ".running_var"), res=res, relu=relu, eps=eps)
+
+        def conv(x, grid, cin, wname, kernel, stride, pad):
+            w = P(wname)
+            cout = w.shape[0]
+            if tuple(kernel) == (1, 1, 1) and tuple(stride) == (1, 1, 1):
+                a = x
+            else:
+                a = A.im2col_cl(x, B, grid, cin, kernel, stride, pad)
+            return A.linear(a, w.permute(0, 2, 3, 4, 1).reshape(cout, -1), None, out_f32=True)
+
+        # stem: Conv3d from the f32 NCTHW clip (no input gradient) + BN + ReLU + MaxPool
+        Ms = B * stem[0] * stem[1] * stem[2]
+        K = 3 * sk[0] * sk[1] * sk[2]
+        a = torch.empty(Ms, _ru(K, 8), dtype=torch.bfloat16, device=video.device)
+        ops.conv3d_im2col(video, "ncthw_f32", B, (T, H, W), 3, sk, (1, 2, 2), sp, a)
+        y = A.linear(a[:, :K], P("blocks.0.conv.weight").reshape(c["stem_dim"], K), None, out_f32=True)
+        x = A.maxpool(bn(y, "blocks.0.norm", True), B, stem, c["stem_dim"], (1, 3, 3), (1, 2, 2), (0, 1, 1))
+        g_in, cin = grids[0], c["stem_dim"]
+        for s, depth in enumerate(c["depths"]):
+            g = grids[s]
+            ss = c["spatial_strides"][s]
+            ka = tuple(c["conv_a_kernels"][s])
+            for i in range(depth):
+                p = f"blocks.{s + 1}.res_blocks.{i}."
+                stride = (1, ss, ss) if i == 0 else (1, 1, 1)
+                gi = g_in if i == 0 else g
+                if p + "branch1_conv.weight" in self._names:
+                    sc = bn(conv(x, gi, cin, p + "branch1_conv.weight", (1, 1, 1), stride, (0, 0, 0)),
+                            p + "branch1_norm", False)
+                else:
+                    sc = x
+                inner = P(p + "branch2.conv_a.weight").shape[0]
+                ya = bn(conv(x, gi, cin, p + "branch2.conv_a.weight", ka, (1, 1, 1), tuple(k // 2 for k in ka)),
+                        p + "branch2.norm_a", True)
+                yb = bn(conv(ya, gi, inner, p + "branch2.conv_b.weight", (1, 3, 3), stride, (0, 1, 1)),
+                        p + "branch2.norm_b", True)
+                x = bn(conv(yb, g, inner, p + "branch2.conv_c.weight", (1, 1, 1), (1, 1, 1), (0, 0, 0)),
+                       p + "branch2.norm_c", True, res=sc)
+                cin = P(p + "branch2.conv_c.weight").shape[0]
+            g_in = g
+        Tf, Hf, Wf = grids[-1]
+        pt, ph, pw = c["head_pool"]
+        if (ph, pw) != (Hf, Wf):
+            raise NotImplementedError("train step head: the pool window must cover the final spatial map")
+        npos = Tf - pt + 1
+        keep = torch.ones(B, npos, cin, device=video.device)
+        if self.head_dropout:
+            keep = keep.bernoulli_(0.5).mul_(2.0)  # nn.Dropout(0.5): keep with prob 0.5, scale 1 / 0.5
+        self._packed = None  # the running statistics were updated in place: re-fold before the next eval
+        return A.resnet_head(x, P("blocks.5.proj.weight"), P("blocks.5.proj.bias"), keep, B, Tf, Hf * Wf, pt)
 
     def forward_logits(self, video: torch.Tensor) -> torch.Tensor:
         x, B, grid, C, ws = self.forward_features(video)

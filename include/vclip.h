@@ -315,6 +315,48 @@ int vc_avgpool_head(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_
                     const int* pool_kernel, const float* Wc, const float* bc, int64_t num_labels, float* work,
                     float* logits, hipStream_t stream);
 
+/* ---- ResNet3D train step (conv3d_bwd.hip; resnet50-3d-video/.../trainers/trainer.py:106-123) ---- */
+
+/* Backward of vc_conv3d_im2col (channels-last bf16 input): dx f32 [B*T*H*W][C] (row stride lddx)
+ * = the sum of the dA [M_out][kt*kh*kw*C] entries that copied each input element (gather order
+ * fixed: deterministic). */
+int vc_col2im_cl(const uint16_t* dA, int64_t lda, int64_t B, int64_t T, int64_t H, int64_t W, int64_t C,
+                 const int* kernel, const int* stride, const int* pad, float* dx, int64_t lddx, hipStream_t stream);
+
+/* Backward of vc_maxpool3d: each output gradient (dy f32, or bf16 when dy_bf16) goes to the first
+ * maximum of its window in (t, h, w) scan order (torch's max_pool3d indices); dx f32. */
+int vc_maxpool3d_bwd(const uint16_t* x, int64_t ldx, const void* dy, int dy_bf16, int64_t lddy, int64_t B, int64_t T,
+                     int64_t H, int64_t W, int64_t C, const int* kernel, const int* stride, const int* pad, float* dx,
+                     int64_t lddx, hipStream_t stream);
+
+/* nn.BatchNorm3d in training mode on channels-last rows y f32 [M][C] (C % 4 == 0): batch mean /
+ * biased variance (two passes, fixed-order reductions) -> stat f32 [2][C] = {mean, rstd}; the
+ * running statistics (if given) updated with `momentum` and the unbiased variance; z bf16 =
+ * relu?(gamma * (y - mean) * rstd + beta (+ res: bf16 if res_bf16 else f32)).  work >= 2*C*splits
+ * floats (splits = clamp(ceil(M / 2048), 1, 1024)). */
+int vc_batchnorm_train_fwd(const float* y, int64_t ldy, int64_t M, int64_t C, const float* gamma, const float* beta,
+                           float eps, float momentum, float* running_mean, float* running_var, const void* res,
+                           int res_bf16, int64_t ldr, int relu, uint16_t* z, int64_t ldz, float* stat, float* work,
+                           int64_t work_elems, hipStream_t stream);
+
+/* Its backward: g = dz (masked by z > 0 when relu); dbeta = sum g, dgamma = sum g * xhat;
+ * dy = gamma * rstd * (g - dbeta / M - xhat * dgamma / M); dres (optional) = g. */
+int vc_batchnorm_train_bwd(const float* y, int64_t ldy, int64_t M, int64_t C, const float* stat, const float* gamma,
+                           const float* dz, int64_t lddz, const uint16_t* z, int64_t ldz, int relu, float* dy,
+                           int64_t lddy, float* dres, int64_t lddr, float* dgamma, float* dbeta, float* work,
+                           int64_t work_elems, hipStream_t stream);
+
+/* pytorchvideo ResNetBasicHead in training mode on the final map x bf16 [B*T*HW][C] (one spatial
+ * pool window = the whole HW): u f32 [B][C] = the AdaptiveAvgPool of the per-position inputs of
+ * the Linear after AvgPool3d((pool_t, ., .), stride 1) and Dropout (keep f32 [B][T-pool_t+1][C] =
+ * 0 or 1/(1-p)); logits = Wc . u + bc (fp32).  Backward: vc_pool_head_bwd (scale 1) gives du, dWc,
+ * dbc; vc_resnet_head_train_bwd spreads du over x. */
+int vc_resnet_head_train(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_t HW, int64_t C, int pool_t,
+                         const float* keep, const float* Wc, const float* bc, int64_t num_labels, float* u,
+                         float* logits, hipStream_t stream);
+int vc_resnet_head_train_bwd(const float* du, int64_t B, int64_t T, int64_t HW, int64_t C, int pool_t, const float* keep,
+                             float* dx, int64_t lddx, hipStream_t stream);
+
 /* ---- ResNet50-LSTM (resnet50-2d-lstm/src/models/model.py:5-60) -----------
  * The per-frame ResNet-50 runs on the 3D conv path with kt = 1 kernels. */
 

@@ -5,7 +5,10 @@ A plain-PyTorch fp32 CPU restatement of the reference's 3D ResNet-50
 `create_resnet(model_depth=50, model_num_class=2, dropout_rate=0.5, stem (3,7,7)/(1,2,2),
 MaxPool3d (1,3,3)/(1,2,2), conv_a kernels ((1,1,1),(1,1,1),(3,1,1),(3,1,1)), conv_b (1,3,3),
 spatial strides (1,2,2,2), head AvgPool3d (4,7,7) + global average)`), in eval mode
-(BatchNorm with running statistics, dropout off).
+(BatchNorm with running statistics, dropout off) or, with `training=True`, in training mode
+(BatchNorm with batch statistics, the running statistics updated in place with momentum 0.1,
+as nn.BatchNorm3d.train(); the head's Dropout as an explicit keep-scale mask `head_keep`
+[B, T_pooled, C], None = dropout off).
 
 PARITY UNPINNED: pytorchvideo is not installed in this image and its source is nowhere on
 disk; the reference does not pin its version.  This follows pytorchvideo's
@@ -35,16 +38,29 @@ RESNET3D_50 = dict(depths=(3, 4, 6, 3), stem_dim=64, conv_a_kernels=((1, 1, 1), 
                    spatial_strides=(1, 2, 2, 2), head_pool=(4, 7, 7), num_classes=2, bn_eps=1e-5)
 
 
-def _bn(x, p, pre, eps):
+def _bn(x, p, pre, eps, training=False):
     return F.batch_norm(x, p[pre + ".running_mean"], p[pre + ".running_var"], p[pre + ".weight"], p[pre + ".bias"],
-                        training=False, eps=eps)
+                        training=training, momentum=0.1, eps=eps)
 
 
-def resnet3d_forward(p: dict, cfg: dict, video: torch.Tensor, return_stages: bool = False):
-    """p: pytorchvideo-named fp32 tensors; video [B, 3, T, H, W] -> logits [B, num_classes]."""
+def resnet3d_forward(p: dict, cfg: dict, video: torch.Tensor, return_stages: bool = False, training: bool = False,
+                     head_keep=None, rounding=None):
+    """p: pytorchvideo-named fp32 tensors; video [B, 3, T, H, W] -> logits [B, num_classes].
+
+    `rounding` (tests only): optional dict of callables {"act", "weight", "conv_out"} applied to
+    every stored activation, every conv weight and every conv output, so a test can restate the
+    storage precisions of a bf16 implementation on this same graph (identity when None)."""
     eps = cfg.get("bn_eps", 1e-5)
-    x = F.conv3d(video, p["blocks.0.conv.weight"], stride=(1, 2, 2), padding=(1, 3, 3))
-    x = F.relu(_bn(x, p, "blocks.0.norm", eps))
+    ident = lambda t: t  # noqa: E731
+    r = rounding or {}
+    ra, rw, ro = r.get("act", ident), r.get("weight", ident), r.get("conv_out", ident)
+    bnf = lambda x, p, pre, eps: _bn(x, p, pre, eps, training)  # noqa: E731
+
+    def conv(x, name, **kw):
+        return ro(F.conv3d(x, rw(p[name]), **kw))
+
+    x = conv(ra(video), "blocks.0.conv.weight", stride=(1, 2, 2), padding=(1, 3, 3))
+    x = ra(F.relu(bnf(x, p, "blocks.0.norm", eps)))
     x = F.max_pool3d(x, kernel_size=(1, 3, 3), stride=(1, 2, 2), padding=(0, 1, 1))
     stages = [x]
     for s, depth in enumerate(cfg["depths"]):
@@ -54,17 +70,19 @@ def resnet3d_forward(p: dict, cfg: dict, video: torch.Tensor, return_stages: boo
             pre = f"blocks.{s + 1}.res_blocks.{i}."
             stride = (1, ss, ss) if i == 0 else (1, 1, 1)
             if pre + "branch1_conv.weight" in p:
-                sc = _bn(F.conv3d(x, p[pre + "branch1_conv.weight"], stride=stride), p, pre + "branch1_norm", eps)
+                sc = ra(bnf(conv(x, pre + "branch1_conv.weight", stride=stride), p, pre + "branch1_norm", eps))
             else:
                 sc = x
-            y = F.conv3d(x, p[pre + "branch2.conv_a.weight"], padding=tuple(k // 2 for k in ka))
-            y = F.relu(_bn(y, p, pre + "branch2.norm_a", eps))
-            y = F.conv3d(y, p[pre + "branch2.conv_b.weight"], stride=stride, padding=(0, 1, 1))
-            y = F.relu(_bn(y, p, pre + "branch2.norm_b", eps))
-            y = _bn(F.conv3d(y, p[pre + "branch2.conv_c.weight"]), p, pre + "branch2.norm_c", eps)
-            x = F.relu(sc + y)
+            y = conv(x, pre + "branch2.conv_a.weight", padding=tuple(k // 2 for k in ka))
+            y = ra(F.relu(bnf(y, p, pre + "branch2.norm_a", eps)))
+            y = conv(y, pre + "branch2.conv_b.weight", stride=stride, padding=(0, 1, 1))
+            y = ra(F.relu(bnf(y, p, pre + "branch2.norm_b", eps)))
+            y = bnf(conv(y, pre + "branch2.conv_c.weight"), p, pre + "branch2.norm_c", eps)
+            x = ra(F.relu(sc + y))
         stages.append(x)
     x = F.avg_pool3d(x, kernel_size=cfg["head_pool"], stride=1)
+    if head_keep is not None:  # Dropout: keep-scale per (clip, pooled position, channel)
+        x = x * head_keep.permute(0, 2, 1).reshape(x.shape[0], x.shape[1], x.shape[2], 1, 1)
     x = x.permute(0, 2, 3, 4, 1) @ p["blocks.5.proj.weight"].T + p["blocks.5.proj.bias"]
     logits = x.mean(dim=(1, 2, 3))
     if return_stages:

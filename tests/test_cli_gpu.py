@@ -98,10 +98,6 @@ def test_eval_and_inference_clis(dataset, tmp_path, fam, extra):
                                str(tmp_path / "models"), "--skip_train", "--checkpoint_path", str(ck_path),
                                "--batch_size", "2"] + extra)
     assert (exp / "test_metrics_uniform.json").exists() and 0.0 <= m["accuracy"] <= 1.0
-    if fam == "resnet3d":  # the TimeSformer / Swin3D train steps exist (test_*_main_trains)
-        with pytest.raises(NotImplementedError):
-            run_main(fam, ["--data_dir", str(dataset), "--log_dir", str(tmp_path / "l2"), "--model_dir",
-                           str(tmp_path / "m2"), "--epochs", "1"] + extra)
     video = sorted((dataset / "test" / "referral").iterdir())[0]
     res = run_inference(fam, ["--video_path", str(video), "--model_path", str(ck_path), "--log_dir",
                               str(tmp_path / "ilogs")] + extra)
@@ -149,3 +145,18 @@ def test_swin_main_trains(dataset, tmp_path):
     ck = torch.load(tmp_path / "models" / "best_model_uniform.pth", weights_only=True)
     assert {"epoch", "model_state_dict", "optimizer_state_dict", "val_loss", "val_acc", "history"} <= set(ck)
 
+
+
+def test_resnet3d_main_trains(dataset, tmp_path):
+    """resnet50-3d-video/main.py trains by default (trainer.py:106-123, Adam at main.py:153): one epoch
+    on the HIP ResNet3D train step (batch-statistic BatchNorm, head dropout), the trainer's checkpoint
+    keys (trainer.py:197-204), then the test split evaluated with the updated running statistics."""
+    from vclip_amd.apps import run_main
+    m, history, exp = run_main("resnet3d", ["--data_dir", str(dataset), "--log_dir", str(tmp_path / "logs"),
+                                            "--model_dir", str(tmp_path / "models"), "--epochs", "1",
+                                            "--batch_size", "2"])
+    assert len(history["train_loss"]) == 1 and np.isfinite(history["train_loss"][0])
+    assert (exp / "test_metrics_uniform.json").exists()
+    ck = torch.load(tmp_path / "models" / "best_model_uniform.pth", weights_only=True)
+    assert {"epoch", "model_state_dict", "optimizer_state_dict", "val_loss", "val_acc", "history"} <= set(ck)
+    assert "blocks.1.res_blocks.0.branch2.norm_a.running_var" in ck["model_state_dict"]

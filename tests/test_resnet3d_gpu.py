@@ -93,7 +93,7 @@ def _model():
     from vclip_amd.resnet3d import ResNet3d
     m = ResNet3d(ref.RESNET3D_50)
     m.load_state_dict(make_resnet3d_weights(ref.RESNET3D_50, seed=0))
-    return m.to(DEV)
+    return m.to(DEV).eval()
 
 
 @pytest.mark.parametrize("T,B", [(8, 2), (32, 1)])
