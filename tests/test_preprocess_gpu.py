@@ -41,6 +41,25 @@ def test_vivit_preprocess_vs_hf_processor():
     assert np.abs(got - want).max() < 1e-5
 
 
+def test_timesformer_preprocess_vs_hf_processor():
+    """timesformer trainer.py:91-97: the facebook/timesformer-base-finetuned-k400 processor
+    (VideoMAEImageProcessor: mean / std 0.45 / 0.225, resize + centre crop to 224 x 224, x / 255)
+    on 224 x 224 frames, per clip; built locally with that checkpoint's settings (no hub)."""
+    transformers = pytest.importorskip("transformers")
+    from vclip_amd.preprocess import timesformer_preprocess
+    cls = getattr(transformers, "VideoMAEImageProcessorPil", None) or transformers.VideoMAEImageProcessor
+    proc = cls(size={"height": 224, "width": 224}, crop_size={"height": 224, "width": 224},
+               image_mean=[0.45, 0.45, 0.45], image_std=[0.225, 0.225, 0.225])
+    rng = np.random.RandomState(2)
+    frames = rng.randint(0, 256, (2, 8, 224, 224, 3)).astype(np.uint8)
+    want = np.concatenate([proc(images=list(frames[b]), return_tensors="np", do_resize=True,
+                                size={"height": 224, "width": 224}, do_center_crop=True,
+                                crop_size={"height": 224, "width": 224})["pixel_values"] for b in range(2)])
+    got = timesformer_preprocess(torch.from_numpy(frames).to(DEV)).cpu().numpy()
+    assert got.shape == want.shape
+    assert np.abs(got - want).max() < 1e-5
+
+
 @pytest.mark.parametrize("F,H,W,T,div255", [(40, 240, 320, 16, False), (12, 224, 224, 32, True), (9, 300, 256, 8, False)])
 def test_video_eval_transform(F, H, W, T, div255):
     from vclip_amd.preprocess import short_side_size, uniform_temporal_subsample_indices, video_eval_transform
