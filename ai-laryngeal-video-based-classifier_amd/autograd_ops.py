@@ -87,12 +87,11 @@ class _Linear(torch.autograd.Function):
         dx = torch.empty(Mp, Kp, dtype=torch.bfloat16, device=dy.device)
         ops.gemm(dyp, wt, torch.zeros(Kp, dtype=torch.float32, device=dy.device), "bias", dx)
         dw = torch.empty(Np, Kp, dtype=torch.float32, device=dy.device)
-        work = torch.empty(2 * Np * Kp, dtype=torch.float32, device=dy.device)
-        ops.wgrad(dyp, xp, dw, work, nscaled=ctx.qrows, scale=ctx.qscale)
+        ops.wgrad(dyp, xp, dw, ops.wgrad_work(Mp, Np, Kp, dy.device), nscaled=ctx.qrows, scale=ctx.qscale)
         db = None
         if ctx.has_bias:
             db = torch.empty(Np, dtype=torch.float32, device=dy.device)
-            ops.colsum(dyp, db, nscaled=ctx.qrows, scale=ctx.qscale)
+            ops.colsum(dyp, db, ops.colsum_work(M, Np, dy.device), m=M, nscaled=ctx.qrows, scale=ctx.qscale)
             db = db[:N]
         dx = dx[:M, :K] if Kp != K else dx[:M]
         dw = dw[:N, :K] if (Np, Kp) != (N, K) else dw
@@ -282,7 +281,7 @@ class _WindowAttention(torch.autograd.Function):
         tab = table.detach().float().contiguous()
         ops.window_attention3d_bwd(qkv, out, d, lse, B, grid, heads, window, shift, full_window, tab, dqkv, part)
         dtab = torch.empty(heads * ntab, dtype=torch.float32, device=qkv.device)
-        ops.colsum(part, dtab)  # sum of the per-(window, head) partials, fixed order
+        ops.colsum(part, dtab, ops.colsum_work(part.shape[0], dtab.numel(), part.device))  # fixed order
         return dqkv, dtab.view(heads, ntab).t(), None, None, None, None, None, None
 
 
@@ -371,7 +370,7 @@ def im2col_cl(x, B, grid, C, kernel, stride, pad):
 
 
 def _bn_work(M, C, device):
-    splits = min(1024, max(1, (M + 2047) // 2048))
+    splits = min(4096, max(1, (M + 127) // 128))  # conv3d_bwd.hip bn_splits
     return torch.empty(splits * 2 * C, dtype=torch.float32, device=device)
 
 

@@ -174,19 +174,34 @@ __global__ void __launch_bounds__(256) bn_partial_kernel(const float* __restrict
 }
 
 //  MODE 0: stat[0][c] = mean;  MODE 1: stat[1][c] = rstd, running stats updated (momentum, the
-//  unbiased variance, as nn.BatchNorm3d);  MODE 2: out0 = dbeta, out1 = dgamma
+//  unbiased variance, as nn.BatchNorm3d);  MODE 2: out0 = dbeta, out1 = dgamma.
+//  One workgroup per channel: thread t sums splits t, t + 256, ..., then a fixed-order LDS tree.
 template <int MODE>
 __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ part, int nsplit, int64_t M, int C,
                                                           float eps, float momentum, float* __restrict__ stat,
                                                           float* __restrict__ run_mean, float* __restrict__ run_var,
                                                           float* __restrict__ out0, float* __restrict__ out1) {
-    const int c = blockIdx.x * 256 + threadIdx.x;
-    if (c >= C) return;
+    __shared__ float red[2][256];
+    const int c = blockIdx.x, t = threadIdx.x;
     float s1 = 0.f, s2 = 0.f;
-    for (int k = 0; k < nsplit; ++k) {
+    for (int k = t; k < nsplit; k += 256) {
         s1 += part[(int64_t)k * 2 * C + c];
-        s2 += part[(int64_t)k * 2 * C + C + c];
+        if (MODE == 2) s2 += part[(int64_t)k * 2 * C + C + c];
     }
+    red[0][t] = s1;
+    red[1][t] = s2;
+    __syncthreads();
+#pragma unroll
+    for (int w = 128; w >= 1; w >>= 1) {
+        if (t < w) {
+            red[0][t] += red[0][t + w];
+            if (MODE == 2) red[1][t] += red[1][t + w];
+        }
+        __syncthreads();
+    }
+    if (t != 0) return;
+    s1 = red[0][0];
+    s2 = red[1][0];
     if (MODE == 0) {
         stat[c] = s1 / (float)M;
     } else if (MODE == 1) {
@@ -359,9 +374,11 @@ int vc_maxpool3d_bwd(const uint16_t* x, int64_t ldx, const void* dy, int dy_bf16
     return check_launch("vc_maxpool3d_bwd");
 }
 
+// row chunks of the partial-sum pass: ~128 rows each (thousands of workgroups at the
+// 400k-row stage-1 maps), at most 4096
 static int64_t bn_splits(int64_t M) {
-    int64_t s = (M + 2047) / 2048;
-    return s < 1 ? 1 : (s > 1024 ? 1024 : s);
+    int64_t s = (M + 127) / 128;
+    return s < 1 ? 1 : (s > 4096 ? 4096 : s);
 }
 
 int vc_batchnorm_train_fwd(const float* y, int64_t ldy, int64_t M, int64_t C, const float* gamma, const float* beta,
@@ -376,7 +393,7 @@ int vc_batchnorm_train_fwd(const float* y, int64_t ldy, int64_t M, int64_t C, co
     const int64_t ns = bn_splits(M), rps = (M + ns - 1) / ns;
     if (work_elems < ns * 2 * C) return fail(VC_ERR_INVALID_ARG, "vc_batchnorm_train_fwd: work too small");
     const dim3 gp((unsigned)((C + 255) / 256), (unsigned)ns);
-    const unsigned gf = (unsigned)((C + 255) / 256);
+    const unsigned gf = (unsigned)C;
     bn_partial_kernel<0><<<gp, 256, 0, stream>>>(y, ldy, M, (int)C, rps, stat, nullptr, 0, nullptr, 0, 0, work);
     bn_finalize_kernel<0><<<gf, 256, 0, stream>>>(work, (int)ns, M, (int)C, eps, momentum, stat, nullptr, nullptr,
                                                   nullptr, nullptr);
@@ -404,7 +421,7 @@ int vc_batchnorm_train_bwd(const float* y, int64_t ldy, int64_t M, int64_t C, co
     if (work_elems < ns * 2 * C) return fail(VC_ERR_INVALID_ARG, "vc_batchnorm_train_bwd: work too small");
     bn_partial_kernel<2><<<dim3((unsigned)((C + 255) / 256), (unsigned)ns), 256, 0, stream>>>(
         y, ldy, M, (int)C, rps, stat, dz, lddz, z, ldz, relu, work);
-    bn_finalize_kernel<2><<<(unsigned)((C + 255) / 256), 256, 0, stream>>>(work, (int)ns, M, (int)C, 0.f, 0.f, nullptr,
+    bn_finalize_kernel<2><<<(unsigned)C, 256, 0, stream>>>(work, (int)ns, M, (int)C, 0.f, 0.f, nullptr,
                                                                           nullptr, nullptr, dbeta, dgamma);
     bn_bwd_kernel<<<(unsigned)((M * C + 255) / 256), 256, 0, stream>>>(y, ldy, M, (int)C, stat, gamma, dbeta, dgamma, dz,
                                                                        lddz, z, ldz, relu, dy, lddy, dres, lddr);

@@ -177,21 +177,32 @@ __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ in, i
         out1[col - n0] = s;
 }
 
+// Column sums in up to three fixed-order levels (deterministic for a given R, N): R rows -> S1 =
+// min(2048, ceil(R / 64)) partial rows (64 rows per block, so a narrow N still spreads over
+// thousands of workgroups) -> S2 = ceil(S1 / 64) -> the output; work >= (S1 + S2) * N floats
+// (fewer splits when it is smaller; no work: one pass with one block per 256 columns).
 template <typename T>
 static int colsum_launch(const T* in, int64_t ld, int64_t R, int64_t N, float* out0, int64_t n0, float* out1,
                          int64_t nscaled, float scale, float* work, int64_t work_elems, hipStream_t stream) {
     const unsigned nbx = (unsigned)((N + 255) / 256);
-    int64_t splits = (R + 127) / 128;  // ~128 rows per block in pass 1
-    if (splits > 256) splits = 256;
-    if (splits * N > work_elems) splits = work_elems / N;
-    if (splits <= 1) {
+    int64_t s1 = (R + 63) / 64;
+    if (s1 > 2048) s1 = 2048;
+    while (s1 > 1 && (s1 + (s1 + 63) / 64) * N > work_elems) s1 /= 2;
+    if (s1 <= 1) {
         colsum_kernel<T><<<dim3(nbx, 1), 256, 0, stream>>>(in, ld, R, N, R, out0, n0, out1, nscaled, scale);
         return 0;
     }
-    const int64_t rps = (R + splits - 1) / splits;
-    splits = (R + rps - 1) / rps;
-    colsum_kernel<T><<<dim3(nbx, (unsigned)splits), 256, 0, stream>>>(in, ld, R, N, rps, work, N, nullptr, 0, 1.0f);
-    colsum_kernel<float><<<dim3(nbx, 1), 256, 0, stream>>>(work, N, splits, N, splits, out0, n0, out1, nscaled, scale);
+    const int64_t rps = (R + s1 - 1) / s1;
+    s1 = (R + rps - 1) / rps;
+    colsum_kernel<T><<<dim3(nbx, (unsigned)s1), 256, 0, stream>>>(in, ld, R, N, rps, work, N, nullptr, 0, 1.0f);
+    if (s1 <= 64) {
+        colsum_kernel<float><<<dim3(nbx, 1), 256, 0, stream>>>(work, N, s1, N, s1, out0, n0, out1, nscaled, scale);
+        return 0;
+    }
+    const int64_t s2 = (s1 + 63) / 64;
+    float* w2 = work + s1 * N;
+    colsum_kernel<float><<<dim3(nbx, (unsigned)s2), 256, 0, stream>>>(work, N, s1, N, 64, w2, N, nullptr, 0, 1.0f);
+    colsum_kernel<float><<<dim3(nbx, 1), 256, 0, stream>>>(w2, N, s2, N, s2, out0, n0, out1, nscaled, scale);
     return 0;
 }
 

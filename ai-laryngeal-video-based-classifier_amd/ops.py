@@ -532,6 +532,22 @@ def colsum(x: torch.Tensor, out: torch.Tensor, work: torch.Tensor | None = None,
     return out
 
 
+def colsum_work(R: int, N: int, device) -> torch.Tensor:
+    """Scratch for vc_colsum's full row split (S1 + S2 partial rows of N floats)."""
+    s1 = min(2048, max(1, (R + 63) // 64))
+    return torch.empty((s1 + (s1 + 63) // 64) * N, dtype=torch.float32, device=device)
+
+
+def wgrad_work(M: int, N1: int, N2: int, device) -> torch.Tensor:
+    """Scratch for vc_wgrad_bf16's split-K partials at the split count the kernel aims for
+    (train.hip vc_wgrad_bf16: ~512 workgroups of 128 x 128, ~256 of 256 x 256)."""
+    if N1 % 256 == 0 and N2 % 256 == 0:
+        sp = min(-(-256 // ((N1 // 256) * (N2 // 256))), (M // 32) // 4)
+    else:
+        sp = min(-(-512 // ((N1 // 128) * (N2 // 128))), (M // 64) // 2)
+    return torch.empty(max(2, sp) * N1 * N2, dtype=torch.float32, device=device)
+
+
 def wgrad(g: torch.Tensor, x: torch.Tensor, out: torch.Tensor, work: torch.Tensor | None = None,
           nscaled: int = 0, scale: float = 1.0, m: int | None = None) -> torch.Tensor:
     """out[n1][n2] = s(n1) * sum_m g[m][n1] x[m][n2]  (g bf16 [M, N1], x bf16 [M, N2], out f32 [N1, N2])."""

@@ -333,7 +333,7 @@ int vc_maxpool3d_bwd(const uint16_t* x, int64_t ldx, const void* dy, int dy_bf16
  * biased variance (two passes, fixed-order reductions) -> stat f32 [2][C] = {mean, rstd}; the
  * running statistics (if given) updated with `momentum` and the unbiased variance; z bf16 =
  * relu?(gamma * (y - mean) * rstd + beta (+ res: bf16 if res_bf16 else f32)).  work >= 2*C*splits
- * floats (splits = clamp(ceil(M / 2048), 1, 1024)). */
+ * floats (splits = clamp(ceil(M / 128), 1, 4096)). */
 int vc_batchnorm_train_fwd(const float* y, int64_t ldy, int64_t M, int64_t C, const float* gamma, const float* beta,
                            float eps, float momentum, float* running_mean, float* running_var, const void* res,
                            int res_bf16, int64_t ldr, int relu, uint16_t* z, int64_t ldz, float* stat, float* work,
@@ -486,7 +486,9 @@ int vc_layernorm_bwd(const float* dy, int64_t lddy, const float* x, int64_t ldx,
 
 /*
  * out[n] = (n < nscaled ? scale : 1) * sum over R rows of in[r][n]; dtype 0 = f32, 1 = bf16
- * (bias gradients of nn.Linear).  work: optional f32 scratch (row-split partials), deterministic.
+ * (bias gradients of nn.Linear).  work: optional f32 scratch for fixed-order row-split partials
+ * (deterministic): S1 = min(2048, ceil(R / 64)) partial rows, then S2 = ceil(S1 / 64); (S1 + S2) * N
+ * floats take the full split, less halves S1, none = one pass.
  */
 int vc_colsum(const void* in, int dtype, int64_t ld, int64_t R, int64_t N, int64_t nscaled, float scale, float* out,
               float* work, int64_t work_elems, hipStream_t stream);
@@ -495,7 +497,11 @@ int vc_colsum(const void* in, int dtype, int64_t ld, int64_t R, int64_t N, int64
  * Weight gradient of nn.Linear / the tubelet Conv3d: out[n1][n2] = s(n1) * sum_m G[m][n1] X[m][n2]
  * (G = output gradient, X = layer input, bf16 [M][*] row-major; fp32 out, overwritten),
  * s(n1) = scale for n1 < nscaled (the q-scale fold), else 1.  N1 % 128 == 0, N2 % 128 == 0,
- * M % 64 == 0 (M % 32 when N1 and N2 are multiples of 256: the 256 x 256 kernel).  work: f32 scratch for split-K partials (>= 2*N1*N2 enables splitting).
+ * M % 64 == 0 (M % 32 when N1 and N2 are multiples of 256: the 256 x 256 kernel).  work: f32 scratch
+ * for split-K partials, splits * N1 * N2 floats (>= 2 * N1 * N2 enables splitting); the kernel aims
+ * at ~512 (128 x 128 tiles) or ~256 (256 x 256 tiles) workgroups: splits = ceil(512 / tiles)
+ * bounded by M / 128 (ceil(256 / tiles) bounded by M / 128 for the 256 x 256 kernel), fewer when
+ * work is smaller (ops.wgrad_work sizes it).
  */
 int vc_wgrad_bf16(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, int64_t M, int64_t N1, int64_t N2,
                   int64_t nscaled, float scale, float* out, int64_t ldo, float* work, int64_t work_elems,
