@@ -11,8 +11,8 @@
 //
 // One workgroup (8 waves) per (window, head): the window's q', K, V and dO rows are gathered by
 // index (the forward's roll / partition read; window_common.hpp) into LDS once (4 x 28 KB at 448
-// padded tokens), with each query's lse and Delta, the head's bias-table column and a private
-// dtable accumulator.  Phase 1: each wave owns 32-key blocks and loops over the query blocks
+// padded tokens), with each query's lse and Delta, each token's relative-position code and
+// region label, the head's bias-table column and a private dtable accumulator.  Phase 1: each wave owns 32-key blocks and loops over the query blocks
 // (S and dP with the key block in registers, dV^T and dK^T accumulated by MFMAs whose other
 // operand is a transposed LDS read); phase 2: each wave owns 32-query blocks for dq'^T.  The bias
 // gradient is summed per (window, head) into the LDS table by ds_add_f32 (its order within a
@@ -35,12 +35,15 @@ struct FullWin {
 };
 
 // torchvision define_relative_position_index for window-local indices q, k (coordinates in the
-// FULL window's flattening, as its [:vol, :vol] slice takes them when the window shrinks)
-__device__ __forceinline__ int rel_index(int q, int k, const FullWin& f) {
+// FULL window's flattening, as its [:vol, :vol] slice takes them when the window shrinks) is
+// linear in the two tokens' coordinates:
+//   idx(q, k) = ((qt - kt + T - 1) (2H - 1) + (qh - kh + H - 1)) (2W - 1) + (qw - kw + W - 1)
+//             = code(q) - code(k) + code_max,   code(n) = nt S1 + nh S2 + nw,
+// S1 = (2H - 1)(2W - 1), S2 = 2W - 1, code_max = (T - 1) S1 + (H - 1) S2 + W - 1; code(n) is
+// computed once per token in the staging pass (no divisions per score).
+__device__ __forceinline__ int rel_code(int n, const FullWin& f) {
     const int hw = f.H * f.W;
-    const int qt = q / hw, qh = (q / f.W) % f.H, qw = q % f.W;
-    const int kt = k / hw, kh = (k / f.W) % f.H, kw = k % f.W;
-    return ((qt - kt + f.T - 1) * (2 * f.H - 1) + (qh - kh + f.H - 1)) * (2 * f.W - 1) + (qw - kw + f.W - 1);
+    return (n / hw) * (2 * f.H - 1) * (2 * f.W - 1) + ((n / f.W) % f.H) * (2 * f.W - 1) + n % f.W;
 }
 
 // transposed fragment of a 64-B-row LDS image (ds_read_b64_tr_b16, rows +0 / +8)
@@ -94,7 +97,7 @@ window_attn_bwd_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const u
     float* del_s = lse_s + NP;
     float* btab = del_s + NP;
     float* dtab = btab + ntab;
-    unsigned* lab4 = reinterpret_cast<unsigned*>(dtab + ntab);  // 4-bit region code per token
+    int* cl_s = reinterpret_cast<int*>(dtab + ntab);  // per token: rel_code << 4 | region label (15: padding)
 
     const int head = blockIdx.y;
     const int nwin = g.nwt * g.nwh * g.nww;
@@ -151,22 +154,19 @@ window_attn_bwd_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const u
         btab[i] = table[(int64_t)i * heads + head] * LOG2E;
         dtab[i] = 0.f;
     }
-    for (int w8 = tid; w8 < NP / 8; w8 += 512) {
-        unsigned v = 0;
-        for (int e = 0; e < 8; ++e) {
-            int lb = 15;
-            if (w8 * 8 + e < vol) {
-                lb = 0;
-                if (masked) token_row(w8 * 8 + e, &lb);
-            }
-            v |= (unsigned)lb << (4 * e);
+    for (int n = tid; n < NP; n += 512) {
+        int lb = 15, code = 0;
+        if (n < vol) {
+            lb = 0;
+            if (masked) token_row(n, &lb);
+            code = rel_code(n, fw);
         }
-        lab4[w8] = v;
+        cl_s[n] = code * 16 + lb;
     }
     __syncthreads();
 
     const int r = lane & 31, h = lane >> 5;
-    auto lab = [&](int n) -> int { return (int)((lab4[n >> 3] >> (4 * (n & 7))) & 15); };
+    const int code_max = (fw.T - 1) * (2 * fw.H - 1) * (2 * fw.W - 1) + (fw.H - 1) * (2 * fw.W - 1) + fw.W - 1;
     // row-fragment offsets (lane (r, h): row r of a 32-row block, chunk 2kk + h) and transposed
     // offsets (rows 4h + tq and +8 of a 16-row k-step, columns gcol .. gcol+3); the swizzle term of
     // both depends only on the row mod 16, so block / k-step offsets are plain multiples of 64 B
@@ -189,7 +189,8 @@ window_attn_bwd_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const u
             kf[kk] = *reinterpret_cast<const v8s*>(Ks + kb * 32 * 64 + roff[kk]);
             vf[kk] = *reinterpret_cast<const v8s*>(Vs + kb * 32 * 64 + roff[kk]);
         }
-        const int klab = key < vol ? lab(key) : 15;
+        const int ckl = cl_s[key];  // padded key: label 15 (matches no query: every query is masked)
+        const int klab = ckl & 15, kbase = code_max - (ckl >> 4);
         v16f dvacc = {}, dkacc = {};
         for (int qb = 0; qb < nblk; ++qb) {
             // S[q][key] - lse[q] + bias: register i holds query 32qb + (i & 3) + 8(i >> 2) + 4h
@@ -198,8 +199,9 @@ window_attn_bwd_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const u
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const int q = qb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                const bool ok = key < vol && q < vol && lab(q) == klab;
-                idx[i] = ok ? rel_index(q, key, fw) : -1;
+                const int cq = cl_s[q];
+                const bool ok = key < vol && (cq & 15) == klab;  // padded q: label 15, never a real key's
+                idx[i] = ok ? (cq >> 4) + kbase : -1;
                 s[i] = ok ? btab[idx[i]] - lse_s[q] : -INFINITY;
                 dp[i] = -del_s[q];
             }
@@ -243,7 +245,8 @@ window_attn_bwd_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const u
             qf[kk] = *reinterpret_cast<const v8s*>(Qs + qb * 32 * 64 + roff[kk]);
             df[kk] = *reinterpret_cast<const v8s*>(Ds + qb * 32 * 64 + roff[kk]);
         }
-        const int qlab = q < vol ? lab(q) : 14;
+        const int cql = cl_s[q];
+        const int qlab = q < vol ? (cql & 15) : 14, qbase = (cql >> 4) + code_max;
         const float lq = lse_s[q], dq_delta = del_s[q];
         v16f dqacc = {};
         for (int kb = 0; kb < nblk; ++kb) {
@@ -252,8 +255,9 @@ window_attn_bwd_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const u
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const int key = kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-                const bool ok = key < vol && q < vol && lab(key) == qlab;
-                st[i] = ok ? btab[rel_index(q, key, fw)] - lq : -INFINITY;
+                const int ck = cl_s[key];
+                const bool ok = (ck & 15) == qlab;  // padded key (15) or padded query (14): masked
+                st[i] = ok ? btab[qbase - (ck >> 4)] - lq : -INFINITY;
                 dpt[i] = -dq_delta;
             }
 #pragma unroll
@@ -306,7 +310,7 @@ extern "C" int vc_window_attention3d_bwd(const uint16_t* qkv, int64_t ld, const 
         lddo % 8 || lddq % 8 || ((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)dout | (uintptr_t)dqkv) & 15)
         return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d_bwd: bad leading dimension / alignment");
     const int ntab = (2 * full_t - 1) * (2 * full_h - 1) * (2 * full_w - 1);
-    const size_t lds = (size_t)4 * NP * 64 + 2 * NP * 4 + 2 * (size_t)ntab * 4 + NP / 8 * 4;
+    const size_t lds = (size_t)4 * NP * 64 + 3 * NP * 4 + 2 * (size_t)ntab * 4;
     if (lds > 160 * 1024) return fail(VC_ERR_UNSUPPORTED, "vc_window_attention3d_bwd: window / table too large for LDS");
     WinGeom g{(int)T, (int)H, (int)W, wt, wh, ww, st, sh, sw, (int)(T / wt), (int)(H / wh), (int)(W / ww)};
     const int64_t nwin = B * g.nwt * g.nwh * g.nww;
