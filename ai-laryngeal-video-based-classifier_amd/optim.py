@@ -45,9 +45,15 @@ class AdamW(torch.optim.Optimizer):
         if g0.untyped_storage().nbytes() // 4 != n:
             return None
         # the single launch updates the WHOLE flat buffer: only when the parameters cover it
-        # exactly (a subset, e.g. fine-tuning the head only, goes tensor by tensor)
+        # exactly, or are every entry of a ViViT flat layout (whose alignment gaps are zero in
+        # both buffers, which AdamW leaves at zero); a subset, e.g. fine-tuning the head only,
+        # goes tensor by tensor
         offs = {p.storage_offset() for p in params}
-        if len(offs) != len(params) or sum(p.numel() for p in params) != n:
+        if len(offs) != len(params):
+            return None
+        tags = {getattr(p, "_vc_flat_layout", None) for p in params}
+        full_layout = len(tags) == 1 and None not in tags and tags == {(n, len(params))}
+        if not full_layout and sum(p.numel() for p in params) != n:
             return None
         flat_p = torch.empty(0, dtype=torch.float32, device=p0.device).set_(p0.untyped_storage(), 0, (n,))
         flat_g = torch.empty(0, dtype=torch.float32, device=p0.device).set_(g0.untyped_storage(), 0, (n,))

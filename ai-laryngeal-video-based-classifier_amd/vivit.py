@@ -174,6 +174,9 @@ class VivitForVideoClassification(torch.nn.Module):
                 v = self._layout.view(flat, n)
                 v.copy_(self.P(n).detach().reshape(v.shape))
                 self.P(n).data = v
+                # the optimizer's one-launch path needs to know that a parameter list covers the
+                # whole layout (its alignment gaps stay zero in both buffers: AdamW keeps them 0)
+                self.P(n)._vc_flat_layout = (self._layout.total, len(self._names))
         self._flat = flat
         self._gflat = torch.zeros_like(flat)
         self._gscratch = None

@@ -114,3 +114,28 @@ def test_optimizer_subset_is_not_flat(rccl):
         changed = not torch.equal(p.detach(), before[n])
         assert changed == ("classifier" in n), n
     np.testing.assert_equal(len(opt.state), 2)
+
+
+def test_optimizer_full_layout_is_one_launch(rccl):
+    """AdamW over every parameter of the ViViT flat layout takes the one-launch path (its alignment
+    gaps stay zero) and matches torch.optim.AdamW on the same gradients."""
+    from vclip_amd.optim import AdamW
+    model, pix, labels = _model_and_batch()
+    opt = AdamW(model.parameters(), lr=1e-3, weight_decay=0.01)
+    model.zero_grad(set_to_none=True)
+    _step(model, pix, labels)
+    before = {n: p.detach().clone() for n, p in model.named_parameters()}
+    grads = _grads(model)
+    opt.step()
+    assert "flat" in opt.state and len(opt.state) == 1
+    ref = {n: torch.nn.Parameter(before[n].clone()) for n in before}
+    for n, q in ref.items():
+        q.grad = grads[n].clone()
+    torch.optim.AdamW(list(ref.values()), lr=1e-3, weight_decay=0.01).step()
+    for n, p in model.named_parameters():
+        torch.testing.assert_close(p.detach(), ref[n].detach(), rtol=1e-6, atol=1e-7)
+    flat = model._flat
+    gaps = torch.ones(flat.numel(), dtype=torch.bool, device=flat.device)
+    for p in model.parameters():
+        gaps[p.storage_offset():p.storage_offset() + p.numel()] = False
+    assert torch.count_nonzero(flat[gaps]) == 0  # the layout's alignment gaps stay zero
