@@ -68,3 +68,28 @@ def test_bench_cites_only_same_build_profiles(tmp_path, monkeypatch):
         if "another" not in n.read_text():
             n.unlink()
     assert bench.measured_traffic("attn_fwd_d64_kernel")[0] is None
+
+
+_NO_ARGS = {"vc_version", "vc_last_error", "vc_num_cus"}
+
+
+def test_every_entry_point_rejects_null_and_empty_inputs(lib):
+    """Every compute entry point of include/vclip.h, called with null pointers and zero sizes, returns
+    a non-zero code and sets vc_last_error (argument validation precedes any HIP call)."""
+    silent = []
+    for name, (argtypes, restype) in L.SIGNATURES.items():
+        if name in _NO_ARGS or restype is not ctypes.c_int:
+            continue
+        args = []
+        for t in argtypes:
+            if t in (ctypes.c_float, ctypes.c_double):
+                args.append(0.0)
+            elif t is ctypes.c_void_p or t is ctypes.c_char_p:
+                args.append(None)
+            else:
+                args.append(0)
+        rc = getattr(lib, name)(*args)
+        msg = lib.vc_last_error().decode(errors="replace")
+        if rc == 0 or not msg:
+            silent.append(name)
+    assert not silent, f"entry points accepting null / empty input silently: {silent}"
