@@ -30,22 +30,6 @@ constexpr float LN2 = 0.6931471805599453f;
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr int NPMAX = 448;
 
-struct FullWin {
-    int T, H, W;  // the model's window_size: the relative-position index is defined on it
-};
-
-// torchvision define_relative_position_index for window-local indices q, k (coordinates in the
-// FULL window's flattening, as its [:vol, :vol] slice takes them when the window shrinks) is
-// linear in the two tokens' coordinates:
-//   idx(q, k) = ((qt - kt + T - 1) (2H - 1) + (qh - kh + H - 1)) (2W - 1) + (qw - kw + W - 1)
-//             = code(q) - code(k) + code_max,   code(n) = nt S1 + nh S2 + nw,
-// S1 = (2H - 1)(2W - 1), S2 = 2W - 1, code_max = (T - 1) S1 + (H - 1) S2 + W - 1; code(n) is
-// computed once per token in the staging pass (no divisions per score).
-__device__ __forceinline__ int rel_code(int n, const FullWin& f) {
-    const int hw = f.H * f.W;
-    return (n / hw) * (2 * f.H - 1) * (2 * f.W - 1) + ((n / f.W) % f.H) * (2 * f.W - 1) + n % f.W;
-}
-
 // transposed fragment of a 64-B-row LDS image (ds_read_b64_tr_b16, rows +0 / +8)
 __device__ __forceinline__ v8s tr_frag(const char* img, int offa, int offb) {
     const v4s va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(img + offa));
@@ -166,7 +150,7 @@ window_attn_bwd_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const u
     __syncthreads();
 
     const int r = lane & 31, h = lane >> 5;
-    const int code_max = (fw.T - 1) * (2 * fw.H - 1) * (2 * fw.W - 1) + (fw.H - 1) * (2 * fw.W - 1) + fw.W - 1;
+    const int code_max = rel_code_max(fw);  // window_common.hpp: idx(q, k) = code(q) - code(k) + code_max
     // row-fragment offsets (lane (r, h): row r of a 32-row block, chunk 2kk + h) and transposed
     // offsets (rows 4h + tq and +8 of a 16-row k-step, columns gcol .. gcol+3); the swizzle term of
     // both depends only on the row mod 16, so block / k-step offsets are plain multiples of 64 B

@@ -39,4 +39,22 @@ __device__ __forceinline__ int64_t win_token_row(const WinGeom& g, int b, int wi
     return (((int64_t)b * g.T + t) * g.H + hh) * g.W + w;
 }
 
+struct FullWin {
+    int T, H, W;  // the model's window_size: the relative-position index is defined on it
+};
+
+// torchvision define_relative_position_index for window-local indices q, k (coordinates in the
+// FULL window's flattening, as its [:vol, :vol] slice takes them when the window shrinks) is
+// linear in the two tokens' coordinates:
+//   idx(q, k) = ((qt - kt + T - 1) (2H - 1) + (qh - kh + H - 1)) (2W - 1) + (qw - kw + W - 1)
+//             = code(q) - code(k) + code_max,   code(n) = nt S1 + nh S2 + nw,
+// S1 = (2H - 1)(2W - 1), S2 = 2W - 1, code_max = (T - 1) S1 + (H - 1) S2 + W - 1.
+__device__ __forceinline__ int rel_code(int n, const FullWin& f) {
+    const int hw = f.H * f.W;
+    return (n / hw) * (2 * f.H - 1) * (2 * f.W - 1) + ((n / f.W) % f.H) * (2 * f.W - 1) + n % f.W;
+}
+__device__ __forceinline__ int rel_code_max(const FullWin& f) {
+    return (f.T - 1) * (2 * f.H - 1) * (2 * f.W - 1) + (f.H - 1) * (2 * f.W - 1) + f.W - 1;
+}
+
 }  // namespace vc
