@@ -74,18 +74,27 @@ window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, 
         *reinterpret_cast<uint4*>(Ks + n * 64 + kchunk_swz(n, ch) * 16) = kval;
         *reinterpret_cast<uint4*>(Vs + n * 64 + ch * 16) = vval;
     }
+    // the shift mask only matters in windows whose tokens span several shift regions (the last
+    // window along a shifted dimension); elsewhere every label is equal and the mask is skipped
+    // (padded keys are -inf through the bias either way)
+    int diff = 0;
     if (masked) {
+        int lb0 = 0;
+        token_row(0, &lb0);
         for (int w8 = tid; w8 < NP / 8; w8 += 256) {
             unsigned v = 0;
             for (int e = 0; e < 8; ++e) {
                 int lb = 15;
-                if (w8 * 8 + e < vol) token_row(w8 * 8 + e, &lb);
+                if (w8 * 8 + e < vol) {
+                    token_row(w8 * 8 + e, &lb);
+                    diff |= lb != lb0;
+                }
                 v |= (unsigned)lb << (4 * e);
             }
             lab4[w8] = v;
         }
     }
-    __syncthreads();
+    const bool mixed = __syncthreads_or(diff) != 0;
 
     const int rr = lane & 31, h = lane >> 5;
     // per-lane LDS offsets: K fragment (key rr of a 32-key block, 16-B chunk 2kk+h)
@@ -140,7 +149,7 @@ window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, 
                     sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kk], sc[kb], 0, 0, 0);
                 }
             }
-            if (masked) {
+            if (mixed) {
 #pragma unroll
                 for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
