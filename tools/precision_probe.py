@@ -76,6 +76,7 @@ def main():
     ap.add_argument("--clips", type=int, default=2)
     ap.add_argument("--layers", type=int, default=12)
     ap.add_argument("--fp16-ablate", action="store_true", help="all fp16, one point at a time back to fp32")
+    ap.add_argument("--mixed", action="store_true", help="fp16 GEMMs with bf16 attention and the converse")
     a = ap.parse_args()
     torch.set_num_threads(os.cpu_count())
     cfg = dict(hidden_size=768, intermediate_size=3072, tubelet_size=[2, 16, 16], num_channels=3, num_frames=32,
@@ -87,6 +88,15 @@ def main():
         ref = forward(sd, cfg, pix, {k: None for k in POINTS})
         print("fp32 logits", ref.numpy().round(4).tolist(), flush=True)
         shipped = {k: bf for k in POINTS}
+        if a.mixed:
+            gemm16 = dict(shipped, pix=hf, w=hf, ln=hf, o=hf, hid=hf)   # attention operands q|k|v, P in bf16
+            attn16 = dict(shipped, qkv=hf, p=hf)                          # GEMM operands in bf16
+            for name, rp in (("fp16 GEMMs, bf16 attention", gemm16), ("bf16 GEMMs, fp16 attention", attn16),
+                             ("fp16 GEMMs except embed", dict(gemm16, pix=bf, qkv=hf, p=hf)),
+                             ("fp16 weights+o+hid, bf16 ln", dict(shipped, w=hf, o=hf, hid=hf, qkv=hf, p=hf))):
+                got = forward(sd, cfg, pix, rp)
+                print(f"{name:40s} max|err| {float((got - ref).abs().max()):.3e}", flush=True)
+            return
         if a.fp16_ablate:
             half = {k: hf for k in POINTS}
             runs = [("all fp16", half)] + [(f"all fp16 except {k} fp32", dict(half, **{k: None})) for k in POINTS]
