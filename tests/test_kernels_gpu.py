@@ -118,7 +118,7 @@ def test_gemm_every_tile_config(cfg, epi):
     if epi == "bias_gelu_tanh":
         ref = gelu_fast(ref)
     out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
-    ops().gemm(a.to(DEV), w.to(DEV), bias.to(DEV), epi, out, cfg=4)
+    ops().gemm(a.to(DEV), w.to(DEV), bias.to(DEV), epi, out, cfg=cfg)
     err = ((out.float().cpu() - ref).abs() / (ref.abs() + 1.0)).max().item()
     assert err < 8e-3, err
 
