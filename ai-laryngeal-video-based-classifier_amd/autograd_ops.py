@@ -46,6 +46,29 @@ def _padded(x: torch.Tensor, rows: int, dtype=None) -> torch.Tensor:
     return out
 
 
+_ZEROS = {}
+
+
+def _zeros_f32(n, device):
+    """A shared all-zero f32 [n] (the dgrad GEMM's bias); never written."""
+    key = (n, str(device))
+    z = _ZEROS.get(key)
+    if z is None:
+        z = _ZEROS[key] = torch.zeros(n, dtype=torch.float32, device=device)
+    return z
+
+
+def _as_operand(x, rows, cols):
+    """x as a bf16 [rows, cols] GEMM operand: x itself when it already is one (contiguous rows,
+    no padding needed), else a zero-padded copy."""
+    if (x.dtype == torch.bfloat16 and x.shape[0] == rows and x.shape[1] == cols and x.stride(1) == 1
+            and x.stride(0) == cols):
+        return x
+    xp = torch.zeros(rows, cols, dtype=torch.bfloat16, device=x.device)
+    xp[: x.shape[0], : x.shape[1]].copy_(x)
+    return xp
+
+
 class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, out_f32: bool, qrows: int, qscale: float):
@@ -54,8 +77,7 @@ class _Linear(torch.autograd.Function):
         # the GEMM tiles need M % 256 (rows), N and K % 128 (both also serve as the dgrad / wgrad
         # GEMMs' output widths): zero rows / columns, exactly 0 through every product
         Mp, Np, Kp = _round_up(M, 256), _round_up(N, 128), _round_up(K, 128)
-        xp = torch.zeros(Mp, Kp, dtype=torch.bfloat16, device=x.device)
-        xp[:M, :K].copy_(x)
+        xp = _as_operand(x.detach(), Mp, Kp)
         wc = w.detach().float()
         if (Np, Kp) != (N, K):
             wc = torch.zeros(Np, Kp, dtype=torch.float32, device=x.device)
@@ -64,8 +86,12 @@ class _Linear(torch.autograd.Function):
         wb = torch.empty(Np, Kp, dtype=torch.bfloat16, device=x.device)
         wt = torch.empty(Kp, Np, dtype=torch.bfloat16, device=x.device)
         ops.pack_weight(wc, wb, wt, nscaled=qrows, scale=qscale)
-        bb = torch.zeros(Np, dtype=torch.float32, device=x.device)
-        if b is not None:
+        if b is None:
+            bb = _zeros_f32(Np, x.device)
+        elif Np == N and not qrows and b.dtype == torch.float32 and b.is_contiguous():
+            bb = b.detach()
+        else:
+            bb = torch.zeros(Np, dtype=torch.float32, device=x.device)
             bb[:N].copy_(b.detach())
             if qrows:
                 bb[:qrows] *= qscale
@@ -82,10 +108,9 @@ class _Linear(torch.autograd.Function):
         Mp, Kp = xp.shape
         Np = wt.shape[1]
         M, N, K = ctx.M, ctx.N, ctx.K
-        dyp = torch.zeros(Mp, Np, dtype=torch.bfloat16, device=dy.device)
-        dyp[:M, :N].copy_(dy)
+        dyp = _as_operand(dy, Mp, Np)
         dx = torch.empty(Mp, Kp, dtype=torch.bfloat16, device=dy.device)
-        ops.gemm(dyp, wt, torch.zeros(Kp, dtype=torch.float32, device=dy.device), "bias", dx)
+        ops.gemm(dyp, wt, _zeros_f32(Kp, dy.device), "bias", dx)
         dw = torch.empty(Np, Kp, dtype=torch.float32, device=dy.device)
         ops.wgrad(dyp, xp, dw, ops.wgrad_work(Mp, Np, Kp, dy.device), nscaled=ctx.qrows, scale=ctx.qscale)
         db = None
