@@ -73,6 +73,32 @@ def window_and_shift(size_thw, window_size, shift_size):
     return w, s
 
 
+_BIAS_INDEX = {}
+
+
+def _bias_gather_index(full_window, window, device):
+    """Flat gather index of expand_bias's fragment order into the table extended by two rows:
+    ntab (-inf: padded keys) and ntab + 1 (0: padded queries).  Built once per geometry."""
+    key = (tuple(full_window), tuple(window), str(device))
+    idx = _BIAS_INDEX.get(key)
+    if idx is not None:
+        return idx
+    vol = window[0] * window[1] * window[2]
+    npad = _ru(vol, 64)
+    ntab = (2 * full_window[0] - 1) * (2 * full_window[1] - 1) * (2 * full_window[2] - 1)
+    rel = relative_position_index(full_window)[:vol, :vol]  # [q, k]
+    full = torch.full((npad, npad), ntab, dtype=torch.int64)  # [k, q]: padded keys -> -inf
+    full[:, vol:] = ntab + 1                                  # padded queries -> 0
+    full[:vol, :vol] = rel.t()
+    ar = torch.arange
+    qb, t, kb, lane, e = torch.meshgrid(ar(npad // 32), ar(npad // 64), ar(2), ar(64), ar(16), indexing="ij")
+    k = t * 64 + kb * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)
+    q = qb * 32 + (lane & 31)
+    idx = full[k, q].reshape(-1).to(device)
+    _BIAS_INDEX[key] = idx
+    return idx
+
+
 def expand_bias(table, full_window, window, device):
     """Relative-position bias of one block in the kernel's fragment order.
 
@@ -80,20 +106,15 @@ def expand_bias(table, full_window, window, device):
     the FULL window's index, sliced when the window shrinks), scaled by log2 e; -inf on padded
     keys k >= vol, 0 on padded queries.  Returned as f32 [heads, np/32, np/64, 2, 64, 16]:
     [h][qb][t][kb][lane][e] = bias[h][q = 32qb + lane%32][k = 64t + 32kb + (e&3) + 8(e>>2) + 4(lane//32)],
-    i.e. each lane's 16 accumulator-layout values of a 32x32 S^T block are contiguous."""
+    i.e. each lane's 16 accumulator-layout values of a 32x32 S^T block are contiguous.  One gather
+    per call from the table extended by a -inf and a 0 row (the index is built once per geometry)."""
     vol = window[0] * window[1] * window[2]
     npad = _ru(vol, 64)
-    idx = relative_position_index(full_window)[:vol, :vol].reshape(-1).to(device)
-    bias = table.to(device=device, dtype=torch.float32)[idx].view(vol, vol, -1).permute(2, 0, 1)  # [h, q, k]
-    heads = bias.shape[0]
-    bt = torch.full((heads, npad, npad), float("-inf"), dtype=torch.float32, device=device)  # [h, k, q]
-    bt[:, :, vol:] = 0.0
-    bt[:, :vol, :vol] = bias.transpose(1, 2) * LOG2E
-    ar = lambda n: torch.arange(n, device=device)  # noqa: E731
-    qb, t, kb, lane, e = torch.meshgrid(ar(npad // 32), ar(npad // 64), ar(2), ar(64), ar(16), indexing="ij")
-    k = t * 64 + kb * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)
-    q = qb * 32 + (lane & 31)
-    return bt[:, k, q].contiguous()
+    tab = table.to(device=device, dtype=torch.float32)
+    heads = tab.shape[1]
+    ext = torch.cat([tab * LOG2E, torch.tensor([[float("-inf")] * heads, [0.0] * heads], device=device)])
+    g = ext.index_select(0, _bias_gather_index(full_window, window, device))  # [slots, heads]
+    return g.t().contiguous().view(heads, npad // 32, npad // 64, 2, 64, 16)
 
 
 class Swin3d(torch.nn.Module):
