@@ -373,7 +373,6 @@ wgrad_big_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __
                  int nJ, int64_t mchunk, float* __restrict__ out, int64_t ldo, int64_t split_stride, int64_t nscaled,
                  float scale) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int MI = 4, NI = 2;
     const int ntiles = gridDim.x;
     const int L = blockIdx.x;
     const int xq = ntiles >> 3, xr = ntiles & 7, xcd = L & 7;
@@ -387,7 +386,6 @@ wgrad_big_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int w2 = wave >> 2, w1 = wave & 3;
-    const int r = lane & 31, h = lane >> 5;
 
     // staging: wave w DMAs pieces q = 2w, 2w+1 of each operand (piece = 8 rows of one panel)
     int64_t gsrc[2], xsrc[2];
@@ -411,44 +409,48 @@ wgrad_big_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __
         }
     };
 
-    // transposed-read offsets within a panel (rows 4h+tq and +8; 32-column block db)
-    const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
-    const int gcol = ((lane >> 4) & 1) * 16 + tp * 4;
-    int offa[2], offb[2];
+    // transposed reads for v_mfma_f32_16x16x32 operands (T10): in each 16-lane group g = lane >> 4,
+    // lane 4q + p addresses row 8g + q (+4 for the second read) and columns 16cb + 4p .. +3 of a
+    // panel, so lane i of the group receives column i with k rows 8g .. 8g + 7 -- the same k order
+    // for both operands, which is all a sum over k needs
+    const int gq = (lane & 15) >> 2, gp = lane & 3, gg = lane >> 4;
+    int off1[4], off2[4];
 #pragma unroll
-    for (int db = 0; db < 2; ++db) {
-        const int col = db * 32 + gcol;
-        const int ra = 4 * h + tq, rb = ra + 8;
-        offa[db] = ra * 128 + bswz(ra, col >> 3) * 16 + (col & 7) * 2;
-        offb[db] = rb * 128 + bswz(rb, col >> 3) * 16 + (col & 7) * 2;
+    for (int cb = 0; cb < 4; ++cb) {
+        const int col = cb * 16 + gp * 4;
+        const int r1 = 8 * gg + gq, r2 = r1 + 4;
+        off1[cb] = r1 * 128 + bswz(r1, col >> 3) * 16 + (col & 7) * 2;
+        off2[cb] = r2 * 128 + bswz(r2, col >> 3) * 16 + (col & 7) * 2;
     }
-    auto read_frags = [&](int t, int kk, v8bf (&fa)[MI], v8bf (&fb)[NI]) {
+    constexpr int MI = 8, NI = 4;  // n2 blocks of 16 (wave: 128), n1 blocks of 16 (wave: 64)
+    auto read_frags = [&](int t, v8bf (&fa)[MI], v8bf (&fb)[NI]) __attribute__((always_inline)) {
         const char* gt = smem + (t % WBNS) * WBSLOT;
         const char* xt = gt + WOPND;
-        const int kr = kk * 16 * 128;
 #pragma unroll
-        for (int i = 0; i < MI; ++i) {  // n2 block: panel 2*w2 + i/2, db = i & 1
-            const char* pn = xt + (2 * w2 + (i >> 1)) * WPANEL + kr;
-            fa[i] = tr_frag(pn, offa[i & 1], offb[i & 1]);
+        for (int i = 0; i < MI; ++i) {  // n2 block i: panel 2*w2 + i/4, column block i % 4
+            const char* pn = xt + (2 * w2 + (i >> 2)) * WPANEL;
+            fa[i] = tr_frag(pn, off1[i & 3], off2[i & 3]);
         }
 #pragma unroll
-        for (int j = 0; j < NI; ++j) {  // n1 block: panel w1, db = j
-            const char* pn = gt + w1 * WPANEL + kr;
-            fb[j] = tr_frag(pn, offa[j], offb[j]);
-        }
+        for (int j = 0; j < NI; ++j) fb[j] = tr_frag(gt + w1 * WPANEL, off1[j], off2[j]);  // n1 block j: panel w1
     };
-    v16f acc[MI][NI];
+    v4f acc[MI][NI];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < NI; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    auto mfmas = [&](const v8bf (&fa)[MI], const v8bf (&fb)[NI]) {
+        for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    auto mfmas = [&](const v8bf (&fa)[MI], const v8bf (&fb)[NI]) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
-            for (int j = 0; j < NI; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < NI; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    };
+    // retire half-tile u + 1 once u + 3 may have been staged (4 pieces per wave per half-tile)
+    auto retire = [&](int u) __attribute__((always_inline)) {
+        if (u + 3 < nk) wg_wait_vm<8>();
+        else if (u + 2 < nk) wg_wait_vm<4>();
+        else wg_wait_vm<0>();
+        wg_sync();
     };
 
     if (nk > 0) {
@@ -460,37 +462,41 @@ wgrad_big_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __
         else if (nk > 1) wg_wait_vm<4>();
         else wg_wait_vm<0>();
         wg_sync();
-        read_frags(0, 0, fa0, fb0);
-        for (int t = 0; t < nk - 1; ++t) {
+        read_frags(0, fa0, fb0);
+        // one 32-deep k-step per half-tile: its MFMAs run while the next half-tile's fragments
+        // are read behind the barrier that publishes it; fragment sets alternate
+        int t = 0;
+        for (; t + 2 < nk; t += 2) {
             if (t + 3 < nk) stage(t + 3);
-            read_frags(t, 1, fa1, fb1);
             mfmas(fa0, fb0);
-            if (t + 3 < nk) wg_wait_vm<8>();
-            else if (t + 2 < nk) wg_wait_vm<4>();
-            else wg_wait_vm<0>();
+            retire(t);
+            read_frags(t + 1, fa1, fb1);
+            if (t + 4 < nk) stage(t + 4);
+            mfmas(fa1, fb1);
+            retire(t + 1);
+            read_frags(t + 2, fa0, fb0);
+        }
+        mfmas(fa0, fb0);
+        if (t + 1 < nk) {
+            wg_wait_vm<0>();
             wg_sync();
-            read_frags(t + 1, 0, fa0, fb0);
+            read_frags(t + 1, fa1, fb1);
             mfmas(fa1, fb1);
         }
-        read_frags(nk - 1, 1, fa1, fb1);
-        mfmas(fa0, fb0);
-        mfmas(fa1, fb1);
     }
 
+    // lane holds n1 = 16j + (lane & 15) and n2 = 16i + 4(lane >> 4) .. +3 of the wave tile
     float* o = out + (int64_t)blockIdx.y * split_stride;
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
-        const int64_t n1 = n1_0 + w1 * 64 + j * 32 + r;
+        const int64_t n1 = n1_0 + w1 * 64 + j * 16 + (lane & 15);
         const float sc = n1 < nscaled ? scale : 1.0f;
 #pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int64_t n2 = n2_0 + w2 * 128 + i * 32 + 8 * g + 4 * h;
-                *reinterpret_cast<float4*>(o + n1 * ldo + n2) =
-                    make_float4(acc[i][j][4 * g] * sc, acc[i][j][4 * g + 1] * sc, acc[i][j][4 * g + 2] * sc,
-                                acc[i][j][4 * g + 3] * sc);
-            }
+        for (int i = 0; i < MI; ++i) {
+            const int64_t n2 = n2_0 + w2 * 128 + i * 16 + 4 * gg;
+            *reinterpret_cast<float4*>(o + n1 * ldo + n2) =
+                make_float4(acc[i][j][0] * sc, acc[i][j][1] * sc, acc[i][j][2] * sc, acc[i][j][3] * sc);
+        }
     }
 }
 
