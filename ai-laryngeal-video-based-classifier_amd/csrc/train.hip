@@ -250,18 +250,16 @@ wgrad_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __rest
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = tid >> 6;
     const int w1 = wave >> 1, w2 = wave & 1;  // n1 panel, n2 panel of this wave
-    const int r = lane & 31, h = lane >> 5;
-
-    // transposed-read offsets (rows 4h+tq, +8; 32-column blocks db)
-    const int gi = lane & 15, tq = gi >> 2, tp = gi & 3;
-    const int gcol = ((lane >> 4) & 1) * 16 + tp * 4;
-    int offa[2], offb[2];
+    // transposed reads for v_mfma_f32_16x16x32 operands (as wgrad_big_kernel): in each 16-lane
+    // group gg, lane 4gq + gp addresses row 8gg + gq (+4) and columns 16cb + 4gp of a panel
+    const int gq = (lane & 15) >> 2, gp = lane & 3, gg = lane >> 4;
+    int off1[4], off2[4];
 #pragma unroll
-    for (int db = 0; db < 2; ++db) {
-        const int col = db * 32 + gcol;
-        const int ra = 4 * h + tq, rb = ra + 8;
-        offa[db] = ra * 128 + bswz(ra, col >> 3) * 16 + (col & 7) * 2;
-        offb[db] = rb * 128 + bswz(rb, col >> 3) * 16 + (col & 7) * 2;
+    for (int cb = 0; cb < 4; ++cb) {
+        const int col = cb * 16 + gp * 4;
+        const int r1 = 8 * gg + gq, r2 = r1 + 4;
+        off1[cb] = r1 * 128 + bswz(r1, col >> 3) * 16 + (col & 7) * 2;
+        off2[cb] = r2 * 128 + bswz(r2, col >> 3) * 16 + (col & 7) * 2;
     }
 
     // staging: 64 rows x 16 chunks of each operand, 4 chunks per thread per operand
@@ -285,13 +283,11 @@ wgrad_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __rest
         }
     };
 
-    v16f acc[2][2];  // [n2 block i][n1 block j]: lane -> n1, regs -> n2
+    v4f acc[4][4];  // [n2 block i][n1 block j] of 16 x 16: lane -> n1, regs -> 4 consecutive n2
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+        for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
     if (nt > 0) {
         load(0);
@@ -303,17 +299,17 @@ wgrad_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __rest
         const char* xt = smem + (t & 1) * WSLOT + WTILE + w2 * 8192;
         if (t + 1 < nt) load(t + 1);
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-            const int kr = ks * 16 * 128;
-            v8bf a[2], b[2];
+        for (int ks = 0; ks < 2; ++ks) {  // two 32-deep k-steps per 64-row tile
+            const int kr = ks * 32 * 128;
+            v8bf a[4], b[4];
 #pragma unroll
-            for (int i = 0; i < 2; ++i) a[i] = tr_frag(xt, offa[i] + kr, offb[i] + kr);
+            for (int i = 0; i < 4; ++i) a[i] = tr_frag(xt, off1[i] + kr, off2[i] + kr);
 #pragma unroll
-            for (int j = 0; j < 2; ++j) b[j] = tr_frag(gt, offa[j] + kr, offb[j] + kr);
+            for (int j = 0; j < 4; ++j) b[j] = tr_frag(gt, off1[j] + kr, off2[j] + kr);
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+            for (int i = 0; i < 4; ++i)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+                for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
         }
         if (t + 1 < nt) store(smem + ((t + 1) & 1) * WSLOT);
         __syncthreads();
@@ -321,18 +317,15 @@ wgrad_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __rest
 
     float* o = out + (int64_t)blockIdx.y * split_stride;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int64_t n1 = n1_0 + w1 * 64 + j * 32 + r;
+    for (int j = 0; j < 4; ++j) {
+        const int64_t n1 = n1_0 + w1 * 64 + j * 16 + (lane & 15);
         const float sc = n1 < nscaled ? scale : 1.0f;
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int64_t n2 = n2_0 + w2 * 64 + i * 32 + 8 * g + 4 * h;
-                *reinterpret_cast<float4*>(o + n1 * ldo + n2) =
-                    make_float4(acc[i][j][4 * g] * sc, acc[i][j][4 * g + 1] * sc, acc[i][j][4 * g + 2] * sc,
-                                acc[i][j][4 * g + 3] * sc);
-            }
+        for (int i = 0; i < 4; ++i) {
+            const int64_t n2 = n2_0 + w2 * 64 + i * 16 + 4 * gg;
+            *reinterpret_cast<float4*>(o + n1 * ldo + n2) =
+                make_float4(acc[i][j][0] * sc, acc[i][j][1] * sc, acc[i][j][2] * sc, acc[i][j][3] * sc);
+        }
     }
 }
 

@@ -160,7 +160,9 @@ def test_colsum(dtype, R, N):
 # ------------------------------------------------------------------------- weight gradient GEMM
 @pytest.mark.parametrize("M,N1,N2,split", [(256, 128, 128, False), (12800, 768, 768, True), (4096, 2304, 768, True),
                                            (12800, 768, 3072, True), (3200, 3072, 768, False), (6272, 768, 1536, True),
-                                           (2080, 256, 512, True), (64, 512, 256, True)])
+                                           (2080, 256, 512, True), (64, 512, 256, True),
+                                           # the 128 x 128 kernel (N1 or N2 not a multiple of 256)
+                                           (3136, 384, 128, True), (12544, 128, 384, True), (1024, 640, 384, False)])
 def test_wgrad(M, N1, N2, split):
     O = ops()
     g = torch.Generator().manual_seed(M + N1 + N2)
