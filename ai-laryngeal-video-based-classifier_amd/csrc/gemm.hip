@@ -415,19 +415,19 @@ gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int BM = 256, BN = 256, BKH = 32, NS = 4;
     constexpr int SLOT = (BM + BN) * 64;   // 32 KiB
-    constexpr int TM = 128, TN = 64, MI = 4, NI = 2;
+    constexpr int TM = 128, TN = 64, MI = 8, NI = 4;  // wave tile of 16 x 16 blocks
 
     const int nwg = nbm * nbn;
     const int bid = blockIdx.x;
-    const int xcd = bid & 7, q = nwg >> 3, rr = nwg & 7;
-    const int wgid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (bid >> 3);
+    const int xcd = bid & 7, xq = nwg >> 3, rr = nwg & 7;
+    const int wgid = (xcd < rr ? xcd * (xq + 1) : rr * (xq + 1) + (xcd - rr) * xq) + (bid >> 3);
     const int tm = wgid / nbn, tn = wgid % nbn;
     const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
-    const int r = lane & 31, h = lane >> 5;
+    const int c16 = lane & 15, q = lane >> 4;
 
     // staging: wave w fills A rows [32w, 32w+32) and W rows [32w, 32w+32), 16 rows per glds
     const uint16_t* asrc[2];
@@ -450,43 +450,37 @@ gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
             glds16(bsrc[i] + k0, __builtin_amdgcn_readfirstlane(s + BM * 64 + (wave * 32 + i * 16) * 64));
     };
 
-    v16f acc[MI][NI];
+    v4f acc[MI][NI];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < NI; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+        for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
     const int nk = K / BKH;
-    // fragments of one 16-deep k-step (kk) of half-tile t
-    auto read_frags = [&](int t, int kk, v8s (&fa)[MI], v8s (&fw)[NI]) {
+    // fragments of half-tile t, one 32-deep k-step of v_mfma_f32_16x16x32: lane (c16, q) reads
+    // row 16i + c16, 16-B chunk q (the persistent kernel's operand map)
+    auto read_frags = [&](int t, v8s (&fa)[MI], v8s (&fw)[NI]) __attribute__((always_inline)) {
         const char* At = smem + (t % NS) * SLOT;
         const char* Wt = At + BM * 64;
-        const int ch = kk * 2 + h;
 #pragma unroll
-        for (int i = 0; i < MI; ++i) fa[i] = lds_frag64(At, wm * TM + i * 32 + r, ch);
+        for (int i = 0; i < MI; ++i) fa[i] = lds_frag64(At, wm * TM + i * 16 + c16, q);
 #pragma unroll
-        for (int j = 0; j < NI; ++j) fw[j] = lds_frag64(Wt, wn * TN + j * 32 + r, ch);
+        for (int j = 0; j < NI; ++j) fw[j] = lds_frag64(Wt, wn * TN + j * 16 + c16, q);
     };
-    auto mfmas = [&](const v8s (&fa)[MI], const v8s (&fw)[NI]) {
+    auto mfmas = [&](const v8s (&fa)[MI], const v8s (&fw)[NI]) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < MI; ++i)
 #pragma unroll
-            for (int j = 0; j < NI; ++j)
-                acc[i][j] = mfma32x16<ET>(fw[j], fa[i], acc[i][j]);
+            for (int j = 0; j < NI; ++j) acc[i][j] = mfma16x32<ET>(fw[j], fa[i], acc[i][j]);
     };
-    // 6 fragment reads ride between 8 MFMAs
-    auto interleave = [&]() {
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+    auto retire = [&](int u) __attribute__((always_inline)) {  // half-tile u + 1 resident
+        if (u + 3 < nk) wait_vm<8>();
+        else if (u + 2 < nk) wait_vm<4>();
+        else wait_vm<0>();
+        block_sync_lds();
     };
 
-    // prologue: half-tiles 0..2 in flight; wait for 0, read its first k-step
+    // prologue: half-tiles 0..2 in flight; wait for 0 and read its fragments
     v8s fa0[MI], fw0[NI], fa1[MI], fw1[NI];
     stage(0);
     if (nk > 1) stage(1);
@@ -495,30 +489,26 @@ gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
     else if (nk > 1) wait_vm<4>();
     else wait_vm<0>();
     block_sync_lds();
-    read_frags(0, 0, fa0, fw0);
+    read_frags(0, fa0, fw0);
 
-    // software pipeline: k-step 0 MFMAs overlap the k-step-1 reads of the same half-tile;
-    // k-step 1 MFMAs overlap the k-step-0 reads of the next half-tile, which is
-    // published by the one barrier per half-tile (vmcnt retires only tile t+1).
-    // (the last half-tile is peeled so the loop body has no join in front of its MFMAs:
-    // a join makes hipcc's wait-count merge fall back to lgkmcnt(0))
-    for (int t = 0; t < nk - 1; ++t) {
+    // half-tile t's 32 MFMAs run while t + 1's fragments are read behind the barrier that
+    // publishes it (vmcnt retires only t + 1); fragment sets alternate (nk = K / 32 is even)
+    for (int t = 0; t < nk - 2; t += 2) {
         if (t + 3 < nk) stage(t + 3);
-        read_frags(t, 1, fa1, fw1);
         mfmas(fa0, fw0);
-        interleave();
-        if (t + 3 < nk) wait_vm<8>();
-        else if (t + 2 < nk) wait_vm<4>();
-        else wait_vm<0>();
-        block_sync_lds();
-        read_frags(t + 1, 0, fa0, fw0);
+        retire(t);
+        read_frags(t + 1, fa1, fw1);
+        if (t + 4 < nk) stage(t + 4);
         mfmas(fa1, fw1);
-        interleave();
+        retire(t + 1);
+        read_frags(t + 2, fa0, fw0);
     }
-    read_frags(nk - 1, 1, fa1, fw1);
     mfmas(fa0, fw0);
+    wait_vm<0>();
+    block_sync_lds();
+    read_frags(nk - 1, fa1, fw1);
     mfmas(fa1, fw1);
-    store_tile<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, r, h, bias, out, ldo, aux, ldaux, G, gstride, goff);
+    store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bias, out, ldo, aux, ldaux, G, gstride, goff);
 }
 
 // ---------------------------------------------------------------------------------
