@@ -93,6 +93,7 @@ SIGNATURES = {
     "vc_cls_head_bwd": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_p, c_i64, c_p, c_p, c_i64, c_p, c_i64, c_p,
                          c_p, c_p, c_p, c_p], c_int),
     "vc_embed_bwd": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_i64, c_p], c_int),
+    "vc_adamw_multi": ([c_p, c_i64, c_i64, c_f, c_f, c_f, c_f, c_f, c_i64, c_f, c_p], c_int),
     "vc_adamw": ([c_p, c_p, c_p, c_p, c_i64, c_f, c_f, c_f, c_f, c_f, c_i64, c_f, c_p], c_int),
     "vc_pack_weight": ([c_p, c_i64, c_i64, c_i64, c_f, c_p, c_p, c_p], c_int),
     # TimeSformer train step

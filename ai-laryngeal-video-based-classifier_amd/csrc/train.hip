@@ -630,22 +630,56 @@ __global__ void __launch_bounds__(256) embed_bwd_kernel(const float* __restrict_
 //   p *= 1 - lr*wd;  m += (1-b1)(g - m);  v = b2 v + (1-b2) g^2;
 //   p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
 // ---------------------------------------------------------------------------------
+// one element of torch.optim.AdamW's update (shared by the single- and multi-tensor kernels, no
+// FMA contraction, so both give the same bits)
+__device__ __forceinline__ void adamw_elem(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                           float* __restrict__ v, int64_t i, float lr, float b1, float b2, float eps,
+                                           float wd, float step_size, float bc2_sqrt, float gscale) {
+#pragma clang fp contract(off)  // plain IEEE mul / add in this order: the same bits in every caller
+    const float gg = g[i] * gscale;
+    float pp = p[i] * (1.0f - lr * wd);
+    float mm = m[i];
+    mm = mm + (1.0f - b1) * (gg - mm);
+    const float vv = v[i] * b2 + (1.0f - b2) * gg * gg;
+    const float denom = sqrtf(vv) / bc2_sqrt + eps;
+    pp = pp - step_size * (mm / denom);
+    p[i] = pp;
+    m[i] = mm;
+    v[i] = vv;
+}
+
 __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v, int64_t n, float lr,
                                                     float b1, float b2, float eps, float wd, float step_size,
                                                     float bc2_sqrt, float gscale) {
     const int64_t stride = (int64_t)gridDim.x * 256;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-        const float gg = g[i] * gscale;
-        float pp = p[i] * (1.0f - lr * wd);
-        float mm = m[i];
-        mm = mm + (1.0f - b1) * (gg - mm);
-        const float vv = v[i] * b2 + (1.0f - b2) * gg * gg;
-        const float denom = sqrtf(vv) / bc2_sqrt + eps;
-        pp = pp - step_size * (mm / denom);
-        p[i] = pp;
-        m[i] = mm;
-        v[i] = vv;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+        adamw_elem(p, g, m, v, i, lr, b1, b2, eps, wd, step_size, bc2_sqrt, gscale);
+}
+
+// Multi-tensor AdamW: tab[i] = {p, g, m, v (addresses), n, chunk0}, chunk0 = the entry's first
+// 1024-element chunk (prefix sum over the entries); one workgroup per chunk finds its entry by
+// binary search over the (uniform, scalar-loaded) table; the element arithmetic is adamw_kernel's.
+__global__ void __launch_bounds__(256) adamw_multi_kernel(const int64_t* __restrict__ tab, int ntab, float lr, float b1,
+                                                          float b2, float eps, float wd, float step_size,
+                                                          float bc2_sqrt, float gscale) {
+    const int64_t c = blockIdx.x;
+    int lo = 0, hi = ntab - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (tab[(int64_t)mid * 6 + 5] <= c) lo = mid;
+        else hi = mid - 1;
+    }
+    const int64_t* e = tab + (int64_t)lo * 6;
+    float* __restrict__ p = reinterpret_cast<float*>(e[0]);
+    const float* __restrict__ g = reinterpret_cast<const float*>(e[1]);
+    float* __restrict__ m = reinterpret_cast<float*>(e[2]);
+    float* __restrict__ v = reinterpret_cast<float*>(e[3]);
+    const int64_t n = e[4], base = (c - e[5]) * 1024;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t i = base + k * 256 + threadIdx.x;
+        if (i < n) adamw_elem(p, g, m, v, i, lr, b1, b2, eps, wd, step_size, bc2_sqrt, gscale);
     }
 }
 
@@ -861,6 +895,19 @@ int vc_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
     adamw_kernel<<<(unsigned)nb, 256, 0, stream>>>(param, grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps,
                                                    weight_decay, step_size, bc2_sqrt, grad_scale);
     return check_launch("vc_adamw");
+}
+
+int vc_adamw_multi(const int64_t* table, int64_t ntab, int64_t nchunks, float lr, float beta1, float beta2, float eps,
+                   float weight_decay, int64_t step, float grad_scale, hipStream_t stream) {
+    if (!table) return fail(VC_ERR_INVALID_ARG, "vc_adamw_multi: null table");
+    if (ntab <= 0 || ntab > (1 << 24) || nchunks <= 0 || nchunks > 0x7fffffff || step <= 0)
+        return fail(VC_ERR_INVALID_ARG, "vc_adamw_multi: ntab, nchunks > 0, step >= 1");
+    if ((uintptr_t)table & 7) return fail(VC_ERR_INVALID_ARG, "vc_adamw_multi: table must be 8-byte aligned");
+    const double bc1 = 1.0 - std::pow((double)beta1, (double)step);
+    const double bc2 = 1.0 - std::pow((double)beta2, (double)step);
+    adamw_multi_kernel<<<(unsigned)nchunks, 256, 0, stream>>>(table, (int)ntab, lr, beta1, beta2, eps, weight_decay,
+                                                              (float)(lr / bc1), (float)std::sqrt(bc2), grad_scale);
+    return check_launch("vc_adamw_multi");
 }
 
 int vc_pack_weight(const float* src, int64_t N, int64_t K, int64_t nscaled, float scale, uint16_t* dst, uint16_t* dstT,

@@ -593,6 +593,35 @@ def adamw(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
               int(step), grad_scale, _stream(param))
 
 
+def adamw_multi(params, grads, exp_avgs, exp_avg_sqs, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0):
+    """vc_adamw on every (param, grad, exp_avg, exp_avg_sq) quadruple in one launch."""
+    rows, c0 = [], 0
+    for p, g, m, v in zip(params, grads, exp_avgs, exp_avg_sqs):
+        _dev(p, g, m, v)
+        n = p.numel()
+        _need(all(t.dtype == torch.float32 and t.is_contiguous() and t.numel() == n for t in (p, g, m, v)),
+              "adamw_multi: contiguous f32 buffers of one size per entry")
+        rows.append([p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), n, c0])
+        c0 += (n + 1023) // 1024
+    if not rows:
+        return
+    # the device table is cached by content: in a steady training loop the caching allocator hands
+    # the gradients the same addresses every step, so the table is uploaded once (a host -> device
+    # copy per step would synchronise the host with the stream)
+    key = tuple(x for r in rows for x in r[:5])
+    tab = _ADAMW_TABLES.get(key)
+    if tab is None or tab.device != params[0].device:
+        if len(_ADAMW_TABLES) >= 8:
+            _ADAMW_TABLES.clear()
+        tab = _ADAMW_TABLES[key] = torch.tensor(rows, dtype=torch.int64).to(params[0].device)
+    _lib.call("vc_adamw_multi", _p(tab), len(rows), c0, lr, beta1, beta2, eps, weight_decay, int(step), grad_scale,
+              _stream(params[0]))
+    return tab
+
+
+_ADAMW_TABLES = {}
+
+
 def pack_weight(src: torch.Tensor, dst: torch.Tensor | None = None, dst_t: torch.Tensor | None = None,
                 nscaled: int = 0, scale: float = 1.0):
     _dev(src)

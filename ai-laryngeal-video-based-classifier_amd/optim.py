@@ -80,12 +80,20 @@ class AdamW(torch.optim.Optimizer):
                 st["step"] += 1
                 ops.adamw(fp, fg, st["exp_avg"], st["exp_avg_sq"], lr, b1, b2, eps, wd, st["step"], self.grad_scale)
             else:
+                # every tensor of the group in one multi-tensor launch per distinct step count
+                by_step = {}
                 for p in params:
                     st = self.state[p]
                     if not st:
                         st.update(exp_avg=torch.zeros_like(p), exp_avg_sq=torch.zeros_like(p), step=0)
                     st["step"] += 1
                     g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-                    ops.adamw(p, g, st["exp_avg"], st["exp_avg_sq"], lr, b1, b2, eps, wd, st["step"], self.grad_scale)
+                    by_step.setdefault(st["step"], []).append((p, g, st["exp_avg"], st["exp_avg_sq"]))
+                for step, quads in by_step.items():
+                    if len(quads) == 1 or not all(q.is_contiguous() for q, _, _, _ in quads):
+                        for p, g, m, v in quads:
+                            ops.adamw(p, g, m, v, lr, b1, b2, eps, wd, step, self.grad_scale)
+                    else:
+                        self._tables = ops.adamw_multi(*zip(*quads), lr, b1, b2, eps, wd, step, self.grad_scale)
         vivit_train.MASTER_EPOCH[0] += 1
         return loss

@@ -552,6 +552,13 @@ int vc_gelu_erf_bwd(const void* dy, int dy_bf16, int64_t lddy, const uint16_t* x
 int vc_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr, float beta1,
              float beta2, float eps, float weight_decay, int64_t step, float grad_scale, hipStream_t stream);
 
+/* Multi-tensor vc_adamw in one launch (the per-tensor optimizer path of the autograd families):
+ * table = device int64 [ntab][6] = {param, grad, exp_avg, exp_avg_sq (f32 device addresses),
+ * numel, chunk0}, chunk0 = prefix sum of ceil(numel / 1024) over the preceding entries, nchunks =
+ * the total; every tensor takes the same step (bias corrections) and hyper-parameters. */
+int vc_adamw_multi(const int64_t* table, int64_t ntab, int64_t nchunks, float lr, float beta1, float beta2, float eps,
+                   float weight_decay, int64_t step, float grad_scale, hipStream_t stream);
+
 /*
  * fp32 master weight [N][K] -> bf16 [N][K] (dst) and/or bf16 [K][N] (dstT, the dgrad operand);
  * rows < nscaled are multiplied by scale first (q projection * softmax scale * log2 e).

@@ -298,3 +298,21 @@ def test_pack_weight(N, K, ns):
     ref[:ns] *= 0.3
     np.testing.assert_array_equal(dst.cpu().float().numpy(), ref.bfloat16().float().numpy())
     np.testing.assert_array_equal(dst_t.cpu().float().numpy(), ref.T.bfloat16().float().numpy())
+
+
+def test_adamw_multi_matches_per_tensor():
+    """One multi-tensor launch (vc_adamw_multi) = vc_adamw per tensor, bit for bit, over sizes that
+    straddle the 1024-element chunks (1, 1023, 1024, 1025, a weight matrix)."""
+    O = ops()
+    g = torch.Generator(device=DEV).manual_seed(5)
+    sizes = [1, 1023, 1024, 1025, 768 * 3072, 7, 4096 + 3]
+    mk = lambda n: torch.randn(n, device=DEV, generator=g)  # noqa: E731
+    ps, gs = [mk(n) for n in sizes], [mk(n) for n in sizes]
+    ms, vs = [mk(n) * 0.1 for n in sizes], [mk(n).abs() * 0.01 for n in sizes]
+    ref = [(p.clone(), m.clone(), v.clone()) for p, m, v in zip(ps, ms, vs)]
+    for (p, m, v), gr in zip(ref, gs):
+        O.adamw(p, gr, m, v, 1e-3, 0.9, 0.999, 1e-8, 0.01, 3, 0.5)
+    O.adamw_multi(ps, gs, ms, vs, 1e-3, 0.9, 0.999, 1e-8, 0.01, 3, 0.5)
+    torch.cuda.synchronize()
+    for (rp, rm, rv), p, m, v in zip(ref, ps, ms, vs):
+        assert torch.equal(p, rp) and torch.equal(m, rm) and torch.equal(v, rv)
