@@ -6,8 +6,8 @@
 //    modeling_timesformer.py:148-180 as called from :332-349): per (sequence, head) the T x T
 //    scores are recomputed from q' (= q * scale * log2 e, the stored q|k|v layout of the forward),
 //    P = softmax, dV = P^T dO, dP = dO V^T, dS = ln2 * P o (dP - rowsum(P o dP)),
-//    dQ' = dS K, dK = dS^T Q'.  T <= 32 keys: VALU work, one wave per (sequence, head), the T x T
-//    tiles in LDS.  Deterministic (no atomics).
+//    dQ' = dS K, dK = dS^T Q'.  T <= 32 keys: VALU work, one wave per (sequence, head), the rows and
+//    the T x T tiles in LDS, every lane busy in every phase.  Deterministic (no atomics).
 //  * gelu_erf_fwd_kernel / gelu_erf_bwd_kernel — exact GELU (TimeSformer / Swin hidden_act
 //    "gelu") as a separate op for the train step: the forward uses the same branch-free
 //    erfc restatement as the fused GEMM epilogue (common.hpp gelu_erf), the backward
@@ -18,108 +18,146 @@ namespace vc {
 
 constexpr float LN2 = 0.6931471805599453f;
 
-__device__ __forceinline__ void load_row64(const uint16_t* src, float (&v)[64]) {
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        const v8s raw = *reinterpret_cast<const v8s*>(src + 8 * c);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[8 * c + j] = bf2f((unsigned short)raw[j]);
-    }
-}
-
-__device__ __forceinline__ float dot_row64(const float (&a)[64], const uint16_t* row) {
-    float s = 0.f;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        const v8s raw = *reinterpret_cast<const v8s*>(row + 8 * c);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) s = __builtin_fmaf(a[8 * c + j], bf2f((unsigned short)raw[j]), s);
-    }
-    return s;
-}
-
-__device__ __forceinline__ void axpy_row64(float (&acc)[64], float a, const uint16_t* row) {
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        const v8s raw = *reinterpret_cast<const v8s*>(row + 8 * c);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[8 * c + j] = __builtin_fmaf(a, bf2f((unsigned short)raw[j]), acc[8 * c + j]);
-    }
-}
-
-__device__ __forceinline__ void store_row64(uint16_t* dst, const float (&v)[64]) {
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-        uint4 w;
-        w.x = pack2bf(v[8 * c + 0], v[8 * c + 1]);
-        w.y = pack2bf(v[8 * c + 2], v[8 * c + 3]);
-        w.z = pack2bf(v[8 * c + 4], v[8 * c + 5]);
-        w.w = pack2bf(v[8 * c + 6], v[8 * c + 7]);
-        *reinterpret_cast<uint4*>(dst + 8 * c) = w;
-    }
-}
-
-// grid (B*P sequences, H heads), 64 threads; lane i < T: query i (pass 1), key i (pass 2).
+// grid (B*P sequences, H heads), one wave; TT = the T bucket (8 / 16 / 32), T <= TT at run time.
 // Rows of sequence n = b*P + p in qkv / dout / dqkv: the clip layout of the forward,
 // b*(1 + P*T) + 1 + p*T + t (CLS row first, patch-major, time-minor; CLS rows untouched).
+// All 64 lanes work in every phase: (1) the q', k, v, dO rows of the (sequence, head) are read
+// with 16-byte loads, 8 lanes per 128-byte row, into fp32 LDS rows; (2) one lane per (query,
+// key) pair forms the score s and dP = dO . v; (3) lane i < T turns its row into P and
+// dS = ln2 P o (dP - delta); (4) lane d (the head dimension) forms column d of dQ', dK, dV;
+// (5) those are staged back through LDS and stored as 16-byte bf16 rows.
+constexpr int TB_LD = 68;  // fp32 LDS row stride: 16-byte aligned rows, banks skewed by 4
+
+template <int TT>
 __global__ void __launch_bounds__(64) temporal_attn_bwd_kernel(const uint16_t* __restrict__ qkv, int64_t ld,
                                                                const uint16_t* __restrict__ dout, int64_t lddo, int P,
                                                                int T, int H, uint16_t* __restrict__ dqkv, int64_t lddq) {
-    __shared__ float Ps[32][33];
-    __shared__ float dSs[32][33];
-    const int n = blockIdx.x, h = blockIdx.y, i = threadIdx.x;
+    __shared__ __attribute__((aligned(16))) float sq[TT][TB_LD], sk[TT][TB_LD], sv[TT][TB_LD], sg[TT][TB_LD];
+    __shared__ __attribute__((aligned(16))) float sP[TT][TT + 4], sD[TT][TT + 4];
+    const int n = blockIdx.x, h = blockIdx.y, l = threadIdx.x;
     const int D = H * 64;
     const int64_t r0 = (int64_t)(n / P) * (1 + (int64_t)P * T) + 1 + (int64_t)(n % P) * T;
     const uint16_t* qb = qkv + r0 * ld + h * 64;
-    const uint16_t* kb = qb + D;
-    const uint16_t* vb = qb + 2 * D;
     const uint16_t* db = dout + r0 * lddo + h * 64;
-    if (i < T) {
-        float q[64], g[64];
-        load_row64(qb + (int64_t)i * ld, q);
-        load_row64(db + (int64_t)i * lddo, g);
-        float m = -INFINITY;
-        for (int u = 0; u < T; ++u) {
-            const float s = dot_row64(q, kb + (int64_t)u * ld);
-            Ps[i][u] = s;
-            m = fmaxf(m, s);
-        }
-        float l = 0.f;
-        for (int u = 0; u < T; ++u) {
-            const float e = exp2f(Ps[i][u] - m);
-            Ps[i][u] = e;
-            l += e;
-        }
-        const float inv = 1.0f / l;
-        float delta = 0.f;
-        for (int u = 0; u < T; ++u) {
-            const float p = Ps[i][u] * inv;
-            Ps[i][u] = p;
-            const float dp = dot_row64(g, vb + (int64_t)u * ld);
-            dSs[i][u] = dp;
-            delta = __builtin_fmaf(p, dp, delta);
-        }
-        float dq[64];
+
+    for (int idx = l; idx < T * 8; idx += 64) {
+        const int t = idx >> 3, c = 8 * (idx & 7);
+        const uint16_t* row = qb + (int64_t)t * ld + c;
+        const v8s rq = *reinterpret_cast<const v8s*>(row);
+        const v8s rk = *reinterpret_cast<const v8s*>(row + D);
+        const v8s rv = *reinterpret_cast<const v8s*>(row + 2 * D);
+        const v8s rg = *reinterpret_cast<const v8s*>(db + (int64_t)t * lddo + c);
 #pragma unroll
-        for (int d = 0; d < 64; ++d) dq[d] = 0.f;
-        for (int u = 0; u < T; ++u) {
-            const float ds = LN2 * Ps[i][u] * (dSs[i][u] - delta);
-            dSs[i][u] = ds;
-            axpy_row64(dq, ds, kb + (int64_t)u * ld);
+        for (int j = 0; j < 8; ++j) {
+            sq[t][c + j] = bf2f((unsigned short)rq[j]);
+            sk[t][c + j] = bf2f((unsigned short)rk[j]);
+            sv[t][c + j] = bf2f((unsigned short)rv[j]);
+            sg[t][c + j] = bf2f((unsigned short)rg[j]);
         }
-        store_row64(dqkv + (r0 + i) * lddq + h * 64, dq);
     }
     __syncthreads();
-    if (i < T) {
-        float dk[64], dv[64];
+
+    for (int pr = l; pr < T * T; pr += 64) {
+        const int i = pr / T, u = pr - i * T;
+        float s = 0.f, dp = 0.f;
 #pragma unroll
-        for (int d = 0; d < 64; ++d) { dk[d] = 0.f; dv[d] = 0.f; }
-        for (int t = 0; t < T; ++t) {
-            axpy_row64(dk, dSs[t][i], qb + (int64_t)t * ld);
-            axpy_row64(dv, Ps[t][i], db + (int64_t)t * lddo);
+        for (int d = 0; d < 64; d += 4) {
+            const float4 a = *reinterpret_cast<const float4*>(&sq[i][d]);
+            const float4 b = *reinterpret_cast<const float4*>(&sk[u][d]);
+            const float4 g = *reinterpret_cast<const float4*>(&sg[i][d]);
+            const float4 v = *reinterpret_cast<const float4*>(&sv[u][d]);
+            s = __builtin_fmaf(a.x, b.x, s);
+            s = __builtin_fmaf(a.y, b.y, s);
+            s = __builtin_fmaf(a.z, b.z, s);
+            s = __builtin_fmaf(a.w, b.w, s);
+            dp = __builtin_fmaf(g.x, v.x, dp);
+            dp = __builtin_fmaf(g.y, v.y, dp);
+            dp = __builtin_fmaf(g.z, v.z, dp);
+            dp = __builtin_fmaf(g.w, v.w, dp);
         }
-        store_row64(dqkv + (r0 + i) * lddq + D + h * 64, dk);
-        store_row64(dqkv + (r0 + i) * lddq + 2 * D + h * 64, dv);
+        sP[i][u] = s;
+        sD[i][u] = dp;
+    }
+    __syncthreads();
+
+    if (l < T) {
+        float m = -INFINITY;
+        for (int u = 0; u < T; ++u) m = fmaxf(m, sP[l][u]);
+        float sum = 0.f;
+        for (int u = 0; u < T; ++u) {
+            const float e = exp2f(sP[l][u] - m);
+            sP[l][u] = e;
+            sum += e;
+        }
+        const float inv = 1.0f / sum;
+        float delta = 0.f;
+        for (int u = 0; u < T; ++u) {
+            const float p = sP[l][u] * inv;
+            sP[l][u] = p;
+            delta = __builtin_fmaf(p, sD[l][u], delta);
+        }
+        for (int u = 0; u < T; ++u) sD[l][u] = LN2 * sP[l][u] * (sD[l][u] - delta);
+    }
+    __syncthreads();
+
+    // lane l = head dimension d: dQ'[i] = sum_u dS[i][u] k[u], dK[u] = sum_i dS[i][u] q'[i],
+    // dV[u] = sum_i P[i][u] dO[i]
+    float col[TT], dq[TT], dk[TT], dv[TT];
+#pragma unroll
+    for (int t = 0; t < TT; ++t) col[t] = t < T ? sk[t][l] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TT; ++i) {
+        float acc = 0.f;
+#pragma unroll
+        for (int u = 0; u < TT; ++u)
+            if (u < T) acc = __builtin_fmaf(sD[i < T ? i : 0][u], col[u], acc);
+        dq[i] = acc;
+    }
+#pragma unroll
+    for (int t = 0; t < TT; ++t) col[t] = t < T ? sq[t][l] : 0.f;
+#pragma unroll
+    for (int u = 0; u < TT; ++u) {
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < TT; ++i)
+            if (i < T) acc = __builtin_fmaf(sD[i][u < T ? u : 0], col[i], acc);
+        dk[u] = acc;
+    }
+#pragma unroll
+    for (int t = 0; t < TT; ++t) col[t] = t < T ? sg[t][l] : 0.f;
+#pragma unroll
+    for (int u = 0; u < TT; ++u) {
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < TT; ++i)
+            if (i < T) acc = __builtin_fmaf(sP[i][u < T ? u : 0], col[i], acc);
+        dv[u] = acc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < TT; ++t)
+        if (t < T) {
+            sq[t][l] = dq[t];
+            sk[t][l] = dk[t];
+            sv[t][l] = dv[t];
+        }
+    __syncthreads();
+
+    for (int idx = l; idx < T * 8; idx += 64) {
+        const int t = idx >> 3, c = 8 * (idx & 7);
+        uint16_t* row = dqkv + (r0 + t) * lddq + h * 64 + c;
+        float (*src[3])[TB_LD] = {sq, sk, sv};
+#pragma unroll
+        for (int part = 0; part < 3; ++part) {
+            const float4 a = *reinterpret_cast<const float4*>(&src[part][t][c]);
+            const float4 b = *reinterpret_cast<const float4*>(&src[part][t][c + 4]);
+            uint4 w;
+            w.x = pack2bf(a.x, a.y);
+            w.y = pack2bf(a.z, a.w);
+            w.z = pack2bf(b.x, b.y);
+            w.w = pack2bf(b.z, b.w);
+            *reinterpret_cast<uint4*>(row + part * D) = w;
+        }
     }
 }
 
@@ -198,8 +236,13 @@ int vc_temporal_attention_bwd(const uint16_t* qkv, int64_t ld, const uint16_t* d
         return fail(VC_ERR_INVALID_ARG, "vc_temporal_attention_bwd: bad shape (T <= 32) / leading dimension");
     if ((((uintptr_t)qkv) | ((uintptr_t)dout) | ((uintptr_t)dqkv)) & 15)
         return fail(VC_ERR_INVALID_ARG, "vc_temporal_attention_bwd: pointers must be 16-byte aligned");
-    temporal_attn_bwd_kernel<<<dim3((unsigned)N, (unsigned)H), 64, 0, stream>>>(qkv, ld, dout, lddo, (int)P, (int)T, (int)H,
-                                                                                dqkv, lddq);
+    const dim3 grid((unsigned)N, (unsigned)H);
+    if (T <= 8)
+        temporal_attn_bwd_kernel<8><<<grid, 64, 0, stream>>>(qkv, ld, dout, lddo, (int)P, (int)T, (int)H, dqkv, lddq);
+    else if (T <= 16)
+        temporal_attn_bwd_kernel<16><<<grid, 64, 0, stream>>>(qkv, ld, dout, lddo, (int)P, (int)T, (int)H, dqkv, lddq);
+    else
+        temporal_attn_bwd_kernel<32><<<grid, 64, 0, stream>>>(qkv, ld, dout, lddo, (int)P, (int)T, (int)H, dqkv, lddq);
     return check_launch("vc_temporal_attention_bwd");
 }
 
