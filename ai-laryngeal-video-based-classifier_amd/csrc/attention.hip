@@ -14,11 +14,16 @@
 //   * swapped QK^T (S^T = K . Q^T): a query's scores live in ONE lane column, so the row
 //     max needs one cross-half exchange and only on the rare re-base path;
 //   * the running row max enters the QK^T MFMA chain as its initial accumulator
-//     (S' = Q'.K^T - m, with scale*log2 e folded into Q'), so the common path per score is
-//     exp2 + a packed add (row sum) + cvt: no per-tile max.  Since every P >= 0, a lane's
-//     partial row sum <= LIM = 2^8 bounds each P of the tile by 2^8 (an overflow shows as
-//     inf/NaN); only when that fails does the tile recompute S' and re-base m on its exact
-//     max (defer-max, cdna_hip_programming.md T13, with the sum as the detector);
+//     (S' = Q'.K^T - m, with scale*log2 e folded into Q'), so the inference path per score
+//     is exp2 + cvt: no per-tile max and no VALU row sum.  The row sum l rides on the matrix
+//     pipe: one v_mfma_f32_16x16x32 per 16-key step multiplies the P^T fragment (already the
+//     B operand of P.V) by a constant 0/1 selector, so l sums exactly the 16-bit P that P.V
+//     consumes.  m is tile 0's exact row max and is never re-based in the common case: P is
+//     exact at any magnitude until exp2 overflows (a score 128 above m), and a row sum above
+//     2^64 (or inf / NaN) makes the workgroup repeat the pass re-basing on every tile's exact
+//     max.  The training forward (WLSE) keeps f32 VALU row sums, which double as the
+//     detector of a grown max (defer-max, cdna_hip_programming.md T13: re-base when a
+//     partial sum exceeds 2^8), so its log-sum-exp is the f32 one the backward assumes;
 //   * S'^T accumulator registers feed P.V directly as the B operand of O^T = V^T . P^T
 //     (§3 "An accumulator tile as the next MFMA's operand"); P never touches LDS;
 //   * software pipeline inside each wave: the QK^T MFMAs of tile t+1 are issued before
@@ -34,7 +39,7 @@ constexpr int AK = 64;                      // keys per tile
 constexpr int KV_TILE_BYTES = AK * 64 * 2;  // 8 KiB (one of K or V)
 constexpr int KV_SLOT = 2 * KV_TILE_BYTES;  // K then V
 constexpr int NSLOT = 4;
-constexpr float LIM = 256.0f;  // partial row-sum bound (P <= 2^8) before the running max is re-based
+constexpr float LIM = 256.0f;  // WLSE: partial row-sum bound (P <= 2^8) before the running max is re-based
 
 __device__ __forceinline__ int kswz(int r, int c) { return c ^ ((r >> 1) & 7); }
 __device__ __forceinline__ int vswz(int r, int c) { return c ^ (((r >> 1) & 1) << 2); }
@@ -161,12 +166,21 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
 
     v16f o[QB][2];   // O^T[d][q] per query block, d-blocks 0/1
     v16f minit[QB];  // -running max of this lane's query, broadcast: initial accumulator of S'
-    v2f l_run[QB];   // packed partial row sums
+    // Row sums.  WLSE (training forward): f32 partial sums on the VALU (packed pairs), which
+    // double as the grown-max detector.  Inference: on the matrix pipe, D = Sel . P^T over a
+    // 16x16x32 block, where the P^T fragment of a 16-key step (lane (r, h) holds P[query r][8
+    // keys]) is read as the 32 x 16 B operand (lane l: k-group l >> 4 = (r >> 4) + 2h, column
+    // l & 15 = r & 15).  Sel[i][k] = 1 when the k-group parity (query r >= 16) equals i >> 3,
+    // so D rows 0-7 sum query j's 16 keys and rows 8-15 query j + 16's; lane l then holds the
+    // sum of query (l & 15) + 16 (l >> 5).  It sums exactly the 16-bit P that P.V consumes.
+    v2f l_run[QB];
+    v4f lsum[QB];
+    v8s sel;
+    {
+        const short one = ET == VC_ELEM_F16 ? (short)0x3C00 : (short)0x3F80;
+        const short v = (((lane >> 4) & 1) == ((lane & 15) >> 3)) ? one : (short)0;
 #pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) { o[qb][0][e] = 0.f; o[qb][1][e] = 0.f; minit[qb][e] = 0.f; }
-        l_run[qb] = v2f{0.f, 0.f};
+        for (int j = 0; j < 8; ++j) sel[j] = v;
     }
 
     // ---- S'^T = K . Q'^T - m for QB query blocks x two 32-key blocks of tile t; each K
@@ -198,15 +212,19 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
                 }
         }
     };
-    // P = exp2(S') in place; this lane's partial row sums (32 keys) as packed pairs
-    auto expsum = [&](v16f (&sc)[QB][2], v2f (&ps)[QB]) {
+    auto exp_all = [&](v16f (&sc)[QB][2]) {
 #pragma unroll
-        for (int qb = 0; qb < QB; ++qb) {
+        for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
                 sc[qb][0][e] = __builtin_amdgcn_exp2f(sc[qb][0][e]);
                 sc[qb][1][e] = __builtin_amdgcn_exp2f(sc[qb][1][e]);
             }
+    };
+    // this lane's partial row sums of P (32 keys) as packed pairs (WLSE path)
+    auto psum = [&](const v16f (&sc)[QB][2], v2f (&ps)[QB]) {
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {
             v2f u[8];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -228,6 +246,34 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
         const float m = fmaxf(m0, m1);
         return fmaxf(m, __shfl_xor(m, 32, 64));
     };
+    // re-base the running max of every query on the exact max of tile t's S' (which is
+    // relative to the old max): O, the row sums, the C operand and tile t+1's S' follow
+    auto rebase = [&](auto next_c, v16f (&sc)[QB][2], v16f (&sn)[QB][2]) {
+        constexpr int NEXT = decltype(next_c)::value;
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) {
+            const float delta = fmaxf(rowmax_of(sc[qb]), 0.f);
+            const float alpha = __builtin_amdgcn_exp2f(-delta);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                sc[qb][0][e] -= delta;
+                sc[qb][1][e] -= delta;
+                o[qb][0][e] *= alpha;
+                o[qb][1][e] *= alpha;
+                minit[qb][e] -= delta;
+            }
+            if constexpr (NEXT != 2) {
+#pragma unroll
+                for (int e = 0; e < 16; ++e) { sn[qb][0][e] -= delta; sn[qb][1][e] -= delta; }
+            }
+            if constexpr (WLSE) {
+                l_run[qb] *= alpha;
+            } else {
+                // lane l's row sum belongs to query (l & 15) + 16 (l >> 5), not to this lane's
+                lsum[qb] *= __shfl(alpha, (lane & 15) + ((lane >> 5) << 4), 64);
+            }
+        }
+    };
 
     const int ntiles = (S + AK - 1) / AK;
     // Static wave priority for one of the two workgroups that share a CU (MI355X_MICROARCH.md
@@ -236,125 +282,161 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
     // L + 256, so prio 1 by bit 8 of L.  +1.2 % (three interleaved A/Bs at B = 8: 259/263,
     // 256/259, 258/261 us; priority by block-id bit 3 instead: neutral).
     if ((L >> 8) & 1) __builtin_amdgcn_s_setprio(1);
-    stage(0);
-    if (ntiles > 1) stage(1);
-    if (ntiles > 2) stage(2);
-    if (ntiles > 2) attn_wait_vm<4>();  // tiles 0 and 1 resident, 2 in flight
-    else attn_wait_vm<0>();
-    attn_sync();
-    // tile 0 establishes the running max m
-    v16f scur[QB][2];
-    qk(smem, 0, scur);
-#pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
-        const float m = rowmax_of(scur[qb]);
-#pragma unroll
-        for (int e = 0; e < 16; ++e) { scur[qb][0][e] -= m; scur[qb][1][e] -= m; minit[qb][e] = -m; }
-    }
 
-    // one iteration: S' of tile t+1 is computed (MFMA) while tile t's softmax runs on the
-    // VALU, then O += P_t V_t.  Ring of NSLOT = 4: slot t (V_t), slot t+1 (K_{t+1}) are
-    // read, t+2 lands, t+3 is staged into the slot read one iteration ago.
-    // NEXT: 0 = tile t+1 is a full tile, 1 = tile t+1 may be partial (masked), 2 = t is last.
-    // In the unrolled main loop the slots are compile-time constants, so every LDS address is
-    // a loop-invariant per-lane VGPR plus an immediate offset.
-    auto iter = [&](auto next_c, const char* slot, const char* nslot, int t) {
-        constexpr int NEXT = decltype(next_c)::value;
-        if (t + NS - 1 < ntiles) stage(t + NS - 1);
-        v16f snext[QB][2];
-        if constexpr (NEXT == 0) qk_mfma(nslot, snext);
-        else if constexpr (NEXT == 1) qk(nslot, t + 1, snext);
-
-        // ---- online softmax with a deferred running max: scores are relative to m already.
-        //      Every P is >= 0, so a partial row sum <= LIM bounds every P of the tile by
-        //      LIM (an overflow shows up as inf); only when it fails is tile t recomputed
-        //      against an exact re-based max.
-        v2f ps[QB];
-        expsum(scur, ps);
-        bool grow = false;
+    // One pass over the keys.  RB = 1 re-bases the running max on every tile (exact max, P <= 1).
+    // RB = 0: WLSE re-bases only when a partial row sum exceeds LIM (P > 2^8 or inf / NaN);
+    // inference never re-bases inside the pass — P is relative to tile 0's max, which is exact
+    // for any magnitude until exp2 overflows — and the caller repeats the pass with RB = 1 when
+    // a row sum came out non-finite or above 2^64.
+    auto pass = [&](auto rb_c) {
+        constexpr bool RB = decltype(rb_c)::value;
 #pragma unroll
-        for (int qb = 0; qb < QB; ++qb) grow = grow || !(ps[qb][0] + ps[qb][1] <= (REBASE_ALWAYS ? -1.0f : LIM));
-        if (__any(grow)) {
-            qk(slot, t, scur);
+        for (int qb = 0; qb < QB; ++qb) {
 #pragma unroll
-            for (int qb = 0; qb < QB; ++qb) {
-                const float delta = fmaxf(rowmax_of(scur[qb]), 0.f);
-                const float alpha = __builtin_amdgcn_exp2f(-delta);
-#pragma unroll
-                for (int e = 0; e < 16; ++e) {
-                    scur[qb][0][e] -= delta;
-                    scur[qb][1][e] -= delta;
-                    o[qb][0][e] *= alpha;
-                    o[qb][1][e] *= alpha;
-                    minit[qb][e] -= delta;
-                }
-                if constexpr (NEXT != 2) {
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) { snext[qb][0][e] -= delta; snext[qb][1][e] -= delta; }
-                }
-                l_run[qb] *= alpha;
-            }
-            expsum(scur, ps);
+            for (int e = 0; e < 16; ++e) { o[qb][0][e] = 0.f; o[qb][1][e] = 0.f; minit[qb][e] = 0.f; }
+            l_run[qb] = v2f{0.f, 0.f};
+            lsum[qb] = v4f{0.f, 0.f, 0.f, 0.f};
         }
+        stage(0);
+        if (ntiles > 1) stage(1);
+        if (ntiles > 2) stage(2);
+        if (ntiles > 2) attn_wait_vm<4>();  // tiles 0 and 1 resident, 2 in flight
+        else attn_wait_vm<0>();
+        attn_sync();
+        // tile 0 establishes the running max m
+        v16f scur[QB][2];
+        qk(smem, 0, scur);
 #pragma unroll
-        for (int qb = 0; qb < QB; ++qb) l_run[qb] += ps[qb];
+        for (int qb = 0; qb < QB; ++qb) {
+            const float m = rowmax_of(scur[qb]);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) { scur[qb][0][e] -= m; scur[qb][1][e] -= m; minit[qb][e] = -m; }
+        }
 
-        // ---- O^T += V^T . P^T: P fragment of (key block kb, k-step s2) = regs 8s2..8s2+7;
-        //      every V^T fragment read from LDS feeds QB MFMAs
+        // one iteration: S' of tile t+1 is computed (MFMA) while tile t's softmax runs on the
+        // VALU, then O += P_t V_t.  Ring of NSLOT = 4: slot t (V_t), slot t+1 (K_{t+1}) are
+        // read, t+2 lands, t+3 is staged into the slot read one iteration ago.
+        // NEXT: 0 = tile t+1 is a full tile, 1 = tile t+1 may be partial (masked), 2 = t is last.
+        // In the unrolled main loop the slots are compile-time constants, so every LDS address is
+        // a loop-invariant per-lane VGPR plus an immediate offset.
+        auto iter = [&](auto next_c, const char* slot, const char* nslot, int t) {
+            constexpr int NEXT = decltype(next_c)::value;
+            if (t + NS - 1 < ntiles) stage(t + NS - 1);
+            v16f snext[QB][2];
+            if constexpr (NEXT == 0) qk_mfma(nslot, snext);
+            else if constexpr (NEXT == 1) qk(nslot, t + 1, snext);
+
+            // ---- online softmax: scores are relative to the running max already
+            if constexpr (WLSE) {
+                // deferred max: every P is >= 0, so a partial row sum <= LIM bounds every P of
+                // the tile by LIM (an overflow shows up as inf); only when it fails is tile t
+                // recomputed against an exact re-based max
+                v2f ps[QB];
+                exp_all(scur);
+                psum(scur, ps);
+                bool grow = RB;
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                v8s pf[QB];
-#pragma unroll
-                for (int qb = 0; qb < QB; ++qb) {
-                    v4u pu;
-#pragma unroll
-                    for (int jj = 0; jj < 4; ++jj)
-                        pu[jj] = pack2<ET>(scur[qb][kb][8 * s2 + 2 * jj], scur[qb][kb][8 * s2 + 2 * jj + 1]);
-                    pf[qb] = __builtin_bit_cast(v8s, pu);
+                for (int qb = 0; qb < QB; ++qb) grow = grow || !(ps[qb][0] + ps[qb][1] <= LIM);
+                if (__any(grow)) {
+                    qk(slot, t, scur);
+                    rebase(next_c, scur, snext);
+                    exp_all(scur);
+                    psum(scur, ps);
                 }
 #pragma unroll
-                for (int db = 0; db < 2; ++db) {
-                    const char* pa = slot + voff[db] + (kb * 32 + 16 * s2) * 128;
-                    v4s va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)pa);
-                    v4s vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(pa + 8 * 128));
-                    v8s vv;
-                    vv[0] = va[0]; vv[1] = va[1]; vv[2] = va[2]; vv[3] = va[3];
-                    vv[4] = vb[0]; vv[5] = vb[1]; vv[6] = vb[2]; vv[7] = vb[3];
-#pragma unroll
-                    for (int qb = 0; qb < QB; ++qb) o[qb][db] = mfma32x16<ET>(vv, pf[qb], o[qb][db]);
-                }
+                for (int qb = 0; qb < QB; ++qb) l_run[qb] += ps[qb];
+            } else {
+                if constexpr (RB) rebase(next_c, scur, snext);
+                exp_all(scur);
             }
 
-        // ---- tile t+2 must be resident for the next iteration's K read (t+3 may stay in
-        //      flight); the barrier also retires every wave's reads of slot t before the
-        //      next iteration stages t+4 into it
-        if (t + 2 < ntiles) {
-            if (t + 3 < ntiles) attn_wait_vm<4>();
-            else attn_wait_vm<0>();
-            attn_sync();
-        }
-        if constexpr (NEXT != 2) {
+            // ---- O^T += V^T . P^T: P fragment of (key block kb, k-step s2) = regs 8s2..8s2+7;
+            //      every V^T fragment read from LDS feeds QB MFMAs; inference also feeds the
+            //      fragment to the row-sum MFMA
 #pragma unroll
-            for (int qb = 0; qb < QB; ++qb) { scur[qb][0] = snext[qb][0]; scur[qb][1] = snext[qb][1]; }
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    v8s pf[QB];
+#pragma unroll
+                    for (int qb = 0; qb < QB; ++qb) {
+                        v4u pu;
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj)
+                            pu[jj] = pack2<ET>(scur[qb][kb][8 * s2 + 2 * jj], scur[qb][kb][8 * s2 + 2 * jj + 1]);
+                        pf[qb] = __builtin_bit_cast(v8s, pu);
+                    }
+#pragma unroll
+                    for (int db = 0; db < 2; ++db) {
+                        const char* pa = slot + voff[db] + (kb * 32 + 16 * s2) * 128;
+                        v4s va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)pa);
+                        v4s vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(pa + 8 * 128));
+                        v8s vv;
+                        vv[0] = va[0]; vv[1] = va[1]; vv[2] = va[2]; vv[3] = va[3];
+                        vv[4] = vb[0]; vv[5] = vb[1]; vv[6] = vb[2]; vv[7] = vb[3];
+#pragma unroll
+                        for (int qb = 0; qb < QB; ++qb) o[qb][db] = mfma32x16<ET>(vv, pf[qb], o[qb][db]);
+                    }
+                    if constexpr (!WLSE) {
+#pragma unroll
+                        for (int qb = 0; qb < QB; ++qb) lsum[qb] = mfma16x32<ET>(sel, pf[qb], lsum[qb]);
+                    }
+                }
+
+            // ---- tile t+2 must be resident for the next iteration's K read (t+3 may stay in
+            //      flight); the barrier also retires every wave's reads of slot t before the
+            //      next iteration stages t+4 into it
+            if (t + 2 < ntiles) {
+                if (t + 3 < ntiles) attn_wait_vm<4>();
+                else attn_wait_vm<0>();
+                attn_sync();
+            }
+            if constexpr (NEXT != 2) {
+#pragma unroll
+                for (int qb = 0; qb < QB; ++qb) { scur[qb][0] = snext[qb][0]; scur[qb][1] = snext[qb][1]; }
+            }
+        };
+
+        using full_c = std::integral_constant<int, 0>;
+        const int nfull = S / AK;  // full tiles
+        int t = 0;
+        for (; t + 5 <= nfull; t += NS) {  // iterations t..t+3 all have a full next tile
+            iter(full_c{}, smem + 0 * KV_SLOT, smem + 1 * KV_SLOT, t);
+            iter(full_c{}, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, t + 1);
+            iter(full_c{}, smem + 2 * KV_SLOT, smem + 3 * KV_SLOT, t + 2);
+            iter(full_c{}, smem + 3 * KV_SLOT, smem + 0 * KV_SLOT, t + 3);
+        }
+        for (; t < ntiles; ++t) {  // at most NS + 1 iterations: runtime slot, mask-checked next tile
+            const char* slot = smem + (t % NS) * KV_SLOT;
+            const char* nslot = smem + ((t + 1) % NS) * KV_SLOT;
+            if (t + 1 < ntiles) iter(std::integral_constant<int, 1>{}, slot, nslot, t);
+            else iter(std::integral_constant<int, 2>{}, slot, nslot, t);
         }
     };
 
-    using full_c = std::integral_constant<int, 0>;
-    const int nfull = S / AK;  // full tiles
-    int t = 0;
-    for (; t + 5 <= nfull; t += NS) {  // iterations t..t+3 all have a full next tile
-        iter(full_c{}, smem + 0 * KV_SLOT, smem + 1 * KV_SLOT, t);
-        iter(full_c{}, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, t + 1);
-        iter(full_c{}, smem + 2 * KV_SLOT, smem + 3 * KV_SLOT, t + 2);
-        iter(full_c{}, smem + 3 * KV_SLOT, smem + 0 * KV_SLOT, t + 3);
-    }
-    for (; t < ntiles; ++t) {  // at most NS + 1 iterations: runtime slot, mask-checked next tile
-        const char* slot = smem + (t % NS) * KV_SLOT;
-        const char* nslot = smem + ((t + 1) % NS) * KV_SLOT;
-        if (t + 1 < ntiles) iter(std::integral_constant<int, 1>{}, slot, nslot, t);
-        else iter(std::integral_constant<int, 2>{}, slot, nslot, t);
+    // total row sum of this lane's query
+    auto row_total = [&](int qb) {
+        if constexpr (WLSE) {
+            const float l_own = l_run[qb][0] + l_run[qb][1];
+            return l_own + __shfl_xor(l_own, 32, 64);
+        } else {
+            // query r's row sum sits in lane (r & 15) + 32 (r >> 4)
+            return __shfl(lsum[qb][0], (r & 15) + ((r >> 4) << 5), 64);
+        }
+    };
+
+    if constexpr (WLSE || REBASE_ALWAYS) {
+        pass(std::integral_constant<bool, REBASE_ALWAYS>{});
+    } else {
+        pass(std::false_type{});
+        // a row sum above 2^64 (some score ~50 or more above tile 0's max, before any P can
+        // overflow at 128) or non-finite (inf / NaN input): the whole workgroup repeats the
+        // pass re-basing on every tile.  Every
+        // tile staged by the first pass was retired inside it, so the ring is free.
+        bool bad = false;
+#pragma unroll
+        for (int qb = 0; qb < QB; ++qb) bad = bad || !(row_total(qb) <= 0x1p64f);
+        if (__syncthreads_or(bad)) pass(std::true_type{});
     }
 
     // ---- normalise and store O[q][d]: reg 4g+e of block db -> d = 32db + 8g + 4h + e;
@@ -363,8 +445,7 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
     for (int qb = 0; qb < QB; ++qb) {
         const int q = qblk * AQ + (wave * QB + qb) * 32 + r;
         const int qc = q < S ? q : S - 1;
-        const float l_own = l_run[qb][0] + l_run[qb][1];
-        const float l_tot = l_own + __shfl_xor(l_own, 32, 64);
+        const float l_tot = row_total(qb);
         const float inv = 1.0f / l_tot;
         if constexpr (WLSE) {
             if (h == 0 && q < S) lse[(int64_t)bh * S + q] = -minit[qb][0] + __log2f(l_tot);
