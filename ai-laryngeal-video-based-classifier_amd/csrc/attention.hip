@@ -184,32 +184,38 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
     }
 
     // ---- S'^T = K . Q'^T - m for QB query blocks x two 32-key blocks of tile t; each K
-    //      fragment feeds QB MFMAs (-m enters as the C operand of the first k-step)
-    auto qk_mfma = [&](const char* slot, v16f (&sc)[QB][2]) {
+    //      fragment feeds QB MFMAs (-m enters as the C operand of the first k-step);
+    //      KB1 = false skips key block 1 (a last tile holding <= 32 keys)
+    auto qk_mfma = [&](const char* slot, v16f (&sc)[QB][2], bool kb1 = true) {
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
             const v8s k0 = *reinterpret_cast<const v8s*>(slot + koff[kk]);
-            const v8s k1 = *reinterpret_cast<const v8s*>(slot + koff[kk] + 4096);
 #pragma unroll
-            for (int qb = 0; qb < QB; ++qb) {
-                sc[qb][0] = mfma32x16<ET>(k0, qf[qb][kk], kk == 0 ? minit[qb] : sc[qb][0]);
-                sc[qb][1] = mfma32x16<ET>(k1, qf[qb][kk], kk == 0 ? minit[qb] : sc[qb][1]);
+            for (int qb = 0; qb < QB; ++qb) sc[qb][0] = mfma32x16<ET>(k0, qf[qb][kk], kk == 0 ? minit[qb] : sc[qb][0]);
+            if (kb1) {
+                const v8s k1 = *reinterpret_cast<const v8s*>(slot + koff[kk] + 4096);
+#pragma unroll
+                for (int qb = 0; qb < QB; ++qb) sc[qb][1] = mfma32x16<ET>(k1, qf[qb][kk], kk == 0 ? minit[qb] : sc[qb][1]);
             }
         }
     };
-    //      keys beyond S masked to -inf (last tile only)
+    //      keys beyond S masked to -inf (last tile only; key block 1 not computed at all when
+    //      the tile holds <= 32 keys: TimeSformer's 197-token rows end 5 keys into their 4th tile)
     auto qk = [&](const char* slot, int t, v16f (&sc)[QB][2]) {
-        qk_mfma(slot, sc);
         const int kv0 = t * AK;
         if (kv0 + AK > S) {
+            const bool kb1 = kv0 + 32 < S;
+            qk_mfma(slot, sc, kb1);
 #pragma unroll
             for (int qb = 0; qb < QB; ++qb)
 #pragma unroll
                 for (int e = 0; e < 16; ++e) {
                     const int key = (e & 3) + 8 * (e >> 2) + 4 * h;
                     if (kv0 + key >= S) sc[qb][0][e] = -INFINITY;
-                    if (kv0 + 32 + key >= S) sc[qb][1][e] = -INFINITY;
+                    if (!kb1 || kv0 + 32 + key >= S) sc[qb][1][e] = -INFINITY;
                 }
+        } else {
+            qk_mfma(slot, sc);
         }
     };
     auto exp_all = [&](v16f (&sc)[QB][2]) {
@@ -288,6 +294,25 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
     // inference never re-bases inside the pass — P is relative to tile 0's max, which is exact
     // for any magnitude until exp2 overflows — and the caller repeats the pass with RB = 1 when
     // a row sum came out non-finite or above 2^64.
+    // a wave whose 32 queries all lie past S (the last query block of a clip) computes
+    // nothing: it only stages its share of every tile and joins the barriers
+    const bool live = qblk * AQ + wave * 32 < S;
+    auto dead_pass = [&]() {
+        stage(0);
+        if (ntiles > 1) stage(1);
+        if (ntiles > 2) stage(2);
+        if (ntiles > 2) attn_wait_vm<4>();
+        else attn_wait_vm<0>();
+        attn_sync();
+        for (int t = 0; t < ntiles; ++t) {
+            if (t + NS - 1 < ntiles) stage(t + NS - 1);
+            if (t + 2 < ntiles) {
+                if (t + 3 < ntiles) attn_wait_vm<4>();
+                else attn_wait_vm<0>();
+                attn_sync();
+            }
+        }
+    };
     auto pass = [&](auto rb_c) {
         constexpr bool RB = decltype(rb_c)::value;
 #pragma unroll
@@ -296,6 +321,10 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
             for (int e = 0; e < 16; ++e) { o[qb][0][e] = 0.f; o[qb][1][e] = 0.f; minit[qb][e] = 0.f; }
             l_run[qb] = v2f{0.f, 0.f};
             lsum[qb] = v4f{0.f, 0.f, 0.f, 0.f};
+        }
+        if (!live) {
+            dead_pass();
+            return;
         }
         stage(0);
         if (ntiles > 1) stage(1);
@@ -353,10 +382,12 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
             // ---- O^T += V^T . P^T: P fragment of (key block kb, k-step s2) = regs 8s2..8s2+7;
             //      every V^T fragment read from LDS feeds QB MFMAs; inference also feeds the
             //      fragment to the row-sum MFMA
+            const bool pv_kb1 = NEXT != 2 || t * AK + 32 < S;
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) {
+                    if (kb == 1 && !pv_kb1) continue;
                     v8s pf[QB];
 #pragma unroll
                     for (int qb = 0; qb < QB; ++qb) {

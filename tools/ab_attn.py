@@ -1,6 +1,6 @@
 """Interleaved timing of attention-kernel builds in ONE process (cdna_hip_programming.md rule 24):
   python tools/ab_attn.py ab/attn/base.so ab/attn/v1.so ... [--rounds R] [--iters N]
-Each library's vc_attention_fwd runs on the same ViViT-B inputs (B=8, S=3137, H=12); outputs are
+Each library's vc_attention_fwd runs on the same ViViT-B inputs (default B=8, S=3137, H=12); outputs are
 compared with the first library's (max |diff|), then R rounds x N launches per library are timed
 with HIP events on the current stream, libraries alternating every round."""
 import argparse
@@ -15,8 +15,9 @@ ap.add_argument("libs", nargs="+")
 ap.add_argument("--rounds", type=int, default=12)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--B", type=int, default=8)
+ap.add_argument("--S", type=int, default=3137)  # 197 with --B 128: TimeSformer-B spatial attention at B=16
 a = ap.parse_args()
-B, S, H = a.B, 3137, 12
+B, S, H = a.B, a.S, 12
 g = torch.Generator(device="cuda").manual_seed(0)
 qkv = (torch.randn(B * S, 3 * H * 64, device="cuda", generator=g) * 1.5).bfloat16()
 st = torch.cuda.current_stream()
