@@ -125,6 +125,33 @@ def test_attention_fp16(B, S, Hh):
     assert out[B * S:].float().abs().sum().item() == 0
 
 
+@pytest.mark.parametrize("jump", [10.0, 20.0, 40.0])
+def test_attention_fp16_late_jump(jump):
+    """fp16 P overflows at 2^16: a late key 20 or 40 (log2 units) above tile 0's max turns a P into inf,
+    the row sum goes non-finite and the workgroup repeats its pass with exact per-tile re-basing;
+    10 stays on the single pass.  All must match the fp32 softmax."""
+    B, S, Hh = 2, 700, 1
+    rows = (B - 1) * S + (S + 63) // 64 * 64 + 64
+    g = torch.Generator().manual_seed(int(jump) + 1)
+    qkv = torch.randn(rows, 192, generator=g) * 0.05
+    qkv[:, 0:64] = 0.0
+    qkv[:, 0] = 1.0
+    qkv[:, 64] = torch.rand(rows, generator=g)
+    qkv[:, 128:] = torch.randn(rows, 64, generator=g)
+    for b in range(B):
+        qkv[b * S + 610, 64] = jump
+    qkv = qkv.to(H)
+    out = torch.zeros(rows, 64, dtype=H, device=DEV)
+    ops().attention(qkv.to(DEV), B, S, Hh, 0.125, out, q_prescaled=True)
+    q = qkv[: B * S].float().view(B, S, 3, 1, 64)
+    c = 0.125 * 1.4426950408889634
+    ref = attention_ref(q[:, :, 0].transpose(1, 2) / c, q[:, :, 1].transpose(1, 2), q[:, :, 2].transpose(1, 2), 0.125)
+    o = out[: B * S].float().cpu()
+    assert torch.isfinite(o).all()
+    err = (o - ref.transpose(1, 2).reshape(B * S, 64)).abs().max().item()
+    assert err < 5e-3, err
+
+
 def _vivit(cfg, dtype):
     from vclip_amd.vivit import VivitConfig, VivitForVideoClassification
     from vclip_amd.weights import make_vivit_weights

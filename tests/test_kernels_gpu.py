@@ -252,6 +252,34 @@ def test_attention_spike_max_jump():
     assert err < 2e-2, err
 
 
+@pytest.mark.parametrize("jump", [6.0, 40.0, 100.0, 200.0])
+def test_attention_late_jump_no_rebase_path(jump):
+    """Inference keeps tile 0's max for the whole pass: a late key `jump` (log2 units) above it gives
+    P = 2^jump, exact while the row sum stays <= 2^64 (jump 6, 40); beyond that (100: row sum 2^100;
+    200: exp2 overflows to inf) the workgroup repeats its pass re-basing on every tile.  All must
+    match the fp32 softmax."""
+    B, S, H = 2, 700, 1
+    rows = (B - 1) * S + (S + 63) // 64 * 64 + 64
+    g = torch.Generator().manual_seed(int(jump))
+    qkv = torch.randn(rows, 192, generator=g) * 0.05
+    qkv[:, 0:64] = 0.0
+    qkv[:, 0] = 1.0                      # q' = e0: the score of key j is k[j][0] (q pre-scaled)
+    qkv[:, 64] = torch.rand(rows, generator=g)  # scores in [0, 1) ...
+    qkv[:, 128:] = torch.randn(rows, 64, generator=g)
+    for b in range(B):
+        qkv[b * S + 610, 64] = jump      # ... except one key in tile 9 of each clip
+    qkv = bf(qkv)
+    out = torch.zeros(rows, 64, dtype=torch.bfloat16, device=DEV)
+    ops().attention(qkv.to(DEV), B, S, H, 0.125, out, q_prescaled=True)
+    q = qkv[: B * S].float().view(B, S, 3, 1, 64)
+    c = 0.125 * 1.4426950408889634
+    ref = attention_ref(q[:, :, 0].transpose(1, 2) / c, q[:, :, 1].transpose(1, 2), q[:, :, 2].transpose(1, 2), 0.125)
+    o = out[: B * S].float().cpu()
+    assert torch.isfinite(o).all()
+    err = (o - ref.transpose(1, 2).reshape(B * S, 64)).abs().max().item()
+    assert err < 2e-2, err
+
+
 @pytest.mark.parametrize("mag", [0.05, 4.0, 12.0])
 def test_attention_score_scales(mag):
     """Tiny scores (no rescale after the first block) up to huge ones (re-basing the running
