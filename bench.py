@@ -359,6 +359,7 @@ def run_family(a, dist, rank, world, dev):
                          "flop_per_step": round(attn_flop / a.steps / 1e9, 2)},
             "model_tflops": round(model_tflops, 1), "model_frac_of_peak": round(model_tflops / PEAK_BF16_TFLOPS, 4),
             "cpu_baseline": cpu,
+            "build": _build_id(),
         }
         print(json.dumps(out), flush=True)
     return out
@@ -425,6 +426,7 @@ def run_train(a, dist, rank, world, dev):
                          "flop_per_launch": f"{TRAIN_ATTN_GFLOP_PER_CLIP_LAYER:.2f} GF/clip x {a.batch} clips"},
             "step_tflops": round(step_tflops, 1), "step_frac_of_peak": round(step_tflops / PEAK_BF16_TFLOPS, 4),
             "cpu_baseline": cpu,
+            "build": _build_id(),
         }
         print(json.dumps(out), flush=True)
     return out
