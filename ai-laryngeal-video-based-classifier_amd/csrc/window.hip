@@ -21,16 +21,21 @@
 #include "window_common.hpp"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace vc {
 
 constexpr int WNP_MAX = 448;  // max padded window volume (8*7*7 = 392 -> 448)
 
-// Softmax with the ViViT kernel's deferred running max (attention.hip): scores are taken relative
-// to a running max m fixed by the first key tile; per tile only exp2, the row sum and the convert
-// run; a lane's partial row sum <= LIM bounds every P of the tile, and only when that fails is m
-// re-based on the tile's exact max (O and l scaled by 2^-delta).  Measured (Swin-T B=4, round 1):
-// 1-5 % faster per launch than a per-tile max.  Where the rest goes: the fragment-order f32 bias
+// Softmax, inference: scores are exponentiated as they come (the bias occupies the QK^T C
+// operand, so a running max would cost a subtraction per score) and the row sums run on the
+// matrix pipe (attention.hip's selector MFMA over the P.V operand); a row sum outside
+// [2^-64, 2^64] (overflow, underflow, inf / NaN) makes the wave repeat the query block with the
+// ViViT kernel's deferred running max: scores relative to a max m fixed by the first key tile,
+// f32 VALU row sums, m re-based when a lane's partial row sum exceeds LIM (O and l scaled by
+// 2^-delta).  The training forward (WLSE) uses the max-free pass with f32 VALU sums.  Measured
+// on Swin-T B=4 (round 2, process-level A/B): 2.915 -> 2.880 ms per forward (+1.2 %).  Round 1:
+// the deferred max was 1-5 % faster per launch than a per-tile max.  Where the rest goes: the fragment-order f32 bias
 // stream (784 KB per (window, head) workgroup, one tile of prefetch) costs 15-20 %; the
 // shift-region mask +15-25 % on the shifted blocks; stages 3-4 fill only 384 / 192 of the 512
 // workgroup slots (splitting a pair's query blocks over more workgroups measured slower: each
@@ -122,6 +127,13 @@ window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, 
         }
     };
 
+    // 0/1 selector A operand of the row-sum MFMA: Sel[i][k] = 1 when k-group parity == i >> 3
+    v8bf sel;
+    {
+        const __bf16 v = (((lane >> 4) & 1) == ((lane & 15) >> 3)) ? (__bf16)1.0f : (__bf16)0.0f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sel[j] = v;
+    }
     // query blocks of this (window, head) are dealt over the 4 waves
     for (int qb = wave; qb < nqb; qb += 4) {
         const int qn = qb * 32 + rr;  // this lane's query (window-local)
@@ -132,89 +144,128 @@ window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, 
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk)
             qf[kk] = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(qkv + qrow * ld + head * 32 + 16 * kk + 8 * h));
-        v16f o = {};
-        float m_run = -1e30f, l_run = 0.f;
-        v16f bnext[2];
-        load_bias(qb, 0, bnext);
-        // (bias fragments two tiles ahead instead of one: 238 VGPRs, 2 % slower per forward)
-        v2f l2 = {0.f, 0.f};
-        for (int t = 0; t < ntile; ++t) {
-            v16f sc[2] = {bnext[0], bnext[1]};
-            if (t + 1 < ntile) load_bias(qb, t + 1, bnext);
+        v16f o;
+        float m_run, l_run;
+        // SAFE = false: scores are used as they come (no running max, no per-score subtraction):
+        // exp2 of a bf16-range score is exact in relative terms until it overflows (a score above
+        // ~127 in log2 units) or every key of the row underflows; a row sum outside
+        // [2^-64, 2^64] (or inf / NaN) makes this wave repeat the query block with SAFE = true,
+        // the deferred running max fixed by tile 0 and re-based when a partial row sum exceeds
+        // WLIM.  Both passes are wave-local (K / V stay in LDS for the whole window).
+        auto attend = [&](auto safe_c) {
+            constexpr bool SAFE = decltype(safe_c)::value;
+            // fast inference pass: row sums on the matrix pipe (attention.hip's selector MFMA over
+            // the P.V operand; lane l ends with the sum of query (l & 15) + 16 (l >> 5)); the
+            // exact pass and the training forward keep f32 VALU sums
+            constexpr bool MSUM = !SAFE && !WLSE;
+            o = v16f{};
+            m_run = SAFE ? -1e30f : 0.f;
+            v4f lsum = {0.f, 0.f, 0.f, 0.f};
+            v16f bnext[2];
+            load_bias(qb, 0, bnext);
+            // (bias fragments two tiles ahead instead of one: 238 VGPRs, 2 % slower per forward)
+            v2f l2 = {0.f, 0.f};
+            for (int t = 0; t < ntile; ++t) {
+                v16f sc[2] = {bnext[0], bnext[1]};
+                if (t + 1 < ntile) load_bias(qb, t + 1, bnext);
 #pragma unroll
-            for (int kk = 0; kk < 2; ++kk) {
+                for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
-                for (int kb = 0; kb < 2; ++kb) {
-                    const v8bf kf = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(Ks + (t * 64 + kb * 32) * 64 + koff[kk]));
-                    sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kk], sc[kb], 0, 0, 0);
-                }
-            }
-            if (mixed) {
-#pragma unroll
-                for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-                    for (int g4 = 0; g4 < 4; ++g4) {
-                        const int k0 = t * 64 + kb * 32 + 8 * g4 + 4 * h;
-                        const unsigned wv = lab4[k0 >> 3] >> (4 * (k0 & 7));
-#pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            if ((int)((wv >> (4 * e)) & 15) != qlab) sc[kb][4 * g4 + e] = -INFINITY;
+                    for (int kb = 0; kb < 2; ++kb) {
+                        const v8bf kf = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(Ks + (t * 64 + kb * 32) * 64 + koff[kk]));
+                        sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kk], sc[kb], 0, 0, 0);
                     }
                 }
-            }
-            auto rowmax = [&]() {
-                float a = fmaxf(sc[0][0], sc[1][0]), c = fmaxf(sc[0][1], sc[1][1]);
+                if (mixed) {
 #pragma unroll
-                for (int e = 2; e < 16; e += 2) {
-                    a = fmaxf(a, fmaxf(sc[0][e], sc[1][e]));
-                    c = fmaxf(c, fmaxf(sc[0][e + 1], sc[1][e + 1]));
+                    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+                        for (int g4 = 0; g4 < 4; ++g4) {
+                            const int k0 = t * 64 + kb * 32 + 8 * g4 + 4 * h;
+                            const unsigned wv = lab4[k0 >> 3] >> (4 * (k0 & 7));
+#pragma unroll
+                            for (int e = 0; e < 4; ++e)
+                                if ((int)((wv >> (4 * e)) & 15) != qlab) sc[kb][4 * g4 + e] = -INFINITY;
+                        }
+                    }
                 }
-                const float x = fmaxf(a, c);
-                return fmaxf(x, __shfl_xor(x, 32, 64));
-            };
-            if (t == 0) m_run = fmaxf(rowmax(), -1e30f);  // first tile fixes m (fully masked rows: -1e30)
-            v16f p[2];
-            auto expsum = [&]() {
+                auto rowmax = [&]() {
+                    float a = fmaxf(sc[0][0], sc[1][0]), c = fmaxf(sc[0][1], sc[1][1]);
+#pragma unroll
+                    for (int e = 2; e < 16; e += 2) {
+                        a = fmaxf(a, fmaxf(sc[0][e], sc[1][e]));
+                        c = fmaxf(c, fmaxf(sc[0][e + 1], sc[1][e + 1]));
+                    }
+                    const float x = fmaxf(a, c);
+                    return fmaxf(x, __shfl_xor(x, 32, 64));
+                };
+                if constexpr (SAFE) {
+                    if (t == 0) m_run = fmaxf(rowmax(), -1e30f);  // first tile fixes m (fully masked rows: -1e30)
+                }
+                v16f p[2];
+                auto expsum = [&]() {
+#pragma unroll
+                    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                        for (int e = 0; e < 16; ++e) p[kb][e] = __builtin_amdgcn_exp2f(SAFE ? sc[kb][e] - m_run : sc[kb][e]);
+                    v2f u[8];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        u[j] = v2f{p[0][4 * j], p[0][4 * j + 1]} + v2f{p[0][4 * j + 2], p[0][4 * j + 3]};
+                        u[4 + j] = v2f{p[1][4 * j], p[1][4 * j + 1]} + v2f{p[1][4 * j + 2], p[1][4 * j + 3]};
+                    }
+                    return ((u[0] + u[1]) + (u[2] + u[3])) + ((u[4] + u[5]) + (u[6] + u[7]));
+                };
+                v2f ps = {0.f, 0.f};
+                if constexpr (MSUM) {
+#pragma unroll
+                    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                        for (int e = 0; e < 16; ++e) p[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e]);
+                } else {
+                    ps = expsum();
+                }
+                if (SAFE && __any(!(ps[0] + ps[1] <= WLIM))) {  // rare: re-base m on this tile's exact max
+                    const float delta = fmaxf(rowmax() - m_run, 0.f);
+                    const float alpha = __builtin_amdgcn_exp2f(-delta);
+                    m_run += delta;
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) o[e] *= alpha;
+                    l2 *= alpha;
+                    ps = expsum();
+                }
+                l2 += ps;
 #pragma unroll
                 for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-                    for (int e = 0; e < 16; ++e) p[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e] - m_run);
-                v2f u[8];
+                    for (int s2 = 0; s2 < 2; ++s2) {
+                        v4u pu;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    u[j] = v2f{p[0][4 * j], p[0][4 * j + 1]} + v2f{p[0][4 * j + 2], p[0][4 * j + 3]};
-                    u[4 + j] = v2f{p[1][4 * j], p[1][4 * j + 1]} + v2f{p[1][4 * j + 2], p[1][4 * j + 3]};
-                }
-                return ((u[0] + u[1]) + (u[2] + u[3])) + ((u[4] + u[5]) + (u[6] + u[7]));
-            };
-            v2f ps = expsum();
-            if (__any(!(ps[0] + ps[1] <= WLIM))) {  // rare: re-base m on this tile's exact max
-                const float delta = fmaxf(rowmax() - m_run, 0.f);
-                const float alpha = __builtin_amdgcn_exp2f(-delta);
-                m_run += delta;
-#pragma unroll
-                for (int e = 0; e < 16; ++e) o[e] *= alpha;
-                l2 *= alpha;
-                ps = expsum();
+                        for (int jj = 0; jj < 4; ++jj) pu[jj] = pack2bf(p[kb][8 * s2 + 2 * jj], p[kb][8 * s2 + 2 * jj + 1]);
+                        const v8bf pf = __builtin_bit_cast(v8bf, pu);
+                        const char* pa = Vs + (t * 64 + kb * 32 + 16 * s2) * 64 + voff;
+                        const v4s va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)pa);
+                        const v4s vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(pa + 8 * 64));
+                        v8s vv;
+                        vv[0] = va[0]; vv[1] = va[1]; vv[2] = va[2]; vv[3] = va[3];
+                        vv[4] = vb[0]; vv[5] = vb[1]; vv[6] = vb[2]; vv[7] = vb[3];
+                        o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf, vv), pf, o, 0, 0, 0);
+                        if constexpr (MSUM) lsum = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf, lsum, 0, 0, 0);
+                    }
             }
-            l2 += ps;
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) {
-                    v8bf pf;
-#pragma unroll
-                    for (int jj = 0; jj < 8; ++jj) pf[jj] = (__bf16)p[kb][8 * s2 + jj];
-                    const char* pa = Vs + (t * 64 + kb * 32 + 16 * s2) * 64 + voff;
-                    const v4s va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)pa);
-                    const v4s vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(pa + 8 * 64));
-                    v8s vv;
-                    vv[0] = va[0]; vv[1] = va[1]; vv[2] = va[2]; vv[3] = va[3];
-                    vv[4] = vb[0]; vv[5] = vb[1]; vv[6] = vb[2]; vv[7] = vb[3];
-                    o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf, vv), pf, o, 0, 0, 0);
-                }
+            if constexpr (MSUM) {
+                // this lane's half of query rr's sum (the caller adds the h = 1 half): the whole
+                // sum sits in lane (rr & 15) + 32 (rr >> 4); halve it for the two lane halves
+                l_run = 0.5f * __shfl(lsum[0], (rr & 15) + ((rr >> 4) << 5), 64);
+            } else {
+                l_run = l2[0] + l2[1];
+            }
+        };
+        attend(std::false_type{});
+        {
+            const float lt = l_run + __shfl_xor(l_run, 32, 64);
+            if (__any(!(lt >= 0x1p-64f && lt <= 0x1p64f))) attend(std::true_type{});
         }
-        l_run = l2[0] + l2[1];
 
         // ---- O^T[d][q]: reg 4g+e -> d = 8g + 4h + e; lane pairs swap halves -> 16-B stores
         const float l_tot = l_run + __shfl_xor(l_run, 32, 64);

@@ -60,8 +60,10 @@ def _window_case(B, grid, C, window, shift, seed):
 ])
 def test_window_attention3d(B, grid, C, window, shift):
     got, want = _window_case(B, grid, C, window, shift, seed=C + sum(shift))
-    err = (got - want).abs().max().item()
-    assert err < 2e-2, err
+    # 2e-2 absolute plus one bf16 step of the output itself (outputs reach |o| ~ 5, where one bf16
+    # step is 2^-5: the rounding of the stored output alone can exceed a flat 2e-2)
+    excess = ((got - want).abs() - (2e-2 + want.abs() / 128)).max().item()
+    assert excess < 0, ((got - want).abs().max().item(), excess)
 
 
 def _model(cfg, seed=0):
