@@ -24,8 +24,9 @@ def _gpu():
     _lib.load()
 
 
-def _window_case(B, grid, C, window, shift, seed):
-    """Oracle attention (qkv from x, identity proj) vs qkv GEMM-free kernel call."""
+def _window_case(B, grid, C, window, shift, seed, qmul=1.0):
+    """Oracle attention (qkv from x, identity proj) vs qkv GEMM-free kernel call; qmul scales the q
+    projection (qmul >> 1: scores far beyond exp2's range, the kernel's exact-max fallback)."""
     from vclip_amd import ops
     g = torch.Generator().manual_seed(seed)
     heads = C // 32
@@ -36,6 +37,8 @@ def _window_case(B, grid, C, window, shift, seed):
     p = {"a.qkv.weight": torch.randn(3 * C, C, generator=g) * C ** -0.5, "a.qkv.bias": torch.randn(3 * C, generator=g) * 0.1,
          "a.proj.weight": torch.eye(C), "a.proj.bias": torch.zeros(C),
          "a.relative_position_bias_table": torch.randn(nb, heads, generator=g) * 0.5}
+    p["a.qkv.weight"][:C] *= qmul
+    p["a.qkv.bias"][:C] *= qmul
     want = ref.window_attention_3d(x, p, "a.", heads, window, shift)
     # device: q|k|v rows with q pre-scaled by d^-1/2 log2 e, rounded to bf16 once
     qkv = x.reshape(-1, C) @ p["a.qkv.weight"].T + p["a.qkv.bias"]
@@ -63,6 +66,16 @@ def test_window_attention3d(B, grid, C, window, shift):
     # 2e-2 absolute plus one bf16 step of the output itself (outputs reach |o| ~ 5, where one bf16
     # step is 2^-5: the rounding of the stored output alone can exceed a flat 2e-2)
     excess = ((got - want).abs() - (2e-2 + want.abs() / 128)).max().item()
+    assert excess < 0, ((got - want).abs().max().item(), excess)
+
+
+@pytest.mark.parametrize("qmul", [8.0, 60.0])
+def test_window_attention3d_large_scores(qmul):
+    """Scores tens to hundreds of log2 units apart: the max-free pass overflows (or its row sum leaves
+    [2^-64, 2^64]) and the wave repeats the query block with the deferred running max."""
+    got, want = _window_case(1, (4, 6, 6), 64, (2, 3, 3), (1, 1, 1), seed=11, qmul=qmul)
+    assert torch.isfinite(got).all()
+    excess = ((got - want).abs() - (3e-2 + want.abs() / 64)).max().item()
     assert excess < 0, ((got - want).abs().max().item(), excess)
 
 
