@@ -76,3 +76,33 @@ def test_vivit_two_stream_split_bit_exact():
     assert m.last_streams == 2
     assert torch.equal(one, two)
     torch.testing.assert_close(m(pixel_values=pix).logits, one, rtol=0, atol=0)
+
+
+def test_vivit_tiny_per_layer_drift():
+    """Hidden-state drift layer by layer against the HF golden (tests/golden/vivit_tiny.npz holds the
+    embeddings output and every layer's output): the GPU forward is run with its first k layers and
+    the f32 residual stream X compared with hidden_states[k].  Reports the drift per layer; the bar is
+    2e-2 of each layer's max |h| (bf16 operands, fp32 residual stream)."""
+    g = np.load(os.path.join(GD, "vivit_tiny.npz"))
+    cfg = json.loads(str(g["config"]))
+    m = _model(cfg)
+    pix = torch.from_numpy(g["pixel_values"]).cuda()
+    m.forward_logits(pix)
+    pk = m._pack(pix.device)
+    full = pk["layers"]
+    B = pix.shape[0]
+    _, S, _, _ = m.geometry(B)
+    drift = []
+    try:
+        for k in range(len(full) + 1):
+            pk["layers"] = full[:k]
+            m._forward_part(pix, 0)
+            torch.cuda.synchronize()
+            x = m._workspace(B, pix.device, 0)["X"][:B * S].float().cpu().numpy().reshape(B, S, -1)
+            ref = g["hidden_states"][k]
+            drift.append(float(np.abs(x - ref).max() / np.abs(ref).max()))
+    finally:
+        pk["layers"] = full
+    print("relative hidden-state drift per layer (embeddings, layer 1, ...):", drift)
+    assert len(drift) == g["hidden_states"].shape[0]
+    assert max(drift) < 2e-2, drift
