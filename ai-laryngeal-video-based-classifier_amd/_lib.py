@@ -71,9 +71,6 @@ SIGNATURES = {
     "vc_resnet_head_train": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_p, c_p, c_p, c_i64, c_p, c_p, c_p],
                              c_int),
     "vc_resnet_head_train_bwd": ([c_p, c_i64, c_i64, c_i64, c_i64, c_int, c_p, c_p, c_i64, c_p], c_int),
-    "vc_global_avgpool": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p], c_int),
-    "vc_lstm_recurrence": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_i64, c_p, c_p], c_int),
-    "vc_mlp_head": ([c_p, c_i64, c_i64, c_p, c_p, c_i64, c_p, c_p, c_i64, c_p, c_p], c_int),
     "vc_resample_u8": ([c_p, c_i64, c_i64, c_i64, c_i64, c_int, c_i64, c_p, c_p, c_i64, c_p, c_p], c_int),
     "vc_resize_linear_u8": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_int, c_p, c_p], c_int),
     "vc_video_transform": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p,

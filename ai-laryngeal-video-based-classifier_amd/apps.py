@@ -147,13 +147,6 @@ class Family:
         self.name, self.prefix, self.model_dir = name, prefix, model_dir
         self.batch_size, self.epochs, self.lr, self.wd, self.optimizer = batch_size, epochs, lr, wd, optimizer
 
-    def sampler(self, method, num_frames, logger):
-        if self.name in ("vivit", "timesformer"):
-            return sampling.VivitSampler(num_frames, method, logger)
-        if self.name == "swin":
-            return sampling.SwinSampler(num_frames, method, logger, fps_of=lambda p: video_io.open_video(p).fps)
-        return sampling.Resnet3dSampler(num_frames, method, logger, fps_of=lambda p: video_io.open_video(p).fps)
-
     def load_clip(self, src, sampler, path, num_frames):
         """Decoded uint8 frames the transform consumes: the sampled frames (ViViT/TimeSformer,
         resized to 224 as dataset.py:271-277), or every frame of the sampled span (Swin/ResNet3D
@@ -253,7 +246,7 @@ def build_parser(fam: Family, inference: bool):
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--patience", type=int, default=7)
     p.add_argument("--early_stopping_delta", type=float, default=0.001)
-    # resnet50-3d-video/main.py:53-58 (offered by every family here: only ViViT can train on the GPU)
+    # resnet50-3d-video/main.py:53-58, offered by every family here (evaluate a checkpoint, no training)
     p.add_argument("--skip_train", action="store_true")
     p.add_argument("--checkpoint_path", type=str, default=None)
     if fam.name == "resnet3d":
@@ -268,29 +261,48 @@ def _device():
     return torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def _batches(fam, split, sampler, args, device, shuffle=False, logger=None):
-    """Batches of (model input, labels); shuffle = the train split (shuffled order, train-time
-    transforms).  A clip that cannot be decoded becomes the reference
-    dataset's gray placeholder (127) with a warning (dataset.py:294-381), so one bad video does
-    not end the epoch."""
-    paths, labels = split
-    order = list(range(len(paths)))
-    if shuffle:
-        random.shuffle(order)
-    for s in range(0, len(order), args.batch_size):
-        ids = order[s:s + args.batch_size]
-        xs = []
-        for i in ids:
-            try:
-                src = video_io.open_video(paths[i])
-                clip = fam.load_clip(src, sampler, paths[i], args.num_frames)
-            except Exception as e:  # noqa: BLE001 - reference: log, placeholder, continue
-                if logger is not None:
-                    logger.warning(f"Failed to load {paths[i]}: {str(e)}; using a placeholder clip")
-                clip = np.full((args.num_frames, 224, 224, 3), 127, np.uint8)
-            fr = torch.from_numpy(clip).to(device)
-            xs.append(fam.to_model_input(fr.unsqueeze(0), args.num_frames, train=shuffle))
-        yield torch.cat(xs), torch.tensor([labels[i] for i in ids], device=device)
+def _loaders(fam, args, logger, exp_dir):
+    """({split: loader}, class labels) from the folder's own data_config drop-in, so `--num_workers`
+    decode workers run as in the reference (vivit_transformer/main.py:93, videoswintransformer/
+    main.py:105, resnet50-3d-video/main.py:94-97 with the sampled-index CSVs in the experiment dir).
+    `--skip_train` builds the test split only (resnet50-3d-video/main.py:53-58 evaluates a checkpoint)."""
+    from torch.utils.data import DataLoader
+
+    from .data_config import FOLDERS, DeviceClipLoader, swin
+    mod = FOLDERS[fam.name]
+    methods = {s: getattr(args, f"{s}_sampling") for s in ("train", "val", "test")}
+    hf = fam.name in ("vivit", "timesformer")
+    binary = ["non-referral", "referral"]  # Swin3D / ResNet3D label = (folder == 'referral')
+    if not args.skip_train:
+        if hf:
+            return mod.create_dataloaders(args, methods, logger)
+        if fam.name == "swin":
+            return mod.create_dataloaders(args, logger), binary
+        return mod.create_dataloaders(args, logger, log_dir=str(exp_dir))[1], binary
+    root = args.test_data_dir or args.data_dir
+    ds = mod.VideoDataset(root, mode="test", sampling_method=methods["test"], num_frames=args.num_frames,
+                          logger=logger)
+    if hf:
+        loader = DataLoader(ds, batch_size=args.batch_size, shuffle=False, num_workers=args.num_workers,
+                            collate_fn=mod.video_collate_fn)
+        return {"test": loader}, ds.class_labels
+    return {"test": DeviceClipLoader(ds, batch_size=args.batch_size, num_workers=args.num_workers,
+                                     collate_fn=swin.video_collate_fn)}, binary
+
+
+def _batches(fam, loader, args, device):
+    """(model input, labels) on the device per loader batch: the HF folders' uint8 clips through the
+    GPU processor (trainer.py:62-104), the Swin3D / ResNet3D clips [B, n, C, T, H, W] flattened to
+    [B * n, C, T, H, W] (videoswintransformer/.../trainers/trainer.py:105-111)."""
+    for batch in loader:
+        if isinstance(batch, dict):
+            pv = batch["pixel_values"]
+            fr = torch.from_numpy(np.stack(pv)) if isinstance(pv, (list, tuple)) else torch.as_tensor(pv)
+            x = fam.to_model_input(fr.to(device), args.num_frames)
+            yield x, batch["labels"].reshape(-1).to(device)
+        else:
+            clips, labels = batch
+            yield clips.reshape(-1, *clips.shape[2:]).to(device), labels.reshape(-1).to(device)
 
 
 def _load_weights(model, path, logger, fam):
@@ -302,10 +314,10 @@ def _load_weights(model, path, logger, fam):
 
 
 @torch.no_grad()
-def evaluate(fam, model, split, sampler, args, device, class_names, exp_dir, method, logger):
+def evaluate(fam, model, loader, args, device, class_names, exp_dir, method, logger):
     model.eval()
     probs, preds, labels = [], [], []
-    for x, y in _batches(fam, split, sampler, args, device, logger=logger):
+    for x, y in _batches(fam, loader, args, device):
         try:
             p = torch.softmax(fam.logits(model, x).float(), dim=1)
         except Exception as e:  # noqa: BLE001 - evaluator.py: log and skip the batch
@@ -332,16 +344,7 @@ def run_main(fam_name, argv=None):
     logger = exp.get_logger()
     logger.info(f"Arguments: {vars(args)}")
     device = _device()
-    splits, samplers = {}, {}
-    class_labels = None
-    for s in ("train", "val", "test"):
-        root = args.test_data_dir if (s == "test" and args.test_data_dir) else args.data_dir
-        if s != "test" and args.skip_train:
-            continue
-        paths, labels, classes = scan_split(root, s, logger)
-        class_labels = class_labels or classes
-        splits[s] = (paths, labels)
-        samplers[s] = fam.sampler(getattr(args, f"{s}_sampling"), args.num_frames, logger)
+    loaders, class_labels = _loaders(fam, args, logger, exp.get_experiment_dir())
     if not hasattr(args, "num_classes"):
         args.num_classes = len(class_labels)
     model = fam.create_model(args, class_labels, device, logger)
@@ -363,7 +366,7 @@ def run_main(fam_name, argv=None):
         for epoch in range(args.epochs):
             model.train()
             tl, tc, tn = 0.0, 0, 0
-            for x, y in _batches(fam, splits["train"], samplers["train"], args, device, shuffle=True, logger=logger):
+            for x, y in _batches(fam, loaders["train"], args, device):
                 try:  # trainer.py:133-167: a failing batch is logged and skipped
                     opt.zero_grad()
                     logits = fam.logits(model, x)
@@ -379,7 +382,7 @@ def run_main(fam_name, argv=None):
             model.eval()
             vl, vc, vn = 0.0, 0, 0
             with torch.no_grad():
-                for x, y in _batches(fam, splits["val"], samplers["val"], args, device, logger=logger):
+                for x, y in _batches(fam, loaders["val"], args, device):
                     try:  # trainer.py:192-210
                         logits = fam.logits(model, x)
                         vl += float(crit(logits, y)) * len(y)
@@ -388,6 +391,12 @@ def run_main(fam_name, argv=None):
                     except Exception as e:  # noqa: BLE001
                         logger.error(f"Error in validation batch: {str(e)}")
                         continue
+            # a batch that fails is logged and skipped (trainer.py:165-167), but an epoch in which EVERY
+            # batch failed (e.g. a kernel fault on each launch) must not go on to save a "best" model
+            if tn == 0 and len(loaders["train"]) > 0:
+                raise RuntimeError(f"epoch {epoch + 1}: every training batch failed (see the log)")
+            if vn == 0 and len(loaders["val"]) > 0:
+                raise RuntimeError(f"epoch {epoch + 1}: every validation batch failed (see the log)")
             tr_loss, tr_acc = tl / max(tn, 1), tc / max(tn, 1)
             va_loss, va_acc = vl / max(vn, 1), vc / max(vn, 1)
             for k, v in (("train_loss", tr_loss), ("train_acc", tr_acc), ("val_loss", va_loss), ("val_acc", va_acc)):
@@ -415,7 +424,7 @@ def run_main(fam_name, argv=None):
                 logger.info("Early stopping triggered")
                 break
         _load_weights(model, best_path, logger, fam)
-    m = evaluate(fam, model, splits["test"], samplers["test"], args, device, class_labels, exp.get_experiment_dir(),
+    m = evaluate(fam, model, loaders["test"], args, device, class_labels, exp.get_experiment_dir(),
                  args.test_sampling, logger)
     logger.info("Training and evaluation pipeline completed successfully")
     return m, history, exp.get_experiment_dir()

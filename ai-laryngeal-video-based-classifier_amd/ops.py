@@ -427,36 +427,6 @@ def avgpool_head(x: torch.Tensor, B: int, grid, C: int, pool_kernel, wc: torch.T
     return out
 
 
-def global_avgpool(x: torch.Tensor, N: int, P: int, C: int, out: torch.Tensor) -> torch.Tensor:
-    """out[n] = mean of rows n*P .. n*P+P-1 of x (bf16 channels-last) -> bf16."""
-    _dev(x, out)
-    _need(x.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and x.shape[0] >= N * P and x.shape[1] >= C and
-          out.shape[0] >= N and out.shape[1] >= C and x.stride(1) == 1 and out.stride(1) == 1, "global_avgpool shapes")
-    _lib.call("vc_global_avgpool", _p(x), x.stride(0), N, P, C, _p(out), out.stride(0), _stream(x))
-    return out
-
-
-def lstm_recurrence(pre: torch.Tensor, B: int, T: int, hidden: int, w_hh: torch.Tensor, h_out: torch.Tensor,
-                    h_last: torch.Tensor) -> torch.Tensor:
-    _dev(pre, w_hh, h_out, h_last)
-    _need(pre.dtype == torch.float32 and pre.shape[0] >= B * T and pre.shape[1] >= 4 * hidden and pre.stride(1) == 1,
-          "lstm pre")
-    _need(w_hh.dtype == torch.float32 and w_hh.is_contiguous() and tuple(w_hh.shape) == (4 * hidden, hidden), "lstm W_hh")
-    _need(h_out.dtype == torch.bfloat16 and h_out.shape[0] >= B * T and h_out.shape[1] >= hidden, "lstm h_out")
-    _need(h_last.dtype == torch.float32 and h_last.is_contiguous() and h_last.numel() >= B * hidden, "lstm h_last")
-    _lib.call("vc_lstm_recurrence", _p(pre), pre.stride(0), B, T, hidden, _p(w_hh), _p(h_out), h_out.stride(0),
-              _p(h_last), _stream(pre))
-    return h_last
-
-
-def mlp_head(h: torch.Tensor, B: int, w1, b1, w2, b2, out: torch.Tensor) -> torch.Tensor:
-    _dev(h, w1, b1, w2, b2, out)
-    _need(all(t.dtype == torch.float32 and t.is_contiguous() for t in (h, w1, b1, w2, b2, out)), "mlp_head f32")
-    _lib.call("vc_mlp_head", _p(h), B, w1.shape[1], _p(w1), _p(b1), w1.shape[0], _p(w2), _p(b2), w2.shape[0], _p(out),
-              _stream(h))
-    return out
-
-
 # ---- train step (SURVEY.md §8 a16) -----------------------------------------------------------
 
 def attention_fwd_lse(qkv: torch.Tensor, B: int, S: int, H: int, out: torch.Tensor, lse: torch.Tensor,

@@ -171,14 +171,15 @@ class ResNet3d(torch.nn.Module):
 
     # ---- forward -----------------------------------------------------------------------
     def forward(self, video: torch.Tensor) -> torch.Tensor:
-        """`model(clips)` -> logits.  In training mode with autograd enabled (the reference's train loop,
-        resnet50-3d-video/video_classifier/trainers/trainer.py:106-123) the logits carry the graph of the
-        HIP train step (_forward_train: BatchNorm with batch statistics, the head's dropout); otherwise
-        the fused inference path (BatchNorm folded) runs."""
+        """`model(clips)` -> logits.  In training mode (the reference's train loop,
+        resnet50-3d-video/video_classifier/trainers/trainer.py:106-123) the HIP train step runs
+        (_forward_train: BatchNorm with batch statistics and running-statistic updates, the head's
+        dropout), with autograd enabled or not -- pytorchvideo in train mode under torch.no_grad keeps
+        those semantics too; in eval mode the fused inference path (BatchNorm folded) runs."""
         if video.device.type != "cuda":
             raise RuntimeError("ResNet3d (vclip_amd) runs on the GPU only: move the clip batch to cuda")
         x = video.contiguous().float() if video.dtype != torch.float32 else video.contiguous()
-        if self.training and torch.is_grad_enabled():
+        if self.training:
             return self._forward_train(x)
         with torch.no_grad():
             return self.forward_logits(x).clone()  # the workspace buffer is reused by the next call

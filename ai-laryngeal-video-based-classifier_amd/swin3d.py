@@ -34,11 +34,13 @@ from .weights import swin3d_param_shapes
 LOG2E = ops.LOG2E
 
 SWIN3D_CONFIGS = {
-    # stochastic_depth_prob: torchvision swin3d_t / _s / _b (train-time only)
+    # stochastic_depth_prob (train-time only): torchvision models/video/swin_transformer.py builds
+    # swin3d_t, swin3d_s and swin3d_b each with stochastic_depth_prob=0.1 (the 2-D swin_t/s/b use
+    # 0.2/0.3/0.5); torchvision is absent from this image, so the value is parity-unpinned
     "tiny": dict(patch_size=(2, 4, 4), embed_dim=96, depths=(2, 2, 6, 2), num_heads=(3, 6, 12, 24),
                  window_size=(8, 7, 7), mlp_ratio=4.0, layer_norm_eps=1e-5, stochastic_depth_prob=0.1),
     "small": dict(patch_size=(2, 4, 4), embed_dim=96, depths=(2, 2, 18, 2), num_heads=(3, 6, 12, 24),
-                  window_size=(8, 7, 7), mlp_ratio=4.0, layer_norm_eps=1e-5, stochastic_depth_prob=0.2),
+                  window_size=(8, 7, 7), mlp_ratio=4.0, layer_norm_eps=1e-5, stochastic_depth_prob=0.1),
     "base": dict(patch_size=(2, 4, 4), embed_dim=128, depths=(2, 2, 18, 2), num_heads=(4, 8, 16, 32),
                  window_size=(8, 7, 7), mlp_ratio=4.0, layer_norm_eps=1e-5, stochastic_depth_prob=0.1),
 }

@@ -43,10 +43,12 @@ def _build_id():
     return source_hash()
 
 
-def _same_build(pattern: str):
-    """Newest committed profiles/<pattern> summary whose "build" (vclip_amd.build.source_hash of
-    the sources it was measured on) is THIS tree's build, or None: a roofline line never cites
-    counters of another build (tools/collect_profiles.py writes the field)."""
+def _same_build(pattern: str, mode: str):
+    """The committed profiles/<pattern> summary of THIS tree's build ("build" =
+    vclip_amd.build.source_hash of the sources it was measured on) AND of this bench mode ("mode":
+    the workload the profiled command ran, stamped by tools/collect_profiles.py), newest by the
+    numbers in its name; (None, reason) when there is none, or when two such files tie: a roofline
+    line never cites counters of another build or of another workload."""
     import glob
     import re
     me = _build_id()
@@ -57,28 +59,50 @@ def _same_build(pattern: str):
                 d = json.load(fh)
         except (OSError, ValueError):
             continue
-        if d.get("build") == me:
+        if d.get("build") == me and d.get("mode") == mode:
             fs.append((f, d))
+    if not fs:
+        return None, f"no {pattern} profile of this build and mode {mode!r} under profiles/"
     key = lambda fd: [int(x) for x in re.findall(r"\d+", os.path.basename(fd[0]))]  # noqa: E731
-    return max(fs, key=key) if fs else (None, None)
+    best = max(key(fd) for fd in fs)
+    top = [fd for fd in fs if key(fd) == best]
+    if len(top) > 1:
+        return None, "ambiguous: " + ", ".join(sorted(os.path.relpath(f, ROOT) for f, _ in top))
+    return top[0]
 
 
-def measured_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE passes over this bench
-    command, tools/profile_round.sh -> profiles/rNN_*_traffic.json) for this build, else None."""
-    f, d = _same_build("r*_traffic.json")
+def measured_traffic(kernels, mode: str = "fwd"):
+    """HBM bytes per launch of `kernels` (one rocprofv3 kernel name, or a list whose per-launch bytes
+    add up) from the FETCH_SIZE x2 + WRITE_SIZE passes over this bench mode's command
+    (tools/profile_round.sh -> profiles/rNN_*_traffic.json) of this build: (bytes, source) or
+    (None, reason)."""
+    f, d = _same_build("r*_traffic.json", mode)
     if not f:
-        return None, "no profile of this build under profiles/"
-    k = d["kernels"].get(kernel)
-    return (k["hbm_bytes_per_launch"] if k else None), os.path.relpath(f, ROOT)
+        return None, d
+    ks = [kernels] if isinstance(kernels, str) else list(kernels)
+    if any(k not in d["kernels"] for k in ks):
+        return None, f"{os.path.relpath(f, ROOT)} has no entry for {ks}"
+    return sum(d["kernels"][k]["hbm_bytes_per_launch"] for k in ks), os.path.relpath(f, ROOT)
 
 
-def measured_pmc(kernel: str):
-    """Per-launch PMC averages of `kernel` for this build (profiles/rNN_*_pmc.json), else None."""
-    f, d = _same_build("r*_pmc.json")
-    if not f or kernel not in d.get("kernels", {}):
-        return None, "no profile of this build under profiles/"
+def measured_pmc(kernel: str, mode: str = "fwd"):
+    """Per-launch PMC averages of `kernel` for this build and mode (profiles/rNN_*_pmc.json), else
+    (None, reason)."""
+    f, d = _same_build("r*_pmc.json", mode)
+    if not f:
+        return None, d
+    if kernel not in d.get("kernels", {}):
+        return None, f"{os.path.relpath(f, ROOT)} has no entry for {kernel}"
     return d["kernels"][kernel], os.path.relpath(f, ROOT)
+
+
+def pmc_rates(pmc):
+    """(MFMA busy, VALU instructions per MFMA) from a kernel's PMC averages:
+    SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs); SQ_INSTS_VALU counts the MFMAs."""
+    if not pmc:
+        return None, None
+    return (round(pmc["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * pmc["GRBM_GUI_ACTIVE"] / 8), 4),
+            round(pmc["SQ_INSTS_VALU"] / pmc["SQ_INSTS_MFMA"], 3))
 
 
 def _spawn_world(n: int) -> int:
@@ -242,6 +266,7 @@ def cpu_lstm_cfg1():
 
 
 TRAIN_ATTN_GFLOP_PER_CLIP_LAYER = 2 * ATTN_GFLOP_PER_CLIP_LAYER  # dV, dP, dK, dQ (recompute of S not counted)
+TRAIN_ATTN_BWD_KERNELS = ("abwd::attn_bwd_prep_kernel", "abwd::attn_bwd_dkdv_kernel", "abwd::attn_bwd_dq_kernel")
 
 
 def cpu_train_baseline(n_clips):
@@ -268,13 +293,16 @@ def cpu_train_baseline(n_clips):
 
 
 FAMILIES = {
-    # mode: (metric, GFLOP per clip, default clips per GPU, BASELINE config, attention kernel)
+    # mode: (metric, GFLOP per clip, default clips per GPU, BASELINE config, attention
+    # kernel, its rocprofv3 name (the key of its counters in profiles/rNN_*_{traffic,pmc}.json))
     "timesformer": ("clips/sec fwd TimeSformer-B 8x224^2 bf16", 391.66, 16,
                     "TimeSformer-B divided space-time attention, 8x224x224 clips, batch 16 per GPU (BASELINE configs[2])",
-                    "attn_fwd_d64_kernel (spatial branch: B*T sequences of 197 tokens)"),
+                    "attn_fwd_d64_kernel (spatial branch: B*T sequences of 197 tokens)",
+                    "attn_fwd_d64_kernel<false, false, 0>"),
     "swin": ("clips/sec fwd Video Swin-T 32x224^2 bf16", 175.53, 4,
              "Video Swin-T 3D shifted-window attention, 32x224x224 clips, batch 4 per GPU = 32 over DP=8 "
-             "(BASELINE configs[3])", "window_attn_d32_kernel (all 12 blocks, head_dim 32)"),
+             "(BASELINE configs[3])", "window_attn_d32_kernel (all 12 blocks, head_dim 32)",
+             "window_attn_d32_kernel<false>"),
 }
 
 
@@ -314,7 +342,7 @@ def run_family(a, dist, rank, world, dev):
     """BASELINE configs[2] / [3]: TimeSformer-B (divided space-time attention) and Video Swin-T
     (3D shifted windows) forwards, clips sharded per rank like the ViViT bench (no collective)."""
     from vclip_amd.weights import make_synthetic_clips, make_synthetic_video
-    metric, gflop, _, workload, kname = FAMILIES[a.mode]
+    metric, gflop, _, workload, kname, kprof = FAMILIES[a.mode]
     if a.mode == "timesformer":
         from vclip_amd.timesformer import create_model
         model = create_model(num_frames=8, device=dev)
@@ -342,6 +370,9 @@ def run_family(a, dist, rank, world, dev):
     model_tflops = gflop * a.batch / (ms_per_step * 1e-3) / 1e3
     out = None
     if rank == 0:
+        traffic, traffic_src = measured_traffic(kprof, a.mode)
+        pmc, pmc_src = measured_pmc(kprof, a.mode)
+        mfma_busy, valu_per_mfma = pmc_rates(pmc)
         cpu, err = None, None
         if world == 1 and not a.no_cpu_baseline:
             cpu, err = cpu_family_baseline(
@@ -354,9 +385,10 @@ def run_family(a, dist, rank, world, dev):
             "config": {"workload": workload, "global_batch": a.batch * world, "parallelism": f"dp{world}"},
             "logit_max_abs_err": err,
             "roofline": {"bound": "mfma", "kernel": kname, "achieved": round(attn_tflops, 1), "peak": PEAK_BF16_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                         "avg_launch_ms": round(attn_s * 1e3 / len(evs), 4),
-                         "flop_per_step": round(attn_flop / a.steps / 1e9, 2)},
+                         "unit": "TFLOP/s", "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src, "avg_launch_ms": round(attn_s * 1e3 / len(evs), 4),
+                         "flop_per_step": round(attn_flop / a.steps / 1e9, 2), "mfma_busy": mfma_busy,
+                         "valu_per_mfma": valu_per_mfma, "pmc_source": pmc_src},
             "model_tflops": round(model_tflops, 1), "model_frac_of_peak": round(model_tflops / PEAK_BF16_TFLOPS, 4),
             "cpu_baseline": cpu,
             "build": _build_id(),
@@ -406,6 +438,10 @@ def run_train(a, dist, rank, world, dev):
     step_tflops = 3 * VIVIT_GFLOP_PER_CLIP * a.batch / (ms_per_step * 1e-3) / 1e3
     out = None
     if rank == 0:
+        # the roofline "launch" is one layer's attention backward: prep + dK/dV + dQ
+        traffic, traffic_src = measured_traffic(TRAIN_ATTN_BWD_KERNELS, "train")
+        pmc, pmc_src = measured_pmc(TRAIN_ATTN_BWD_KERNELS[1], "train")
+        mfma_busy, valu_per_mfma = pmc_rates(pmc)
         cpu = None if (world > 1 or a.no_cpu_baseline) else cpu_train_baseline(a.cpu_clips)
         out = {
             "metric": "clips/sec train step (fwd+bwd+AdamW) ViViT-B 32x224^2 bf16",
@@ -421,8 +457,9 @@ def run_train(a, dist, rank, world, dev):
             "loss_first_last": [round(float(losses[0]), 5), round(float(losses[-1]), 5)],
             "roofline": {"bound": "mfma", "kernel": "attention backward (attn_bwd_dkdv + attn_bwd_dq + prep)",
                          "achieved": round(attn_tflops, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4), "traffic": None,
-                         "avg_launch_ms": round(attn_ms, 4),
+                         "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src, "avg_launch_ms": round(attn_ms, 4),
+                         "mfma_busy_dkdv": mfma_busy, "valu_per_mfma_dkdv": valu_per_mfma, "pmc_source": pmc_src,
                          "flop_per_launch": f"{TRAIN_ATTN_GFLOP_PER_CLIP_LAYER:.2f} GF/clip x {a.batch} clips"},
             "step_tflops": round(step_tflops, 1), "step_frac_of_peak": round(step_tflops / PEAK_BF16_TFLOPS, 4),
             "cpu_baseline": cpu,
@@ -529,13 +566,9 @@ def main():
     if rank == 0:
         cpu = None
         logit_err = logit_err16 = None
-        traffic, traffic_src = measured_traffic(ATTN_KERNEL)
-        pmc, pmc_src = measured_pmc(ATTN_KERNEL)
-        mfma_busy = valu_per_mfma = None
-        if pmc:
-            # SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs); VALU per MFMA
-            mfma_busy = round(pmc["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * pmc["GRBM_GUI_ACTIVE"] / 8), 4)
-            valu_per_mfma = round(pmc["SQ_INSTS_VALU"] / pmc["SQ_INSTS_MFMA"], 3)  # VALU count includes the MFMAs
+        traffic, traffic_src = measured_traffic(ATTN_KERNEL, "fwd")
+        pmc, pmc_src = measured_pmc(ATTN_KERNEL, "fwd")
+        mfma_busy, valu_per_mfma = pmc_rates(pmc)
         if world == 1 and not a.no_cpu_baseline:
             shape_cfg = dict(cfg.as_shape_cfg(), num_attention_heads=cfg.num_attention_heads,
                              layer_norm_eps=cfg.layer_norm_eps)

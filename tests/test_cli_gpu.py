@@ -54,7 +54,7 @@ def test_vivit_main_trains_and_inference_predicts(dataset, tmp_path):
     log_dir, model_dir = tmp_path / "logs", tmp_path / "models"
     m, history, exp = run_main("vivit", ["--data_dir", str(dataset), "--log_dir", str(log_dir), "--model_dir",
                                          str(model_dir), "--epochs", "1", "--batch_size", "2",
-                                         "--train_sampling", "random_window"])
+                                         "--train_sampling", "random_window", "--num_workers", "2"])
     assert len(history["train_loss"]) == 1 and np.isfinite(history["train_loss"][0])
     metrics = json.load(open(exp / "test_metrics_uniform.json"))
     for k in ("accuracy", "confusion_matrix", "f1_score", "precision", "recall", "auroc"):
@@ -96,7 +96,7 @@ def test_eval_and_inference_clis(dataset, tmp_path, fam, extra):
     torch.save({"model_state_dict": model.state_dict(), "id2label": {0: "non-referral", 1: "referral"}}, ck_path)
     m, _, exp = run_main(fam, ["--data_dir", str(dataset), "--log_dir", str(tmp_path / "logs"), "--model_dir",
                                str(tmp_path / "models"), "--skip_train", "--checkpoint_path", str(ck_path),
-                               "--batch_size", "2"] + extra)
+                               "--batch_size", "2", "--num_workers", "0"] + extra)
     assert (exp / "test_metrics_uniform.json").exists() and 0.0 <= m["accuracy"] <= 1.0
     video = sorted((dataset / "test" / "referral").iterdir())[0]
     res = run_inference(fam, ["--video_path", str(video), "--model_path", str(ck_path), "--log_dir",
@@ -114,7 +114,8 @@ def test_vivit_main_skips_unreadable_clip(dataset, tmp_path):
     (root / "train" / "referral" / "zz_broken.npy").write_bytes(b"\x00 not a clip")
     from vclip_amd.apps import run_main
     m, history, exp = run_main("vivit", ["--data_dir", str(root), "--log_dir", str(tmp_path / "logs"), "--model_dir",
-                                         str(tmp_path / "models"), "--epochs", "1", "--batch_size", "2"])
+                                         str(tmp_path / "models"), "--epochs", "1", "--batch_size", "2",
+                                         "--num_workers", "0"])
     assert len(history["train_loss"]) == 1 and np.isfinite(history["train_loss"][0])
     log = "".join(p.read_text() for p in Path(exp).rglob("*.log"))
     assert "zz_broken.npy" in log
@@ -126,7 +127,7 @@ def test_timesformer_main_trains(dataset, tmp_path):
     from vclip_amd.apps import run_main
     m, history, exp = run_main("timesformer", ["--data_dir", str(dataset), "--log_dir", str(tmp_path / "logs"),
                                                "--model_dir", str(tmp_path / "models"), "--epochs", "1",
-                                               "--batch_size", "2", "--num_frames", "8"])
+                                               "--batch_size", "2", "--num_frames", "8", "--num_workers", "0"])
     assert len(history["train_loss"]) == 1 and np.isfinite(history["train_loss"][0])
     assert (exp / "test_metrics_uniform.json").exists()
     ck = torch.load(tmp_path / "models" / "best_model_uniform.pth", weights_only=True)
@@ -139,7 +140,7 @@ def test_swin_main_trains(dataset, tmp_path):
     from vclip_amd.apps import run_main
     m, history, exp = run_main("swin", ["--data_dir", str(dataset), "--log_dir", str(tmp_path / "logs"),
                                         "--model_dir", str(tmp_path / "models"), "--epochs", "1", "--batch_size", "2",
-                                        "--num_frames", "8", "--model_size", "tiny"])
+                                        "--num_frames", "8", "--model_size", "tiny", "--num_workers", "0"])
     assert len(history["train_loss"]) == 1 and np.isfinite(history["train_loss"][0])
     assert (exp / "test_metrics_uniform.json").exists()
     ck = torch.load(tmp_path / "models" / "best_model_uniform.pth", weights_only=True)
@@ -154,9 +155,12 @@ def test_resnet3d_main_trains(dataset, tmp_path):
     from vclip_amd.apps import run_main
     m, history, exp = run_main("resnet3d", ["--data_dir", str(dataset), "--log_dir", str(tmp_path / "logs"),
                                             "--model_dir", str(tmp_path / "models"), "--epochs", "1",
-                                            "--batch_size", "2"])
+                                            "--batch_size", "2", "--num_workers", "0"])
     assert len(history["train_loss"]) == 1 and np.isfinite(history["train_loss"][0])
     assert (exp / "test_metrics_uniform.json").exists()
+    # the reference's sampled-index CSVs, one per split (resnet50-3d-video/main.py:94-97, dataset.py:245-289)
+    for split in ("train", "val", "test"):
+        assert (exp / f"sampled_frames_{split}_uniform.csv").exists()
     ck = torch.load(tmp_path / "models" / "best_model_uniform.pth", weights_only=True)
     assert {"epoch", "model_state_dict", "optimizer_state_dict", "val_loss", "val_acc", "history"} <= set(ck)
     assert "blocks.1.res_blocks.0.branch2.norm_a.running_var" in ck["model_state_dict"]

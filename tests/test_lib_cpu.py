@@ -48,8 +48,10 @@ def test_ops_reject_cpu_tensors():
 
 def test_bench_cites_only_same_build_profiles(tmp_path, monkeypatch):
     """bench.py's roofline traffic / PMC numbers come from the newest profiles/ summary measured on
-    THIS build (vclip_amd.build.source_hash): r01_v10 beats r01_v7 (natural order), a newer summary
-    of another build is ignored, and with none of this build the line says so instead of citing one."""
+    THIS build (vclip_amd.build.source_hash) AND on the benchmarked workload (its "mode"): r01_v10
+    beats r01_v7 (natural order), a newer summary of another build or of another mode is ignored,
+    two same-build same-mode summaries that tie on their numbers cite nothing (the round-2 line
+    cited TimeSformer counters for ViViT that way), and with none of this build the line says so."""
     import json as _json
     import bench
     prof = tmp_path / "profiles"
@@ -57,13 +59,21 @@ def test_bench_cites_only_same_build_profiles(tmp_path, monkeypatch):
     me = bench._build_id()
     k = {"kernels": {"attn_fwd_d64_kernel": {"hbm_bytes_per_launch": 1.0}}}
     for n in ("r01_v7_traffic.json", "r01_v10_traffic.json", "r01_v9_traffic.json"):
-        (prof / n).write_text(_json.dumps(dict(k, build=me)))
-    (prof / "r03_v1_traffic.json").write_text(_json.dumps(dict(k, build="another-build")))
+        (prof / n).write_text(_json.dumps(dict(k, build=me, mode="fwd")))
+    (prof / "r03_v1_traffic.json").write_text(_json.dumps(dict(k, build="another-build", mode="fwd")))
+    (prof / "r03_v2_timesformer_traffic.json").write_text(_json.dumps(dict(k, build=me, mode="timesformer")))
     monkeypatch.setattr(bench, "ROOT", str(tmp_path))
-    assert bench._same_build("r*_traffic.json")[0].endswith("r01_v10_traffic.json")
-    (prof / "r02_v1_traffic.json").write_text(_json.dumps(dict(k, build=me)))
+    assert bench._same_build("r*_traffic.json", "fwd")[0].endswith("r01_v10_traffic.json")
+    assert bench._same_build("r*_traffic.json", "timesformer")[0].endswith("r03_v2_timesformer_traffic.json")
+    (prof / "r02_v1_traffic.json").write_text(_json.dumps(dict(k, build=me, mode="fwd")))
     assert bench.measured_traffic("attn_fwd_d64_kernel") == (1.0, "profiles/r02_v1_traffic.json")
-    assert bench._same_build("r*_nothing.json") == (None, None)
+    assert bench.measured_traffic(["attn_fwd_d64_kernel"] * 2) == (2.0, "profiles/r02_v1_traffic.json")
+    assert bench.measured_traffic("other_kernel")[0] is None
+    # a tie between two same-build same-mode files: nothing is cited
+    (prof / "r02_v1_copy_traffic.json").write_text(_json.dumps(dict(k, build=me, mode="fwd")))
+    v, why = bench.measured_traffic("attn_fwd_d64_kernel")
+    assert v is None and why.startswith("ambiguous")
+    assert bench._same_build("r*_nothing.json", "fwd")[0] is None
     for n in list(prof.iterdir()):
         if "another" not in n.read_text():
             n.unlink()

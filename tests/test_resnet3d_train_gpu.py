@@ -267,3 +267,23 @@ def test_reference_training_loop_with_adam():
         ev = model(video.to(DEV)).cpu()
         rv = ref.resnet3d_forward({k: v.cpu() for k, v in model.state_dict().items()}, SMALL, video)
     np.testing.assert_allclose(ev.numpy(), rv.numpy(), rtol=0, atol=2e-2)
+
+
+def test_train_mode_forward_under_no_grad_keeps_train_semantics():
+    """A train-mode forward under torch.no_grad runs the train step's forward as pytorchvideo does:
+    batch-statistic BatchNorm (same logits as the grad-enabled forward) and updated running
+    statistics; eval mode then runs the folded inference path on those statistics."""
+    model, sd, video, labels = _setup(SMALL, 2, 4, 64)
+    x = video.to(DEV)
+    name = "blocks.1.res_blocks.0.branch2.norm_a.running_mean"
+    rm0 = model.state_dict()[name].clone()
+    with torch.no_grad():
+        lo_ng = model(x)
+    rm1 = model.state_dict()[name].clone()
+    assert not torch.equal(rm0, rm1)  # running statistics moved
+    lo_g = model(x)  # grad-enabled train forward on the same weights: batch statistics again
+    torch.testing.assert_close(lo_ng, lo_g.detach(), rtol=0, atol=0)
+    model.eval()
+    with torch.no_grad():
+        lo_eval = model(x)
+    assert not torch.allclose(lo_eval, lo_ng)  # running vs batch statistics

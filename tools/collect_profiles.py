@@ -48,12 +48,23 @@ def per_kernel(d):
             for k, cs in acc.items()}
 
 
+def bench_mode(command: str) -> str:
+    """bench.py's --mode in a command line ("fwd" when absent): the workload a summary measured."""
+    m = re.search(r"--mode[= ](\w+)", command)
+    return m.group(1) if m else "fwd"
+
+
 def main():
     tag = sys.argv[1]
     src = os.path.join(ROOT, "gpurun_out", tag)
     dst = os.path.join(ROOT, "profiles")
     bench = json.loads(open(os.path.join(src, "bench.json")).read())
     build = bench.get("build")
+    cf = os.path.join(src, "pmc_command.txt")
+    if not os.path.exists(cf):
+        raise SystemExit(f"{cf} missing: profile with tools/profile_round.sh, which records the command")
+    command = open(cf).read().strip()
+    mode = bench_mode(command)
     with open(os.path.join(dst, f"{tag}_bench.json"), "w") as f:
         json.dump(bench, f, indent=1)
     stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
@@ -61,7 +72,7 @@ def main():
         shutil.copy(stats[0], os.path.join(dst, f"{tag}_kernel_stats.csv"))
     fe, wr = per_kernel(os.path.join(src, "pmc_FETCH_SIZE")), per_kernel(os.path.join(src, "pmc_WRITE_SIZE"))
     if fe and wr:
-        out = {"build": build, "command": "python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline",
+        out = {"build": build, "mode": mode, "command": command,
                "correction": "FETCH_SIZE x2 (gfx950 half-count), counters in KiB", "kernels": {}}
         for k in sorted(set(fe) | set(wr)):
             fb = 2.0 * 1024.0 * fe.get(k, {}).get("FETCH_SIZE", 0.0)
@@ -78,11 +89,11 @@ def main():
             for k, cs in per_kernel(g).items():
                 merged[k].update(cs)
         with open(os.path.join(dst, f"{tag}_pmc.json"), "w") as f:
-            json.dump({"build": build, "command": "python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline",
+            json.dump({"build": build, "mode": mode, "command": command,
                        "note": "per-dispatch means; SQ_* cycle counters in quad-cycles except "
                                "SQ_VALU_MFMA_BUSY_CYCLES; GRBM_GUI_ACTIVE summed over 8 XCDs",
                        "kernels": merged}, f, indent=1)
-    print(f"collected {tag} (build {build}) into profiles/")
+    print(f"collected {tag} (build {build}, mode {mode}) into profiles/")
 
 
 if __name__ == "__main__":

@@ -2,6 +2,27 @@
 // per-frame global average pool of the ResNet-50 features, the LSTM recurrence (the input
 // projections of all T steps run before it as one MFMA GEMM) and the 256 -> 64 -> 1 head.
 #include "common.hpp"
+#include "lstm.h"
+
+// Out-of-scope experiment (the ResNet50-LSTM is BASELINE configs[0], a CPU
+// reference path): built by tools/lstm_gpu/build.py into tools/lstm_gpu/liblstm.so, NOT part of
+// libvclip.so.  It carries its own copy of the error helpers common.hpp declares.
+namespace vc {
+static thread_local std::string g_lstm_err;
+void set_error(const std::string& msg) { g_lstm_err = msg; }
+int fail(int code, const std::string& msg) {
+    g_lstm_err = msg;
+    return code;
+}
+int check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        g_lstm_err = std::string(what) + ": " + hipGetErrorString(e);
+        return (int)e;
+    }
+    return 0;
+}
+}  // namespace vc
 
 namespace vc {
 
@@ -114,5 +135,7 @@ int vc_mlp_head(const float* h, int64_t B, int64_t hidden, const float* W1, cons
     mlp_head_kernel<<<(unsigned)B, 256, 0, stream>>>(h, (int)hidden, W1, b1, (int)H1, W2, b2, (int)num_labels, logits);
     return check_launch("vc_mlp_head");
 }
+
+const char* lstm_last_error(void) { return vc::g_lstm_err.c_str(); }
 
 }  // extern "C"

@@ -14,6 +14,9 @@ echo "== bench"
 timeout -k 10 300 python3 bench.py --steps $STEPS $BENCH_ARGS > $OUT/bench.log 2>&1
 rc=$?; tail -c 600 $OUT/bench.log; echo; [ $rc -eq 0 ] || exit $rc
 grep '^{' $OUT/bench.log | tail -1 > $OUT/bench.json
+# the profiled command, recorded beside its outputs (tools/collect_profiles.py stamps it and the
+# bench mode on every summary: bench.py cites only counters of its own build AND mode)
+echo "python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline $BENCH_ARGS" > $OUT/pmc_command.txt
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 echo "== kernel trace"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- \
