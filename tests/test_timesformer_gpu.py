@@ -140,6 +140,23 @@ def test_timesformer_b_full_logits():
     assert err < 1e-2, (err, lg, g["logits"])
 
 
+def test_timesformer_b_batch16_logits_configs2():
+    """BASELINE configs[2] at its own workload: TimeSformer-B 8x224^2, batch 16, against transformers'
+    TimesformerForVideoClassification at batch 16 (tests/golden/timesformer_b16.json), bf16 bar 1e-2."""
+    with open(os.path.join(GD, "timesformer_b16.json")) as f:
+        g = json.load(f)
+    cfg = g["config"]
+    m = _model(cfg)
+    pix = torch.from_numpy(make_synthetic_clips(g["batch"], cfg["num_frames"], cfg["image_size"],
+                                                seed=g["input_seed"])).cuda()
+    lg = m(pixel_values=pix).logits.cpu().numpy()
+    lf = m.forward_logits(pix).cpu().numpy()  # bench.py --mode timesformer's call
+    ref = np.array(g["logits"])
+    errs = (float(np.abs(lg - ref).max()), float(np.abs(lf - ref).max()))
+    print("TimeSformer-B B=16 max |logit - HF golden| (model(), forward_logits):", errs)
+    assert max(errs) < 1e-2, (errs, lg, ref)
+
+
 def test_timesformer_batch_invariance():
     with open(os.path.join(GD, "timesformer_full.json")) as f:
         cfg = json.load(f)["config"]

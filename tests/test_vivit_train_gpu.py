@@ -153,3 +153,65 @@ def test_train_step_deterministic():
         torch.nn.functional.cross_entropy(model(pixel_values=x).logits, y).backward()
         gs.append(model._gflat.clone())
     assert torch.equal(gs[0], gs[1])
+
+
+# BASELINE configs[4]'s own geometry: ViViT-B/16x2 (12 layers, S = 3137, D = 768, 12 heads), 32x224^2,
+# 4 clips per GPU (the reference CLI's --batch_size 4, vivit_transformer/main.py:47)
+VIVIT_B = dict(WIDE, num_hidden_layers=12)
+
+
+def _oracle_on(dev, sd, cfg, pix, labels):
+    """The fp32 oracle's autograd step, run by torch on `dev`.  At configs[4]'s size the eager
+    attention keeps [4, 12, 3137, 3137] fp32 scores per layer for the backward (~70 GB), so the
+    oracle runs on the GPU (torch fp32 ops: hipBLASLt fp32 GEMMs, no reduced-precision mode on gfx950)."""
+    from oracle.vivit_ref import vivit_forward
+    ref = {k: torch.from_numpy(v).to(dev).requires_grad_() for k, v in sd.items()}
+    logits = vivit_forward(ref, cfg, pix.to(dev))
+    loss = torch.nn.functional.cross_entropy(logits, labels.to(dev))
+    loss.backward()
+    return float(loss), logits.detach().cpu(), {k: v.grad.cpu() for k, v in ref.items()}, ref
+
+
+def test_train_step_configs4_geometry():
+    """BASELINE configs[4] at its own workload (12 layers, 32x224^2, B = 4): logits <= 1e-2, loss, and
+    every parameter's gradient (rel L2 <= 5e-2, cos >= 0.998; classifier, final LN, layers 11 .. 0 and
+    the embeddings) against the fp32 oracle's autograd on the same weights and clips; then a 3-step
+    AdamW(lr 1e-3, wd 0.01) loss trajectory against torch AdamW on the oracle.  Anchors:
+    vivit_transformer/vivit_classifier/trainers/trainer.py:140-146, TF5 modeling_vivit.py:462-566."""
+    from oracle.vivit_ref import vivit_forward
+    from vclip_amd.optim import AdamW
+    cfg, B = VIVIT_B, 4
+    model, sd, pix, labels = _setup(cfg, B)
+    x, y = pix.to(DEV), labels.to(DEV)
+    out = model(pixel_values=x)
+    loss = torch.nn.functional.cross_entropy(out.logits, y)
+    loss.backward()
+    ref_loss, ref_logits, ref_grads, ref = _oracle_on(DEV, sd, cfg, pix, labels)
+    lerr = float((out.logits.detach().cpu() - ref_logits).abs().max())
+    print(f"configs[4] geometry: logits max err {lerr:.3e}, loss {float(loss):.6f} vs {ref_loss:.6f}")
+    assert lerr < 1e-2 and abs(float(loss) - ref_loss) < 1e-2
+    worst = _compare(model, ref_grads)
+    print("worst gradient (rel L2, name, cos):", worst)
+    for n in ("classifier.weight", "vivit.layernorm.weight", "vivit.layers.11.mlp.fc2.weight",
+              "vivit.layers.0.attention.q_proj.weight", "vivit.embeddings.patch_embeddings.projection.weight",
+              "vivit.embeddings.position_embeddings", "vivit.embeddings.cls_token"):
+        assert n in ref_grads, n
+    # three steps of the reference loop on both sides (step 1's gradients are the ones checked above)
+    opt = AdamW(model.parameters(), lr=1e-3, weight_decay=0.01)
+    ropt = torch.optim.AdamW(list(ref.values()), lr=1e-3, weight_decay=0.01)
+    losses, rlosses = [float(loss)], [ref_loss]
+    opt.step()
+    ropt.step()
+    for _ in range(2):
+        opt.zero_grad()
+        ls = torch.nn.functional.cross_entropy(model(pixel_values=x).logits, y)
+        ls.backward()
+        opt.step()
+        losses.append(float(ls))
+        ropt.zero_grad()
+        rl = torch.nn.functional.cross_entropy(vivit_forward(ref, cfg, x), y)
+        rl.backward()
+        ropt.step()
+        rlosses.append(float(rl))
+    print("configs[4] AdamW loss trajectory (HIP, oracle):", losses, rlosses)
+    np.testing.assert_allclose(losses, rlosses, rtol=0, atol=2e-2)

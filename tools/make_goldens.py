@@ -343,10 +343,25 @@ def gen_timesformer(skip_full):
     print("timesformer_full logits", r["logits"])
 
 
+def gen_baseline_batches():
+    for name, fn, cfg, b in (("vivit_b8.json", _vivit_golden, VIVIT_B, 8),
+                             ("timesformer_b16.json", _timesformer_golden, TSF_B, 16)):
+        r = fn(cfg, batch=b, wseed=0, xseed=1, full=True)
+        model = "VivitForVideoClassification (eager attention)" if fn is _vivit_golden else \
+            "TimesformerForVideoClassification"
+        with open(os.path.join(GOLDEN, name), "w") as f:
+            json.dump({"config": cfg, "batch": b, "weights_seed": 0, "input_seed": 1,
+                       "logits": r["logits"].tolist(), "weights_sha256": r["weights_sha256"],
+                       "pixel_sha256": r["pixel_sha256"],
+                       "baseline_config": "configs[1]" if fn is _vivit_golden else "configs[2]",
+                       "oracle": f"transformers {model}, fp32 CPU"}, f, indent=1)
+        print(name, r["logits"])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-full", action="store_true")
-    ap.add_argument("--only", choices=["sampling", "vivit", "timesformer"], default=None)
+    ap.add_argument("--only", choices=["sampling", "vivit", "timesformer", "baseline_batches"], default=None)
     a = ap.parse_args()
     os.makedirs(GOLDEN, exist_ok=True)
     if a.only in (None, "sampling"):
@@ -355,6 +370,8 @@ def main():
         gen_vivit(a.skip_full)
     if a.only in (None, "timesformer"):
         gen_timesformer(a.skip_full)
+    if a.only == "baseline_batches" or (a.only is None and not a.skip_full):
+        gen_baseline_batches()  # BASELINE configs[1] / configs[2] at their own batch sizes
 
 
 if __name__ == "__main__":
