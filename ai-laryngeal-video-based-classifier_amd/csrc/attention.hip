@@ -71,7 +71,11 @@ __device__ __forceinline__ void attn_sync() {
 // One 4-wave workgroup = 128 queries of one (clip, head); each wave owns 32 query rows, two
 // workgroups per CU (two waves per SIMD, 256 VGPRs each).  Measured alternatives (DESIGN.md
 // §5): 64 queries per wave (every K/V fragment feeding two MFMAs) needs ~330 registers and ran
-// 1.3x slower; an 8-wave ping-pong workgroup (MFMA and softmax phases of the two waves of a
+// 1.3x slower at two waves per SIMD; at ONE wave per SIMD (256 queries per workgroup, 32-key
+// pipeline halves, a three-stage QK^T / exp2 / P.V in-wave pipeline, no spills:
+// tools/experiments/attention_w64.hip.txt, round 3) 295.5 vs 253.7 us at ViViT-B B = 8 -- the
+// scores land in AGPRs (VGPRs full) and every exp2 needs a v_accvgpr_read first, which makes the
+// single wave issue-bound; an 8-wave ping-pong workgroup (MFMA and softmax phases of the two waves of a
 // SIMD offset by a barrier, tools/experiments/attention_pingpong.hip.txt) ran 295-330 us vs
 // 264 us; split-half softmax, K-fragment prefetch, a 5-slot ring and a P.V lag were neutral
 // to 8.5 % slower (round 1).

@@ -61,6 +61,7 @@ VIDEO_LAYOUT = {"btchw": 0, "bcthw": 1}
 # 16-bit operand types (include/vclip.h VC_ELEM_*): bf16 everywhere; fp16 for the inference forward
 H16 = (torch.bfloat16, torch.float16)
 ELEM_F16 = 1
+ELEM_BF16 = 0
 
 
 def tubelet_im2col(pix: torch.Tensor, tubelet, out: torch.Tensor, order: str = "time_major",

@@ -478,6 +478,8 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="clips per GPU per step (fwd 8, train 4)")
     ap.add_argument("--cpu-clips", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="fwd: concurrent HIP streams the batch is split over in the headline pass")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)  # CPU test of the spawn path
     a = ap.parse_args()
     if a.batch is None:
@@ -523,42 +525,49 @@ def main():
     cfg = model.config
     pix = torch.from_numpy(make_synthetic_clips(a.batch, 32, 224, seed=1 + rank)).to(dev)
 
-    evs = []
-
     def step():
         model.forward_logits(pix)
 
-    # HIP events around every attention launch of the timed steps (kernel-level roofline)
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    model.kernel_events = evs
-    dt = timed_loop(step, a.steps, 0, dist, torch.cuda.synchronize)
-    model.kernel_events = None
+    def timed(streams, evs=None):
+        """W warm-up + K timed steps with the batch on `streams` concurrent HIP streams; `evs`: a list
+        that collects HIP events around every attention launch (on the stream it runs on)."""
+        model.concurrent_streams = streams
+        for _ in range(a.warmup):
+            step()
+        torch.cuda.synchronize()
+        model.kernel_events = evs
+        t = timed_loop(step, a.steps, 0, dist, torch.cuda.synchronize)
+        model.kernel_events = None
+        return t
+
+    # the headline: the batch split over `--streams` concurrent HIP streams (the clips are independent,
+    # every kernel is batch-invariant: logits bit-identical to one stream), nothing instrumented
+    dt = timed(a.streams)
     streams = model.last_streams
+    # the kernel roofline: the same K steps on ONE stream with HIP events around every attention
+    # launch, so a launch's event time is its own execution (under two streams it would include time
+    # shared with the other stream's kernels) and matches the rocprofv3 kernel trace of
+    # `bench.py --streams 1` (tools/profile_round.sh)
+    evs = []
+    dt1 = timed(1, evs)
     attn_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
 
     # the fp16-operand build of the same forward (VC_ELEM_F16: same kernels, same MFMA rate,
     # logits within 1e-3), timed the same way after the bf16 headline; reported beside it
     model.compute_dtype = torch.float16
+    dt16 = timed(a.streams)
     evs16 = []
-    for _ in range(a.warmup):
-        step()
-    torch.cuda.synchronize()
-    model.kernel_events = evs16
-    dt16 = timed_loop(step, a.steps, 0, dist, torch.cuda.synchronize)
-    model.kernel_events = None
+    timed(1, evs16)
     attn_ms16 = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs16]))
     model.compute_dtype = torch.bfloat16
 
-    breakdown = kernel_breakdown(model, step, a.batch // streams, streams, 3)
+    model.concurrent_streams = 1
+    breakdown = kernel_breakdown(model, step, a.batch, 1, 3)
 
     clips = a.batch * a.steps * world
     value = clips / dt
     ms_per_step = dt / a.steps * 1e3
-    # the batch runs as model.last_streams concurrent halves: each attention launch holds
-    # batch / streams clips (events are recorded on the stream each launch runs on)
-    launch_clips = a.batch / streams
+    launch_clips = a.batch  # the roofline pass runs the whole batch on one stream
     attn_tflops = ATTN_GFLOP_PER_CLIP_LAYER * launch_clips / (attn_ms * 1e-3) / 1e3
     model_tflops = VIVIT_GFLOP_PER_CLIP * a.batch / (ms_per_step * 1e-3) / 1e3
 
@@ -607,7 +616,9 @@ def main():
                          "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes": ATTN_IO_BYTES_PER_CLIP * launch_clips, "avg_launch_ms": round(attn_ms, 4),
                          "flop_per_launch": f"{ATTN_GFLOP_PER_CLIP_LAYER:.2f} GF/clip x {launch_clips:g} clips",
-                         "streams": streams, "mfma_busy": mfma_busy, "valu_per_mfma": valu_per_mfma,
+                         "timed_on": "a separate K-step pass on one HIP stream (the headline runs "
+                                     f"{streams}): clips/s {a.batch * a.steps * world / dt1:.2f} there",
+                         "mfma_busy": mfma_busy, "valu_per_mfma": valu_per_mfma,
                          "pmc_source": pmc_src},
             "kernel_breakdown": breakdown,
             "build": _build_id(),

@@ -190,12 +190,30 @@ def test_train_step_configs4_geometry():
     lerr = float((out.logits.detach().cpu() - ref_logits).abs().max())
     print(f"configs[4] geometry: logits max err {lerr:.3e}, loss {float(loss):.6f} vs {ref_loss:.6f}")
     assert lerr < 1e-2 and abs(float(loss) - ref_loss) < 1e-2
-    worst = _compare(model, ref_grads)
-    print("worst gradient (rel L2, name, cos):", worst)
-    for n in ("classifier.weight", "vivit.layernorm.weight", "vivit.layers.11.mlp.fc2.weight",
-              "vivit.layers.0.attention.q_proj.weight", "vivit.embeddings.patch_embeddings.projection.weight",
-              "vivit.embeddings.position_embeddings", "vivit.embeddings.cls_token"):
-        assert n in ref_grads, n
+    # the verdict's named tensors at rel L2 <= 5e-2: the classifier, the final LN, layers 11 and 0 and
+    # the embeddings; every other tensor at <= 1e-1 / cos >= 0.995 (12 layers of bf16 operands: the
+    # q / k projections of the middle layers, whose gradients pass through dS = P o (dP - Delta),
+    # land at 5-6e-2)
+    named = {"classifier.weight", "classifier.bias", "vivit.layernorm.weight", "vivit.layernorm.bias",
+             "vivit.embeddings.patch_embeddings.projection.weight", "vivit.embeddings.patch_embeddings.projection.bias",
+             "vivit.embeddings.position_embeddings", "vivit.embeddings.cls_token"}
+    named |= {n for n in ref_grads if n.startswith(("vivit.layers.11.", "vivit.layers.0."))}
+    errs = []
+    for n, p in model.hf_state_dict().items():
+        if n.endswith("k_proj.bias"):
+            continue  # exact gradient 0 (softmax is invariant to a key bias): rounding noise on both sides
+        g = p.grad.detach().cpu().double().reshape(-1)
+        r = ref_grads[n].double().reshape(-1)
+        l2 = float((g - r).norm() / r.norm())
+        cos = float(g @ r / (g.norm() * r.norm()))
+        errs.append((l2, n, cos))
+        if n in named:
+            assert l2 < 5e-2 and cos > 0.998, (n, l2, cos)
+        else:
+            assert l2 < 1e-1 and cos > 0.995, (n, l2, cos)
+    errs.sort(reverse=True)
+    print("worst gradients (rel L2, name, cos):", errs[:6])
+    print("named tensors, worst:", max(e for e in errs if e[1] in named))
     # three steps of the reference loop on both sides (step 1's gradients are the ones checked above)
     opt = AdamW(model.parameters(), lr=1e-3, weight_decay=0.01)
     ropt = torch.optim.AdamW(list(ref.values()), lr=1e-3, weight_decay=0.01)
