@@ -515,6 +515,11 @@ static void launch_attn(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, i
                                                                                    out, ldo, lse);
 }
 
+// attention_short.hip: one workgroup per (sequence, head) with all keys in LDS, for S <= 256
+int launch_attn_short(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, float c_log2, uint16_t* out,
+                      int64_t ldo, int elem, hipStream_t stream);
+constexpr int64_t SHORT_MAX_S = 256;
+
 }  // namespace vc
 
 using namespace vc;
@@ -535,6 +540,7 @@ extern "C" int vc_attention_fwd(const uint16_t* qkv, int64_t ld, int64_t B, int6
                                 float scale, int q_prescaled, uint16_t* out, int64_t ldo, hipStream_t stream) {
     if (int rc = attn_checks(qkv, ld, B, S, H, head_dim, out, ldo)) return rc;
     const float c_log2 = q_prescaled ? 1.0f : scale * 1.4426950408889634f;
+    if (S <= SHORT_MAX_S) return launch_attn_short(qkv, ld, B, S, H, c_log2, out, ldo, VC_ELEM_BF16, stream);
     launch_attn<false, false>(qkv, ld, B, S, H, c_log2, out, ldo, stream);
     return check_launch("vc_attention_fwd");
 }
@@ -546,6 +552,8 @@ extern "C" int vc_attention_fwd_h16(const uint16_t* qkv, int64_t ld, int64_t B, 
                                     int64_t ldo, hipStream_t stream) {
     if (int rc = attn_checks(qkv, ld, B, S, H, head_dim, out, ldo)) return rc;
     const float c_log2 = q_prescaled ? 1.0f : scale * 1.4426950408889634f;
+    if (S <= SHORT_MAX_S && (elem == VC_ELEM_F16 || elem == VC_ELEM_BF16))
+        return launch_attn_short(qkv, ld, B, S, H, c_log2, out, ldo, elem, stream);
     if (elem == VC_ELEM_F16) launch_attn<false, false, VC_ELEM_F16>(qkv, ld, B, S, H, c_log2, out, ldo, stream);
     else if (elem == VC_ELEM_BF16) launch_attn<false, false>(qkv, ld, B, S, H, c_log2, out, ldo, stream);
     else return fail(VC_ERR_INVALID_ARG, "vc_attention_fwd_h16: bad elem");

@@ -1,0 +1,246 @@
+// Short-sequence attention forward (S <= 256 tokens, head_dim 64): TimeSformer's spatial branch,
+// B*T sequences of 1 + 196 tokens per head (TF5/models/timesformer/modeling_timesformer.py:148-180,
+// the spatial half of the divided layer :332-398).
+//
+// The long-sequence kernel (attention.hip) streams 64-key tiles with an online softmax; at S = 197 it
+// runs two 128-query workgroups per (sequence, head), each re-reading the sequence's K/V, four key
+// tiles of which the last is 5/64 full, the running-max machinery for four tiles, and a second
+// workgroup with one dead wave.  Here ONE 4-wave workgroup owns a (sequence, head):
+//   * the whole K and V of the sequence (S rounded up to 32 keys: 224 at S = 197, 56 KiB) are staged
+//     into LDS once by LDS-DMA (K image XOR-swizzled for ds_read_b128, V for ds_read_b64_tr_b16, the
+//     long kernel's images);
+//   * the sequence's ceil(S / 32) query blocks of 32 are dealt round-robin over the 4 waves (7 blocks
+//     at S = 197: waves 0-2 take two, wave 3 one);
+//   * per query block: S'^T = K . Q'^T over all keys in registers (swapped QK^T: a query's scores in
+//     one lane column), the EXACT row max once (no re-basing, P <= 1 at any score magnitude), P =
+//     exp2(S' - m) packed to 16 bits straight from the accumulators as the B operand of
+//     O^T = V^T . P^T, the row sum on the matrix pipe (P^T times a 0/1 selector, as attention.hip),
+//     then 16-byte output stores;
+//   * two workgroups per CU (56 KiB of LDS and <= 256 registers each): the two waves on a SIMD come
+//     from different workgroups and overlap one's exponentials with the other's MFMAs.
+#include "common.hpp"
+
+namespace vc {
+namespace ashort {
+
+constexpr int MAXS = 256;                   // longest sequence
+constexpr int ROWB = 128;                   // bytes per K / V row (64 x 16 bit)
+
+__device__ __forceinline__ int kswz(int r, int c) { return c ^ ((r >> 1) & 7); }
+__device__ __forceinline__ int vswz(int r, int c) { return c ^ (((r >> 1) & 1) << 2); }
+
+__device__ __forceinline__ void adma16s(const void* sbase, uint32_t voff, uint32_t lds_addr) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+                 :
+                 : "v"(voff), "s"(sbase), "s"(lds_addr)
+                 : "memory", "m0");
+}
+
+// NKB: 32-key blocks staged and computed (ceil(S / 32), compile time so the score array stays in
+// registers); S: real keys (masked beyond).
+template <int ET, int NKB>
+__global__ void __launch_bounds__(256, 2)
+attn_short_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, float c_log2,
+                      uint16_t* __restrict__ out, int64_t ldo) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int NROW = NKB * 32;
+    char* ktile = smem;
+    char* vtile = smem + NROW * ROWB;
+
+    const int bh = blockIdx.x;
+    const int b = bh / H, hh = bh % H;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, h = lane >> 5;
+
+    const int64_t tok0 = (int64_t)b * S;
+    const uint16_t* qbase = qkv + hh * 64;
+    const uint16_t* kbase = qkv + (int64_t)H * 64 + hh * 64 + tok0 * ld;
+    const uint16_t* vbase = qkv + (int64_t)2 * H * 64 + hh * 64 + tok0 * ld;
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem);
+
+    // ---- stage all NROW rows of K and V: piece p = rows 8p .. 8p+7 (1 KiB), wave w takes p = w, w+4, ..
+    {
+        const int spc = lane & 7;
+#pragma unroll
+        for (int p = wave; p < NROW / 8; p += 4) {
+            const int row = 8 * p + (lane >> 3);
+            const uint32_t ko = (uint32_t)(row * ld + kswz(row, spc) * 8) * 2;
+            const uint32_t vo = (uint32_t)(row * ld + vswz(row, spc) * 8) * 2;
+            adma16s(kbase, ko, __builtin_amdgcn_readfirstlane(lds0 + p * 8 * ROWB));
+            adma16s(vbase, vo, __builtin_amdgcn_readfirstlane(lds0 + NROW * ROWB + p * 8 * ROWB));
+        }
+    }
+
+    // per-lane constant LDS offsets: K row reads (key block 0; block kb at + 32 kb rows) and the
+    // V^T transpose reads of d-block db
+    int koff[4];
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) koff[kk] = r * ROWB + kswz(r, kk * 2 + h) * 16;
+    int voff[2];
+    {
+        const int gi = lane & 15;
+        const int tq = gi >> 2, tp = gi & 3;
+        const int gcol = ((lane >> 4) & 1) * 16 + tp * 4;
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+            const int col = db * 32 + gcol;
+            const int ra = 4 * h + tq;
+            voff[db] = ra * ROWB + vswz(ra, col >> 3) * 16 + (col & 7) * 2;
+        }
+    }
+    v8s sel;
+    {
+        const short one = ET == VC_ELEM_F16 ? (short)0x3C00 : (short)0x3F80;
+        const short v = (((lane >> 4) & 1) == ((lane & 15) >> 3)) ? one : (short)0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sel[j] = v;
+    }
+
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's pieces landed
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();        // ... and every other wave's
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+
+    const int nqb = (S + 31) / 32;
+    for (int qbk = wave; qbk < nqb; qbk += 4) {
+        // Q'^T fragments of this block (query rows past S clamp to S - 1; not stored)
+        const int q = qbk * 32 + r;
+        const int qc = q < S ? q : S - 1;
+        v8s qf[4];
+        {
+            const uint16_t* qrow = qbase + (tok0 + qc) * ld + 8 * h;
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const v8s raw = *reinterpret_cast<const v8s*>(qrow + 16 * kk);
+                if (c_log2 == 1.0f) {
+                    qf[kk] = raw;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) qf[kk][j] = (short)to16<ET>(from16<ET>((unsigned short)raw[j]) * c_log2);
+                }
+            }
+        }
+        // S'^T over all NKB key blocks
+        v16f sc[NKB];
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb) {
+            v16f acc = v16f{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) {
+                const v8s kf = *reinterpret_cast<const v8s*>(ktile + kb * 32 * ROWB + koff[kk]);
+                acc = mfma32x16<ET>(kf, qf[kk], acc);
+            }
+            sc[kb] = acc;
+            // one key block's K reads in flight at a time (hoisting all of them costs 4 registers per
+            // read on top of the 16 per block of scores, and spilled)
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // keys past S (the last block only) -> -inf; exact row max over all keys of this query
+        if (NKB * 32 > S) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int key = (NKB - 1) * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                if (key >= S) sc[NKB - 1][e] = -INFINITY;
+            }
+        }
+        float m0 = sc[0][0], m1 = sc[0][1];
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int e = (kb == 0 ? 2 : 0); e < 16; e += 2) {
+                m0 = fmaxf(m0, sc[kb][e]);
+                m1 = fmaxf(m1, sc[kb][e + 1]);
+            }
+        float m = fmaxf(m0, m1);
+        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        // O^T += V^T . P^T block by block; P = exp2(S' - m) <= 1 packed from the accumulators
+        v16f o[2];
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+            o[db] = v16f{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        v4f lsum = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kb = 0; kb < NKB; ++kb)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                v4u pu;
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj)
+                    pu[jj] = pack2<ET>(__builtin_amdgcn_exp2f(sc[kb][8 * s2 + 2 * jj] - m),
+                                       __builtin_amdgcn_exp2f(sc[kb][8 * s2 + 2 * jj + 1] - m));
+                const v8s pf = __builtin_bit_cast(v8s, pu);
+#pragma unroll
+                for (int db = 0; db < 2; ++db) {
+                    const char* pa = vtile + voff[db] + (kb * 32 + 16 * s2) * ROWB;
+                    v4s va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)pa);
+                    v4s vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(pa + 8 * ROWB));
+                    v8s vv;
+                    vv[0] = va[0]; vv[1] = va[1]; vv[2] = va[2]; vv[3] = va[3];
+                    vv[4] = vb[0]; vv[5] = vb[1]; vv[6] = vb[2]; vv[7] = vb[3];
+                    o[db] = mfma32x16<ET>(vv, pf, o[db]);
+                }
+                lsum = mfma16x32<ET>(sel, pf, lsum);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        // query r's row sum sits in lane (r & 15) + 32 (r >> 4)
+        const float inv = 1.0f / __shfl(lsum[0], (r & 15) + ((r >> 4) << 5), 64);
+        unsigned pk[2][4][2];
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                pk[db][g][0] = pack2<ET>(o[db][4 * g + 0] * inv, o[db][4 * g + 1] * inv);
+                pk[db][g][1] = pack2<ET>(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv);
+            }
+        uint16_t* orow = out + (tok0 + qc) * ldo + hh * 64;
+#pragma unroll
+        for (int db = 0; db < 2; ++db)
+#pragma unroll
+            for (int g = 0; g < 4; g += 2) {
+                auto x0 = __builtin_amdgcn_permlane32_swap(pk[db][g][0], pk[db][g + 1][0], false, false);
+                auto x1 = __builtin_amdgcn_permlane32_swap(pk[db][g][1], pk[db][g + 1][1], false, false);
+                uint4 v;
+                v.x = x0[0]; v.y = x1[0]; v.z = x0[1]; v.w = x1[1];
+                if (q < S) *reinterpret_cast<uint4*>(orow + db * 32 + g * 8 + h * 8) = v;
+            }
+    }
+}
+
+template <int ET, int NKB>
+static int launch_nkb(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, float c_log2, uint16_t* out,
+                      int64_t ldo, hipStream_t stream) {
+    const int lds = 2 * NKB * 32 * ROWB;
+    attn_short_d64_kernel<ET, NKB><<<(unsigned)(B * H), 256, lds, stream>>>(qkv, ld, (int)S, (int)H, c_log2, out, ldo);
+    return 0;
+}
+
+template <int ET>
+static int launch_et(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, float c_log2, uint16_t* out,
+                     int64_t ldo, hipStream_t stream) {
+    switch ((S + 31) / 32) {
+        case 1: return launch_nkb<ET, 1>(qkv, ld, B, S, H, c_log2, out, ldo, stream);
+        case 2: return launch_nkb<ET, 2>(qkv, ld, B, S, H, c_log2, out, ldo, stream);
+        case 3: return launch_nkb<ET, 3>(qkv, ld, B, S, H, c_log2, out, ldo, stream);
+        case 4: return launch_nkb<ET, 4>(qkv, ld, B, S, H, c_log2, out, ldo, stream);
+        case 5: return launch_nkb<ET, 5>(qkv, ld, B, S, H, c_log2, out, ldo, stream);
+        case 6: return launch_nkb<ET, 6>(qkv, ld, B, S, H, c_log2, out, ldo, stream);
+        case 7: return launch_nkb<ET, 7>(qkv, ld, B, S, H, c_log2, out, ldo, stream);
+        default: return launch_nkb<ET, 8>(qkv, ld, B, S, H, c_log2, out, ldo, stream);
+    }
+}
+
+}  // namespace ashort
+
+// attention.hip routes S <= 256 here (inference forward)
+int launch_attn_short(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, float c_log2, uint16_t* out,
+                      int64_t ldo, int elem, hipStream_t stream) {
+    if (S < 1 || S > ashort::MAXS) return fail(VC_ERR_INVALID_ARG, "attention (short): S must be in [1, 256]");
+    if (elem == VC_ELEM_F16) ashort::launch_et<VC_ELEM_F16>(qkv, ld, B, S, H, c_log2, out, ldo, stream);
+    else ashort::launch_et<VC_ELEM_BF16>(qkv, ld, B, S, H, c_log2, out, ldo, stream);
+    return check_launch("vc_attention_fwd (short)");
+}
+
+}  // namespace vc
