@@ -5,19 +5,20 @@
 // The long-sequence kernel (attention.hip) streams 64-key tiles with an online softmax; at S = 197 it
 // runs two 128-query workgroups per (sequence, head), each re-reading the sequence's K/V, four key
 // tiles of which the last is 5/64 full, the running-max machinery for four tiles, and a second
-// workgroup with one dead wave.  Here ONE 4-wave workgroup owns a (sequence, head):
+// workgroup with one dead wave.  Here ONE 8-wave workgroup owns a (sequence, head):
 //   * the whole K and V of the sequence (S rounded up to 32 keys: 224 at S = 197, 56 KiB) are staged
 //     into LDS once by LDS-DMA (K image XOR-swizzled for ds_read_b128, V for ds_read_b64_tr_b16, the
 //     long kernel's images);
-//   * the sequence's ceil(S / 32) query blocks of 32 are dealt round-robin over the 4 waves (7 blocks
-//     at S = 197: waves 0-2 take two, wave 3 one);
-//   * per query block: S'^T = K . Q'^T over all keys in registers (swapped QK^T: a query's scores in
-//     one lane column), the EXACT row max once (no re-basing, P <= 1 at any score magnitude), P =
-//     exp2(S' - m) packed to 16 bits straight from the accumulators as the B operand of
-//     O^T = V^T . P^T, the row sum on the matrix pipe (P^T times a 0/1 selector, as attention.hip),
-//     then 16-byte output stores;
-//   * two workgroups per CU (56 KiB of LDS and <= 256 registers each): the two waves on a SIMD come
-//     from different workgroups and overlap one's exponentials with the other's MFMAs.
+//   * the sequence's ceil(S / 32) query blocks of 32 are dealt round-robin over 8 waves (7 blocks at
+//     S = 197: one each), whose Q fragments load while K / V stage;
+//   * per query block, 32 keys at a time: S'^T = K . Q'^T (swapped QK^T: a query's scores in one lane
+//     column), P = exp2(S') packed to 16 bits straight from the accumulators as the B operand of
+//     O^T = V^T . P^T, the row sum on the matrix pipe (P^T times a 0/1 selector, as attention.hip);
+//     no running max at all (exp2 is exact in relative terms until it overflows): a row sum outside
+//     [2^-64, 2^64] makes the wave repeat the block against the exact row max; the QK^T of the next
+//     32 keys overlaps the current block's exponentials; 16-byte output stores;
+//   * two workgroups per CU (56 KiB of LDS and <= 128 registers each): four waves per SIMD from two
+//     workgroups overlap one's exponentials with another's MFMAs.
 #include "common.hpp"
 
 namespace vc {
@@ -38,8 +39,10 @@ __device__ __forceinline__ void adma16s(const void* sbase, uint32_t voff, uint32
 
 // NKB: 32-key blocks staged and computed (ceil(S / 32), compile time so the score array stays in
 // registers); S: real keys (masked beyond).
+constexpr int NW = 8;  // waves per workgroup
+
 template <int ET, int NKB>
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(NW * 64, 2 * NW / 4)
 attn_short_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, float c_log2,
                       uint16_t* __restrict__ out, int64_t ldo) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -60,11 +63,24 @@ attn_short_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem);
 
-    // ---- stage all NROW rows of K and V: piece p = rows 8p .. 8p+7 (1 KiB), wave w takes p = w, w+4, ..
+    // ---- Q'^T fragments of the wave's first query block: issued before the K / V staging so their
+    //      latency overlaps it (query rows past S clamp to S - 1; not stored)
+    const int nqb = (S + 31) / 32;
+    auto load_q = [&](int qbk, v8s (&qf)[4]) __attribute__((always_inline)) {
+        const int q = qbk * 32 + r;
+        const int qc = q < S ? q : S - 1;
+        const uint16_t* qrow = qbase + (tok0 + qc) * ld + 8 * h;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) qf[kk] = *reinterpret_cast<const v8s*>(qrow + 16 * kk);
+    };
+    v8s qf[4];
+    if (wave < nqb) load_q(wave, qf);
+
+    // ---- stage all NROW rows of K and V: piece p = rows 8p .. 8p+7 (1 KiB), wave w takes p = w, w+NW, ..
     {
         const int spc = lane & 7;
 #pragma unroll
-        for (int p = wave; p < NROW / 8; p += 4) {
+        for (int p = wave; p < NROW / 8; p += NW) {
             const int row = 8 * p + (lane >> 3);
             const uint32_t ko = (uint32_t)(row * ld + kswz(row, spc) * 8) * 2;
             const uint32_t vo = (uint32_t)(row * ld + vswz(row, spc) * 8) * 2;
@@ -104,73 +120,45 @@ attn_short_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
 
-    const int nqb = (S + 31) / 32;
-    for (int qbk = wave; qbk < nqb; qbk += 4) {
-        // Q'^T fragments of this block (query rows past S clamp to S - 1; not stored)
+    for (int qbk = wave; qbk < nqb; qbk += NW) {
         const int q = qbk * 32 + r;
         const int qc = q < S ? q : S - 1;
-        v8s qf[4];
-        {
-            const uint16_t* qrow = qbase + (tok0 + qc) * ld + 8 * h;
+        if (qbk != wave) load_q(qbk, qf);
+        if (c_log2 != 1.0f) {  // q not pre-scaled by the producer: fold scale * log2 e here
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {
-                const v8s raw = *reinterpret_cast<const v8s*>(qrow + 16 * kk);
-                if (c_log2 == 1.0f) {
-                    qf[kk] = raw;
-                } else {
+            for (int kk = 0; kk < 4; ++kk)
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) qf[kk][j] = (short)to16<ET>(from16<ET>((unsigned short)raw[j]) * c_log2);
-                }
-            }
+                for (int j = 0; j < 8; ++j) qf[kk][j] = (short)to16<ET>(from16<ET>((unsigned short)qf[kk][j]) * c_log2);
         }
-        // S'^T over all NKB key blocks
-        v16f sc[NKB];
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb) {
+        v16f o[2];
+        v4f lsum;
+        // one 32-key block: S'^T = K_kb . Q'^T
+        auto qk = [&](int kb) __attribute__((always_inline)) {
             v16f acc = v16f{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int kk = 0; kk < 4; ++kk) {
                 const v8s kf = *reinterpret_cast<const v8s*>(ktile + kb * 32 * ROWB + koff[kk]);
                 acc = mfma32x16<ET>(kf, qf[kk], acc);
             }
-            sc[kb] = acc;
-            // one key block's K reads in flight at a time (hoisting all of them costs 4 registers per
-            // read on top of the 16 per block of scores, and spilled)
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        // keys past S (the last block only) -> -inf; exact row max over all keys of this query
-        if (NKB * 32 > S) {
+            if (kb == NKB - 1 && NKB * 32 > S) {  // keys past S -> -inf
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int key = (NKB - 1) * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-                if (key >= S) sc[NKB - 1][e] = -INFINITY;
+                for (int e = 0; e < 16; ++e) {
+                    const int key = kb * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                    if (key >= S) acc[e] = -INFINITY;
+                }
             }
-        }
-        float m0 = sc[0][0], m1 = sc[0][1];
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
-#pragma unroll
-            for (int e = (kb == 0 ? 2 : 0); e < 16; e += 2) {
-                m0 = fmaxf(m0, sc[kb][e]);
-                m1 = fmaxf(m1, sc[kb][e + 1]);
-            }
-        float m = fmaxf(m0, m1);
-        m = fmaxf(m, __shfl_xor(m, 32, 64));
-        // O^T += V^T . P^T block by block; P = exp2(S' - m) <= 1 packed from the accumulators
-        v16f o[2];
-#pragma unroll
-        for (int db = 0; db < 2; ++db)
-            o[db] = v16f{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        v4f lsum = v4f{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kb = 0; kb < NKB; ++kb)
+            return acc;
+        };
+        // P = exp2(S' - m) of one key block (packed, the B operand of P.V) and O^T += V^T . P^T,
+        // the row sum on the matrix pipe
+        auto pv = [&](int kb, const v16f& sc, float m) __attribute__((always_inline)) {
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
                 v4u pu;
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj)
-                    pu[jj] = pack2<ET>(__builtin_amdgcn_exp2f(sc[kb][8 * s2 + 2 * jj] - m),
-                                       __builtin_amdgcn_exp2f(sc[kb][8 * s2 + 2 * jj + 1] - m));
+                    pu[jj] = pack2<ET>(__builtin_amdgcn_exp2f(sc[8 * s2 + 2 * jj] - m),
+                                       __builtin_amdgcn_exp2f(sc[8 * s2 + 2 * jj + 1] - m));
                 const v8s pf = __builtin_bit_cast(v8s, pu);
 #pragma unroll
                 for (int db = 0; db < 2; ++db) {
@@ -183,8 +171,47 @@ attn_short_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H
                     o[db] = mfma32x16<ET>(vv, pf, o[db]);
                 }
                 lsum = mfma16x32<ET>(sel, pf, lsum);
+            }
+        };
+        auto reset = [&]() __attribute__((always_inline)) {
+#pragma unroll
+            for (int db = 0; db < 2; ++db)
+                o[db] = v16f{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            lsum = v4f{0.f, 0.f, 0.f, 0.f};
+        };
+        // fast pass, no max at all: exp2 of a score is exact in relative terms until it overflows
+        // (a score above ~127 in log2 units) or the whole row underflows; the QK^T of block kb+1 is
+        // independent of block kb's exp2 / P.V, so the scheduler overlaps them.
+        reset();
+        {
+            v16f cur = qk(0);
+#pragma unroll
+            for (int kb = 0; kb < NKB; ++kb) {
+                v16f nxt;
+                if (kb + 1 < NKB) nxt = qk(kb + 1);
+                pv(kb, cur, 0.f);
+                if (kb + 1 < NKB) cur = nxt;
+                // one key block of look-ahead (hoisting every block's QK^T keeps 16 registers of
+                // scores per block live and spilled)
                 __builtin_amdgcn_sched_barrier(0);
             }
+        }
+        // a row sum outside [2^-64, 2^64] (overflow, underflow, inf / NaN input): repeat the block
+        // against the exact row max (two passes over the keys; rare)
+        const float l_fast = __shfl(lsum[0], (r & 15) + ((r >> 4) << 5), 64);
+        if (__any(!(l_fast >= 0x1p-64f && l_fast <= 0x1p64f))) {
+            float m = -INFINITY;
+#pragma unroll 1
+            for (int kb = 0; kb < NKB; ++kb) {
+                const v16f sc = qk(kb);
+#pragma unroll
+                for (int e = 0; e < 16; ++e) m = fmaxf(m, sc[e]);
+            }
+            m = fmaxf(m, __shfl_xor(m, 32, 64));
+            reset();
+#pragma unroll 1
+            for (int kb = 0; kb < NKB; ++kb) pv(kb, qk(kb), m);
+        }
         // query r's row sum sits in lane (r & 15) + 32 (r >> 4)
         const float inv = 1.0f / __shfl(lsum[0], (r & 15) + ((r >> 4) << 5), 64);
         unsigned pk[2][4][2];
@@ -213,7 +240,7 @@ template <int ET, int NKB>
 static int launch_nkb(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, int64_t H, float c_log2, uint16_t* out,
                       int64_t ldo, hipStream_t stream) {
     const int lds = 2 * NKB * 32 * ROWB;
-    attn_short_d64_kernel<ET, NKB><<<(unsigned)(B * H), 256, lds, stream>>>(qkv, ld, (int)S, (int)H, c_log2, out, ldo);
+    attn_short_d64_kernel<ET, NKB><<<(unsigned)(B * H), NW * 64, lds, stream>>>(qkv, ld, (int)S, (int)H, c_log2, out, ldo);
     return 0;
 }
 

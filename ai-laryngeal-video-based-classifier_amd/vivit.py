@@ -116,6 +116,11 @@ class VivitForVideoClassification(torch.nn.Module):
         self.concurrent_streams = None  # None / 1: one stream; n > 1: batch split over n HIP streams
         self.last_streams = 1
         self.kernel_events = None
+        # per-GEMM tile config override {"qkv" | "o_proj" | "fc1" | "fc2": vc_gemm cfg} (None / absent:
+        # vc_gemm's own pick) and the GEMM / LayerNorm row count: "pad" = every padded row (Mpad),
+        # "tight" = B*S rounded up to the tile height (the padding rows keep their initial zeros)
+        self.gemm_cfg = {}
+        self.rows = "pad"
         # q|k|v and fc2 as whole-round + tail launches (ops.gemm_rounds): bit-identical, 5-7 %
         # faster per GEMM in isolation but 0.6 % SLOWER in the model (tools/ab_model.py
         # round_split, interleaved, B = 8: 9.340 vs 9.285 ms/step), so off by default
@@ -400,18 +405,32 @@ class VivitForVideoClassification(torch.nn.Module):
         act = "bias_gelu_tanh" if c.hidden_act in ("gelu_fast", "gelu_pytorch_tanh", "gelu_new") else "bias_gelu_erf"
         scale = 1.0 / math.sqrt(D // c.num_attention_heads)
         if self.round_split:
-            qkv_gemm = functools.partial(ops.gemm_rounds, main_cfg=4, tail_cfg=5)
-            fc2_gemm = functools.partial(ops.gemm_rounds, main_cfg=5, tail_cfg=1)
+            qkv_gemm = lambda *a, cfg=-1, **k: ops.gemm_rounds(*a, main_cfg=4, tail_cfg=5, **k)  # noqa: E731
+            fc2_gemm = lambda *a, cfg=-1, **k: ops.gemm_rounds(*a, main_cfg=5, tail_cfg=1, **k)  # noqa: E731
         else:
             qkv_gemm = fc2_gemm = ops.gemm
+        gc = self.gemm_cfg
+        tight = self.rows == "tight"
+
+        def rows(name):
+            """(m, cfg) of one GEMM: every padded row, or B*S up to its tile height (256 rows for the
+            256-row configs 0/3/4 and for vc_gemm's own pick, which prefers them, else 128)"""
+            cfg = gc.get(name)
+            if not tight:
+                return None, -1 if cfg is None else cfg
+            h = 128 if cfg in (1, 2, 5, 7) else 256
+            return _round_up(B * S, h), -1 if cfg is None else cfg
+
+        m_ln = B * S if tight else None
+        (m_qkv, c_qkv), (m_o, c_o), (m_1, c_1), (m_2, c_2) = rows("qkv"), rows("o_proj"), rows("fc1"), rows("fc2")
         for L in pk["layers"]:
-            run("layernorm", ops.layernorm, X, L["ln1_g"], L["ln1_b"], eps, Y)
-            run("qkv", qkv_gemm, Y, L["w_qkv"], L["b_qkv"], "bias", QKV)
+            run("layernorm", ops.layernorm, X, L["ln1_g"], L["ln1_b"], eps, Y, m=m_ln)
+            run("qkv", qkv_gemm, Y, L["w_qkv"], L["b_qkv"], "bias", QKV, m=m_qkv, cfg=c_qkv)
             run("attention", ops.attention, QKV, B, S, c.num_attention_heads, scale, O, q_prescaled=True)
-            run("o_proj", ops.gemm, O, L["w_o"], L["b_o"], "bias_resid_f32", X)
-            run("layernorm", ops.layernorm, X, L["ln2_g"], L["ln2_b"], eps, Y)
-            run("fc1", ops.gemm, Y, L["w_1"], L["b_1"], act, Hd)
-            run("fc2", fc2_gemm, Hd, L["w_2"], L["b_2"], "bias_resid_f32", X)
+            run("o_proj", ops.gemm, O, L["w_o"], L["b_o"], "bias_resid_f32", X, m=m_o, cfg=c_o)
+            run("layernorm", ops.layernorm, X, L["ln2_g"], L["ln2_b"], eps, Y, m=m_ln)
+            run("fc1", ops.gemm, Y, L["w_1"], L["b_1"], act, Hd, m=m_1, cfg=c_1)
+            run("fc2", fc2_gemm, Hd, L["w_2"], L["b_2"], "bias_resid_f32", X, m=m_2, cfg=c_2)
         return ops.cls_head(X, B, S, pk["lnf_g"], pk["lnf_b"], eps, pk["w_cls"], pk["b_cls"],
                             out=ws["logits"] if out is None else out)
 
