@@ -1,0 +1,35 @@
+"""Batch split over concurrent HIP streams for the inference forwards (ViViT, TimeSformer, Swin3D).
+
+Clips are independent and every kernel is batch-invariant, so the logits of a batch split into n parts
+that run on n HIP streams (each part with its own workspace) are bit-identical to one stream; what the
+split buys is overlap: one part's GEMM tail rounds and short launches run beside another part's
+kernels (ViViT-B B = 8: 840 -> 916 clips/s with 2 streams, tools/exp_streams.py, round 3).
+"""
+from __future__ import annotations
+
+import torch
+
+
+def run_split(owner, x: torch.Tensor, ns: int, part_fn, num_labels: int) -> torch.Tensor:
+    """part_fn(x_part, part_index, out=logits_rows) for each of `ns` contiguous batch parts, part i on
+    owner._streams[i]; returns the [B, num_labels] logits (a buffer of `owner`, reused per call)."""
+    dev = x.device
+    B = x.shape[0]
+    ns = max(1, min(int(ns), B))
+    if owner._streams is None or len(owner._streams) < ns or owner._streams[0].device != dev:
+        owner._streams = [torch.cuda.Stream(device=dev) for _ in range(ns)]
+    key = (B, str(dev), "split_logits")
+    if key not in owner._split_out:
+        owner._split_out[key] = torch.zeros(B, num_labels, dtype=torch.float32, device=dev)
+    logits = owner._split_out[key]
+    cur = torch.cuda.current_stream(dev)
+    bounds = [B * i // ns for i in range(ns + 1)]
+    for i in range(ns):
+        st = owner._streams[i]
+        st.wait_stream(cur)
+        x.record_stream(st)  # x may be freed by the caller while the side streams still read it
+        with torch.cuda.stream(st):
+            part_fn(x[bounds[i]:bounds[i + 1]], i, out=logits[bounds[i]:bounds[i + 1]])
+    for i in range(ns):
+        cur.wait_stream(owner._streams[i])
+    return logits

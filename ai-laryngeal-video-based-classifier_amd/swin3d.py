@@ -138,6 +138,9 @@ class Swin3d(torch.nn.Module):
         self._bias_cache = {}
         self._ws = {}
         self.kernel_events = None  # list: HIP events around each window-attention launch (bench.py)
+        self.concurrent_streams = None  # n > 1: the inference batch split over n HIP streams
+        self._streams = None
+        self._split_out = {}
         self.stochastic_depth = True  # train step: torchvision's StochasticDepth on the residual branches
 
     def state_dict(self, *a, **k):
@@ -250,10 +253,12 @@ class Swin3d(torch.nn.Module):
             g.append((t, (h + 1) // 2, (w + 1) // 2))
         return g
 
-    def _workspace(self, B, grids, device):
-        key = (B, tuple(grids), str(device))
+    def _workspace(self, B, grids, device, part: int = 0):
+        key = (B, tuple(grids), str(device), part)
         if key in self._ws:
             return self._ws[key]
+        if len(self._ws) >= 8:
+            self._ws = {}
         c = self.cfg
         bf, f32 = torch.bfloat16, torch.float32
         z = lambda r, cols, dt=bf: torch.zeros((r, cols), dtype=dt, device=device)  # noqa: E731
@@ -273,7 +278,7 @@ class Swin3d(torch.nn.Module):
             ws["stages"].append(st)
         ws["logits"] = torch.zeros((B, self.num_classes), dtype=f32, device=device)
         ws["pool_work"] = torch.zeros(B * 64 * c["embed_dim"] * 2 ** (len(grids) - 1), dtype=f32, device=device)
-        self._ws = {key: ws}
+        self._ws[key] = ws
         return ws
 
     # ---- forward -------------------------------------------------------------------
@@ -357,13 +362,24 @@ class Swin3d(torch.nn.Module):
                            t * h * w, eps)
 
     def forward_logits(self, video: torch.Tensor) -> torch.Tensor:
-        c = self.cfg
-        B, Cin, T, H, W = video.shape
+        """logits f32 [B, classes] (a workspace buffer, overwritten by the next call); with
+        `concurrent_streams = n > 1` the batch is split over n HIP streams (vclip_amd.streams):
+        one part's small late-stage launches run beside another part's early stages."""
+        B, Cin = video.shape[0], video.shape[1]
         if Cin != 3:
             raise ValueError("video must be [B, 3, T, H, W]")
+        ns = max(1, min(int(self.concurrent_streams or 1), B))
+        if ns == 1:
+            return self._forward_part(video, 0)
+        from .streams import run_split
+        return run_split(self, video, ns, self._forward_part, self.num_classes)
+
+    def _forward_part(self, video: torch.Tensor, part: int, out=None) -> torch.Tensor:
+        c = self.cfg
+        B, Cin, T, H, W = video.shape
         pk = self._pack(video.device)
         grids = self.geometry(B, T, H, W)
-        ws = self._workspace(B, grids, video.device)
+        ws = self._workspace(B, grids, video.device, part)
         eps = c["layer_norm_eps"]
         pt, ph, pw = c["patch_size"]
         t0, h0, w0 = grids[0]
@@ -402,7 +418,7 @@ class Swin3d(torch.nn.Module):
                 ops.gemm(sw["Mg"], st["w_red"], st["b_red"], "bias_f32", nxt["X"], m=nxt["M"])
         t, h, w = grids[-1]
         return ops.pool_head(ws["stages"][-1]["X"], B, t * h * w, pk["norm"][0], pk["norm"][1], eps, pk["w_head"],
-                             pk["b_head"], out=ws["logits"], work=ws["pool_work"])
+                             pk["b_head"], out=ws["logits"] if out is None else out, work=ws["pool_work"])
 
 
 def create_model(logger=None, model_size="tiny", pretrained=True, num_classes=2, device="cuda", weights_seed: int = 0):

@@ -98,6 +98,9 @@ class TimesformerForVideoClassification(torch.nn.Module):
         shapes = timesformer_param_shapes(c.as_shape_cfg())
         self._names = list(shapes.keys())
         self.kernel_events = None  # list: HIP events around each spatial-attention launch (bench.py)
+        self.concurrent_streams = None  # n > 1: the inference batch split over n HIP streams
+        self._streams = None
+        self._split_out = {}
         for name, shape in shapes.items():
             self.params[name.replace(".", "__")] = torch.nn.Parameter(torch.zeros(shape))
         self._packed = None
@@ -193,10 +196,12 @@ class TimesformerForVideoClassification(torch.nn.Module):
         Memb = _round_up(B * P * T, 128)
         return P, T, S, Mpad, Memb
 
-    def _workspace(self, B, device):
-        key = (B, str(device))
+    def _workspace(self, B, device, part: int = 0):
+        key = (B, str(device), part)
         if key in self._ws:
             return self._ws[key]
+        if len(self._ws) >= 8:
+            self._ws = {}
         c = self.config
         D, I = c.hidden_size, c.intermediate_size
         P, T, S, Mpad, Memb = self.geometry(B)
@@ -205,7 +210,7 @@ class TimesformerForVideoClassification(torch.nn.Module):
         ws = dict(A_emb=z(Memb, c.num_channels * c.patch_size * c.patch_size), X=z(Mpad, D, dt=torch.float32),
                   Hc=z(Mpad, D), Hf=z(Mpad, D), QKV=z(Mpad, 3 * D), O=z(Mpad, D), Yb=z(Mpad, D), Hd=z(Mpad, I),
                   logits=z(B, c.num_labels, dt=torch.float32))
-        self._ws = {key: ws}
+        self._ws[key] = ws
         return ws
 
     def forward(self, pixel_values: torch.Tensor = None, labels: torch.Tensor = None, **kw):
@@ -228,13 +233,24 @@ class TimesformerForVideoClassification(torch.nn.Module):
         return ClassifierOutput(logits, loss)
 
     def forward_logits(self, pix: torch.Tensor) -> torch.Tensor:
+        """logits f32 [B, labels] (a workspace buffer, overwritten by the next call); with
+        `concurrent_streams = n > 1` the batch is split over n HIP streams (vclip_amd.streams)."""
         c = self.config
         B, T, C, H, W = pix.shape
         if T != c.num_frames or H != c.image_size or W != c.image_size or C != c.num_channels:
             raise ValueError(f"pixel_values {tuple(pix.shape)} do not match config "
                              f"(T={c.num_frames}, C={c.num_channels}, {c.image_size}^2)")
+        ns = max(1, min(int(self.concurrent_streams or 1), B))
+        if ns == 1:
+            return self._forward_part(pix, 0)
+        from .streams import run_split
+        return run_split(self, pix, ns, self._forward_part, c.num_labels)
+
+    def _forward_part(self, pix: torch.Tensor, part: int, out=None) -> torch.Tensor:
+        c = self.config
+        B = pix.shape[0]
         pk = self._pack(pix.device)
-        ws = self._workspace(B, pix.device)
+        ws = self._workspace(B, pix.device, part)
         P, T, S, Mpad, Memb = self.geometry(B)
         Hn = c.num_attention_heads
         eps = c.layer_norm_eps
@@ -268,7 +284,8 @@ class TimesformerForVideoClassification(torch.nn.Module):
             ops.divided_add_layernorm(X, Yb, B, P, T, L["ln2_g"], L["ln2_b"], eps, "spatial_to_mlp", Hc)
             ops.gemm(Hc, L["w_1"], L["b_1"], act, Hd)
             ops.gemm(Hd, L["w_2"], L["b_2"], "bias_resid_f32", X)
-        return ops.cls_head(X, B, S, pk["lnf_g"], pk["lnf_b"], eps, pk["w_cls"], pk["b_cls"], out=ws["logits"])
+        return ops.cls_head(X, B, S, pk["lnf_g"], pk["lnf_b"], eps, pk["w_cls"], pk["b_cls"],
+                            out=ws["logits"] if out is None else out)
 
 
     def _forward_train(self, pix: torch.Tensor) -> torch.Tensor:

@@ -304,7 +304,7 @@ class VivitForVideoClassification(torch.nn.Module):
         key = (B, str(device), part, self.compute_dtype)
         if key in self._ws:
             return self._ws[key]
-        if len(self._ws) >= 4:
+        if len(self._ws) >= 8:  # (1 + 2 stream parts) x {bf16, fp16} + the split logits fit
             self._ws = {}
         c = self.config
         D, I = c.hidden_size, c.intermediate_size
@@ -341,12 +341,12 @@ class VivitForVideoClassification(torch.nn.Module):
         """logits f32 [B, labels] (a workspace buffer, overwritten by the next call).
 
         `concurrent_streams = n > 1` splits the batch over n HIP streams, each part with its own
-        workspace, so one part's GEMM epilogues and kernel tails overlap another part's work:
-        +3-5 % clips/s at B = 8 with 2 streams (tools/try_streams.py; 4 streams were slower).
-        Off by default: under overlap a kernel's stream-event duration includes time queued
-        behind the other stream's kernels and no longer matches its rocprof kernel-trace
-        duration, which the benchmark's per-kernel roofline is checked against.  Logits are
-        bit-identical either way (every kernel is batch-invariant)."""
+        workspace, so one part's kernels fill the CUs another part's tail rounds and short launches
+        leave idle: ViViT-B B = 8 840 -> 916 and 857 -> 911 clips/s with 2 streams on two boxes
+        (tools/exp_streams.py; 3 streams 813-855).  bench.py's headline runs 2 streams; its kernel
+        roofline is timed in a separate one-stream pass (under overlap a launch's event time
+        includes time shared with the other stream's kernels).  Logits are bit-identical either
+        way (every kernel is batch-invariant)."""
         c = self.config
         B, T, C, H, W = pix.shape
         if T != c.num_frames or H != c.image_size or W != c.image_size or C != c.num_channels:
@@ -366,13 +366,17 @@ class VivitForVideoClassification(torch.nn.Module):
         logits = self._ws[key]
         cur = torch.cuda.current_stream(dev)
         bounds = [B * i // ns for i in range(ns + 1)]
-        for i in range(ns):
-            st = self._streams[i]
+        sts = self._streams[:ns]
+        # whole parts enqueued one after the other (measured, tools/exp_streams.py: enqueueing the
+        # parts layer by layer round robin ran 725 vs 911 clips/s, chaining their attention launches
+        # across the streams 721, and starting part i+1 at a fixed op of part i's first layer 887-906)
+        for i, st in enumerate(sts):
             st.wait_stream(cur)
+            pix.record_stream(st)
             with torch.cuda.stream(st):
                 self._forward_part(pix[bounds[i]:bounds[i + 1]], i, out=logits[bounds[i]:bounds[i + 1]])
-        for i in range(ns):
-            cur.wait_stream(self._streams[i])
+        for st in sts:
+            cur.wait_stream(st)
         return logits
 
     def _forward_part(self, pix: torch.Tensor, part: int, out=None) -> torch.Tensor:

@@ -155,3 +155,14 @@ def test_layernorm_f32_out(M, D):
     ops.layernorm_f32(x.to(DEV), gam.to(DEV), bet.to(DEV), 1e-5, y)
     want = torch.nn.functional.layer_norm(x, (D,), gam, bet, 1e-5)
     np.testing.assert_allclose(y.cpu().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+
+
+def test_swin3d_two_stream_split_bit_exact():
+    """concurrent_streams = 2 splits the batch over two HIP streams: logits equal one stream bit for bit."""
+    m = _model(TINY)
+    x = torch.from_numpy(make_synthetic_video(3, 8, 48, seed=4)).cuda()
+    m.concurrent_streams = 1
+    one = m.forward_logits(x).clone()
+    m.concurrent_streams = 2
+    two = m.forward_logits(x).clone()
+    assert torch.equal(one, two)

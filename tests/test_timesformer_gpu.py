@@ -165,3 +165,16 @@ def test_timesformer_batch_invariance():
     full = m(pixel_values=pix).logits.clone()
     one = m(pixel_values=pix[1:2].contiguous()).logits.clone()
     assert torch.equal(full[1:2], one)
+
+
+def test_timesformer_two_stream_split_bit_exact():
+    """concurrent_streams = 2 splits the batch over two HIP streams (vclip_amd.streams): logits
+    equal the one-stream run bit for bit."""
+    from vclip_amd.timesformer import create_model
+    m = create_model(num_frames=8, device="cuda")
+    pix = torch.from_numpy(make_synthetic_clips(5, 8, 224, seed=3)).cuda()
+    m.concurrent_streams = 1
+    one = m.forward_logits(pix).clone()
+    m.concurrent_streams = 2
+    two = m.forward_logits(pix).clone()
+    assert torch.equal(one, two)
