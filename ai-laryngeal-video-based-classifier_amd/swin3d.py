@@ -405,9 +405,11 @@ class Swin3d(torch.nn.Module):
                 ops.window_attention3d(QKV, B, (t, h, w), st["heads"], window, shift, biasT, O)
                 if ev is not None:
                     e1.record()
-                    # QK^T + PV over each token's window (window clipped to the grid), head_dim 32
+                    # QK^T + PV over each token's window (window clipped to the grid), head_dim 32;
+                    # algorithmic bytes: q, k, v read and the output written once (4 x 32 x 2 B per
+                    # token-head)
                     n = window[0] * window[1] * window[2]
-                    ev.append((e0, e1, 4.0 * ntok * n * 32 * st["heads"]))
+                    ev.append((e0, e1, 4.0 * ntok * n * 32 * st["heads"], 256.0 * ntok * st["heads"]))
                 ops.gemm(O, blk["w_proj"], blk["b_proj"], "bias_resid_f32", X)
                 ops.layernorm(X, blk["ln2"][0], blk["ln2"][1], eps, Y, m=ntok)
                 ops.gemm(Y, blk["w_1"], blk["b_1"], "bias_gelu_erf", Hd)

@@ -278,7 +278,9 @@ class TimesformerForVideoClassification(torch.nn.Module):
             ops.attention(QKV, B * T, 1 + P, Hn, scale, O, q_prescaled=True)
             if ev is not None:
                 e1.record()
-                ev.append((e0, e1, 4.0 * (1 + P) * (1 + P) * 64 * Hn * B * T))
+                # flop, algorithmic bytes (q, k, v read and the output written once: 4 x 64 x 2 B
+                # per token-head)
+                ev.append((e0, e1, 4.0 * (1 + P) * (1 + P) * 64 * Hn * B * T, 512.0 * (1 + P) * Hn * B * T))
             ops.gemm(O, L["w_o"], L["b_o"], "bias", Yb)
             # MLP (clip layout)
             ops.divided_add_layernorm(X, Yb, B, P, T, L["ln2_g"], L["ln2_b"], eps, "spatial_to_mlp", Hc)

@@ -297,8 +297,9 @@ FAMILIES = {
     # kernel, its rocprofv3 name (the key of its counters in profiles/rNN_*_{traffic,pmc}.json))
     "timesformer": ("clips/sec fwd TimeSformer-B 8x224^2 bf16", 391.66, 16,
                     "TimeSformer-B divided space-time attention, 8x224x224 clips, batch 16 per GPU (BASELINE configs[2])",
-                    "attn_fwd_d64_kernel (spatial branch: B*T sequences of 197 tokens)",
-                    "attn_fwd_d64_kernel<false, false, 0>"),
+                    "attn_short_d64_kernel (spatial branch: B*T sequences of 197 tokens, one 8-wave "
+                    "workgroup per (sequence, head), all keys in LDS)",
+                    "ashort::attn_short_d64_kernel<0, 7>"),
     "swin": ("clips/sec fwd Video Swin-T 32x224^2 bf16", 175.53, 4,
              "Video Swin-T 3D shifted-window attention, 32x224x224 clips, batch 4 per GPU = 32 over DP=8 "
              "(BASELINE configs[3])", "window_attn_d32_kernel (all 12 blocks, head_dim 32)",
@@ -371,9 +372,18 @@ def run_family(a, dist, rank, world, dev):
     evs = []
     dt1 = timed(1, evs)
     model.concurrent_streams = 1
-    attn_s = sum(e0.elapsed_time(e1) for e0, e1, _ in evs) * 1e-3
-    attn_flop = sum(f for _, _, f in evs)
+    attn_s = sum(e0.elapsed_time(e1) for e0, e1, _, _ in evs) * 1e-3
+    attn_flop = sum(f for _, _, f, _ in evs)
+    attn_bytes = sum(b for _, _, _, b in evs)
     attn_tflops = attn_flop / attn_s / 1e12
+    # algorithmic bytes (from the model, per launch): q, k, v read and the output written once per
+    # (sequence | window, head), 4 x N x head_dim x 2 B against 4 N^2 head_dim flop: N / 2 flop per
+    # byte with N the tokens per attention unit (197 = 1 + 14^2 per frame; 392 = 8 x 7 x 7 per Swin
+    # window)
+    unit_name = "sequence" if a.mode == "timesformer" else "window"
+    intensity = attn_flop / attn_bytes
+    attn_gbs = attn_bytes / attn_s / 1e9
+    bound = "hbm" if intensity * PEAK_HBM_GBS * 1e9 < PEAK_BF16_TFLOPS * 1e12 else "mfma"
     value = a.batch * a.steps * world / dt
     ms_per_step = dt / a.steps * 1e3
     model_tflops = gflop * a.batch / (ms_per_step * 1e-3) / 1e3
@@ -393,10 +403,21 @@ def run_family(a, dist, rank, world, dev):
             "data": "synthetic (uint8 frames RandomState(1+rank) -> the family's processor affine; weights RandomState(0))",
             "config": {"workload": workload, "global_batch": a.batch * world, "parallelism": f"dp{world}"},
             "logit_max_abs_err": err,
-            "roofline": {"bound": "mfma", "kernel": kname, "achieved": round(attn_tflops, 1), "peak": PEAK_BF16_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
-                         "traffic_source": traffic_src, "avg_launch_ms": round(attn_s * 1e3 / len(evs), 4),
+            "roofline": {"bound": bound, "kernel": kname,
+                         "achieved": round(attn_gbs, 1) if bound == "hbm" else round(attn_tflops, 1),
+                         "peak": PEAK_HBM_GBS if bound == "hbm" else PEAK_BF16_TFLOPS,
+                         "unit": "GB/s" if bound == "hbm" else "TFLOP/s",
+                         "frac": round(attn_gbs / PEAK_HBM_GBS if bound == "hbm" else attn_tflops / PEAK_BF16_TFLOPS, 4),
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "avg_launch_ms": round(attn_s * 1e3 / len(evs), 4),
+                         "bytes_per_step": round(attn_bytes / a.steps / 1e6, 2), "bytes_unit": "MB",
                          "flop_per_step": round(attn_flop / a.steps / 1e9, 2),
+                         "intensity_flop_per_byte": round(intensity, 1),
+                         "achieved_tflops": round(attn_tflops, 1),
+                         "mfma_frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4),
+                         "bound_note": f"{intensity:.0f} flop/B (keys per {unit_name} / 2: q, k, v read and the output "
+                                       f"written once, 8 B per token x head-dim element) is below the MFMA/HBM ridge "
+                                       f"{PEAK_BF16_TFLOPS / PEAK_HBM_GBS * 1e3:.0f} flop/B, so HBM bounds the kernel",
                          "timed_on": f"a separate K-step pass on one HIP stream (the headline runs {a.streams}): "
                                      f"clips/s {a.batch * a.steps * world / dt1:.2f} there",
                          "mfma_busy": mfma_busy,

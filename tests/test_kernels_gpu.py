@@ -236,6 +236,55 @@ def test_attention(B, S, H):
     assert o[B * S:].abs().sum().item() == 0  # nothing written past the last token
 
 
+@pytest.mark.parametrize("B,S,H", [(160, 197, 3), (130, 33, 4), (64, 256, 12), (257, 1, 1), (100, 224, 7)])
+def test_attention_short_many_items(B, S, H):
+    """S <= 256 runs the short kernel (one 8-wave workgroup per (sequence, head), all keys in LDS):
+    (sequence, head) counts above the CU count and not a multiple of it, and key-block counts 1 (S
+    = 1), 2 (33), 7 (224: whole blocks), 8 (256).  Must match the fp32 softmax; the caller's
+    padding rows hold huge values that must not leak into any output (padding keys are masked,
+    padding query rows are never stored) nor trip the exact-max fallback of a real query."""
+    g = torch.Generator().manual_seed(B * 1000 + S * 10 + H)
+    rows = (B - 1) * S + (S + 63) // 64 * 64 + 64
+    qkv = torch.randn(rows, 3 * H * 64, generator=g)
+    qkv[B * S:] = 3.0e4  # padding rows: padding queries overflow exp2, padding keys are masked
+    qkv = bf(qkv)
+    out = torch.zeros(rows, H * 64, dtype=torch.bfloat16, device=DEV)
+    ops().attention(qkv.to(DEV), B, S, H, 1 / 8.0, out)
+    o = out.float().cpu()
+    q = qkv[: B * S].float().view(B, S, 3, H, 64)
+    ref = attention_ref(q[:, :, 0].transpose(1, 2), q[:, :, 1].transpose(1, 2), q[:, :, 2].transpose(1, 2), 1 / 8.0)
+    ref = ref.transpose(1, 2).reshape(B * S, H * 64)
+    assert torch.isfinite(o[: B * S]).all()
+    err = (o[: B * S] - ref).abs().max().item()
+    assert err < 2.5e-2, err
+    assert o[B * S:].abs().sum().item() == 0
+
+
+@pytest.mark.parametrize("jump", [40.0, 200.0])
+def test_attention_short_fallback_many_items(jump):
+    """The short kernel's exact-max fallback (row sum outside [2^-64, 2^64]: jump 200 overflows
+    exp2) in every 7th sequence, the fast pass in the others (jump 40: exact without a max)."""
+    B, S, H = 600, 197, 1
+    rows = (B - 1) * S + 256 + 64
+    g = torch.Generator().manual_seed(int(jump) + 7)
+    qkv = torch.randn(rows, 192, generator=g) * 0.05
+    qkv[:, 0:64] = 0.0
+    qkv[:, 0] = 1.0
+    qkv[:, 64] = torch.rand(rows, generator=g)
+    for b in range(0, B, 7):
+        qkv[b * S + 150, 64] = jump
+    qkv = bf(qkv)
+    out = torch.zeros(rows, 64, dtype=torch.bfloat16, device=DEV)
+    ops().attention(qkv.to(DEV), B, S, H, 0.125, out, q_prescaled=True)
+    q = qkv[: B * S].float().view(B, S, 3, 1, 64)
+    c = 0.125 * 1.4426950408889634
+    ref = attention_ref(q[:, :, 0].transpose(1, 2) / c, q[:, :, 1].transpose(1, 2), q[:, :, 2].transpose(1, 2), 0.125)
+    o = out[: B * S].float().cpu()
+    assert torch.isfinite(o).all()
+    err = (o - ref.transpose(1, 2).reshape(B * S, 64)).abs().max().item()
+    assert err < 2e-2, err
+
+
 def test_attention_spike_max_jump():
     """Force the running max to jump at a late KV tile (online-softmax rescale path)."""
     B, S, H = 1, 700, 1
