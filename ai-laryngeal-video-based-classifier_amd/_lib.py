@@ -48,6 +48,8 @@ SIGNATURES = {
     "vc_temporal_attention": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_int, c_p, c_i64, c_p], c_int),
     "vc_window_attention3d": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_int, c_int,
                                c_int, c_p, c_i64, c_p, c_i64, c_p], c_int),
+    "vc_window_attention3d_mb": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_int, c_int,
+                               c_int, c_p, c_i64, c_p, c_i64, c_p], c_int),
     "vc_window_attention3d_lse": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_int,
                                    c_int, c_int, c_p, c_i64, c_p, c_i64, c_p, c_p], c_int),
     "vc_window_attention3d_bwd": ([c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64,

@@ -292,6 +292,359 @@ window_attn_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, 
 }
 
 // ---------------------------------------------------------------------------------
+// Inference kernel with the relative-position bias and the shift mask on the matrix pipe.
+//
+// The kernel above adds the bias as the QK^T MFMA's C operand: 16 f32 values per lane per 32-key
+// block streamed from L2 (784 KB per (window, head) workgroup) and copied into the accumulators,
+// and applies the shift mask as three VALU ops per score.  Timing ablations of that kernel on
+// Swin-T B=4 (all 12 launches of a forward): 745 us; without the bias stream 525; without bias
+// and mask 438.  Here both become MFMAs on operands the matrix pipe reads directly:
+//   * bias: S^T += I . Bias^T, I the 32x32 identity as two 16-deep A fragments (constant per
+//     lane), Bias^T the B operand: 8 bf16 per lane per 16 keys, a 16-B load (half the f32 bytes,
+//     no register copies);
+//   * shift mask (windows spanning several shift regions only): S^T += A_m . B_m with A_m[k] =
+//     (one-hot of key k's 3-bit region code, 1) and B_m[q] = (2^14 x one-hot of query q's code,
+//     -2^14): 0 where the codes agree and -2^14 elsewhere (exp2 -> 0, as torchvision's -100 and
+//     the kernel above's -inf); the key rows (32 B each) are staged in LDS with K and V.
+// The mask MFMA runs first and the bias second, both exact (products 0 / +-2^14 / one bias
+// value), so an unmasked score is bias + q'.k accumulated as before; a padded key's bias is
+// -2^14.  The bias is bf16 (2^-9 relative: ~3e-4 in log2 units at the table's magnitudes).
+// ---------------------------------------------------------------------------------
+constexpr float WMB_BIG = 16384.0f;
+
+__global__ void __launch_bounds__(256, 2)
+window_attn_mb_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom g, int heads, int vol, int NP,
+                          const uint16_t* __restrict__ biasB, int masked, uint16_t* __restrict__ out, int64_t ldo) {
+    __shared__ __attribute__((aligned(16))) char kv[2 * WNP_MAX * 64];
+    __shared__ __attribute__((aligned(16))) char kon[WNP_MAX * 32];  // per key: one-hot region code | (1, 0 x 7)
+
+    // (window, head) of this workgroup: head pairs (2p, 2p + 1) outermost, so the workgroups in
+    // flight share two heads' bias (the L2 working set stays ~2 x 364 KB at any head count); within
+    // a pair, ids i and i + 8 are the two heads of one window, on the same XCD (id mod 8) and
+    // dispatched together, so the 128-B line holding both heads' 64-B q / k / v slices of a token
+    // is fetched into that XCD's L2 once
+    const int nwin_all = (int)(gridDim.x / heads);
+    int head, wlin;
+    {
+        const int id = blockIdx.x;
+        const int pair_ids = 2 * nwin_all;
+        const int full = (heads / 2) * pair_ids;
+        if (id < full) {
+            const int pr = id / pair_ids;
+            const int rem = id - pr * pair_ids;
+            const int full8 = (nwin_all / 8) * 16;
+            int hh;
+            if (rem < full8) {
+                hh = (rem >> 3) & 1;
+                wlin = (rem >> 4) * 8 + (rem & 7);
+            } else {
+                const int tail = nwin_all & 7, rem2 = rem - full8;
+                hh = rem2 / tail;
+                wlin = (nwin_all & ~7) + rem2 - hh * tail;
+            }
+            head = 2 * pr + hh;
+        } else {  // odd head count: the last head alone
+            head = heads - 1;
+            wlin = id - full;
+        }
+    }
+    const int nwin = g.nwt * g.nwh * g.nww;
+    const int b = wlin / nwin;
+    int r = wlin - b * nwin;
+    const int wi_t = r / (g.nwh * g.nww);
+    r -= wi_t * g.nwh * g.nww;
+    const int wi_h = r / g.nww, wi_w = r - (r / g.nww) * g.nww;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int C = heads * 32;
+
+    auto token_row = [&](int n, int* label) -> int64_t { return win_token_row(g, b, wi_t, wi_h, wi_w, n, label); };
+
+    // ---- stage K (swizzled 16-B chunks) and V (plain 64-B rows) of this window/head in LDS
+    char* Ks = kv;
+    char* Vs = kv + WNP_MAX * 64;
+    {
+        // every load issued before the first LDS write (a rolled loop waited out one gather
+        // latency per 256 chunks): <= 7 chunks of 16 B per thread at NP = 448
+        constexpr int NCH = WNP_MAX * 4 / 256;
+        uint4 kval[NCH], vval[NCH];
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            const int c = tid + 256 * j, n = c >> 2, ch = c & 3;
+            kval[j] = make_uint4(0, 0, 0, 0);
+            vval[j] = make_uint4(0, 0, 0, 0);
+            if (n < vol) {
+                const int64_t row = token_row(n, nullptr);
+                const uint16_t* src = qkv + row * ld + head * 32 + ch * 8;
+                kval[j] = *reinterpret_cast<const uint4*>(src + C);
+                vval[j] = *reinterpret_cast<const uint4*>(src + 2 * C);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            const int c = tid + 256 * j, n = c >> 2, ch = c & 3;
+            if (n < NP) {
+                *reinterpret_cast<uint4*>(Ks + n * 64 + kchunk_swz(n, ch) * 16) = kval[j];
+                *reinterpret_cast<uint4*>(Vs + n * 64 + ch * 16) = vval[j];
+            }
+        }
+    }
+    // region codes: the mask matters only in windows whose tokens span several shift regions
+    int diff = 0;
+    if (masked) {
+        int lb0 = 0;
+        token_row(0, &lb0);
+        for (int n = tid; n < NP; n += 256) {
+            int lb = 15;  // padding key: no region (its bias is -2^14 anyway)
+            if (n < vol) {
+                token_row(n, &lb);
+                diff |= lb != lb0;
+            }
+            unsigned w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w[j] = (lb >> 1) == j ? 0x3F80u << (16 * (lb & 1)) : 0u;
+            *reinterpret_cast<uint4*>(kon + n * 32) = make_uint4(w[0], w[1], w[2], w[3]);
+            *reinterpret_cast<uint4*>(kon + n * 32 + 16) = make_uint4(0x3F80u, 0u, 0u, 0u);
+        }
+    }
+    const bool mixed = __syncthreads_or(diff) != 0;
+
+    const int rr = lane & 31, h = lane >> 5;
+    int koff[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) koff[kk] = rr * 64 + kchunk_swz(rr, 2 * kk + h) * 16;
+    const int gi = lane & 15;
+    const int tq = gi >> 2, tp = gi & 3;
+    const int gcol = ((lane >> 4) & 1) * 16 + tp * 4;
+    const int voff = (4 * h + tq) * 64 + gcol * 2;
+    const int nqb = (vol + 31) / 32;
+    const int ntile = NP / 64;
+
+    // identity A fragments: lane (rr, h) of slice s holds I[rr][16s + 8h + m], m = 0..7
+    v8s ident[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int m = 0; m < 8; ++m) ident[s2][m] = rr == 16 * s2 + 8 * h + m ? (short)0x3F80 : (short)0;
+    v8bf sel;
+    {
+        const __bf16 v = (((lane >> 4) & 1) == ((lane & 15) >> 3)) ? (__bf16)1.0f : (__bf16)0.0f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sel[j] = v;
+    }
+
+    // this wave's query blocks qb = wave, wave + 4, ..: the next block's Q fragments and the next
+    // tile's bias fragments (the next block's tile 0 across a block boundary) are loaded while the
+    // current tile computes
+    struct QBlock {
+        v8bf qf[2];
+        v8s qm;  // B operand of the mask MFMA: h = 0 lanes 2^14 x one-hot(code), h = 1 lanes (-2^14, 0 x 7)
+        int64_t qrow;
+    };
+    auto load_qblock = [&](int qb, QBlock& Q) __attribute__((always_inline)) {
+        const int qn = qb * 32 + rr;
+        const int qc = qn < vol ? qn : vol - 1;
+        int qlab = 0;
+        Q.qrow = token_row(qc, masked ? &qlab : nullptr);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+            Q.qf[kk] = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(qkv + Q.qrow * ld + head * 32 + 16 * kk + 8 * h));
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+            Q.qm[m] = h == 0 ? (m == qlab ? (short)0x4680 : (short)0) : (m == 0 ? (short)0xC680 : (short)0);
+    };
+    // bias fragments of (query block, tile): [t][kb][s] 1 KiB each (64 lanes x 16 B)
+    // (a wave-uniform base in SGPRs + the lane's constant 16-B offset: no address VGPR that a later
+    // instruction overwrites while the load is in flight)
+    // bias fragments of (query block, tile): [t][kb][s] 1 KiB each (64 lanes x 16 B), from a
+    // wave-uniform base
+    auto load_bias = [&](int qb, int t, v8s (&bf)[4]) __attribute__((always_inline)) {
+        typedef const __attribute__((address_space(1))) v8s gv8s;
+        const uint64_t a = (uint64_t)(uintptr_t)(biasB + (((int64_t)head * (NP / 32) + qb) * ntile + t) * 4 * 512);
+        // readfirstlane returns int: each half goes through uint32_t, or a low word with bit 31 set
+        // would sign-extend over the high word
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+        gv8s* bq = reinterpret_cast<gv8s*>(((uint64_t)hi << 32) | (uint64_t)lo) + lane;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bf[j] = bq[j * 64];
+    };
+    // S'^T of 64 keys: (mask) + bias + K . Q'^T
+    auto scores = [&](auto mixed_c, const QBlock& Q, int t, const v8s (&bf)[4], v16f (&sc)[2]) __attribute__((always_inline)) {
+        constexpr bool MIXED = decltype(mixed_c)::value;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            v16f acc = v16f{};
+            if constexpr (MIXED) {
+                const v8s km = *reinterpret_cast<const v8s*>(kon + (t * 64 + kb * 32 + rr) * 32 + h * 16);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf, km), __builtin_bit_cast(v8bf, Q.qm),
+                                                              acc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf, ident[s2]),
+                                                              __builtin_bit_cast(v8bf, bf[kb * 2 + s2]), acc, 0, 0, 0);
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                const v8bf kf = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(Ks + (t * 64 + kb * 32) * 64 + koff[kk]));
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, Q.qf[kk], acc, 0, 0, 0);
+            }
+            sc[kb] = acc;
+        }
+    };
+    // O^T += V^T . P^T for one tile (P packed from p); row sums on the matrix pipe (lsum) or none
+    // (the exact pass keeps f32 VALU sums)
+    v16f o;
+    auto pv = [&](int t, const v16f (&p)[2], v4f* lsum) __attribute__((always_inline)) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                v4u pu;
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) pu[jj] = pack2bf(p[kb][8 * s2 + 2 * jj], p[kb][8 * s2 + 2 * jj + 1]);
+                const v8bf pf = __builtin_bit_cast(v8bf, pu);
+                const char* pa = Vs + (t * 64 + kb * 32 + 16 * s2) * 64 + voff;
+                const v4s va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)pa);
+                const v4s vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(pa + 8 * 64));
+                v8s vv;
+                vv[0] = va[0]; vv[1] = va[1]; vv[2] = va[2]; vv[3] = va[3];
+                vv[4] = vb[0]; vv[5] = vb[1]; vv[6] = vb[2]; vv[7] = vb[3];
+                o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf, vv), pf, o, 0, 0, 0);
+                if (lsum) *lsum = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf, *lsum, 0, 0, 0);
+            }
+    };
+    // exact pass of one block (rare: a row sum outside [2^-64, 2^64], inf / NaN): the deferred
+    // running max fixed by tile 0, re-based on a tile's exact max when a lane's partial row sum
+    // exceeds WLIM
+    auto exact = [&](auto mixed_c, const QBlock& Q, int qb) __attribute__((always_inline)) {
+        o = v16f{};
+        float m_run = -1e30f;
+        v2f l2 = {0.f, 0.f};
+        for (int t = 0; t < ntile; ++t) {
+            v8s bf[4];
+            load_bias(qb, t, bf);
+            v16f sc[2];
+            scores(mixed_c, Q, t, bf, sc);
+            auto rowmax = [&]() {
+                float a = fmaxf(sc[0][0], sc[1][0]), c = fmaxf(sc[0][1], sc[1][1]);
+#pragma unroll
+                for (int e = 2; e < 16; e += 2) {
+                    a = fmaxf(a, fmaxf(sc[0][e], sc[1][e]));
+                    c = fmaxf(c, fmaxf(sc[0][e + 1], sc[1][e + 1]));
+                }
+                const float x = fmaxf(a, c);
+                return fmaxf(x, __shfl_xor(x, 32, 64));
+            };
+            if (t == 0) m_run = fmaxf(rowmax(), -1e30f);
+            v16f p[2];
+            auto expsum = [&]() {
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) p[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e] - m_run);
+                v2f u[8];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    u[j] = v2f{p[0][4 * j], p[0][4 * j + 1]} + v2f{p[0][4 * j + 2], p[0][4 * j + 3]};
+                    u[4 + j] = v2f{p[1][4 * j], p[1][4 * j + 1]} + v2f{p[1][4 * j + 2], p[1][4 * j + 3]};
+                }
+                return ((u[0] + u[1]) + (u[2] + u[3])) + ((u[4] + u[5]) + (u[6] + u[7]));
+            };
+            v2f ps = expsum();
+            if (__any(!(ps[0] + ps[1] <= WLIM))) {
+                const float delta = fmaxf(rowmax() - m_run, 0.f);
+                const float alpha = __builtin_amdgcn_exp2f(-delta);
+                m_run += delta;
+#pragma unroll
+                for (int e = 0; e < 16; ++e) o[e] *= alpha;
+                l2 *= alpha;
+                ps = expsum();
+            }
+            l2 += ps;
+            pv(t, p, nullptr);
+        }
+        const float l_run = l2[0] + l2[1];
+        return l_run + __shfl_xor(l_run, 32, 64);
+    };
+    // the wave's blocks: fast pass (scores exponentiated as they come, no running max, row sums on
+    // the matrix pipe), the exact pass when a row sum leaves [2^-64, 2^64], 16-B output stores
+    // Loads in flight are never carried across a loop back edge: the next tile's bias fragments
+    // are issued at the top of a tile and moved into place at its bottom, the next block's Q at
+    // the top of the block's last tile (a prefetch held across the tile loop, or left to the
+    // scheduler, was waited for at the first MFMA of the next tile).
+    // nt_c: the tile count as a compile-time constant (7: 392-token windows, every standard Swin
+    // config; the loop unrolls fully and the bias hand-over is a rename, no copies) or 0 (any
+    // window: rolled loop)
+    auto run = [&](auto mixed_c, auto nt_c) __attribute__((always_inline)) {
+        constexpr int NT = decltype(nt_c)::value;
+        const int nt = NT ? NT : ntile;
+        QBlock cur, nxt;
+        v8s bcur[4], bnxt[4];
+        if (wave >= nqb) return;
+        load_qblock(wave, cur);
+        load_bias(wave, 0, bcur);
+        for (int qb = wave; qb < nqb; qb += 4) {
+            const bool more = qb + 4 < nqb;
+            o = v16f{};
+            v4f lsum = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int t = 0; t < nt; ++t) {
+                const bool last = t + 1 == nt;
+                if (!last) load_bias(qb, t + 1, bnxt);
+                else if (more) {
+                    load_bias(qb + 4, 0, bnxt);
+                    load_qblock(qb + 4, nxt);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                v16f sc[2];
+                scores(mixed_c, cur, t, bcur, sc);
+                v16f p[2];
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) p[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e]);
+                pv(t, p, &lsum);
+                if (!last || more) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) bcur[j] = bnxt[j];
+                }
+            }
+            // query rr's sum sits in lane (rr & 15) + 32 (rr >> 4)
+            float l_tot = __shfl(lsum[0], (rr & 15) + ((rr >> 4) << 5), 64);
+            const int qn = qb * 32 + rr;
+            if (__any(qn < vol && !(l_tot >= 0x1p-64f && l_tot <= 0x1p64f))) l_tot = exact(mixed_c, cur, qb);
+            // ---- O^T[d][q]: reg 4g+e -> d = 8g + 4h + e; lane pairs swap halves -> 16-B stores
+            const float inv = 1.0f / l_tot;
+            unsigned pk[4][2];
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                pk[g4][0] = pack2bf(o[4 * g4 + 0] * inv, o[4 * g4 + 1] * inv);
+                pk[g4][1] = pack2bf(o[4 * g4 + 2] * inv, o[4 * g4 + 3] * inv);
+            }
+            uint16_t* orow = out + cur.qrow * ldo + head * 32;
+#pragma unroll
+            for (int g4 = 0; g4 < 4; g4 += 2) {
+                auto x0 = __builtin_amdgcn_permlane32_swap(pk[g4][0], pk[g4 + 1][0], false, false);
+                auto x1 = __builtin_amdgcn_permlane32_swap(pk[g4][1], pk[g4 + 1][1], false, false);
+                uint4 v;
+                v.x = x0[0]; v.y = x1[0]; v.z = x0[1]; v.w = x1[1];
+                if (qn < vol) *reinterpret_cast<uint4*>(orow + g4 * 8 + h * 8) = v;
+            }
+            if (more) cur = nxt;
+        }
+    };
+    using NT7 = std::integral_constant<int, 7>;
+    using NTX = std::integral_constant<int, 0>;
+    if (ntile == 7) {
+        if (mixed) run(std::true_type{}, NT7{});
+        else run(std::false_type{}, NT7{});
+    } else {
+        if (mixed) run(std::true_type{}, NTX{});
+        else run(std::false_type{}, NTX{});
+    }
+}
+
+// ---------------------------------------------------------------------------------
 // PatchMerging gather + LayerNorm(4C): out[(b,t,i,j)] = LN(cat(x[2i,2j], x[2i+1,2j],
 // x[2i,2j+1], x[2i+1,2j+1])) (zero rows past an odd H/W edge, torchvision _patch_merging_pad).
 // One wave per output token, 4C <= 4096.
@@ -504,6 +857,30 @@ int vc_window_attention3d(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T,
                           int64_t head_dim, int wt, int wh, int ww, int st, int sh, int sw, const float* biasF,
                           int64_t np, uint16_t* out, int64_t ldo, hipStream_t stream) {
     return window_fwd(qkv, ld, B, T, H, W, heads, head_dim, wt, wh, ww, st, sh, sw, biasF, np, out, ldo, nullptr, stream);
+}
+
+int vc_window_attention3d_mb(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T, int64_t H, int64_t W, int64_t heads,
+                             int64_t head_dim, int wt, int wh, int ww, int st, int sh, int sw, const uint16_t* biasB,
+                             int64_t np, uint16_t* out, int64_t ldo, hipStream_t stream) {
+    if (!qkv || !biasB || !out) return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d_mb: null pointer");
+    if (head_dim != 32) return fail(VC_ERR_UNSUPPORTED, "vc_window_attention3d_mb: head_dim must be 32");
+    if (wt <= 0 || wh <= 0 || ww <= 0 || T % wt || H % wh || W % ww)
+        return fail(VC_ERR_UNSUPPORTED, "vc_window_attention3d_mb: the token grid must be whole windows (no padding)");
+    if (st < 0 || sh < 0 || sw < 0 || st >= wt || sh >= wh || sw >= ww)
+        return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d_mb: shift must be in [0, window)");
+    const int vol = wt * wh * ww;
+    if (np != (vol + 63) / 64 * 64 || np > WNP_MAX)
+        return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d_mb: np must be roundup(window volume, 64) <= 448");
+    if (ld < 3 * heads * 32 || ldo < heads * 32 || ld % 8 || ldo % 8 || ((uintptr_t)qkv | (uintptr_t)out) & 15)
+        return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d_mb: bad leading dimension / alignment");
+    if ((uintptr_t)biasB & 15) return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d_mb: biasB must be 16-B aligned");
+    WinGeom g{(int)T, (int)H, (int)W, wt, wh, ww, st, sh, sw, (int)(T / wt), (int)(H / wh), (int)(W / ww)};
+    const int64_t nwin = B * g.nwt * g.nwh * g.nww;
+    if (nwin > 0x7fffffff || heads > 65535) return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d_mb: grid too large");
+    if (nwin * heads > 0x7fffffff) return fail(VC_ERR_INVALID_ARG, "vc_window_attention3d_mb: grid too large");
+    const int mk = (st | sh | sw) ? 1 : 0;
+    window_attn_mb_d32_kernel<<<(unsigned)(nwin * heads), 256, 0, stream>>>(qkv, ld, g, (int)heads, vol, (int)np, biasB, mk, out, ldo);
+    return check_launch("vc_window_attention3d_mb");
 }
 
 int vc_window_attention3d_lse(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T, int64_t H, int64_t W,

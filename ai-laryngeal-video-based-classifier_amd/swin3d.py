@@ -119,6 +119,47 @@ def expand_bias(table, full_window, window, device):
     return g.t().contiguous().view(heads, npad // 32, npad // 64, 2, 64, 16)
 
 
+_BIAS_MB_INDEX = {}
+MB_MASKED = -16384.0  # padded keys in the matrix-pipe bias (exp2 -> 0; finite, as the identity MFMA needs)
+
+
+def _bias_mb_gather_index(full_window, window, device):
+    """Flat gather index of expand_bias_mb's operand-fragment order into the table extended by two
+    rows: ntab (padded keys) and ntab + 1 (padded queries).  Built once per geometry."""
+    key = (tuple(full_window), tuple(window), str(device))
+    idx = _BIAS_MB_INDEX.get(key)
+    if idx is not None:
+        return idx
+    vol = window[0] * window[1] * window[2]
+    npad = _ru(vol, 64)
+    ntab = (2 * full_window[0] - 1) * (2 * full_window[1] - 1) * (2 * full_window[2] - 1)
+    rel = relative_position_index(full_window)[:vol, :vol]  # [q, k]
+    full = torch.full((npad, npad), ntab, dtype=torch.int64)  # [k, q]: padded keys
+    full[:, vol:] = ntab + 1                                  # padded queries
+    full[:vol, :vol] = rel.t()
+    ar = torch.arange
+    qb, t, kb, s, lane, m = torch.meshgrid(ar(npad // 32), ar(npad // 64), ar(2), ar(2), ar(64), ar(8), indexing="ij")
+    k = t * 64 + kb * 32 + s * 16 + 8 * (lane >> 5) + m
+    q = qb * 32 + (lane & 31)
+    idx = full[k, q].reshape(-1).to(device)
+    _BIAS_MB_INDEX[key] = idx
+    return idx
+
+
+def expand_bias_mb(table, full_window, window, device):
+    """Relative-position bias of one block as the bf16 B operand of the matrix-pipe bias
+    (vc_window_attention3d_mb): [heads, np/32, np/64, 2, 2, 64, 8], element [h][qb][t][kb][s][lane][m]
+    = log2 e * bias[h][q = 32qb + lane%32][k = 64t + 32kb + 16s + 8(lane//32) + m] (the same
+    torchvision bias as expand_bias), MB_MASKED on padded keys, 0 on padded queries."""
+    vol = window[0] * window[1] * window[2]
+    npad = _ru(vol, 64)
+    tab = table.to(device=device, dtype=torch.float32)
+    heads = tab.shape[1]
+    ext = torch.cat([tab * LOG2E, torch.tensor([[MB_MASKED] * heads, [0.0] * heads], device=device)])
+    g = ext.index_select(0, _bias_mb_gather_index(full_window, window, device))  # [slots, heads]
+    return g.t().to(torch.bfloat16).contiguous().view(heads, npad // 32, npad // 64, 2, 2, 64, 8)
+
+
 class Swin3d(torch.nn.Module):
     """fp32 master parameters in torchvision naming; bf16 / fp32 packed device copies."""
 
@@ -236,10 +277,12 @@ class Swin3d(torch.nn.Module):
         return pk
 
     def _biasT(self, s, i, window, device):
+        """Block (s, i)'s relative-position bias in the inference kernel's layout (expand_bias_mb:
+        bf16 operand fragments of vc_window_attention3d_mb), built once per packed weights."""
         key = (s, i, tuple(window), str(device))
         if key not in self._bias_cache:
             tab = self._packed["stages"][s]["blocks"][i]["table"]
-            self._bias_cache[key] = expand_bias(tab, self.cfg["window_size"], window, device)
+            self._bias_cache[key] = expand_bias_mb(tab, self.cfg["window_size"], window, device)
         return self._bias_cache[key]
 
     def geometry(self, B, T, H, W):

@@ -377,6 +377,18 @@ int vc_window_attention3d(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T,
                           int64_t head_dim, int wt, int wh, int ww, int st, int sh, int sw, const float* biasF,
                           int64_t np, uint16_t* out, int64_t ldo, hipStream_t stream);
 
+/*
+ * vc_window_attention3d with the bias and the shift mask on the matrix pipe (the inference path):
+ * biasB: bf16, the log2(e)-scaled bias as MFMA B-operand fragments [heads][np/32][np/64][2][2][64][8]:
+ * element [h][qb][t][kb][s][lane][m] = log2(e) * bias[h][q][k] with q = 32qb + lane%32,
+ * k = 64t + 32kb + 16s + 8(lane/32) + m; -16384 for k >= vol, 0 for q >= vol (swin3d.expand_bias_mb).
+ * The kernel adds it as S^T += I . Bias^T (identity A fragments) and the mask as a one-hot product
+ * (-16384 between shift regions; exp2 -> 0 as the f32 kernel's -inf).  Same arguments otherwise.
+ */
+int vc_window_attention3d_mb(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T, int64_t H, int64_t W,
+                             int64_t heads, int64_t head_dim, int wt, int wh, int ww, int st, int sh, int sw,
+                             const uint16_t* biasB, int64_t np, uint16_t* out, int64_t ldo, hipStream_t stream);
+
 /* Train-step forward: vc_window_attention3d plus lse[row * heads + head] = base-2 log-sum-exp of
  * each query's scores (row = its global token row), kept for the backward. */
 int vc_window_attention3d_lse(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T, int64_t H, int64_t W,

@@ -24,9 +24,11 @@ def _gpu():
     _lib.load()
 
 
-def _window_case(B, grid, C, window, shift, seed, qmul=1.0):
+def _window_case(B, grid, C, window, shift, seed, qmul=1.0, mb=False):
     """Oracle attention (qkv from x, identity proj) vs qkv GEMM-free kernel call; qmul scales the q
-    projection (qmul >> 1: scores far beyond exp2's range, the kernel's exact-max fallback)."""
+    projection (qmul >> 1: scores far beyond exp2's range, the kernel's exact-max fallback); mb:
+    the inference kernel with bias and shift mask on the matrix pipe (bf16 bias operand,
+    swin3d.expand_bias_mb) instead of the f32 C-operand bias."""
     from vclip_amd import ops
     g = torch.Generator().manual_seed(seed)
     heads = C // 32
@@ -44,9 +46,9 @@ def _window_case(B, grid, C, window, shift, seed, qmul=1.0):
     qkv = x.reshape(-1, C) @ p["a.qkv.weight"].T + p["a.qkv.bias"]
     qkv[:, :C] *= 32 ** -0.5 * ops.LOG2E
     qkv_d = qkv.bfloat16().to(DEV)
-    from vclip_amd.swin3d import expand_bias
+    from vclip_amd.swin3d import expand_bias, expand_bias_mb
     w_eff, s_eff = ref.window_and_shift(grid, window, shift)
-    biasT = expand_bias(p["a.relative_position_bias_table"], window, w_eff, torch.device(DEV))
+    biasT = (expand_bias_mb if mb else expand_bias)(p["a.relative_position_bias_table"], window, w_eff, torch.device(DEV))
     out = torch.zeros(B * T * H * W + 8, C, dtype=torch.bfloat16, device=DEV)
     ops.window_attention3d(qkv_d, B, grid, heads, w_eff, s_eff, biasT, out)
     got = out[:B * T * H * W].float().cpu().reshape(B, T, H, W, C)
@@ -61,8 +63,9 @@ def _window_case(B, grid, C, window, shift, seed, qmul=1.0):
     (1, (16, 7, 7), 64, (8, 7, 7), (4, 3, 3)),   # window == feature size in h, w: shift dropped there
     (1, (2, 6, 6), 32, (2, 3, 3), (1, 1, 1)),    # t == window: t shift dropped
 ])
-def test_window_attention3d(B, grid, C, window, shift):
-    got, want = _window_case(B, grid, C, window, shift, seed=C + sum(shift))
+@pytest.mark.parametrize("mb", [False, True])
+def test_window_attention3d(B, grid, C, window, shift, mb):
+    got, want = _window_case(B, grid, C, window, shift, seed=C + sum(shift), mb=mb)
     # 2e-2 absolute plus one bf16 step of the output itself (outputs reach |o| ~ 5, where one bf16
     # step is 2^-5: the rounding of the stored output alone can exceed a flat 2e-2)
     excess = ((got - want).abs() - (2e-2 + want.abs() / 128)).max().item()
@@ -70,12 +73,13 @@ def test_window_attention3d(B, grid, C, window, shift):
 
 
 @pytest.mark.parametrize("qmul", [8.0, 25.0, 80.0])
-def test_window_attention3d_large_scores(qmul):
+@pytest.mark.parametrize("mb", [False, True])
+def test_window_attention3d_large_scores(qmul, mb):
     """Scores tens to hundreds of log2 units apart: P up to ~2^30 on the max-free pass (8), row sums
     beyond 2^64 (25) and exp2 overflow (80) send the wave to the deferred-max pass.  The q rows are
     rounded to bf16 AFTER the scale, so a score error of ~|s| 2^-9 is inherent at these magnitudes
     (nearly one-hot rows can flip): the bar is finiteness and a small mean error."""
-    got, want = _window_case(1, (4, 6, 6), 64, (2, 3, 3), (1, 1, 1), seed=11, qmul=qmul)
+    got, want = _window_case(1, (4, 6, 6), 64, (2, 3, 3), (1, 1, 1), seed=11, qmul=qmul, mb=mb)
     assert torch.isfinite(got).all()
     err = (got - want).abs().mean().item()
     # at qmul 80 (|s| in the hundreds) the deferred-max kernel of the previous build measured the
