@@ -27,7 +27,8 @@
 //   * S'^T accumulator registers feed P.V directly as the B operand of O^T = V^T . P^T
 //     (§3 "An accumulator tile as the next MFMA's operand"); P never touches LDS;
 //   * software pipeline inside each wave: the QK^T MFMAs of tile t+1 are issued before
-//     tile t's softmax, so the MFMA pipe runs them while the VALU does exp2/sum/cvt;
+//     tile t's softmax, so the MFMA pipe runs them while the VALU does exp2/cvt (inference:
+//     pinned by sched_barrier fences, see iter());
 //   * output rows widened to 16-byte stores with v_permlane32_swap (T21).
 #include "common.hpp"
 
@@ -352,15 +353,69 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
         // NEXT: 0 = tile t+1 is a full tile, 1 = tile t+1 may be partial (masked), 2 = t is last.
         // In the unrolled main loop the slots are compile-time constants, so every LDS address is
         // a loop-invariant per-lane VGPR plus an immediate offset.
+        // V^T fragments of 16-key step g (key rows 16g .. 16g + 15 of the slot) for d-blocks 0 / 1
+        auto vread = [&](const char* slot, int g, v8s (&vv)[2]) {
+#pragma unroll
+            for (int db = 0; db < 2; ++db) {
+                const char* pa = slot + voff[db] + g * 16 * 128;
+                const v4s va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)pa);
+                const v4s vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(pa + 8 * 128));
+                vv[db][0] = va[0]; vv[db][1] = va[1]; vv[db][2] = va[2]; vv[db][3] = va[3];
+                vv[db][4] = vb[0]; vv[db][5] = vb[1]; vv[db][6] = vb[2]; vv[db][7] = vb[3];
+            }
+        };
         auto iter = [&](auto next_c, const char* slot, const char* nslot, int t) {
             constexpr int NEXT = decltype(next_c)::value;
+            // PIPE (inference, full next tile): the in-wave software pipeline pinned by sched_barrier
+            // fences.  Left to itself hipcc sank tile t+1's QK^T MFMAs below tile t's P.V (ISA of
+            // round 2's build): the 8 QK^T MFMAs ran back to back with this wave's VALU idle, and the
+            // 32 exp2 stalled the P.V MFMAs that consume them.  Phase A: per k-step the next k-step's
+            // K fragments (after the last one: the first 16-key step's V^T), then tile t+1's two QK^T
+            // MFMAs with 3 exp2 of tile t in each one's shadow (8 + 3 x 8 issue cycles ~ one 32-cycle
+            // MFMA); phase B: per 16-key step the next step's V^T reads, P.V (2) + row sum (1), then
+            // the next step's 4 P packs.  Bit-identical; ViViT-B B = 8 247.8 -> 244.2 us, B = 4
+            // 133.9 -> 129.7 us per launch (tools/ab_attn.py, interleaved in one process, round 3;
+            // fences around every MFMA as well: 245.1 / 129.0, not kept).
+            constexpr bool PIPE = !WLSE && !RB && NEXT == 0 && QB == 1;
             if (t + NS - 1 < ntiles) stage(t + NS - 1);
             v16f snext[QB][2];
-            if constexpr (NEXT == 0) qk_mfma(nslot, snext);
-            else if constexpr (NEXT == 1) qk(nslot, t + 1, snext);
+            v8s vcur[2], vnxt[2];  // PIPE: V^T fragments (d-blocks 0 / 1) of the current / next 16-key step
+            if constexpr (PIPE) {
+                // exp2 of tile t's scores in 16-key-step order (step g = regs 8 (g & 1) .. of key block
+                // g >> 1), so step g's P can be packed as soon as its 8 exp2 are done
+                auto ex = [&](int i) { scur[0][i >> 4][i & 15] = __builtin_amdgcn_exp2f(scur[0][i >> 4][i & 15]); };
+                v8s ka = *reinterpret_cast<const v8s*>(nslot + koff[0]);
+                v8s kb = *reinterpret_cast<const v8s*>(nslot + koff[0] + 4096);
+                ex(0); ex(1); ex(2); ex(3);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    v8s na, nb;
+                    if (kk < 3) {
+                        na = *reinterpret_cast<const v8s*>(nslot + koff[kk + 1]);
+                        nb = *reinterpret_cast<const v8s*>(nslot + koff[kk + 1] + 4096);
+                    } else {
+                        vread(slot, 0, vcur);
+                    }
+                    snext[0][0] = mfma32x16<ET>(ka, qf[0][kk], kk == 0 ? minit[0] : snext[0][0]);
+                    ex(4 + 6 * kk); ex(5 + 6 * kk); ex(6 + 6 * kk);
+                    snext[0][1] = mfma32x16<ET>(kb, qf[0][kk], kk == 0 ? minit[0] : snext[0][1]);
+                    ex(7 + 6 * kk); ex(8 + 6 * kk); ex(9 + 6 * kk);
+                    ka = na;
+                    kb = nb;
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                ex(28); ex(29); ex(30); ex(31);
+            } else if constexpr (NEXT == 0) {
+                qk_mfma(nslot, snext);
+            } else if constexpr (NEXT == 1) {
+                qk(nslot, t + 1, snext);
+            }
 
             // ---- online softmax: scores are relative to the running max already
-            if constexpr (WLSE) {
+            if constexpr (PIPE) {
+                // exp2 done in phase A
+            } else if constexpr (WLSE) {
                 // deferred max: every P is >= 0, so a partial row sum <= LIM bounds every P of
                 // the tile by LIM (an overflow shows up as inf); only when it fails is tile t
                 // recomputed against an exact re-based max
@@ -387,6 +442,32 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
             //      every V^T fragment read from LDS feeds QB MFMAs; inference also feeds the
             //      fragment to the row-sum MFMA
             const bool pv_kb1 = NEXT != 2 || t * AK + 32 < S;
+            if constexpr (PIPE) {
+                // 16-key step g: step g + 1's V^T reads, then step g's P.V (2) and row-sum MFMAs, then
+                // step g + 1's P packs (in the MFMAs' shadow); one scheduling group per step
+                auto pack = [&](int g) {
+                    v4u pu;
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj)
+                        pu[jj] = pack2<ET>(scur[0][g >> 1][8 * (g & 1) + 2 * jj], scur[0][g >> 1][8 * (g & 1) + 2 * jj + 1]);
+                    return __builtin_bit_cast(v8s, pu);
+                };
+                v8s pf = pack(0);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    if (g < 3) vread(slot, g + 1, vnxt);
+                    o[0][0] = mfma32x16<ET>(vcur[0], pf, o[0][0]);
+                    o[0][1] = mfma32x16<ET>(vcur[1], pf, o[0][1]);
+                    lsum[0] = mfma16x32<ET>(sel, pf, lsum[0]);
+                    if (g < 3) {
+                        pf = pack(g + 1);
+                        vcur[0] = vnxt[0];
+                        vcur[1] = vnxt[1];
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            } else
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb)
 #pragma unroll

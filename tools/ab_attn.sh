@@ -9,5 +9,7 @@ out=$root/ab/attn; mkdir -p "$out"
 inc="-I $root/include -I $root/ai-laryngeal-video-based-classifier_amd/csrc"
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $inc -Wno-unused-result "$@" -c "$src" -o "$out/$name.o" 2>/dev/null
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -c "$root/tools/ab_attn_stub.cpp" -o "$out/stub.o"
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$out/$name.so" "$out/$name.o" "$out/stub.o"
+# attention.hip dispatches S <= 256 to attention_short.hip's launcher: link the tree's copy
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $inc -c "$root/ai-laryngeal-video-based-classifier_amd/csrc/attention_short.hip" -o "$out/short.o" 2>/dev/null
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$out/$name.so" "$out/$name.o" "$out/short.o" "$out/stub.o"
 echo "$out/$name.so"
