@@ -50,11 +50,13 @@ __device__ __forceinline__ v8bf tr_frag(const char* tile, int offa, int offb) {
     return __builtin_bit_cast(v8bf, vv);
 }
 
+// regs 8 s2 .. 8 s2 + 7 of an accumulator as an MFMA operand: four v_cvt_pk_bf16_f32 (RNE, as the
+// element-wise cast, which hipcc lowered to conversions plus v_perm / v_alignbit repacking)
 __device__ __forceinline__ v8bf to_bf8(const v16f& x, int s2) {
-    v8bf f;
+    v4u u;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = (__bf16)x[8 * s2 + j];
-    return f;
+    for (int j = 0; j < 4; ++j) u[j] = pack2bf(x[8 * s2 + 2 * j], x[8 * s2 + 2 * j + 1]);
+    return __builtin_bit_cast(v8bf, u);
 }
 
 // per-lane LDS byte offsets of the transposed reads (rows 4h + tq and +8), per 32-column block
@@ -221,25 +223,21 @@ attn_bwd_dkdv_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const uint16_
         const char* di = cur + TILE_BYTES;
         const float* fl = reinterpret_cast<const float*>(cur + 2 * TILE_BYTES);  // [0,64) lse, [64,128) Delta
         if (t + 1 < nt) ABWD_LOAD_A(t + 1);
+        // the two 32-query blocks' chains interleaved (sched_barrier fences pin the group order):
+        // QK0 + dP0 | QK1 || exp0 | dV0 || dS0 | dP1 || exp1 | dK0 || dS1 | dV1 | dK1
+        v16f s0, dp0, s1, dp1;
 #pragma unroll
-        for (int qb = 0; qb < 2; ++qb) {
-            // accumulator inits: register 4g+e holds query 32qb + 8g + 4h + e
-            v16f s, dp;
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float4 L = *reinterpret_cast<const float4*>(fl + qb * 32 + 8 * g + 4 * h);
-                const float4 Dl = *reinterpret_cast<const float4*>(fl + 64 + qb * 32 + 8 * g + 4 * h);
-                s[4 * g + 0] = L.x; s[4 * g + 1] = L.y; s[4 * g + 2] = L.z; s[4 * g + 3] = L.w;
-                dp[4 * g + 0] = Dl.x; dp[4 * g + 1] = Dl.y; dp[4 * g + 2] = Dl.z; dp[4 * g + 3] = Dl.w;
-            }
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-                s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(qi, qb * 4096 + roff[kk]), kf[kk], s, 0, 0, 0);
-            // P = exp2(S - lse[q])
-            v16f p;
-#pragma unroll
-            for (int e = 0; e < 16; ++e) p[e] = __builtin_amdgcn_exp2f(s[e]);
-            // dV^T += dO^T . P
+        for (int g = 0; g < 4; ++g) {
+            const float4 L0 = *reinterpret_cast<const float4*>(fl + 8 * g + 4 * h);
+            const float4 D0 = *reinterpret_cast<const float4*>(fl + 64 + 8 * g + 4 * h);
+            const float4 L1 = *reinterpret_cast<const float4*>(fl + 32 + 8 * g + 4 * h);
+            const float4 D1 = *reinterpret_cast<const float4*>(fl + 64 + 32 + 8 * g + 4 * h);
+            s0[4 * g + 0] = L0.x; s0[4 * g + 1] = L0.y; s0[4 * g + 2] = L0.z; s0[4 * g + 3] = L0.w;
+            dp0[4 * g + 0] = D0.x; dp0[4 * g + 1] = D0.y; dp0[4 * g + 2] = D0.z; dp0[4 * g + 3] = D0.w;
+            s1[4 * g + 0] = L1.x; s1[4 * g + 1] = L1.y; s1[4 * g + 2] = L1.z; s1[4 * g + 3] = L1.w;
+            dp1[4 * g + 0] = D1.x; dp1[4 * g + 1] = D1.y; dp1[4 * g + 2] = D1.z; dp1[4 * g + 3] = D1.w;
+        }
+        auto dv_mfma = [&](int qb, const v16f& p) {
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
                 const v8bf pf = to_bf8(p, s2);
@@ -249,24 +247,47 @@ attn_bwd_dkdv_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const uint16_
                     dv[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(di, tro.a[db] + kr, tro.b[db] + kr), pf,
                                                                      dv[db], 0, 0, 0);
             }
-            // dP - Delta = dO . V^T - Delta[q]
-#pragma unroll
-            for (int kk = 0; kk < 4; ++kk)
-                dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(di, qb * 4096 + roff[kk]), vf[kk], dp, 0, 0, 0);
-            // dS = P o (dP - Delta)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) dp[e] = p[e] * dp[e];
-            // dK^T += Q'^T . dS
+        };
+        auto dk_mfma = [&](int qb, const v16f& ds) {
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
-                const v8bf sf = to_bf8(dp, s2);
+                const v8bf sf = to_bf8(ds, s2);
                 const int kr = (qb * 32 + 16 * s2) * 128;
 #pragma unroll
                 for (int db = 0; db < 2; ++db)
                     dk[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(qi, tro.a[db] + kr, tro.b[db] + kr), sf,
                                                                      dk[db], 0, 0, 0);
             }
-        }
+        };
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+            s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(qi, roff[kk]), kf[kk], s0, 0, 0, 0);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+            dp0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(di, roff[kk]), vf[kk], dp0, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+            s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(qi, 4096 + roff[kk]), kf[kk], s1, 0, 0, 0);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) s0[e] = __builtin_amdgcn_exp2f(s0[e]);
+        __builtin_amdgcn_sched_barrier(0);
+        dv_mfma(0, s0);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) dp0[e] = s0[e] * dp0[e];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+            dp1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(di, 4096 + roff[kk]), vf[kk], dp1, 0, 0, 0);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) s1[e] = __builtin_amdgcn_exp2f(s1[e]);
+        __builtin_amdgcn_sched_barrier(0);
+        dk_mfma(0, dp0);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) dp1[e] = s1[e] * dp1[e];
+        __builtin_amdgcn_sched_barrier(0);
+        dv_mfma(1, s1);
+        dk_mfma(1, dp1);
         if (t + 1 < nt) ABWD_STORE_A(smem + ((t + 1) & 1) * SLOT_A);
         __syncthreads();
     }
@@ -350,44 +371,60 @@ attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const uint16_t*
     ABWD_STORE_B(smem);
     __syncthreads();
 
-    // accumulator inits: S^T - lse (keys past S of the last tile: -inf, i.e. P = 0) and dP^T - Delta;
-    // register 4g+e of key block kb holds key t*64 + 32kb + 8g + 4h + e
-    v16f negL, negD, negL_last[2];
-    const int klast = (nt - 1) * 64;
+    // accumulator inits: S^T - lse and dP^T - Delta; register 4g+e of key block kb holds key
+    // t*64 + 32kb + 8g + 4h + e (keys past S of the last tile are set to -inf after the MFMAs, P = 0)
+    v16f negL, negD;
 #pragma unroll
     for (int e = 0; e < 16; ++e) {
         negL[e] = -lq;
         negD[e] = -dq_delta;
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-            negL_last[kb][e] = klast + kb * 32 + 8 * (e >> 2) + 4 * h + (e & 3) < S ? -lq : -INFINITY;
     }
+    auto dq_mfma = [&](const char* ki, int kb, const v16f& ds) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const v8bf sf = to_bf8(ds, s2);
+            const int kr = (kb * 32 + 16 * s2) * 128;
+#pragma unroll
+            for (int db = 0; db < 2; ++db)
+                dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(ki, tro.a[db] + kr, tro.b[db] + kr), sf, dq[db],
+                                                                 0, 0, 0);
+        }
+    };
     for (int t = 0; t < nt; ++t) {
         const char* ki = smem + (t & 1) * SLOT_B;
         const char* vi = ki + TILE_BYTES;
         if (t + 1 < nt) ABWD_LOAD_B(t + 1);
-        const bool last = t == nt - 1;
+        // the two 32-key blocks' chains interleaved (sched_barrier fences pin the group order):
+        // S0, dP0 | S1, dP1 || dS0 = exp2(S0) dP0 | dQ0 || dS1 | dQ1
+        v16f st0 = negL, dpt0 = negD, st1 = negL, dpt1 = negD;
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-            v16f st = last ? negL_last[kb] : negL, dpt = negD;
+        for (int kk = 0; kk < 4; ++kk) {
+            st0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(ki, roff[kk]), qf[kk], st0, 0, 0, 0);
+            dpt0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(vi, roff[kk]), df[kk], dpt0, 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int kk = 0; kk < 4; ++kk) {
-                st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(ki, kb * 4096 + roff[kk]), qf[kk], st, 0, 0, 0);
-                dpt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(vi, kb * 4096 + roff[kk]), df[kk], dpt, 0, 0, 0);
-            }
-            // dS^T = P^T o (dP^T - Delta)
+        for (int kk = 0; kk < 4; ++kk) {
+            st1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(ki, 4096 + roff[kk]), qf[kk], st1, 0, 0, 0);
+            dpt1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(row_frag(vi, 4096 + roff[kk]), df[kk], dpt1, 0, 0, 0);
+        }
+        if (t == nt - 1) {
+            const int k0 = t * 64;
 #pragma unroll
-            for (int e = 0; e < 16; ++e) st[e] = __builtin_amdgcn_exp2f(st[e]) * dpt[e];
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                const v8bf sf = to_bf8(st, s2);
-                const int kr = (kb * 32 + 16 * s2) * 128;
-#pragma unroll
-                for (int db = 0; db < 2; ++db)
-                    dq[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag(ki, tro.a[db] + kr, tro.b[db] + kr), sf,
-                                                                     dq[db], 0, 0, 0);
+            for (int e = 0; e < 16; ++e) {
+                if (k0 + 8 * (e >> 2) + 4 * h + (e & 3) >= S) st0[e] = -INFINITY;
+                if (k0 + 32 + 8 * (e >> 2) + 4 * h + (e & 3) >= S) st1[e] = -INFINITY;
             }
         }
+        // dS^T = P^T o (dP^T - Delta)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) st0[e] = __builtin_amdgcn_exp2f(st0[e]) * dpt0[e];
+        __builtin_amdgcn_sched_barrier(0);
+        dq_mfma(ki, 0, st0);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) st1[e] = __builtin_amdgcn_exp2f(st1[e]) * dpt1[e];
+        __builtin_amdgcn_sched_barrier(0);
+        dq_mfma(ki, 1, st1);
         if (t + 1 < nt) ABWD_STORE_B(smem + ((t + 1) & 1) * SLOT_B);
         __syncthreads();
     }
