@@ -302,8 +302,9 @@ FAMILIES = {
                     "ashort::attn_short_d64_kernel<0, 7>"),
     "swin": ("clips/sec fwd Video Swin-T 32x224^2 bf16", 175.53, 4,
              "Video Swin-T 3D shifted-window attention, 32x224x224 clips, batch 4 per GPU = 32 over DP=8 "
-             "(BASELINE configs[3])", "window_attn_d32_kernel (all 12 blocks, head_dim 32)",
-             "window_attn_d32_kernel<false>"),
+             "(BASELINE configs[3])", "window_attn_mb_d32_kernel (all 12 blocks, head_dim 32; relative-position bias "
+             "and shift mask on the matrix pipe)",
+             "window_attn_mb_d32_kernel"),
 }
 
 
