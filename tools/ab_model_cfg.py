@@ -1,0 +1,46 @@
+"""Interleaved A/B of ViViT-B forward GEMM tile choices in one process (cdna_hip_programming.md §5.4
+rule 24): python tools/ab_model_cfg.py '{}' '{"o_proj": 7, "fc2": 7}' [--B 8] [--streams 2] —
+times model.forward_logits under each model.gemm_cfg in alternating rounds; logits must match."""
+import argparse
+import json
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+from vclip_amd.vivit import create_model  # noqa: E402
+from vclip_amd.weights import make_synthetic_clips  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("cfgs", nargs="+")
+ap.add_argument("--B", type=int, default=8)
+ap.add_argument("--streams", type=int, default=2)
+ap.add_argument("--rounds", type=int, default=8)
+a = ap.parse_args()
+dev = torch.device("cuda", 0)
+pix = torch.from_numpy(make_synthetic_clips(a.B, 32, 224, seed=1)).to(dev)
+m = create_model(num_frames=32, device=dev)
+m.concurrent_streams = a.streams
+cfgs = [json.loads(c) for c in a.cfgs]
+outs = []
+for c in cfgs:
+    m.gemm_cfg = c
+    outs.append(m.forward_logits(pix).clone())
+print("logits identical:", [bool(torch.equal(o, outs[0])) for o in outs], flush=True)
+res = [[] for _ in cfgs]
+for r in range(a.rounds):
+    for i in (range(len(cfgs)) if r % 2 == 0 else reversed(range(len(cfgs)))):
+        m.gemm_cfg = cfgs[i]
+        for _ in range(2):
+            m.forward_logits(pix)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(10):
+            m.forward_logits(pix)
+        torch.cuda.synchronize()
+        res[i].append((time.perf_counter() - t0) / 10 * 1e3)
+for c, t in zip(a.cfgs, res):
+    print(f"gemm_cfg={c}: median {np.median(t):.3f} ms/step  min {min(t):.3f}  ({a.B / np.median(t) * 1e3:.1f} clips/s)",
+          flush=True)
