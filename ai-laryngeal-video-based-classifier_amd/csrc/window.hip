@@ -468,6 +468,26 @@ window_attn_mb_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom 
 #pragma unroll
         for (int j = 0; j < 4; ++j) bf[j] = bq[j * 64];
     };
+    // S'^T of 32 keys (key block kb of tile t): (mask) + bias + K . Q'^T
+    auto scores_kb = [&](auto mixed_c, const QBlock& Q, int t, const v8s (&bf)[4], int kb) __attribute__((always_inline)) {
+        constexpr bool MIXED = decltype(mixed_c)::value;
+        v16f acc = v16f{};
+        if constexpr (MIXED) {
+            const v8s km = *reinterpret_cast<const v8s*>(kon + (t * 64 + kb * 32 + rr) * 32 + h * 16);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf, km), __builtin_bit_cast(v8bf, Q.qm),
+                                                          acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf, ident[s2]),
+                                                          __builtin_bit_cast(v8bf, bf[kb * 2 + s2]), acc, 0, 0, 0);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const v8bf kf = __builtin_bit_cast(v8bf, *reinterpret_cast<const v8s*>(Ks + (t * 64 + kb * 32) * 64 + koff[kk]));
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, Q.qf[kk], acc, 0, 0, 0);
+        }
+        return acc;
+    };
     // S'^T of 64 keys: (mask) + bias + K . Q'^T
     auto scores = [&](auto mixed_c, const QBlock& Q, int t, const v8s (&bf)[4], v16f (&sc)[2]) __attribute__((always_inline)) {
         constexpr bool MIXED = decltype(mixed_c)::value;
@@ -512,6 +532,24 @@ window_attn_mb_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom 
                 o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf, vv), pf, o, 0, 0, 0);
                 if (lsum) *lsum = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf, *lsum, 0, 0, 0);
             }
+    };
+    // the same for key block kb only (the fast pass's pipelined order; accumulation order unchanged)
+    auto pv_kb = [&](int t, const v16f& p, int kb, v4f& lsum) __attribute__((always_inline)) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            v4u pu;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) pu[jj] = pack2bf(p[8 * s2 + 2 * jj], p[8 * s2 + 2 * jj + 1]);
+            const v8bf pf = __builtin_bit_cast(v8bf, pu);
+            const char* pa = Vs + (t * 64 + kb * 32 + 16 * s2) * 64 + voff;
+            const v4s va = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)pa);
+            const v4s vb = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(pa + 8 * 64));
+            v8s vv;
+            vv[0] = va[0]; vv[1] = va[1]; vv[2] = va[2]; vv[3] = va[3];
+            vv[4] = vb[0]; vv[5] = vb[1]; vv[6] = vb[2]; vv[7] = vb[3];
+            o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8bf, vv), pf, o, 0, 0, 0);
+            lsum = __builtin_amdgcn_mfma_f32_16x16x32_bf16(sel, pf, lsum, 0, 0, 0);
+        }
     };
     // exact pass of one block (rare: a row sum outside [2^-64, 2^64], inf / NaN): the deferred
     // running max fixed by tile 0, re-based on a tile's exact max when a lane's partial row sum
@@ -596,14 +634,20 @@ window_attn_mb_d32_kernel(const uint16_t* __restrict__ qkv, int64_t ld, WinGeom 
                     load_qblock(qb + 4, nxt);
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                v16f sc[2];
-                scores(mixed_c, cur, t, bcur, sc);
-                v16f p[2];
+                // key block 1's score MFMAs run under key block 0's exp2, key block 0's P.V under
+                // key block 1's exp2 (sched_barrier fences pin the groups; hipcc had issued every
+                // score MFMA of the tile before the first exp2)
+                v16f s0 = scores_kb(mixed_c, cur, t, bcur, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                v16f s1 = scores_kb(mixed_c, cur, t, bcur, 1);
 #pragma unroll
-                for (int kb = 0; kb < 2; ++kb)
+                for (int e = 0; e < 16; ++e) s0[e] = __builtin_amdgcn_exp2f(s0[e]);
+                __builtin_amdgcn_sched_barrier(0);
+                pv_kb(t, s0, 0, lsum);
 #pragma unroll
-                    for (int e = 0; e < 16; ++e) p[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e]);
-                pv(t, p, &lsum);
+                for (int e = 0; e < 16; ++e) s1[e] = __builtin_amdgcn_exp2f(s1[e]);
+                __builtin_amdgcn_sched_barrier(0);
+                pv_kb(t, s1, 1, lsum);
                 if (!last || more) {
 #pragma unroll
                     for (int j = 0; j < 4; ++j) bcur[j] = bnxt[j];

@@ -58,4 +58,15 @@ for _ in range(3):
         step()
     torch.cuda.synchronize()
     ts.append((time.perf_counter() - t0) / (steps // 3) * 1e3)
-print(f"{path} {mode}: {min(ts):.3f} ms/step (min of 3), {B / min(ts) * 1e3:.1f} clips/s", flush=True)
+extra = ""
+if mode in ("swin", "fwd", "timesformer") and hasattr(m, "kernel_events"):
+    # mean attention launch (HIP events on the launching stream; one stream)
+    m.concurrent_streams = 1
+    evs = []
+    m.kernel_events = evs
+    for _ in range(3):
+        step()
+    m.kernel_events = None
+    torch.cuda.synchronize()
+    extra = f", attention {np.mean([e[0].elapsed_time(e[1]) for e in evs]) * 1e3:.1f} us/launch"
+print(f"{path} {mode}: {min(ts):.3f} ms/step (min of 3), {B / min(ts) * 1e3:.1f} clips/s{extra}", flush=True)
