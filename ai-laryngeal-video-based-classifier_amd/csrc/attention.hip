@@ -376,7 +376,7 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
             // the next step's 4 P packs.  Bit-identical; ViViT-B B = 8 247.8 -> 244.2 us, B = 4
             // 133.9 -> 129.7 us per launch (tools/ab_attn.py, interleaved in one process, round 3;
             // fences around every MFMA as well: 245.1 / 129.0, not kept).
-            constexpr bool PIPE = !WLSE && !RB && NEXT == 0 && QB == 1;
+            constexpr bool PIPE = !RB && NEXT == 0 && QB == 1;
             if (t + NS - 1 < ntiles) stage(t + NS - 1);
             v16f snext[QB][2];
             v8s vcur[2], vnxt[2];  // PIPE: V^T fragments (d-blocks 0 / 1) of the current / next 16-key step
@@ -414,7 +414,18 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
 
             // ---- online softmax: scores are relative to the running max already
             if constexpr (PIPE) {
-                // exp2 done in phase A
+                // exp2 done in phase A; the training forward's f32 row sums and grown-max check follow
+                if constexpr (WLSE) {
+                    v2f ps[QB];
+                    psum(scur, ps);
+                    if (__any(!(ps[0][0] + ps[0][1] <= LIM))) {
+                        qk(slot, t, scur);
+                        rebase(next_c, scur, snext);
+                        exp_all(scur);
+                        psum(scur, ps);
+                    }
+                    l_run[0] += ps[0];
+                }
             } else if constexpr (WLSE) {
                 // deferred max: every P is >= 0, so a partial row sum <= LIM bounds every P of
                 // the tile by LIM (an overflow shows up as inf); only when it fails is tile t
@@ -459,7 +470,7 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
                     if (g < 3) vread(slot, g + 1, vnxt);
                     o[0][0] = mfma32x16<ET>(vcur[0], pf, o[0][0]);
                     o[0][1] = mfma32x16<ET>(vcur[1], pf, o[0][1]);
-                    lsum[0] = mfma16x32<ET>(sel, pf, lsum[0]);
+                    if constexpr (!WLSE) lsum[0] = mfma16x32<ET>(sel, pf, lsum[0]);
                     if (g < 3) {
                         pf = pack(g + 1);
                         vcur[0] = vnxt[0];

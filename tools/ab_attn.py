@@ -16,19 +16,25 @@ ap.add_argument("--rounds", type=int, default=12)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--B", type=int, default=8)
 ap.add_argument("--S", type=int, default=3137)  # 197 with --B 128: TimeSformer-B spatial attention at B=16
+ap.add_argument("--lse", action="store_true", help="time the training forward vc_attention_fwd_lse")
 a = ap.parse_args()
 B, S, H = a.B, a.S, 12
 g = torch.Generator(device="cuda").manual_seed(0)
 qkv = (torch.randn(B * S, 3 * H * 64, device="cuda", generator=g) * 1.5).bfloat16()
 st = torch.cuda.current_stream()
 fns = []
+lse = torch.zeros(B * H * S, device="cuda", dtype=torch.float32)
 for p in a.libs:
     lib = ctypes.CDLL(os.path.abspath(p), mode=os.RTLD_LOCAL)
-    f = lib.vc_attention_fwd
+    f = lib.vc_attention_fwd_lse if a.lse else lib.vc_attention_fwd
     f.restype = ctypes.c_int
     f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
-                  ctypes.c_float, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
-    fns.append(f)
+                  ctypes.c_float, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64] + ([ctypes.c_void_p] if a.lse else []) + \
+                 [ctypes.c_void_p]
+    if a.lse:
+        fns.append(lambda q, ld, B_, S_, H_, d, sc, pre, o, ldo, s, f=f: f(q, ld, B_, S_, H_, d, sc, pre, o, ldo, lse.data_ptr(), s))
+    else:
+        fns.append(f)
 outs = []
 for f in fns:
     o = torch.zeros(B * S, H * 64, device="cuda", dtype=torch.bfloat16)
