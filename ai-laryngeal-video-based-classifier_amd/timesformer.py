@@ -99,6 +99,11 @@ class TimesformerForVideoClassification(torch.nn.Module):
         self._names = list(shapes.keys())
         self.kernel_events = None  # list: HIP events around each spatial-attention launch (bench.py)
         self.concurrent_streams = None  # n > 1: the inference batch split over n HIP streams
+        # tile config of the two 768 x 768 bf16-output projections per layer (temporal dense, spatial
+        # output): the 128x128 kernel (cfg 5), not vc_gemm's pick (the persistent 256x256 kernel,
+        # 297 tiles = 1.16 rounds of 256 CUs at B=16): 37.9 vs 46.9 us at M = 25344 and 24.7 vs 25.4
+        # at the two-stream M = 12800 (tools/ab_gemm_cfg.py, round 3); None: vc_gemm's pick
+        self.proj_cfg = 5
         self._streams = None
         self._split_out = {}
         for name, shape in shapes.items():
@@ -267,7 +272,7 @@ class TimesformerForVideoClassification(torch.nn.Module):
             ops.layernorm(X, L["lnt_g"], L["lnt_b"], eps, Hc, m=B * S)
             ops.gemm(Hc, L["w_qkv_t"], L["b_qkv_t"], "bias", QKV)
             ops.temporal_attention(QKV, B, P, T, Hn, scale, O, q_prescaled=True)
-            ops.gemm(O, L["w_t"], L["b_t"], "bias", Yb)
+            ops.gemm(O, L["w_t"], L["b_t"], "bias", Yb, cfg=-1 if self.proj_cfg is None else self.proj_cfg)
             # spatial branch (frame layout)
             ops.divided_add_layernorm(X, Yb, B, P, T, L["ln1_g"], L["ln1_b"], eps, "temporal_to_spatial", Hf)
             ops.gemm(Hf, L["w_qkv_s"], L["b_qkv_s"], "bias", QKV)
@@ -281,7 +286,7 @@ class TimesformerForVideoClassification(torch.nn.Module):
                 # flop, algorithmic bytes (q, k, v read and the output written once: 4 x 64 x 2 B
                 # per token-head)
                 ev.append((e0, e1, 4.0 * (1 + P) * (1 + P) * 64 * Hn * B * T, 512.0 * (1 + P) * Hn * B * T))
-            ops.gemm(O, L["w_o"], L["b_o"], "bias", Yb)
+            ops.gemm(O, L["w_o"], L["b_o"], "bias", Yb, cfg=-1 if self.proj_cfg is None else self.proj_cfg)
             # MLP (clip layout)
             ops.divided_add_layernorm(X, Yb, B, P, T, L["ln2_g"], L["ln2_b"], eps, "spatial_to_mlp", Hc)
             ops.gemm(Hc, L["w_1"], L["b_1"], act, Hd)
