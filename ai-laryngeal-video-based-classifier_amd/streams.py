@@ -33,3 +33,43 @@ def run_split(owner, x: torch.Tensor, ns: int, part_fn, num_labels: int) -> torc
     for i in range(ns):
         cur.wait_stream(owner._streams[i])
     return logits
+
+
+class GraphReplay:
+    """An inference forward captured once into a hipGraph (torch.cuda.CUDAGraph) and replayed.
+
+    One entry per key (the caller's input address / shape / strides / dtype plus whatever selects
+    the kernels: stream count, operand type, weights version).  A replay re-runs every kernel of
+    the forward on the CURRENT contents of the input it was captured on, so in-place updates of
+    that tensor are seen; the entry holds references to the input, the packed weights and the
+    workspaces the graph's kernels address (`keep()`, read after the capture), so none of them is
+    freed under it.  `run` returns the owner's logits buffer (overwritten by the next call), as the
+    eager forward does."""
+
+    def __init__(self, max_entries: int = 4):
+        self.max_entries = max_entries
+        self._entries = {}
+
+    def clear(self):
+        self._entries = {}
+
+    def run(self, key, x: torch.Tensor, forward, keep=lambda: ()):
+        e = self._entries.get(key)
+        if e is None:
+            if len(self._entries) >= self.max_entries:
+                self._entries = {}
+            dev = x.device
+            cur = torch.cuda.current_stream(dev)
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                forward(x)  # first launches (kernel attributes), packing and workspaces outside the capture
+            cur.wait_stream(side)
+            torch.cuda.synchronize(dev)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                out = forward(x)
+            e = self._entries[key] = (g, out, (x,) + tuple(keep()))
+        g, out, _ = e
+        g.replay()
+        return out

@@ -182,6 +182,10 @@ class Swin3d(torch.nn.Module):
         self.concurrent_streams = None  # n > 1: the inference batch split over n HIP streams
         self._streams = None
         self._split_out = {}
+        # True: the inference forward is captured once per input / configuration into a hipGraph and
+        # replayed (streams.GraphReplay); bit-identical logits
+        self.graph_replay = False
+        self._graphs = None
         self.stochastic_depth = True  # train step: torchvision's StochasticDepth on the residual branches
 
     def state_dict(self, *a, **k):
@@ -411,6 +415,18 @@ class Swin3d(torch.nn.Module):
         B, Cin = video.shape[0], video.shape[1]
         if Cin != 3:
             raise ValueError("video must be [B, 3, T, H, W]")
+        if self.graph_replay and self.kernel_events is None and not torch.cuda.is_current_stream_capturing():
+            from .streams import GraphReplay
+            if self._graphs is None:
+                self._graphs = GraphReplay()
+            key = (video.data_ptr(), tuple(video.shape), tuple(video.stride()), video.dtype, self.concurrent_streams,
+                   str(video.device), self._weights_version())
+            return self._graphs.run(key, video, self._forward_eager,
+                                    keep=lambda: (self._packed, self._ws, self._split_out))
+        return self._forward_eager(video)
+
+    def _forward_eager(self, video: torch.Tensor) -> torch.Tensor:
+        B = video.shape[0]
         ns = max(1, min(int(self.concurrent_streams or 1), B))
         if ns == 1:
             return self._forward_part(video, 0)

@@ -106,6 +106,10 @@ class TimesformerForVideoClassification(torch.nn.Module):
         self.proj_cfg = 5
         self._streams = None
         self._split_out = {}
+        # True: the inference forward is captured once per input / configuration into a hipGraph and
+        # replayed (streams.GraphReplay); bit-identical logits
+        self.graph_replay = False
+        self._graphs = None
         for name, shape in shapes.items():
             self.params[name.replace(".", "__")] = torch.nn.Parameter(torch.zeros(shape))
         self._packed = None
@@ -245,6 +249,19 @@ class TimesformerForVideoClassification(torch.nn.Module):
         if T != c.num_frames or H != c.image_size or W != c.image_size or C != c.num_channels:
             raise ValueError(f"pixel_values {tuple(pix.shape)} do not match config "
                              f"(T={c.num_frames}, C={c.num_channels}, {c.image_size}^2)")
+        if self.graph_replay and self.kernel_events is None and not torch.cuda.is_current_stream_capturing():
+            from .streams import GraphReplay
+            if self._graphs is None:
+                self._graphs = GraphReplay()
+            key = (pix.data_ptr(), tuple(pix.shape), tuple(pix.stride()), pix.dtype, self.concurrent_streams, self.proj_cfg,
+                   str(pix.device), self._weights_version())
+            return self._graphs.run(key, pix, self._forward_eager,
+                                    keep=lambda: (self._packed, self._ws, self._split_out))
+        return self._forward_eager(pix)
+
+    def _forward_eager(self, pix: torch.Tensor) -> torch.Tensor:
+        c = self.config
+        B = pix.shape[0]
         ns = max(1, min(int(self.concurrent_streams or 1), B))
         if ns == 1:
             return self._forward_part(pix, 0)

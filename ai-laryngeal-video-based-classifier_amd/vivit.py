@@ -26,6 +26,7 @@ import numpy as np
 import torch
 
 from . import ops
+from .streams import GraphReplay
 from .vivit_train import FlatLayout, TrainEngine, VivitTrainFn
 from .weights import vivit_param_shapes
 
@@ -116,6 +117,10 @@ class VivitForVideoClassification(torch.nn.Module):
         self.concurrent_streams = None  # None / 1: one stream; n > 1: batch split over n HIP streams
         self.last_streams = 1
         self.kernel_events = None
+        # True: the inference forward is captured once per input / configuration into a hipGraph
+        # and replayed (streams.GraphReplay); bit-identical logits
+        self.graph_replay = False
+        self._graphs = GraphReplay()
         # per-GEMM tile config override {"qkv" | "o_proj" | "fc1" | "fc2": vc_gemm cfg} (None / absent:
         # vc_gemm's own pick) and the GEMM / LayerNorm row count: "pad" = every padded row (Mpad),
         # "tight" = B*S rounded up to the tile height (the padding rows keep their initial zeros)
@@ -165,6 +170,7 @@ class VivitForVideoClassification(torch.nn.Module):
         self._packed = None
         self._ws = {}
         self._streams = None
+        self._graphs.clear()
         return out
 
     # ---- training (vclip_amd/vivit_train.py) --------------------------
@@ -352,6 +358,16 @@ class VivitForVideoClassification(torch.nn.Module):
         if T != c.num_frames or H != c.image_size or W != c.image_size or C != c.num_channels:
             raise ValueError(f"pixel_values {tuple(pix.shape)} do not match config "
                              f"(T={c.num_frames}, C={c.num_channels}, {c.image_size}^2)")
+        if self.graph_replay and self.kernel_events is None and not torch.cuda.is_current_stream_capturing():
+            key = (pix.data_ptr(), tuple(pix.shape), tuple(pix.stride()), pix.dtype, self.concurrent_streams,
+                   self.compute_dtype, self._weights_version(), tuple(sorted(self.gemm_cfg.items())), self.rows,
+                   self.round_split)
+            return self._graphs.run(key, pix, self._forward_eager, keep=lambda: (self._packed, self._ws))
+        return self._forward_eager(pix)
+
+    def _forward_eager(self, pix: torch.Tensor) -> torch.Tensor:
+        c = self.config
+        B = pix.shape[0]
         ns = self.concurrent_streams or 1
         ns = max(1, min(int(ns), B))
         self.last_streams = ns

@@ -354,6 +354,8 @@ def run_family(a, dist, rank, world, dev):
         model = create_model(model_size="tiny", device=dev)
         x = torch.from_numpy(make_synthetic_video(a.batch, 32, 224, seed=1 + rank)).to(dev)
 
+    model.graph_replay = bool(a.graph)
+
     def step():
         model.forward_logits(x)
 
@@ -370,6 +372,7 @@ def run_family(a, dist, rank, world, dev):
     # headline: the batch over `--streams` HIP streams; roofline: a one-stream pass with HIP events
     # around every attention launch (the fwd mode's scheme)
     dt = timed(a.streams)
+    model.graph_replay = False  # the passes below are event-instrumented or one-off calls
     evs = []
     dt1 = timed(1, evs)
     model.concurrent_streams = 1
@@ -402,7 +405,8 @@ def run_family(a, dist, rank, world, dev):
             "warmup": a.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (uint8 frames RandomState(1+rank) -> the family's processor affine; weights RandomState(0))",
-            "config": {"workload": workload, "global_batch": a.batch * world, "parallelism": f"dp{world}"},
+            "config": {"workload": workload, "global_batch": a.batch * world, "parallelism": f"dp{world}",
+                       "streams": a.streams, "hip_graph": bool(a.graph)},
             "logit_max_abs_err": err,
             "roofline": {"bound": bound, "kernel": kname,
                          "achieved": round(attn_gbs, 1) if bound == "hbm" else round(attn_tflops, 1),
@@ -514,6 +518,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=2,
                     help="fwd: concurrent HIP streams the batch is split over in the headline pass")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="inference modes: 1 = the headline forward replayed from its captured hipGraph "
+                         "(model.graph_replay; the event-instrumented roofline passes stay eager), 0 = eager")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)  # CPU test of the spawn path
     a = ap.parse_args()
     if a.batch is None:
@@ -559,6 +566,8 @@ def main():
     cfg = model.config
     pix = torch.from_numpy(make_synthetic_clips(a.batch, 32, 224, seed=1 + rank)).to(dev)
 
+    model.graph_replay = bool(a.graph)
+
     def step():
         model.forward_logits(pix)
 
@@ -578,6 +587,8 @@ def main():
     # every kernel is batch-invariant: logits bit-identical to one stream), nothing instrumented
     dt = timed(a.streams)
     streams = model.last_streams
+    graphed = model.graph_replay
+    model.graph_replay = False  # the event-instrumented passes and one-off calls below run eagerly
     # the kernel roofline: the same K steps on ONE stream with HIP events around every attention
     # launch, so a launch's event time is its own execution (under two streams it would include time
     # shared with the other stream's kernels) and matches the rocprofv3 kernel trace of
@@ -589,7 +600,9 @@ def main():
     # the fp16-operand build of the same forward (VC_ELEM_F16: same kernels, same MFMA rate,
     # logits within 1e-3), timed the same way after the bf16 headline; reported beside it
     model.compute_dtype = torch.float16
+    model.graph_replay = graphed
     dt16 = timed(a.streams)
+    model.graph_replay = False
     evs16 = []
     timed(1, evs16)
     attn_ms16 = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs16]))
@@ -643,7 +656,8 @@ def main():
             "data": "synthetic (uint8 frames RandomState(1+rank) -> ViViT processor affine; weights RandomState(0))",
             "config": {"workload": "ViViT-B/16x2 forward, 32x224x224 clips, batch 8 per GPU (BASELINE configs[1])",
                        "model": "ViViT-B/16x2 (joint space-time, 12L, d768, 12H, 3137 tokens)",
-                       "global_batch": a.batch * world, "seq_len": 3137, "parallelism": f"dp{world}"},
+                       "global_batch": a.batch * world, "seq_len": 3137, "parallelism": f"dp{world}",
+                       "streams": a.streams, "hip_graph": bool(a.graph)},
             "logit_max_abs_err": logit_err,
             "roofline": {"bound": "mfma", "kernel": ATTN_KERNEL, "achieved": round(attn_tflops, 1),
                          "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4),

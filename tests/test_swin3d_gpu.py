@@ -170,3 +170,20 @@ def test_swin3d_two_stream_split_bit_exact():
     m.concurrent_streams = 2
     two = m.forward_logits(x).clone()
     assert torch.equal(one, two)
+
+
+@pytest.mark.parametrize("streams", [1, 2])
+def test_swin3d_graph_replay_bit_identical(streams):
+    """forward_logits replayed from its captured hipGraph (model.graph_replay) == the eager forward,
+    bit for bit, including after an in-place update of the captured input."""
+    video = torch.from_numpy(make_synthetic_video(2, 8, 48, seed=4)).to(DEV)
+    video2 = torch.flip(video, dims=[0]).contiguous()
+    m = _model(TINY)
+    m.concurrent_streams = streams
+    eager = [m.forward_logits(v).clone() for v in (video, video2)]
+    m.graph_replay = True
+    buf = video.clone()
+    for _ in range(2):
+        assert torch.equal(m.forward_logits(buf), eager[0])
+    buf.copy_(video2)
+    assert torch.equal(m.forward_logits(buf), eager[1])

@@ -178,3 +178,21 @@ def test_timesformer_two_stream_split_bit_exact():
     m.concurrent_streams = 2
     two = m.forward_logits(pix).clone()
     assert torch.equal(one, two)
+
+
+@pytest.mark.parametrize("streams", [1, 2])
+def test_timesformer_graph_replay_bit_identical(streams):
+    """forward_logits replayed from its captured hipGraph (model.graph_replay) == the eager forward,
+    bit for bit, including after an in-place update of the captured input."""
+    g = np.load(os.path.join(GD, "timesformer_tiny.npz"))
+    m = _model(json.loads(str(g["config"])))
+    m.concurrent_streams = streams
+    pix = torch.from_numpy(g["pixel_values"]).cuda()
+    pix2 = torch.flip(pix, dims=[0]).contiguous()
+    eager = [m.forward_logits(p).clone() for p in (pix, pix2)]
+    m.graph_replay = True
+    buf = pix.clone()
+    for _ in range(2):
+        assert torch.equal(m.forward_logits(buf), eager[0])
+    buf.copy_(pix2)
+    assert torch.equal(m.forward_logits(buf), eager[1])

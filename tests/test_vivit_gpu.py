@@ -126,3 +126,26 @@ def test_vivit_tiny_per_layer_drift():
     print("relative hidden-state drift per layer (embeddings, layer 1, ...):", drift)
     assert len(drift) == g["hidden_states"].shape[0]
     assert max(drift) < 2e-2, drift
+
+
+@pytest.mark.parametrize("streams", [1, 2])
+def test_vivit_graph_replay_bit_identical(streams):
+    """The forward replayed from its captured hipGraph (model.graph_replay, streams.GraphReplay)
+    gives the eager forward's logits bit for bit, sees in-place updates of the captured input, and
+    re-captures for another input tensor."""
+    g = np.load(os.path.join(GD, "vivit_tiny.npz"))
+    cfg = json.loads(str(g["config"]))
+    m = _model(cfg)
+    m.concurrent_streams = streams
+    pix = torch.from_numpy(g["pixel_values"]).cuda()
+    pix2 = torch.flip(pix, dims=[0]).contiguous()
+    eager = [m.forward_logits(p).clone() for p in (pix, pix2)]
+    m.graph_replay = True
+    for _ in range(2):
+        assert torch.equal(m.forward_logits(pix), eager[0])
+    assert torch.equal(m.forward_logits(pix2), eager[1])  # another input: its own capture
+    buf = pix.clone()
+    assert torch.equal(m.forward_logits(buf), eager[0])
+    buf.copy_(pix2)  # in place: the replay reads the current contents
+    assert torch.equal(m.forward_logits(buf), eager[1])
+    assert np.abs(m.forward_logits(pix).cpu().numpy() - g["logits"]).max() < 1e-2

@@ -1,0 +1,78 @@
+"""Forward replayed from a captured HIP graph vs eager enqueue, interleaved rounds in one process.
+
+usage: python tools/exp_graph.py [vivit|timesformer|swin] [B]
+Each variant: the model's own forward_logits (1 or 2 concurrent HIP streams) enqueued eagerly, or
+the same call captured once into a torch.cuda.CUDAGraph (hipGraph) and replayed.  Logits must be
+bit-identical; every round's clips/s is printed (the box spread matters)."""
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+from vclip_amd.weights import make_synthetic_clips  # noqa: E402
+
+fam = sys.argv[1] if len(sys.argv) > 1 else "vivit"
+dev = torch.device("cuda", 0)
+if fam == "vivit":
+    from vclip_amd.vivit import create_model
+    B = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+    m = create_model(num_frames=32, device=dev)
+    pix = torch.from_numpy(make_synthetic_clips(B, 32, 224, seed=1)).to(dev)
+elif fam == "timesformer":
+    from vclip_amd.timesformer import create_model
+    B = int(sys.argv[2]) if len(sys.argv) > 2 else 16
+    m = create_model(num_frames=8, device=dev)
+    pix = torch.from_numpy(make_synthetic_clips(B, 8, 224, seed=1)).to(dev)
+else:
+    raise SystemExit(f"unknown family {fam}")
+m.eval()
+
+
+def eager(ns):
+    def f():
+        m.concurrent_streams = ns
+        return m.forward_logits(pix)
+    return f
+
+
+def graphed(ns):
+    m.concurrent_streams = ns
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            m.forward_logits(pix)
+    torch.cuda.current_stream(dev).wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = m.forward_logits(pix)
+
+    def f():
+        g.replay()
+        return out
+    return f
+
+
+ref = eager(1)().clone()
+VAR = {"eager1": eager(1), "eager2": eager(2), "graph1": graphed(1), "graph2": graphed(2)}
+for k, f in VAR.items():
+    got = f().clone()
+    torch.cuda.synchronize()
+    print(k, "bit-identical" if torch.equal(got, ref) else f"DIFF {float((got - ref).abs().max()):.3e}", flush=True)
+res = {v: [] for v in VAR}
+for rnd in range(6):
+    for k, f in VAR.items():
+        for _ in range(2):
+            f()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(12):
+            f()
+        torch.cuda.synchronize()
+        res[k].append(B * 12 / (time.perf_counter() - t0))
+    print("round", rnd, {k: round(v[-1], 1) for k, v in res.items()}, flush=True)
+for v, x in res.items():
+    print(f"{fam} B={B} {v}: median {np.median(x):.1f} min {min(x):.1f} max {max(x):.1f}", flush=True)
