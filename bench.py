@@ -518,7 +518,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--streams", type=int, default=2,
                     help="fwd: concurrent HIP streams the batch is split over in the headline pass")
-    ap.add_argument("--graph", type=int, default=0,
+    ap.add_argument("--graph", type=int, default=1,
                     help="inference modes: 1 = the headline forward replayed from its captured hipGraph "
                          "(model.graph_replay; the event-instrumented roofline passes stay eager), 0 = eager")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)  # CPU test of the spawn path

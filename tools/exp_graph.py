@@ -25,6 +25,12 @@ elif fam == "timesformer":
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 16
     m = create_model(num_frames=8, device=dev)
     pix = torch.from_numpy(make_synthetic_clips(B, 8, 224, seed=1)).to(dev)
+elif fam == "swin":
+    from vclip_amd.swin3d import create_model
+    from vclip_amd.weights import make_synthetic_video
+    B = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+    m = create_model(model_size="tiny", device=dev)
+    pix = torch.from_numpy(make_synthetic_video(B, 32, 224, seed=1)).to(dev)
 else:
     raise SystemExit(f"unknown family {fam}")
 m.eval()
