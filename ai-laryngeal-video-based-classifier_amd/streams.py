@@ -43,8 +43,10 @@ class GraphReplay:
     the forward on the CURRENT contents of the input it was captured on, so in-place updates of
     that tensor are seen; the entry holds references to the input, the packed weights and the
     workspaces the graph's kernels address (`keep()`, read after the capture), so none of them is
-    freed under it.  `run` returns the owner's logits buffer (overwritten by the next call), as the
-    eager forward does."""
+    freed under it: torch.cuda.graph empties the allocator's cache when a capture starts, which
+    unmaps freed blocks, so a graph whose buffers were merely dropped from a model cache would
+    fault on replay after the next capture.  `run` returns the owner's logits buffer (overwritten by
+    the next call), as the eager forward does."""
 
     def __init__(self, max_entries: int = 4):
         self.max_entries = max_entries

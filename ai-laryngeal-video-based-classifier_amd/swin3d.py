@@ -422,7 +422,7 @@ class Swin3d(torch.nn.Module):
             key = (video.data_ptr(), tuple(video.shape), tuple(video.stride()), video.dtype, self.concurrent_streams,
                    str(video.device), self._weights_version())
             return self._graphs.run(key, video, self._forward_eager,
-                                    keep=lambda: (self._packed, self._ws, self._split_out))
+                                    keep=lambda: (self._packed, self._ws, self._split_out, self._bias_cache))
         return self._forward_eager(video)
 
     def _forward_eager(self, video: torch.Tensor) -> torch.Tensor:

@@ -149,3 +149,32 @@ def test_vivit_graph_replay_bit_identical(streams):
     buf.copy_(pix2)  # in place: the replay reads the current contents
     assert torch.equal(m.forward_logits(buf), eager[1])
     assert np.abs(m.forward_logits(pix).cpu().numpy() - g["logits"]).max() < 1e-2
+
+
+def test_vivit_graph_replay_survives_workspace_cache_reset():
+    """A captured forward keeps the workspaces it addresses alive: after enough other batch sizes /
+    stream splits / operand types to reset the model's workspace cache (8 entries) and another
+    capture (torch.cuda.graph empties the allocator cache), the first graph still replays correctly."""
+    g = np.load(os.path.join(GD, "vivit_tiny.npz"))
+    cfg = json.loads(str(g["config"]))
+    m = _model(cfg)
+    pix = torch.from_numpy(g["pixel_values"]).cuda()
+    pix3 = torch.cat([pix, pix[:1]]).contiguous()
+    m.concurrent_streams = 2
+    want = m.forward_logits(pix).clone()
+    m.graph_replay = True
+    assert torch.equal(m.forward_logits(pix), want)
+    m.graph_replay = False
+    for dt in (torch.bfloat16, torch.float16):
+        m.compute_dtype = dt
+        for ns in (1, 2):
+            m.concurrent_streams = ns
+            for x in (pix[:1], pix, pix3):
+                m.forward_logits(x.contiguous())
+    m.compute_dtype = torch.bfloat16
+    m.concurrent_streams = 1
+    m.graph_replay = True
+    m.forward_logits(pix3)  # another capture
+    m.concurrent_streams = 2
+    assert torch.equal(m.forward_logits(pix), want)
+    torch.cuda.synchronize()

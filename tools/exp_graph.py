@@ -1,6 +1,6 @@
 """Forward replayed from a captured HIP graph vs eager enqueue, interleaved rounds in one process.
 
-usage: python tools/exp_graph.py [vivit|timesformer|swin] [B]
+usage: python tools/exp_graph.py [vivit|timesformer|swin] [B] [graph3,graph4,graph2_rs]
 Each variant: the model's own forward_logits (1 or 2 concurrent HIP streams) enqueued eagerly, or
 the same call captured once into a torch.cuda.CUDAGraph (hipGraph) and replayed.  Logits must be
 bit-identical; every round's clips/s is printed (the box spread matters)."""
@@ -55,15 +55,38 @@ def graphed(ns):
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         out = m.forward_logits(pix)
+    # the graph addresses the model's workspaces: hold them, since a later capture's warm-up may
+    # drop the model's workspace cache (TimeSformer B=16 over 1-4 streams makes 10 part workspaces,
+    # past the cache's 8) and torch.cuda.graph empties the allocator cache at capture start, which
+    # would unmap them under this graph (an illegal-address fault in round 3's first version)
+    keep = (m._packed, m._ws, getattr(m, "_split_out", None), getattr(m, "_bias_cache", None))
 
-    def f():
+    def f(keep=keep):
         g.replay()
         return out
     return f
 
 
+def graphed_with(ns, **attrs):
+    """a graph captured with model attributes set (e.g. ViViT round_split), restored after capture"""
+    old = {k: getattr(m, k) for k in attrs}
+    for k, v in attrs.items():
+        setattr(m, k, v)
+    f = graphed(ns)
+    for k, v in old.items():
+        setattr(m, k, v)
+    return f
+
+
 ref = eager(1)().clone()
-VAR = {"eager1": eager(1), "eager2": eager(2), "graph1": graphed(1), "graph2": graphed(2)}
+extra = sys.argv[3].split(",") if len(sys.argv) > 3 else []
+VAR = {"eager2": eager(2), "graph2": graphed(2)} if extra else \
+    {"eager1": eager(1), "eager2": eager(2), "graph1": graphed(1), "graph2": graphed(2)}
+for v in extra:  # graph3, graph4, graph2_rs (ViViT round_split)
+    if v.startswith("graph") and v[5:].isdigit():
+        VAR[v] = graphed(int(v[5:]))
+    elif v == "graph2_rs":
+        VAR[v] = graphed_with(2, round_split=True)
 for k, f in VAR.items():
     got = f().clone()
     torch.cuda.synchronize()
