@@ -516,13 +516,16 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="clips per GPU per step (fwd 8, train 4)")
     ap.add_argument("--cpu-clips", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--streams", type=int, default=2,
-                    help="fwd: concurrent HIP streams the batch is split over in the headline pass")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="inference modes: concurrent HIP streams the batch is split over in the headline pass "
+                         "(default 2; swin 4: its late stages' short launches, measured under graph replay)")
     ap.add_argument("--graph", type=int, default=1,
                     help="inference modes: 1 = the headline forward replayed from its captured hipGraph "
                          "(model.graph_replay; the event-instrumented roofline passes stay eager), 0 = eager")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)  # CPU test of the spawn path
     a = ap.parse_args()
+    if a.streams is None:
+        a.streams = 4 if a.mode == "swin" else 2
     if a.batch is None:
         a.batch = {"fwd": 8, "train": 4}.get(a.mode) or FAMILIES[a.mode][2]
     if a.cpu_clips is None:
