@@ -69,7 +69,10 @@ class GraphReplay:
             cur.wait_stream(side)
             torch.cuda.synchronize(dev)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            # thread_local: HIP calls other threads make meanwhile (e.g. a process group's watchdog)
+            # neither break this capture nor are broken by it.  A refused capture raises (measured:
+            # after one, the next launch on the device fails too, so there is no eager fallback)
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 out = forward(x)
             e = self._entries[key] = (g, out, (x,) + tuple(keep()))
         g, out, _ = e

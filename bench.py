@@ -132,6 +132,11 @@ def _dist():
     return None, 0, 1, 0
 
 
+def _graph_used(model, a) -> bool:
+    """the headline replayed a captured hipGraph (--graph 1 on a model with graph replay)"""
+    return bool(a.graph) and getattr(model, "_graphs", None) is not None
+
+
 def timed_loop(step, steps: int, warmup: int, dist=None, sync=None):
     """W untimed warm-up steps, then exactly `steps` timed steps bracketed by a barrier and
     a device sync on both sides; returns the MAX elapsed seconds over ranks (the job's
@@ -406,7 +411,7 @@ def run_family(a, dist, rank, world, dev):
             "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (uint8 frames RandomState(1+rank) -> the family's processor affine; weights RandomState(0))",
             "config": {"workload": workload, "global_batch": a.batch * world, "parallelism": f"dp{world}",
-                       "streams": a.streams, "hip_graph": bool(a.graph)},
+                       "streams": a.streams, "hip_graph": _graph_used(model, a)},
             "logit_max_abs_err": err,
             "roofline": {"bound": bound, "kernel": kname,
                          "achieved": round(attn_gbs, 1) if bound == "hbm" else round(attn_tflops, 1),
@@ -660,7 +665,7 @@ def main():
             "config": {"workload": "ViViT-B/16x2 forward, 32x224x224 clips, batch 8 per GPU (BASELINE configs[1])",
                        "model": "ViViT-B/16x2 (joint space-time, 12L, d768, 12H, 3137 tokens)",
                        "global_batch": a.batch * world, "seq_len": 3137, "parallelism": f"dp{world}",
-                       "streams": a.streams, "hip_graph": bool(a.graph)},
+                       "streams": a.streams, "hip_graph": _graph_used(model, a)},
             "logit_max_abs_err": logit_err,
             "roofline": {"bound": "mfma", "kernel": ATTN_KERNEL, "achieved": round(attn_tflops, 1),
                          "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4),

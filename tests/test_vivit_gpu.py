@@ -178,3 +178,4 @@ def test_vivit_graph_replay_survives_workspace_cache_reset():
     m.concurrent_streams = 2
     assert torch.equal(m.forward_logits(pix), want)
     torch.cuda.synchronize()
+
