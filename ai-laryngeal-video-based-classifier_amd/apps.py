@@ -279,6 +279,19 @@ def _loaders(fam, args, logger, exp_dir):
         if fam.name == "swin":
             return mod.create_dataloaders(args, logger), binary
         return mod.create_dataloaders(args, logger, log_dir=str(exp_dir))[1], binary
+    if fam.name == "resnet3d":
+        # resnet50-3d-video/main.py:94-98 builds every split with the experiment dir before it looks
+        # at --skip_train, so the sampled-index CSVs (its only golden artefact) are written for train,
+        # val and test; a dataset without train/val splits still gets its test CSV
+        try:
+            return {"test": mod.create_dataloaders(args, logger, log_dir=str(exp_dir))[1]["test"]}, binary
+        except Exception as e:  # noqa: BLE001 - the reference raises here; evaluating the test split is still possible
+            logger.warning(f"create_dataloaders failed ({e}); building the test split only")
+            ds = mod.VideoDataset(args.test_data_dir or args.data_dir, mode="test", sampling_method=methods["test"],
+                                  num_frames=args.num_frames, logger=logger, log_dir=str(exp_dir))
+            ds.save_sampled_indices()
+            return {"test": DeviceClipLoader(ds, batch_size=args.batch_size, num_workers=args.num_workers,
+                                             collate_fn=swin.video_collate_fn)}, binary
     root = args.test_data_dir or args.data_dir
     ds = mod.VideoDataset(root, mode="test", sampling_method=methods["test"], num_frames=args.num_frames,
                           logger=logger)

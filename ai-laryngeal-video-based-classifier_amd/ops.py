@@ -290,7 +290,7 @@ def window_attention3d(qkv: torch.Tensor, B: int, grid, heads: int, window, shif
     """Swin 3D shifted-window attention (head_dim 32) on the token layout [B][T][H][W]:
     qkv bf16 [>= B*T*H*W, >= 3*heads*32] (q pre-scaled by d^-1/2 * log2 e) -> out bf16 [rows,
     >= heads*32].  biasT: the f32 accumulator-fragment bias of swin3d.expand_bias (the bias as
-    the QK^T C operand; also the train-step form with `lse`), or the bf16 operand-fragment bias
+    the QK^T C operand; also the train-step form with `lse`), or the fp16 operand-fragment bias
     of swin3d.expand_bias_mb (inference: bias and shift mask on the matrix pipe,
     vc_window_attention3d_mb).  See include/vclip.h."""
     _dev(qkv, biasT, out)
@@ -301,12 +301,12 @@ def window_attention3d(qkv: torch.Tensor, B: int, grid, heads: int, window, shif
     np_ = (vol + 63) // 64 * 64
     _need(qkv.dtype == torch.bfloat16 and out.dtype == torch.bfloat16 and qkv.stride(1) == 1 and out.stride(1) == 1,
           "window_attention3d dtypes")
-    _need(biasT.dtype in (torch.float32, torch.bfloat16) and biasT.is_contiguous() and biasT.numel() == heads * np_ * np_,
-          "window_attention3d bias: f32 (swin3d.expand_bias) or bf16 (swin3d.expand_bias_mb) table of heads*np*np")
+    _need(biasT.dtype in (torch.float32, torch.float16) and biasT.is_contiguous() and biasT.numel() == heads * np_ * np_,
+          "window_attention3d bias: f32 (swin3d.expand_bias) or fp16 (swin3d.expand_bias_mb) table of heads*np*np")
     _need(qkv.shape[0] >= B * T * H * W and out.shape[0] >= B * T * H * W, "window_attention3d rows")
     _need(qkv.shape[1] >= 3 * heads * 32 and out.shape[1] >= heads * 32, "window_attention3d columns")
     _need(T % wt == 0 and H % wh == 0 and W % ww == 0, "window_attention3d: grid must be whole windows")
-    if biasT.dtype == torch.bfloat16:
+    if biasT.dtype == torch.float16:
         _need(lse is None, "window_attention3d: the train-step form (lse) takes the f32 bias")
         _lib.call("vc_window_attention3d_mb", _p(qkv), qkv.stride(0), B, T, H, W, heads, 32, wt, wh, ww, st, sh, sw,
                   _p(biasT), np_, _p(out), out.stride(0), _stream(qkv))

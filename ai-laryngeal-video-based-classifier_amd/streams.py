@@ -10,10 +10,17 @@ from __future__ import annotations
 import torch
 
 
-def run_split(owner, x: torch.Tensor, ns: int, part_fn, num_labels: int) -> torch.Tensor:
+def run_split(owner, x: torch.Tensor, ns: int, part_fn, num_labels: int, prepare=None) -> torch.Tensor:
     """part_fn(x_part, part_index, out=logits_rows) for each of `ns` contiguous batch parts, part i on
-    owner._streams[i]; returns the [B, num_labels] logits (a buffer of `owner`, reused per call)."""
+    owner._streams[i]; returns the [B, num_labels] logits (a buffer of `owner`, reused per call).
+
+    `prepare()` builds the state every part reads (packed weights, bias caches) on the CALLER's
+    stream before the fork: built inside part 0 on stream 0, it would be read by parts 1..n-1 on
+    streams that wait only on the caller's stream (a cross-stream read-before-write), and the
+    allocator would record those tensors on stream 0 alone."""
     dev = x.device
+    if prepare is not None:
+        prepare()
     B = x.shape[0]
     ns = max(1, min(int(ns), B))
     if owner._streams is None or len(owner._streams) < ns or owner._streams[0].device != dev:
@@ -38,43 +45,64 @@ def run_split(owner, x: torch.Tensor, ns: int, part_fn, num_labels: int) -> torc
 class GraphReplay:
     """An inference forward captured once into a hipGraph (torch.cuda.CUDAGraph) and replayed.
 
-    One entry per key (the caller's input address / shape / strides / dtype plus whatever selects
-    the kernels: stream count, operand type, weights version).  A replay re-runs every kernel of
-    the forward on the CURRENT contents of the input it was captured on, so in-place updates of
-    that tensor are seen; the entry holds references to the input, the packed weights and the
-    workspaces the graph's kernels address (`keep()`, read after the capture), so none of them is
-    freed under it: torch.cuda.graph empties the allocator's cache when a capture starts, which
-    unmaps freed blocks, so a graph whose buffers were merely dropped from a model cache would
-    fault on replay after the next capture.  `run` returns the owner's logits buffer (overwritten by
-    the next call), as the eager forward does."""
+    Static-input contract.  `key` = (the caller's input address, shape, strides, dtype, whatever
+    selects the kernels: stream count, operand type, weights version); the first key's capture runs on
+    the caller's own tensor, and a replay re-runs every kernel of the forward on the CURRENT contents
+    of that tensor, so in-place updates of it are seen.  A caller that passes a NEW tensor of an
+    already-captured shape (a DataLoader loop: one tensor per batch) does not recapture per batch:
+    its input is copied into one internal static buffer per shape, captured once, and replayed.
+
+    Each entry holds references to its input, the packed weights and the workspaces its kernels
+    address (`keep()`, read after the capture: pass only this batch size's workspaces), so none of
+    them is freed under it: torch.cuda.graph empties the allocator's cache when a capture starts, which
+    unmaps freed blocks, so a graph whose buffers were merely dropped from a model cache would fault
+    on replay after the next capture.  `run` returns the owner's logits buffer (overwritten by the
+    next call), as the eager forward does."""
 
     def __init__(self, max_entries: int = 4):
         self.max_entries = max_entries
         self._entries = {}
+        self.captures = 0
 
     def clear(self):
         self._entries = {}
 
+    def _capture(self, key, x, forward, keep):
+        if len(self._entries) >= self.max_entries:
+            self._entries = {}
+        dev = x.device
+        cur = torch.cuda.current_stream(dev)
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            forward(x)  # first launches (kernel attributes), packing and workspaces outside the capture
+        cur.wait_stream(side)
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        # thread_local: HIP calls other threads make meanwhile (e.g. a process group's watchdog)
+        # neither break this capture nor are broken by it.  A refused capture raises (measured:
+        # after one, the next launch on the device fails too, so there is no eager fallback)
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+            out = forward(x)
+        self.captures += 1
+        e = self._entries[key] = (g, out, x, (x,) + tuple(keep()))
+        return e
+
     def run(self, key, x: torch.Tensor, forward, keep=lambda: ()):
         e = self._entries.get(key)
         if e is None:
-            if len(self._entries) >= self.max_entries:
-                self._entries = {}
-            dev = x.device
-            cur = torch.cuda.current_stream(dev)
-            side = torch.cuda.Stream(device=dev)
-            side.wait_stream(cur)
-            with torch.cuda.stream(side):
-                forward(x)  # first launches (kernel attributes), packing and workspaces outside the capture
-            cur.wait_stream(side)
-            torch.cuda.synchronize(dev)
-            g = torch.cuda.CUDAGraph()
-            # thread_local: HIP calls other threads make meanwhile (e.g. a process group's watchdog)
-            # neither break this capture nor are broken by it.  A refused capture raises (measured:
-            # after one, the next launch on the device fails too, so there is no eager fallback)
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                out = forward(x)
-            e = self._entries[key] = (g, out, (x,) + tuple(keep()))
-        g, out, _ = e
+            # key[1:] = everything but the input address: a new tensor of a captured configuration
+            skey = ("static",) + tuple(key[1:])
+            if skey in self._entries or any(k[0] != "static" and tuple(k[1:]) == tuple(key[1:]) for k in self._entries):
+                e = self._entries.get(skey)
+                if e is None:
+                    e = self._capture(skey, torch.empty_like(x).copy_(x), forward, keep)
+                else:
+                    e[2].copy_(x)
+                g, out, _, _ = e
+                g.replay()
+                return out
+            e = self._capture(key, x, forward, keep)
+        g, out, _, _ = e
         g.replay()
         return out

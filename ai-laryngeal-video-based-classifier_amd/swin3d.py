@@ -147,7 +147,7 @@ def _bias_mb_gather_index(full_window, window, device):
 
 
 def expand_bias_mb(table, full_window, window, device):
-    """Relative-position bias of one block as the bf16 B operand of the matrix-pipe bias
+    """Relative-position bias of one block as the fp16 B operand of the matrix-pipe bias
     (vc_window_attention3d_mb): [heads, np/32, np/64, 2, 2, 64, 8], element [h][qb][t][kb][s][lane][m]
     = log2 e * bias[h][q = 32qb + lane%32][k = 64t + 32kb + 16s + 8(lane//32) + m] (the same
     torchvision bias as expand_bias), MB_MASKED on padded keys, 0 on padded queries."""
@@ -157,7 +157,8 @@ def expand_bias_mb(table, full_window, window, device):
     heads = tab.shape[1]
     ext = torch.cat([tab * LOG2E, torch.tensor([[MB_MASKED] * heads, [0.0] * heads], device=device)])
     g = ext.index_select(0, _bias_mb_gather_index(full_window, window, device))  # [slots, heads]
-    return g.t().to(torch.bfloat16).contiguous().view(heads, npad // 32, npad // 64, 2, 2, 64, 8)
+    # fp16 (2^-12 relative; bf16 would round trained tables by ~1e-2 log2 units)
+    return g.t().to(torch.float16).contiguous().view(heads, npad // 32, npad // 64, 2, 2, 64, 8)
 
 
 class Swin3d(torch.nn.Module):
@@ -178,6 +179,7 @@ class Swin3d(torch.nn.Module):
         self._packed = None
         self._bias_cache = {}
         self._ws = {}
+        self._ws_used = []
         self.kernel_events = None  # list: HIP events around each window-attention launch (bench.py)
         self.concurrent_streams = None  # n > 1: the inference batch split over n HIP streams
         self._streams = None
@@ -282,7 +284,7 @@ class Swin3d(torch.nn.Module):
 
     def _biasT(self, s, i, window, device):
         """Block (s, i)'s relative-position bias in the inference kernel's layout (expand_bias_mb:
-        bf16 operand fragments of vc_window_attention3d_mb), built once per packed weights."""
+        fp16 operand fragments of vc_window_attention3d_mb), built once per packed weights."""
         key = (s, i, tuple(window), str(device))
         if key not in self._bias_cache:
             tab = self._packed["stages"][s]["blocks"][i]["table"]
@@ -303,7 +305,10 @@ class Swin3d(torch.nn.Module):
     def _workspace(self, B, grids, device, part: int = 0):
         key = (B, tuple(grids), str(device), part)
         if key in self._ws:
-            return self._ws[key]
+            ws = self._ws[key]
+            if not any(w is ws for w in self._ws_used):
+                self._ws_used.append(ws)
+            return ws
         if len(self._ws) >= 8:
             self._ws = {}
         c = self.cfg
@@ -326,6 +331,7 @@ class Swin3d(torch.nn.Module):
         ws["logits"] = torch.zeros((B, self.num_classes), dtype=f32, device=device)
         ws["pool_work"] = torch.zeros(B * 64 * c["embed_dim"] * 2 ** (len(grids) - 1), dtype=f32, device=device)
         self._ws[key] = ws
+        self._ws_used.append(ws)
         return ws
 
     # ---- forward -------------------------------------------------------------------
@@ -422,16 +428,29 @@ class Swin3d(torch.nn.Module):
             key = (video.data_ptr(), tuple(video.shape), tuple(video.stride()), video.dtype, self.concurrent_streams,
                    str(video.device), self._weights_version())
             return self._graphs.run(key, video, self._forward_eager,
-                                    keep=lambda: (self._packed, self._ws, self._split_out, self._bias_cache))
+                                    keep=lambda: (self._packed, tuple(self._ws_used), self._bias_cache))
         return self._forward_eager(video)
 
     def _forward_eager(self, video: torch.Tensor) -> torch.Tensor:
+        self._ws_used = []  # the workspaces this forward addresses (a captured graph keeps exactly these)
         B = video.shape[0]
         ns = max(1, min(int(self.concurrent_streams or 1), B))
         if ns == 1:
             return self._forward_part(video, 0)
         from .streams import run_split
-        return run_split(self, video, ns, self._forward_part, self.num_classes)
+        return run_split(self, video, ns, self._forward_part, self.num_classes, prepare=lambda: self._prepare(video))
+
+    def _prepare(self, video: torch.Tensor):
+        """Packed weights and every block's bias operand for this clip geometry, built on the current
+        stream (streams.run_split builds them before the batch is forked over the side streams)."""
+        _, _, T, H, W = video.shape
+        self._pack(video.device)
+        c = self.cfg
+        for s, (t, h, w) in enumerate(self.geometry(video.shape[0], T, H, W)):
+            for i in range(c["depths"][s]):
+                shift_full = [0 if i % 2 == 0 else k // 2 for k in c["window_size"]]
+                window, _ = window_and_shift((t, h, w), c["window_size"], shift_full)
+                self._biasT(s, i, window, video.device)
 
     def _forward_part(self, video: torch.Tensor, part: int, out=None) -> torch.Tensor:
         c = self.cfg

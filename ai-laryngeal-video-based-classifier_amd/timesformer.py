@@ -114,6 +114,7 @@ class TimesformerForVideoClassification(torch.nn.Module):
             self.params[name.replace(".", "__")] = torch.nn.Parameter(torch.zeros(shape))
         self._packed = None
         self._ws = {}
+        self._ws_used = []
 
     def state_dict(self, *a, **k):
         return OrderedDict((n, self.params[n.replace(".", "__")].detach()) for n in self._names)
@@ -208,7 +209,10 @@ class TimesformerForVideoClassification(torch.nn.Module):
     def _workspace(self, B, device, part: int = 0):
         key = (B, str(device), part)
         if key in self._ws:
-            return self._ws[key]
+            ws = self._ws[key]
+            if not any(w is ws for w in self._ws_used):
+                self._ws_used.append(ws)
+            return ws
         if len(self._ws) >= 8:
             self._ws = {}
         c = self.config
@@ -220,6 +224,7 @@ class TimesformerForVideoClassification(torch.nn.Module):
                   Hc=z(Mpad, D), Hf=z(Mpad, D), QKV=z(Mpad, 3 * D), O=z(Mpad, D), Yb=z(Mpad, D), Hd=z(Mpad, I),
                   logits=z(B, c.num_labels, dt=torch.float32))
         self._ws[key] = ws
+        self._ws_used.append(ws)
         return ws
 
     def forward(self, pixel_values: torch.Tensor = None, labels: torch.Tensor = None, **kw):
@@ -256,17 +261,18 @@ class TimesformerForVideoClassification(torch.nn.Module):
             key = (pix.data_ptr(), tuple(pix.shape), tuple(pix.stride()), pix.dtype, self.concurrent_streams, self.proj_cfg,
                    str(pix.device), self._weights_version())
             return self._graphs.run(key, pix, self._forward_eager,
-                                    keep=lambda: (self._packed, self._ws, self._split_out))
+                                    keep=lambda: (self._packed, tuple(self._ws_used)))
         return self._forward_eager(pix)
 
     def _forward_eager(self, pix: torch.Tensor) -> torch.Tensor:
+        self._ws_used = []  # the workspaces this forward addresses (a captured graph keeps exactly these)
         c = self.config
         B = pix.shape[0]
         ns = max(1, min(int(self.concurrent_streams or 1), B))
         if ns == 1:
             return self._forward_part(pix, 0)
         from .streams import run_split
-        return run_split(self, pix, ns, self._forward_part, c.num_labels)
+        return run_split(self, pix, ns, self._forward_part, c.num_labels, prepare=lambda: self._pack(pix.device))
 
     def _forward_part(self, pix: torch.Tensor, part: int, out=None) -> torch.Tensor:
         c = self.config

@@ -113,6 +113,7 @@ class VivitForVideoClassification(torch.nn.Module):
         self.grad_ready_hooks = []  # fn(stage, start, end, gflat): a slice of gflat is final (enqueued)
         self._packed = None
         self._ws = {}
+        self._ws_used = []
         self._streams = None
         self.concurrent_streams = None  # None / 1: one stream; n > 1: batch split over n HIP streams
         self.last_streams = 1
@@ -309,7 +310,10 @@ class VivitForVideoClassification(torch.nn.Module):
     def _workspace(self, B, device, part: int = 0):
         key = (B, str(device), part, self.compute_dtype)
         if key in self._ws:
-            return self._ws[key]
+            ws = self._ws[key]
+            if not any(w is ws for w in self._ws_used):
+                self._ws_used.append(ws)
+            return ws
         if len(self._ws) >= 8:  # (1 + 2 stream parts) x {bf16, fp16} + the split logits fit
             self._ws = {}
         c = self.config
@@ -321,6 +325,7 @@ class VivitForVideoClassification(torch.nn.Module):
         ws = dict(A_emb=z(Memb, c.num_channels * kt * kh * kw), X=z(Mpad, D, dt=torch.float32), Y=z(Mpad, D),
                   QKV=z(Mpad, 3 * D), O=z(Mpad, D), Hd=z(Mpad, I), logits=z(B, c.num_labels, dt=torch.float32))
         self._ws[key] = ws
+        self._ws_used.append(ws)
         return ws
 
     # ---- forward -----------------------------------------------------------------
@@ -362,10 +367,11 @@ class VivitForVideoClassification(torch.nn.Module):
             key = (pix.data_ptr(), tuple(pix.shape), tuple(pix.stride()), pix.dtype, self.concurrent_streams,
                    self.compute_dtype, self._weights_version(), tuple(sorted(self.gemm_cfg.items())), self.rows,
                    self.round_split)
-            return self._graphs.run(key, pix, self._forward_eager, keep=lambda: (self._packed, self._ws))
+            return self._graphs.run(key, pix, self._forward_eager, keep=lambda: (self._packed, tuple(self._ws_used)))
         return self._forward_eager(pix)
 
     def _forward_eager(self, pix: torch.Tensor) -> torch.Tensor:
+        self._ws_used = []  # the workspaces this forward addresses (a captured graph keeps exactly these)
         c = self.config
         B = pix.shape[0]
         ns = self.concurrent_streams or 1
@@ -381,6 +387,9 @@ class VivitForVideoClassification(torch.nn.Module):
             self._ws[key] = torch.zeros(B, c.num_labels, dtype=torch.float32, device=dev)
         logits = self._ws[key]
         cur = torch.cuda.current_stream(dev)
+        # the packed weights every part reads are built on the caller's stream before the fork
+        # (streams.run_split's rule): packed inside part 0 they would race parts 1..n-1
+        self._pack(dev)
         bounds = [B * i // ns for i in range(ns + 1)]
         sts = self._streams[:ns]
         # whole parts enqueued one after the other (measured, tools/exp_streams.py: enqueueing the

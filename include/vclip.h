@@ -379,7 +379,7 @@ int vc_window_attention3d(const uint16_t* qkv, int64_t ld, int64_t B, int64_t T,
 
 /*
  * vc_window_attention3d with the bias and the shift mask on the matrix pipe (the inference path):
- * biasB: bf16, the log2(e)-scaled bias as MFMA B-operand fragments [heads][np/32][np/64][2][2][64][8]:
+ * biasB: fp16, the log2(e)-scaled bias as MFMA B-operand fragments [heads][np/32][np/64][2][2][64][8]:
  * element [h][qb][t][kb][s][lane][m] = log2(e) * bias[h][q][k] with q = 32qb + lane%32,
  * k = 64t + 32kb + 16s + 8(lane/32) + m; -16384 for k >= vol, 0 for q >= vol (swin3d.expand_bias_mb).
  * The kernel adds it as S^T += I . Bias^T (identity A fragments) and the mask as a one-hot product

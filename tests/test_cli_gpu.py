@@ -98,6 +98,9 @@ def test_eval_and_inference_clis(dataset, tmp_path, fam, extra):
                                str(tmp_path / "models"), "--skip_train", "--checkpoint_path", str(ck_path),
                                "--batch_size", "2", "--num_workers", "0"] + extra)
     assert (exp / "test_metrics_uniform.json").exists() and 0.0 <= m["accuracy"] <= 1.0
+    if fam == "resnet3d":  # main.py:94-98 writes every split's sampled-index CSV before --skip_train applies
+        for split in ("train", "val", "test"):
+            assert (exp / f"sampled_frames_{split}_uniform.csv").exists(), split
     video = sorted((dataset / "test" / "referral").iterdir())[0]
     res = run_inference(fam, ["--video_path", str(video), "--model_path", str(ck_path), "--log_dir",
                               str(tmp_path / "ilogs")] + extra)

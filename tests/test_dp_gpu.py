@@ -139,3 +139,38 @@ def test_optimizer_full_layout_is_one_launch(rccl):
     for p in model.parameters():
         gaps[p.storage_offset():p.storage_offset() + p.numel()] = False
     assert torch.count_nonzero(flat[gaps]) == 0  # the layout's alignment gaps stay zero
+
+
+def test_graph_capture_under_live_rccl_group(rccl):
+    """bench.py --gpus N > 1 captures each rank's forward into a hipGraph while its RCCL process
+    group is up (capture_error_mode="thread_local": the group's watchdog thread keeps making HIP
+    calls).  Here, after a collective has run on the group, the ViViT and Swin3D forwards are
+    captured and replayed on two streams: logits bit-identical to the eager forward, and another
+    collective still runs afterwards."""
+    from vclip_amd.swin3d import Swin3d
+    from vclip_amd.vivit import VivitConfig, VivitForVideoClassification
+    from vclip_amd.weights import make_swin3d_weights, make_synthetic_clips, make_synthetic_video, make_vivit_weights
+    t = torch.ones(4, device="cuda")
+    rccl.all_reduce(t)  # the communicator and its watchdog are live
+    torch.cuda.synchronize()
+    vm = VivitForVideoClassification(VivitConfig(**CFG, id2label={0: "a", 1: "b"}))
+    vm.load_state_dict(make_vivit_weights(CFG, seed=0))
+    vm = vm.cuda().eval()
+    pix = torch.from_numpy(make_synthetic_clips(2, 4, 32, seed=1)).cuda()
+    swin_cfg = dict(patch_size=(2, 4, 4), embed_dim=32, depths=(2, 2), num_heads=(1, 2), window_size=(2, 3, 3),
+                    mlp_ratio=4.0, layer_norm_eps=1e-5, num_classes=2)
+    sm = Swin3d({k: v for k, v in swin_cfg.items() if k != "num_classes"}, num_classes=2)
+    sm.load_state_dict(make_swin3d_weights(swin_cfg, seed=0))
+    sm = sm.cuda().eval()
+    video = torch.from_numpy(make_synthetic_video(2, 8, 48, seed=4)).cuda()
+    for m, x in ((vm, pix), (sm, video)):
+        m.concurrent_streams = 2
+        want = m.forward_logits(x).clone()
+        m.graph_replay = True
+        for _ in range(3):
+            assert torch.equal(m.forward_logits(x), want)
+        assert m._graphs.captures == 1
+        m.graph_replay = False
+    rccl.all_reduce(t)
+    torch.cuda.synchronize()
+    assert torch.equal(t.cpu(), torch.ones(4))  # world 1: the sum is the identity

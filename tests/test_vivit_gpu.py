@@ -179,3 +179,40 @@ def test_vivit_graph_replay_survives_workspace_cache_reset():
     assert torch.equal(m.forward_logits(pix), want)
     torch.cuda.synchronize()
 
+
+
+def test_vivit_graph_replay_new_tensors_share_one_static_capture():
+    """Static-input contract (streams.GraphReplay): a caller that passes a new tensor of a captured
+    shape every call (a DataLoader loop) is served by ONE internal static buffer captured once, not
+    by a capture per tensor; every replay gives that tensor's eager logits bit for bit."""
+    g = np.load(os.path.join(GD, "vivit_tiny.npz"))
+    cfg = json.loads(str(g["config"]))
+    m = _model(cfg)
+    m.concurrent_streams = 2
+    pix = torch.from_numpy(g["pixel_values"]).cuda()
+    xs = [pix, torch.flip(pix, dims=[0]).contiguous(), (pix * 0.5).contiguous(), (pix + 0.25).contiguous()]
+    eager = [m.forward_logits(x).clone() for x in xs]
+    m.graph_replay = True
+    for _ in range(2):
+        for x, want in zip(xs, eager):
+            assert torch.equal(m.forward_logits(x.clone()), want)  # a fresh tensor every call
+    assert m._graphs.captures == 2  # the first tensor's own capture + the shared static buffer
+
+
+def test_vivit_weight_update_then_split_forward():
+    """Weights changed right before a two-stream forward: the packed weights are rebuilt on the
+    caller's stream BEFORE the batch is forked (streams.run_split's rule), so both parts read the new
+    weights; logits equal a fresh one-stream model's bit for bit."""
+    from vclip_amd.vivit import VivitConfig, VivitForVideoClassification
+    g = np.load(os.path.join(GD, "vivit_tiny.npz"))
+    cfg = json.loads(str(g["config"]))
+    pix = torch.from_numpy(g["pixel_values"]).cuda()
+    m = _model(cfg)
+    m.concurrent_streams = 2
+    m.forward_logits(pix)
+    m.load_state_dict(make_vivit_weights(cfg, seed=7))
+    got = m.forward_logits(pix).clone()
+    fresh = VivitForVideoClassification(VivitConfig(**cfg, id2label={0: "non-referral", 1: "referral"}))
+    fresh.load_state_dict(make_vivit_weights(cfg, seed=7))
+    fresh = fresh.cuda().eval()
+    assert torch.equal(got, fresh.forward_logits(pix))
