@@ -39,6 +39,7 @@ SIGNATURES = {
     "vc_attention_fwd_rebase_always": ([c_p, c_i64, c_i64, c_i64, c_i64, c_f, c_p, c_i64, c_p], c_int),
     "vc_patch_im2col_h16": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_int, c_int, c_int, c_p,
                              c_i64, c_p], c_int),
+    "vc_gemm_pick": ([c_i64, c_i64, c_i64, c_int, c_i64, c_i64, c_p], c_int),
     "vc_gemm_h16": ([c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_int, c_p, c_i64, c_p, c_i64,
                      c_i64, c_i64, c_i64, c_int, c_int, c_p], c_int),
     "vc_layernorm_f32_h16": ([c_p, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_int, c_p, c_i64, c_p], c_int),

@@ -955,6 +955,16 @@ extern "C" int vc_gemm_h16(const uint16_t* A, int64_t lda, const uint16_t* W, in
     return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad epilogue");
 }
 
+// the tile config vc_gemm_bf16 / vc_gemm_h16 run with cfg = -1 (host only: no launch, no GPU)
+extern "C" int vc_gemm_pick(int64_t M, int64_t N, int64_t K, int epilogue, int64_t ldo, int64_t ldaux,
+                            const void* aux) {
+    const bool st16_ok =
+        ldo % 8 == 0 && (epilogue != VC_EPI_BIAS_GELU_TANH_SAVE || (ldaux % 8 == 0 && !((uintptr_t)aux & 15)));
+    int cfg = pick_cfg(M, N, K, epilogue);
+    if (cfg == 4 && !st16_ok) cfg = 5;
+    return cfg;
+}
+
 extern "C" int vc_gemm_bf16_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int64_t M, int64_t N,
                                 int64_t K, const float* bias, int epilogue, void* out, int64_t ldo, const float* aux,
                                 int64_t ldaux, int64_t G, int64_t group_stride, int64_t group_offset, int cfg,

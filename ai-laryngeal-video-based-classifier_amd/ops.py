@@ -89,11 +89,108 @@ def tubelet_im2col(pix: torch.Tensor, tubelet, out: torch.Tensor, order: str = "
     return out
 
 
+class OpRecorder:
+    """HIP events around every launch an instrumented forward makes while this recorder is installed
+    (`with ops.recording(rec):`), on the stream each launch runs on.  Entries (kernel, op, e0, e1,
+    work, unit): `kernel` names the kernel instantiation the launch ran (GEMMs: the tile config vc_gemm
+    picked and the epilogue, i.e. one rocprofv3 kernel name), `work` its algorithmic work (FLOP or
+    bytes, unit "flop" / "byte") as the caller states it (real rows and channels, not the padding)."""
+
+    def __init__(self):
+        self.entries = []
+
+    def begin(self):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        return e0
+
+    def end(self, e0, kernel, op, work, unit):
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        self.entries.append((kernel, op, e0, e1, float(work), unit))
+
+    def summary(self, n_steps: int, step_ms: float):
+        """per kernel: launches per step, mean launch ms, share of the step, achieved rate (TFLOP/s or
+        GB/s of algorithmic work), the ops that ran it; sorted by share"""
+        agg = {}
+        for kernel, op, e0, e1, work, unit in self.entries:
+            a = agg.setdefault(kernel, {"ms": [], "work": 0.0, "unit": unit, "ops": set()})
+            a["ms"].append(e0.elapsed_time(e1))
+            a["work"] += work
+            a["ops"].add(op)
+        out = {}
+        for k, a in agg.items():
+            tot = sum(a["ms"])
+            rate = a["work"] / (tot * 1e-3) / (1e12 if a["unit"] == "flop" else 1e9)
+            out[k] = {"launches_per_step": round(len(a["ms"]) / n_steps, 2), "avg_launch_ms": round(tot / len(a["ms"]), 4),
+                      "share_of_step": round(tot / n_steps / step_ms, 4), "achieved": round(rate, 1),
+                      "unit": "TFLOP/s" if a["unit"] == "flop" else "GB/s", "ops": sorted(a["ops"])}
+        return dict(sorted(out.items(), key=lambda kv: -kv[1]["share_of_step"]))
+
+
+_REC = [None]
+
+
+class recording:
+    """`with ops.recording(rec): model.forward_logits(x)`: instrumented launches append to rec."""
+
+    def __init__(self, rec: OpRecorder):
+        self.rec = rec
+
+    def __enter__(self):
+        self.prev = _REC[0]
+        _REC[0] = self.rec
+        return self.rec
+
+    def __exit__(self, *exc):
+        _REC[0] = self.prev
+
+
+def timed(kernel: str, op: str, work: float, unit: str, fn, *args, **kw):
+    """fn(*args, **kw), between HIP events when a recorder is installed (one attribute test otherwise)"""
+    rec = _REC[0]
+    if rec is None:
+        return fn(*args, **kw)
+    e0 = rec.begin()
+    r = fn(*args, **kw)
+    rec.end(e0, kernel, op, work, unit)
+    return r
+
+
+# rocprofv3 names of the GEMM kernels per tile config (csrc/gemm.hip kCfgs; E = the epilogue, ET = 0 bf16)
+GEMM_KERNEL = {0: "gemm_bf16_kernel<256, 128, 4, 2, {E}, 3, {ET}>", 1: "gemm_bf16_kernel<128, 128, 2, 4, {E}, 3, {ET}>",
+               2: "gemm_bf16_kernel<128, 256, 2, 4, {E}, 3, {ET}>", 3: "gemm_bf16_big_kernel<{E}, {ET}>",
+               4: "gemm_bf16_persist_kernel<{E}, {ET}>", 5: "gemm_bf16_kernel<128, 128, 2, 4, {E}, 2, {ET}>",
+               7: "gemm_bf16_kernel<64, 128, 2, 4, {E}, 2, {ET}>"}
+
+
+def gemm_kernel_name(M, N, K, epilogue: str, out, aux=None, cfg: int = -1, f16: bool = False) -> str:
+    e = EPI[epilogue]
+    if cfg < 0:
+        cfg = _lib.load().vc_gemm_pick(M, N, K, e, out.stride(0), aux.stride(0) if aux is not None else 0,
+                                       _p(aux) if aux is not None else None)
+    return GEMM_KERNEL.get(cfg, f"gemm cfg {cfg}").format(E=e, ET=1 if f16 else 0)
+
+
 def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: str, out: torch.Tensor,
          aux: torch.Tensor | None = None, group: int = 0, group_stride: int = 0, group_offset: int = 0,
-         m: int | None = None, cfg: int = -1) -> torch.Tensor:
+         m: int | None = None, cfg: int = -1, flop: float | None = None, op: str = "gemm") -> torch.Tensor:
     """out (+)= epilogue(a[:m] @ w.T + bias).  a bf16 [M,K], w bf16 [N,K], bias f32 [N]; or a, w (and the
-    16-bit out) fp16 for the inference epilogues (bias / gelu / resid_f32 / embed_f32)."""
+    16-bit out) fp16 for the inference epilogues (bias / gelu / resid_f32 / embed_f32).  `flop` / `op`:
+    the algorithmic work and op name an installed OpRecorder files this launch under (default
+    2 M N K of the operand shapes)."""
+    rec = _REC[0]
+    if rec is not None:
+        M_ = a.shape[0] if m is None else m
+        e0 = rec.begin()
+        _gemm(a, w, bias, epilogue, out, aux, group, group_stride, group_offset, m, cfg)
+        rec.end(e0, gemm_kernel_name(M_, w.shape[0], a.shape[1], epilogue, out, aux, cfg, a.dtype == torch.float16), op,
+                2.0 * M_ * w.shape[0] * a.shape[1] if flop is None else flop, "flop")
+        return out
+    return _gemm(a, w, bias, epilogue, out, aux, group, group_stride, group_offset, m, cfg)
+
+
+def _gemm(a, w, bias, epilogue, out, aux, group, group_stride, group_offset, m, cfg):
     _dev(a, w, bias, out)
     M = a.shape[0] if m is None else m
     K = a.shape[1]
@@ -145,7 +242,8 @@ def _num_cus(dev: torch.device) -> int:
 
 
 def gemm_rounds(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: str, out: torch.Tensor,
-                main_cfg: int, tail_cfg: int, m: int | None = None) -> torch.Tensor:
+                main_cfg: int, tail_cfg: int, m: int | None = None, flop: float | None = None,
+                op: str = "gemm") -> torch.Tensor:
     """gemm() as two launches when the tiles of `main_cfg` leave a partial last round on the
     CUs: the main launch covers whole rounds (rows rounded down to its row tile), the tail
     launch the remaining rows with the smaller tiles of `tail_cfg` in one round of its own.

@@ -48,6 +48,14 @@ class ResNet3d(torch.nn.Module):
             self.params[n.replace(".", "__")] = torch.nn.Parameter(torch.zeros(s), requires_grad=not stat)
         self._packed = None
         self._ws = {}
+        self._ws_used = []
+        self.concurrent_streams = None  # n > 1: the inference batch split over n HIP streams (vclip_amd.streams)
+        self._streams = None
+        self._split_out = {}
+        # True: the inference forward is captured once per input / configuration into a hipGraph and
+        # replayed (streams.GraphReplay); bit-identical logits
+        self.graph_replay = False
+        self._graphs = None
         self.head_dropout = True  # train step: the head's Dropout(0.5) (pytorchvideo create_resnet dropout_rate)
 
     def state_dict(self, *a, **k):
@@ -135,10 +143,15 @@ class ResNet3d(torch.nn.Module):
             g.append(ops.conv_out_size(g[-1], (1, 3, 3), (1, st, st), (0, 1, 1)))
         return stem, g
 
-    def _workspace(self, B, T, H, W, device):
-        key = (B, T, H, W, str(device))
+    def _workspace(self, B, T, H, W, device, part: int = 0):
+        key = (B, T, H, W, str(device), part)
         if key in self._ws:
-            return self._ws[key]
+            ws = self._ws[key]
+            if not any(w is ws for w in self._ws_used):
+                self._ws_used.append(ws)
+            return ws
+        if len(self._ws) >= 4:
+            self._ws = {}
         c = self.cfg
         stem, grids = self.geometry(T, H, W)
         bf = torch.bfloat16
@@ -166,7 +179,8 @@ class ResNet3d(torch.nn.Module):
         ws["col"] = torch.zeros(big, dtype=bf, device=device)
         ws["head_work"] = torch.zeros(B * T * 2048 * 33, dtype=torch.float32, device=device)
         ws["logits"] = torch.zeros((B, c["num_classes"]), dtype=torch.float32, device=device)
-        self._ws = {key: ws}
+        self._ws[key] = ws
+        self._ws_used.append(ws)
         return ws
 
     # ---- forward -----------------------------------------------------------------------
@@ -257,19 +271,49 @@ class ResNet3d(torch.nn.Module):
         return A.resnet_head(x, P("blocks.5.proj.weight"), P("blocks.5.proj.bias"), keep, B, Tf, Hf * Wf, pt)
 
     def forward_logits(self, video: torch.Tensor) -> torch.Tensor:
-        x, B, grid, C, ws = self.forward_features(video)
-        pk = self._packed
-        return ops.avgpool_head(x, B, grid, C, self.cfg["head_pool"], pk["w_head"], pk["b_head"], ws["head_work"],
-                                ws["logits"])
+        """logits f32 [B, classes] (a workspace buffer, overwritten by the next call); with
+        `concurrent_streams = n > 1` the batch is split over n HIP streams (vclip_amd.streams) and with
+        `graph_replay` the forward is replayed from a captured hipGraph (bit-identical either way)."""
+        if video.shape[1] != 3:
+            raise ValueError("video must be [B, 3, T, H, W]")
+        if self.graph_replay and not torch.cuda.is_current_stream_capturing():
+            from .streams import GraphReplay
+            if self._graphs is None:
+                self._graphs = GraphReplay()
+            key = (video.data_ptr(), tuple(video.shape), tuple(video.stride()), video.dtype, self.concurrent_streams,
+                   str(video.device), self._weights_version())
+            return self._graphs.run(key, video, self._forward_eager, keep=lambda: (self._packed, tuple(self._ws_used)))
+        return self._forward_eager(video)
 
-    def forward_features(self, video: torch.Tensor):
+    def _forward_eager(self, video: torch.Tensor) -> torch.Tensor:
+        self._ws_used = []  # the workspaces this forward addresses (a captured graph keeps exactly these)
+        B = video.shape[0]
+        ns = max(1, min(int(self.concurrent_streams or 1), B))
+        if ns == 1:
+            return self._forward_part(video, 0)
+        from .streams import run_split
+        return run_split(self, video, ns, self._forward_part, self.cfg["num_classes"],
+                         prepare=lambda: self._pack(video.device))
+
+    def _forward_part(self, video: torch.Tensor, part: int, out=None) -> torch.Tensor:
+        x, B, grid, C, ws = self.forward_features(video, part)
+        pk = self._packed
+        c = self.cfg
+        Tf, Hf, Wf = grid
+        pt, ph, pw = c["head_pool"]
+        npos = (Tf - pt + 1) * (Hf - ph + 1) * (Wf - pw + 1)
+        return ops.timed("avgpool_head", "head", B * Tf * Hf * Wf * C * 2 + npos * B * C * 4, "byte", ops.avgpool_head,
+                         x, B, grid, C, c["head_pool"], pk["w_head"], pk["b_head"], ws["head_work"],
+                         ws["logits"] if out is None else out)
+
+    def forward_features(self, video: torch.Tensor, part: int = 0):
         """Stem + the four stages; returns (last activations [rows, C] bf16, B, (T, H, W), C, workspace)."""
         c = self.cfg
         B, C, T, H, W = video.shape
         if C != 3:
             raise ValueError("video must be [B, 3, T, H, W]")
         pk = self._pack(video.device)
-        ws = self._workspace(B, T, H, W, video.device)
+        ws = self._workspace(B, T, H, W, video.device, part)
         stem, grids = self.geometry(T, H, W)
         rows = lambda g: _ru(B * g[0] * g[1] * g[2], 256)  # noqa: E731
 
@@ -277,13 +321,21 @@ class ResNet3d(torch.nn.Module):
             return ws["col"][: m * k].view(m, k)
 
         # stem: conv (3,7,7)/(1,2,2) + BN + ReLU, then MaxPool (1,3,3)/(1,2,2)
+        # (algorithmic work per launch for an installed ops.OpRecorder: real rows and channels; the
+        # GEMMs run on rows padded to 256 and output channels padded to 128)
+        tm = ops.timed
+        vol = lambda g: B * g[0] * g[1] * g[2]  # noqa: E731
+        sk = c.get("stem_kernel", (3, 7, 7))
+        ks = 3 * sk[0] * sk[1] * sk[2]
         Kst = pk["stem"][0].shape[1]
         A = col(rows(stem), Kst)
-        ops.conv3d_im2col(video, "ncthw_f32", B, (T, H, W), 3, c.get("stem_kernel", (3, 7, 7)), (1, 2, 2),
-                          c.get("stem_pad", (1, 3, 3)), A)
-        ops.gemm(A, pk["stem"][0], pk["stem"][1], "bias_relu", ws["stem_out"])
+        tm("conv3d_im2col_kernel", "im2col", B * 3 * T * H * W * 4 + vol(stem) * ks * 2, "byte", ops.conv3d_im2col,
+           video, "ncthw_f32", B, (T, H, W), 3, sk, (1, 2, 2), c.get("stem_pad", (1, 3, 3)), A)
+        ops.gemm(A, pk["stem"][0], pk["stem"][1], "bias_relu", ws["stem_out"], flop=2.0 * vol(stem) * c["stem_dim"] * ks,
+                 op="stem")
         x = ws["x0"]
-        ops.maxpool3d(ws["stem_out"], B, stem, c["stem_dim"], (1, 3, 3), (1, 2, 2), (0, 1, 1), x)
+        tm("maxpool3d_kernel", "maxpool", (vol(stem) + vol(grids[0])) * c["stem_dim"] * 2, "byte", ops.maxpool3d,
+           ws["stem_out"], B, stem, c["stem_dim"], (1, 3, 3), (1, 2, 2), (0, 1, 1), x)
         g_in, cin = grids[0], c["stem_dim"]
         for s, (st, act) in enumerate(zip(pk["stages"], ws["acts"])):
             g = grids[s]
@@ -296,29 +348,36 @@ class ResNet3d(torch.nn.Module):
                 xin = x
                 # branch1: 1x1x1 conv (+ stride) + BN, or the identity
                 if "b1" in blk:
+                    fl = 2.0 * vol(g) * dout * cin
                     if stride == (1, 1, 1):
-                        ops.gemm(xin, blk["b1"][0], blk["b1"][1], "bias", act["sc"], m=rows(g))
+                        ops.gemm(xin, blk["b1"][0], blk["b1"][1], "bias", act["sc"], m=rows(g), flop=fl, op="branch1")
                     else:
                         A = col(rows(g), cin)
-                        ops.conv3d_im2col(xin, "cl_bf16", B, gi, cin, (1, 1, 1), stride, (0, 0, 0), A)
-                        ops.gemm(A, blk["b1"][0], blk["b1"][1], "bias", act["sc"])
+                        tm("conv3d_im2col_kernel", "im2col", (vol(gi) + vol(g)) * cin * 2, "byte", ops.conv3d_im2col,
+                           xin, "cl_bf16", B, gi, cin, (1, 1, 1), stride, (0, 0, 0), A)
+                        ops.gemm(A, blk["b1"][0], blk["b1"][1], "bias", act["sc"], flop=fl, op="branch1")
                     skip = act["sc"]
                 else:
                     skip = xin
                 # conv_a (+ BN + ReLU) at the block's input resolution
+                fl = 2.0 * vol(gi) * inner * cin * ka[0] * ka[1] * ka[2]
                 if tuple(ka) == (1, 1, 1):
-                    ops.gemm(xin, blk["a"][0], blk["a"][1], "bias_relu", act["a"], m=rows(gi))
+                    ops.gemm(xin, blk["a"][0], blk["a"][1], "bias_relu", act["a"], m=rows(gi), flop=fl, op="conv_a")
                 else:
                     A = col(rows(gi), ka[0] * cin)
-                    ops.conv3d_im2col(xin, "cl_bf16", B, gi, cin, ka, (1, 1, 1), tuple(k // 2 for k in ka), A)
-                    ops.gemm(A, blk["a"][0], blk["a"][1], "bias_relu", act["a"])
+                    tm("conv3d_im2col_kernel", "im2col", vol(gi) * cin * 2 * (1 + ka[0]), "byte", ops.conv3d_im2col,
+                       xin, "cl_bf16", B, gi, cin, ka, (1, 1, 1), tuple(k // 2 for k in ka), A)
+                    ops.gemm(A, blk["a"][0], blk["a"][1], "bias_relu", act["a"], flop=fl, op="conv_a")
                 # conv_b (1,3,3) with the stage stride (+ BN + ReLU)
                 A = col(rows(g), 9 * inner)
-                ops.conv3d_im2col(act["a"], "cl_bf16", B, gi, inner, (1, 3, 3), stride, (0, 1, 1), A)
-                ops.gemm(A, blk["b"][0], blk["b"][1], "bias_relu", act["b"])
+                tm("conv3d_im2col_kernel", "im2col", (vol(gi) + 9 * vol(g)) * inner * 2, "byte", ops.conv3d_im2col,
+                   act["a"], "cl_bf16", B, gi, inner, (1, 3, 3), stride, (0, 1, 1), A)
+                ops.gemm(A, blk["b"][0], blk["b"][1], "bias_relu", act["b"], flop=2.0 * vol(g) * inner * inner * 9,
+                         op="conv_b")
                 # conv_c 1x1x1 + BN + skip + ReLU
                 out = act["x"] if xin is not act["x"] else act["x2"]
-                ops.gemm(act["b"][:, :inner], blk["c"][0], blk["c"][1], "bias_resid_relu", out, aux=skip)
+                ops.gemm(act["b"][:, :inner], blk["c"][0], blk["c"][1], "bias_resid_relu", out, aux=skip,
+                         flop=2.0 * vol(g) * dout * inner, op="conv_c")
                 x, cin = out, dout
             g_in = g
         return x, B, grids[-1], cin, ws

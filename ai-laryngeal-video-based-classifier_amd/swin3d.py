@@ -462,40 +462,57 @@ class Swin3d(torch.nn.Module):
         pt, ph, pw = c["patch_size"]
         t0, h0, w0 = grids[0]
         M0 = ws["stages"][0]["M"]
-        ops.tubelet_im2col(video, (pt, ph, pw), ws["A_emb"], layout="bcthw")
-        ops.gemm(ws["A_emb"], pk["w_emb"], pk["b_emb"], "bias_f32", ws["E"], m=M0)
+        tm = ops.timed
+        C0 = c["embed_dim"]
+        n0 = B * t0 * h0 * w0
+        K0 = 3 * pt * ph * pw
+        # algorithmic work per launch for an installed ops.OpRecorder: real tokens and channels (the
+        # GEMMs run on channels padded to 128)
+        tm("im2col_kernel", "im2col", B * 3 * T * H * W * 4 + n0 * K0 * 2, "byte", ops.tubelet_im2col, video,
+           (pt, ph, pw), ws["A_emb"], layout="bcthw")
+        ops.gemm(ws["A_emb"], pk["w_emb"], pk["b_emb"], "bias_f32", ws["E"], m=M0, flop=2.0 * n0 * C0 * K0, op="embed")
         X = ws["stages"][0]["X"]
-        ops.layernorm_f32(ws["E"], pk["ln_emb"][0], pk["ln_emb"][1], eps, X, m=B * t0 * h0 * w0)
+        tm("layernorm_f32", "layernorm", n0 * C0 * 8, "byte", ops.layernorm_f32, ws["E"], pk["ln_emb"][0],
+           pk["ln_emb"][1], eps, X, m=n0)
         for s, (st, sw) in enumerate(zip(pk["stages"], ws["stages"])):
             t, h, w = grids[s]
             ntok = B * t * h * w
+            C, hid = st["C"], st["hid"]
             X, Y, QKV, O, Hd = sw["X"], sw["Y"], sw["QKV"], sw["O"], sw["Hd"]
             for i, blk in enumerate(st["blocks"]):
                 shift_full = [0 if i % 2 == 0 else k // 2 for k in c["window_size"]]
                 window, shift = window_and_shift((t, h, w), c["window_size"], shift_full)
                 biasT = self._biasT(s, i, window, video.device)
-                ops.layernorm(X, blk["ln1"][0], blk["ln1"][1], eps, Y, m=ntok)
-                ops.gemm(Y, blk["w_qkv"], blk["b_qkv"], "bias", QKV)
+                tm("layernorm_grp_kernel", "layernorm", ntok * C * 6, "byte", ops.layernorm, X, blk["ln1"][0],
+                   blk["ln1"][1], eps, Y, m=ntok)
+                ops.gemm(Y, blk["w_qkv"], blk["b_qkv"], "bias", QKV, flop=2.0 * ntok * 3 * C * C, op="qkv")
                 ev = self.kernel_events
                 if ev is not None:  # recorded on the current stream, the one the kernel runs on
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
-                ops.window_attention3d(QKV, B, (t, h, w), st["heads"], window, shift, biasT, O)
+                n = window[0] * window[1] * window[2]
+                tm("window_attn_mb_d32_kernel", "window_attention", 4.0 * ntok * n * 32 * st["heads"], "flop",
+                   ops.window_attention3d, QKV, B, (t, h, w), st["heads"], window, shift, biasT, O)
                 if ev is not None:
                     e1.record()
                     # QK^T + PV over each token's window (window clipped to the grid), head_dim 32;
                     # algorithmic bytes: q, k, v read and the output written once (4 x 32 x 2 B per
                     # token-head)
-                    n = window[0] * window[1] * window[2]
                     ev.append((e0, e1, 4.0 * ntok * n * 32 * st["heads"], 256.0 * ntok * st["heads"]))
-                ops.gemm(O, blk["w_proj"], blk["b_proj"], "bias_resid_f32", X)
-                ops.layernorm(X, blk["ln2"][0], blk["ln2"][1], eps, Y, m=ntok)
-                ops.gemm(Y, blk["w_1"], blk["b_1"], "bias_gelu_erf", Hd)
-                ops.gemm(Hd, blk["w_2"], blk["b_2"], "bias_resid_f32", X)
+                ops.gemm(O, blk["w_proj"], blk["b_proj"], "bias_resid_f32", X, flop=2.0 * ntok * C * C, op="proj")
+                tm("layernorm_grp_kernel", "layernorm", ntok * C * 6, "byte", ops.layernorm, X, blk["ln2"][0],
+                   blk["ln2"][1], eps, Y, m=ntok)
+                ops.gemm(Y, blk["w_1"], blk["b_1"], "bias_gelu_erf", Hd, flop=2.0 * ntok * hid * C, op="fc1")
+                ops.gemm(Hd, blk["w_2"], blk["b_2"], "bias_resid_f32", X, flop=2.0 * ntok * C * hid, op="fc2")
             if s < len(grids) - 1:
-                ops.patch_merge_layernorm(X, B, (t, h, w), st["C"], st["merge_ln"][0], st["merge_ln"][1], eps, sw["Mg"])
                 nxt = ws["stages"][s + 1]
-                ops.gemm(sw["Mg"], st["w_red"], st["b_red"], "bias_f32", nxt["X"], m=nxt["M"])
+                t2, h2, w2 = grids[s + 1]
+                n2 = B * t2 * h2 * w2
+                tm("patch_merge_ln_grp_kernel", "patch_merge_layernorm", ntok * C * 4 + n2 * 4 * C * 2, "byte",
+                   ops.patch_merge_layernorm, X, B, (t, h, w), st["C"], st["merge_ln"][0], st["merge_ln"][1], eps,
+                   sw["Mg"])
+                ops.gemm(sw["Mg"], st["w_red"], st["b_red"], "bias_f32", nxt["X"], m=nxt["M"],
+                         flop=2.0 * n2 * 2 * C * 4 * C, op="reduction")
         t, h, w = grids[-1]
         return ops.pool_head(ws["stages"][-1]["X"], B, t * h * w, pk["norm"][0], pk["norm"][1], eps, pk["w_head"],
                              pk["b_head"], out=ws["logits"] if out is None else out, work=ws["pool_work"])

@@ -284,36 +284,49 @@ class TimesformerForVideoClassification(torch.nn.Module):
         eps = c.layer_norm_eps
         X, Hc, Hf, QKV, O, Yb, Hd = (ws[k] for k in ("X", "Hc", "Hf", "QKV", "O", "Yb", "Hd"))
         pc = c.patch_size
-        ops.tubelet_im2col(pix, (1, pc, pc), ws["A_emb"], order="patch_major")
+        D, I = c.hidden_size, c.intermediate_size
+        Kemb = c.num_channels * pc * pc
+        tm = ops.timed
+        # algorithmic work per launch for an installed ops.OpRecorder: clip rows B*S (temporal
+        # branch and MLP), frame rows B*T*(1+P) (spatial branch), no padding
+        Mc, Mf = B * S, B * T * (1 + P)
+        tm("im2col_kernel", "im2col", B * T * (c.num_channels * c.image_size ** 2 * 4 + P * Kemb * 2), "byte",
+           ops.tubelet_im2col, pix, (1, pc, pc), ws["A_emb"], order="patch_major")
         ops.gemm(ws["A_emb"], pk["w_emb"], pk["b_emb"], "embed_f32", X, aux=pk["pos_time"], group=P * T,
-                 group_stride=S, group_offset=1, m=Memb)
+                 group_stride=S, group_offset=1, m=Memb, flop=2.0 * B * P * T * D * Kemb, op="embed")
         ops.cls_init(pk["cls"], pk["pos"], X, B, S)
         act = "bias_gelu_erf" if c.hidden_act == "gelu" else "bias_gelu_tanh"
         scale = 1.0 / math.sqrt(c.hidden_size // Hn)
+        pcfg = -1 if self.proj_cfg is None else self.proj_cfg
         for L in pk["layers"]:
             # temporal branch (clip layout)
-            ops.layernorm(X, L["lnt_g"], L["lnt_b"], eps, Hc, m=B * S)
-            ops.gemm(Hc, L["w_qkv_t"], L["b_qkv_t"], "bias", QKV)
-            ops.temporal_attention(QKV, B, P, T, Hn, scale, O, q_prescaled=True)
-            ops.gemm(O, L["w_t"], L["b_t"], "bias", Yb, cfg=-1 if self.proj_cfg is None else self.proj_cfg)
-            # spatial branch (frame layout)
-            ops.divided_add_layernorm(X, Yb, B, P, T, L["ln1_g"], L["ln1_b"], eps, "temporal_to_spatial", Hf)
-            ops.gemm(Hf, L["w_qkv_s"], L["b_qkv_s"], "bias", QKV)
+            tm("layernorm_kernel", "layernorm", Mc * D * 6, "byte", ops.layernorm, X, L["lnt_g"], L["lnt_b"], eps, Hc,
+               m=B * S)
+            ops.gemm(Hc, L["w_qkv_t"], L["b_qkv_t"], "bias", QKV, flop=2.0 * Mc * 3 * D * D, op="qkv_temporal")
+            tm("temporal_attn_lds_kernel", "temporal_attention", 4.0 * T * T * 64 * Hn * B * P, "flop",
+               ops.temporal_attention, QKV, B, P, T, Hn, scale, O, q_prescaled=True)
+            ops.gemm(O, L["w_t"], L["b_t"], "bias", Yb, cfg=pcfg, flop=2.0 * Mc * D * D, op="proj_temporal")
+            # spatial branch (frame layout): X += temporal output, LayerNorm in the frame layout
+            tm("tsf_add_ln_kernel", "add_layernorm", Mc * D * (4 + 2 + 4) + Mf * D * 2, "byte",
+               ops.divided_add_layernorm, X, Yb, B, P, T, L["ln1_g"], L["ln1_b"], eps, "temporal_to_spatial", Hf)
+            ops.gemm(Hf, L["w_qkv_s"], L["b_qkv_s"], "bias", QKV, flop=2.0 * Mf * 3 * D * D, op="qkv_spatial")
             ev = self.kernel_events
             if ev is not None:  # recorded on the current stream, the one the kernel runs on
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-            ops.attention(QKV, B * T, 1 + P, Hn, scale, O, q_prescaled=True)
+            tm("attn_short_d64_kernel", "spatial_attention", 4.0 * (1 + P) * (1 + P) * 64 * Hn * B * T, "flop",
+               ops.attention, QKV, B * T, 1 + P, Hn, scale, O, q_prescaled=True)
             if ev is not None:
                 e1.record()
                 # flop, algorithmic bytes (q, k, v read and the output written once: 4 x 64 x 2 B
                 # per token-head)
                 ev.append((e0, e1, 4.0 * (1 + P) * (1 + P) * 64 * Hn * B * T, 512.0 * (1 + P) * Hn * B * T))
-            ops.gemm(O, L["w_o"], L["b_o"], "bias", Yb, cfg=-1 if self.proj_cfg is None else self.proj_cfg)
+            ops.gemm(O, L["w_o"], L["b_o"], "bias", Yb, cfg=pcfg, flop=2.0 * Mf * D * D, op="o_proj")
             # MLP (clip layout)
-            ops.divided_add_layernorm(X, Yb, B, P, T, L["ln2_g"], L["ln2_b"], eps, "spatial_to_mlp", Hc)
-            ops.gemm(Hc, L["w_1"], L["b_1"], act, Hd)
-            ops.gemm(Hd, L["w_2"], L["b_2"], "bias_resid_f32", X)
+            tm("tsf_add_ln_kernel", "add_layernorm", Mf * D * 2 + Mc * D * (4 + 4 + 2), "byte",
+               ops.divided_add_layernorm, X, Yb, B, P, T, L["ln2_g"], L["ln2_b"], eps, "spatial_to_mlp", Hc)
+            ops.gemm(Hc, L["w_1"], L["b_1"], act, Hd, flop=2.0 * Mc * I * D, op="fc1")
+            ops.gemm(Hd, L["w_2"], L["b_2"], "bias_resid_f32", X, flop=2.0 * Mc * D * I, op="fc2")
         return ops.cls_head(X, B, S, pk["lnf_g"], pk["lnf_b"], eps, pk["w_cls"], pk["b_cls"],
                             out=ws["logits"] if out is None else out)
 

@@ -411,6 +411,7 @@ class VivitForVideoClassification(torch.nn.Module):
         ws = self._workspace(B, pix.device, part)
         D = c.hidden_size
         npatch, S, Mpad, Memb = self.geometry(B)
+        kt_, kh_, kw_ = c.tubelet_size
         eps = c.layer_norm_eps
         X, Y, QKV, O, Hd = ws["X"], ws["Y"], ws["QKV"], ws["O"], ws["Hd"]
         # optional per-launch HIP-event timing (bench.py), recorded on this part's stream, the
@@ -427,9 +428,17 @@ class VivitForVideoClassification(torch.nn.Module):
             (ev.setdefault(name, []) if isinstance(ev, dict) else ev).append((e0, e1))
             return r
 
-        run("im2col", ops.tubelet_im2col, pix, c.tubelet_size, ws["A_emb"])
+        # algorithmic work per launch for an installed ops.OpRecorder (B*S token rows, no padding)
+        M = B * S
+        I = c.intermediate_size
+        Kemb = c.num_channels * kt_ * kh_ * kw_
+        T_, H_ = c.num_frames, c.image_size
+        ln_bytes = M * D * (4 + 2)
+        tm = ops.timed
+        run("im2col", tm, "im2col_kernel", "im2col", B * (T_ * c.num_channels * H_ * H_ * 4 + npatch * Kemb * 2), "byte",
+            ops.tubelet_im2col, pix, c.tubelet_size, ws["A_emb"])
         run("embed", ops.gemm, ws["A_emb"], pk["w_emb"], pk["b_emb"], "embed_f32", X, aux=pk["pos"][1:],
-            group=npatch, group_stride=S, group_offset=1, m=Memb)
+            group=npatch, group_stride=S, group_offset=1, m=Memb, flop=2.0 * B * npatch * D * Kemb, op="embed")
         ops.cls_init(pk["cls"], pk["pos"], X, B, S)
         act = "bias_gelu_tanh" if c.hidden_act in ("gelu_fast", "gelu_pytorch_tanh", "gelu_new") else "bias_gelu_erf"
         scale = 1.0 / math.sqrt(D // c.num_attention_heads)
@@ -452,14 +461,22 @@ class VivitForVideoClassification(torch.nn.Module):
 
         m_ln = B * S if tight else None
         (m_qkv, c_qkv), (m_o, c_o), (m_1, c_1), (m_2, c_2) = rows("qkv"), rows("o_proj"), rows("fc1"), rows("fc2")
+        Hn = c.num_attention_heads
+        attn_flop = 4.0 * S * S * (D // Hn) * Hn * B
         for L in pk["layers"]:
-            run("layernorm", ops.layernorm, X, L["ln1_g"], L["ln1_b"], eps, Y, m=m_ln)
-            run("qkv", qkv_gemm, Y, L["w_qkv"], L["b_qkv"], "bias", QKV, m=m_qkv, cfg=c_qkv)
-            run("attention", ops.attention, QKV, B, S, c.num_attention_heads, scale, O, q_prescaled=True)
-            run("o_proj", ops.gemm, O, L["w_o"], L["b_o"], "bias_resid_f32", X, m=m_o, cfg=c_o)
-            run("layernorm", ops.layernorm, X, L["ln2_g"], L["ln2_b"], eps, Y, m=m_ln)
-            run("fc1", ops.gemm, Y, L["w_1"], L["b_1"], act, Hd, m=m_1, cfg=c_1)
-            run("fc2", fc2_gemm, Hd, L["w_2"], L["b_2"], "bias_resid_f32", X, m=m_2, cfg=c_2)
+            run("layernorm", tm, "layernorm_kernel", "layernorm", ln_bytes, "byte", ops.layernorm, X, L["ln1_g"],
+                L["ln1_b"], eps, Y, m=m_ln)
+            run("qkv", qkv_gemm, Y, L["w_qkv"], L["b_qkv"], "bias", QKV, m=m_qkv, cfg=c_qkv, flop=2.0 * M * 3 * D * D,
+                op="qkv")
+            run("attention", tm, "attn_fwd_d64_kernel", "attention", attn_flop, "flop", ops.attention, QKV, B, S, Hn,
+                scale, O, q_prescaled=True)
+            run("o_proj", ops.gemm, O, L["w_o"], L["b_o"], "bias_resid_f32", X, m=m_o, cfg=c_o, flop=2.0 * M * D * D,
+                op="o_proj")
+            run("layernorm", tm, "layernorm_kernel", "layernorm", ln_bytes, "byte", ops.layernorm, X, L["ln2_g"],
+                L["ln2_b"], eps, Y, m=m_ln)
+            run("fc1", ops.gemm, Y, L["w_1"], L["b_1"], act, Hd, m=m_1, cfg=c_1, flop=2.0 * M * I * D, op="fc1")
+            run("fc2", fc2_gemm, Hd, L["w_2"], L["b_2"], "bias_resid_f32", X, m=m_2, cfg=c_2, flop=2.0 * M * D * I,
+                op="fc2")
         return ops.cls_head(X, B, S, pk["lnf_g"], pk["lnf_b"], eps, pk["w_cls"], pk["b_cls"],
                             out=ws["logits"] if out is None else out)
 

@@ -7,6 +7,7 @@ max-abs-error vs the fp32 CPU reference and a roofline line for the dominant ker
                                        # AdamW) bf16, 4 clips per GPU, RCCL gradient all-reduce
   python bench.py --mode timesformer   # BASELINE configs[2]: TimeSformer-B 8f, 16 clips per GPU
   python bench.py --mode swin          # BASELINE configs[3]: Video Swin-T 32f, 4 clips per GPU
+  python bench.py --mode resnet3d      # the resnet50-3d-video family: ResNet3D-50 32f, 4 clips per GPU
 
 One process per GPU (torch.distributed.run for N > 1, backend nccl = RCCL).  Clips
 shard as independent data-parallel units: each rank runs its own batch and no
@@ -310,7 +311,52 @@ FAMILIES = {
              "(BASELINE configs[3])", "window_attn_mb_d32_kernel (all 12 blocks, head_dim 32; relative-position bias "
              "and shift mask on the matrix pipe)",
              "window_attn_mb_d32_kernel"),
+    "resnet3d": ("clips/sec fwd ResNet3D-50 32x224^2 bf16", 349.0, 4,
+                 "ResNet3D-50 (pytorchvideo create_resnet as resnet50-3d-video configures it), 32x224x224 clips, "
+                 "batch 4 per GPU", None, None),
 }
+
+# rocprofv3 name prefixes of the non-GEMM kernels the recorder labels (ops.timed labels); GEMM labels
+# are already rocprofv3 names (ops.GEMM_KERNEL)
+PROF_NAME = {"attn_short_d64_kernel": "ashort::attn_short_d64_kernel<0, 7>",
+             "window_attn_mb_d32_kernel": "window_attn_mb_d32_kernel",
+             "attn_fwd_d64_kernel": ATTN_KERNEL}
+
+
+def op_breakdown(model, step, n_steps: int):
+    """`n_steps` extra (untimed) one-stream steps with HIP events around EVERY launch (ops.OpRecorder):
+    per kernel instantiation its launches, mean launch time, share of the step and achieved rate on the
+    algorithmic work the model states for it.  Returns (table sorted by share, step ms)."""
+    from vclip_amd import ops
+    rec = ops.OpRecorder()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with ops.recording(rec):
+        for _ in range(n_steps):
+            step()
+    torch.cuda.synchronize()
+    step_ms = (time.perf_counter() - t0) / n_steps * 1e3
+    return rec.summary(n_steps, step_ms), step_ms
+
+
+def dominant_roofline(table, mode):
+    """The roofline line of the kernel with the largest share of the step (op_breakdown's first row):
+    GEMMs and attention against the bf16 MFMA peak, byte-moving kernels against HBM; traffic and PMC
+    figures only from profiles/ of this build and mode."""
+    kernel, row = next(iter(table.items()))
+    mfma = row["unit"] == "TFLOP/s"
+    peak = PEAK_BF16_TFLOPS if mfma else PEAK_HBM_GBS
+    prof = PROF_NAME.get(kernel, kernel)
+    traffic, traffic_src = measured_traffic(prof, mode)
+    pmc, pmc_src = measured_pmc(prof, mode)
+    mfma_busy, valu_per_mfma = pmc_rates(pmc)
+    return {"bound": "mfma" if mfma else "hbm", "kernel": kernel, "ops": row["ops"], "achieved": row["achieved"],
+            "peak": peak, "unit": row["unit"], "frac": round(row["achieved"] / peak, 4),
+            "share_of_step": row["share_of_step"], "avg_launch_ms": row["avg_launch_ms"],
+            "launches_per_step": row["launches_per_step"], "traffic": traffic, "traffic_source": traffic_src,
+            "mfma_busy": mfma_busy, "valu_per_mfma": valu_per_mfma, "pmc_source": pmc_src,
+            "timed_on": "HIP events around every launch of 3 extra one-stream steps (ops.OpRecorder); algorithmic "
+                        "work = real token rows and channels (no padding)"}
 
 
 def cpu_family_baseline(mode, n_clips, gpu_logits_fn):
@@ -326,11 +372,18 @@ def cpu_family_baseline(mode, n_clips, gpu_logits_fn):
                    hidden_act=c.hidden_act)
         sd = make_timesformer_weights(c.as_shape_cfg(), seed=0)
         x = make_synthetic_clips(n_clips, 8, 224, seed=1)
-    else:
+    elif mode == "swin":
         from oracle.swin3d_ref import swin3d_forward as fwd
         from vclip_amd.swin3d import SWIN3D_CONFIGS
         cfg = dict(SWIN3D_CONFIGS["tiny"], num_classes=2)
         sd = make_swin3d_weights(cfg, seed=0)
+        x = make_synthetic_video(n_clips, 32, 224, seed=1)
+    else:
+        from oracle.resnet3d_ref import resnet3d_forward as fwd
+        from vclip_amd.resnet3d import RESNET3D_50
+        from vclip_amd.weights import make_resnet3d_weights
+        cfg = dict(RESNET3D_50)
+        sd = make_resnet3d_weights(cfg, seed=0)
         x = make_synthetic_video(n_clips, 32, 224, seed=1)
     sd = {k: torch.from_numpy(v) for k, v in sd.items()}
     cores = torch.get_num_threads()
@@ -339,8 +392,12 @@ def cpu_family_baseline(mode, n_clips, gpu_logits_fn):
         t0 = time.perf_counter()
         ref = [fwd(sd, cfg, torch.from_numpy(x[i:i + 1])) for i in range(n_clips)]
         dt = time.perf_counter() - t0
-    err = float(np.abs(gpu_logits_fn(x) - torch.cat(ref).numpy()).max())
-    name = "oracle/timesformer_ref.py" if mode == "timesformer" else "oracle/swin3d_ref.py"
+    ref = torch.cat(ref).numpy()
+    got = gpu_logits_fn(x)
+    err = float(np.abs(got - ref).max())
+    if mode == "resnet3d":  # random-init logits are O(5): the bar (tests/test_resnet3d_gpu.py) is relative
+        err = err / max(1.0, float(np.abs(ref).max()))
+    name = {"timesformer": "oracle/timesformer_ref.py", "swin": "oracle/swin3d_ref.py"}.get(mode, "oracle/resnet3d_ref.py")
     return {"value": n_clips / dt, "unit": "clips/s", "cores": cores, "kind": "port",
             "sample": f"{n_clips} clips fp32 forward, B=1 each, {name}, torch CPU {cores} threads"}, err
 
@@ -354,9 +411,13 @@ def run_family(a, dist, rank, world, dev):
         from vclip_amd.timesformer import create_model
         model = create_model(num_frames=8, device=dev)
         x = torch.from_numpy(make_synthetic_clips(a.batch, 8, 224, seed=1 + rank)).to(dev)
-    else:
+    elif a.mode == "swin":
         from vclip_amd.swin3d import create_model
         model = create_model(model_size="tiny", device=dev)
+        x = torch.from_numpy(make_synthetic_video(a.batch, 32, 224, seed=1 + rank)).to(dev)
+    else:
+        from vclip_amd.resnet3d import create_model
+        model = create_model(device=dev).eval()
         x = torch.from_numpy(make_synthetic_video(a.batch, 32, 224, seed=1 + rank)).to(dev)
 
     model.graph_replay = bool(a.graph)
@@ -364,43 +425,50 @@ def run_family(a, dist, rank, world, dev):
     def step():
         model.forward_logits(x)
 
-    def timed(streams, evs=None):
+    def timed(streams):
         model.concurrent_streams = streams
         for _ in range(a.warmup):
             step()
         torch.cuda.synchronize()
-        model.kernel_events = evs
-        t = timed_loop(step, a.steps, 0, dist, torch.cuda.synchronize)
-        model.kernel_events = None
-        return t
+        return timed_loop(step, a.steps, 0, dist, torch.cuda.synchronize)
 
-    # headline: the batch over `--streams` HIP streams; roofline: a one-stream pass with HIP events
-    # around every attention launch (the fwd mode's scheme)
+    # headline: the batch over `--streams` HIP streams (graph replay), nothing instrumented; then the
+    # per-kernel table of 3 one-stream steps with HIP events around every launch, whose largest row is
+    # the roofline line (the step's dominant kernel)
     dt = timed(a.streams)
     model.graph_replay = False  # the passes below are event-instrumented or one-off calls
-    evs = []
-    dt1 = timed(1, evs)
+    dt1 = timed(1)
+    table, instr_ms = op_breakdown(model, step, 3)
     model.concurrent_streams = 1
-    attn_s = sum(e0.elapsed_time(e1) for e0, e1, _, _ in evs) * 1e-3
-    attn_flop = sum(f for _, _, f, _ in evs)
-    attn_bytes = sum(b for _, _, _, b in evs)
-    attn_tflops = attn_flop / attn_s / 1e12
-    # algorithmic bytes (from the model, per launch): q, k, v read and the output written once per
-    # (sequence | window, head), 4 x N x head_dim x 2 B against 4 N^2 head_dim flop: N / 2 flop per
-    # byte with N the tokens per attention unit (197 = 1 + 14^2 per frame; 392 = 8 x 7 x 7 per Swin
-    # window)
-    unit_name = "sequence" if a.mode == "timesformer" else "window"
-    intensity = attn_flop / attn_bytes
-    attn_gbs = attn_bytes / attn_s / 1e9
-    bound = "hbm" if intensity * PEAK_HBM_GBS * 1e9 < PEAK_BF16_TFLOPS * 1e12 else "mfma"
     value = a.batch * a.steps * world / dt
     ms_per_step = dt / a.steps * 1e3
     model_tflops = gflop * a.batch / (ms_per_step * 1e-3) / 1e3
     out = None
     if rank == 0:
-        traffic, traffic_src = measured_traffic(kprof, a.mode)
-        pmc, pmc_src = measured_pmc(kprof, a.mode)
-        mfma_busy, valu_per_mfma = pmc_rates(pmc)
+        roof = dominant_roofline(table, a.mode)
+        roof["one_stream_clips_s"] = round(a.batch * a.steps * world / dt1, 2)
+        attn = None
+        if kprof is not None:
+            # the family's attention kernel beside it: intensity N / 2 flop per byte (N keys per
+            # sequence | window; q, k, v read and the output written once, 8 B per token x head-dim
+            # element) puts it below the 312 flop/B ridge, so HBM is its algorithmic bound
+            akey = next(k for k in table if k in PROF_NAME and PROF_NAME[k] == kprof)
+            arow = table[akey]
+            unit_n = 197 if a.mode == "timesformer" else 392
+            gbs = arow["achieved"] * 1e3 / (unit_n / 2)
+            traffic, traffic_src = measured_traffic(kprof, a.mode)
+            pmc, pmc_src = measured_pmc(kprof, a.mode)
+            mfma_busy, valu_per_mfma = pmc_rates(pmc)
+            attn = {"kernel": kname, "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(gbs / PEAK_HBM_GBS, 4), "achieved_tflops": arow["achieved"],
+                    "mfma_frac": round(arow["achieved"] / PEAK_BF16_TFLOPS, 4), "share_of_step": arow["share_of_step"],
+                    "avg_launch_ms": arow["avg_launch_ms"], "intensity_flop_per_byte": unit_n / 2,
+                    "traffic": traffic, "traffic_source": traffic_src, "mfma_busy": mfma_busy,
+                    "valu_per_mfma": valu_per_mfma, "pmc_source": pmc_src,
+                    "executed_work_note": ("window_attn_mb_d32_kernel issues 2 identity-bias MFMAs (+1 mask MFMA in "
+                                           "shifted windows) per 32-key block beside the 2 QK^T MFMAs and streams its "
+                                           "fp16 bias operand from L2: executed MFMA work ~2x the algorithmic flops "
+                                           "counted here" if a.mode == "swin" else None)}
         cpu, err = None, None
         if world == 1 and not a.no_cpu_baseline:
             cpu, err = cpu_family_baseline(
@@ -413,25 +481,11 @@ def run_family(a, dist, rank, world, dev):
             "config": {"workload": workload, "global_batch": a.batch * world, "parallelism": f"dp{world}",
                        "streams": a.streams, "hip_graph": _graph_used(model, a)},
             "logit_max_abs_err": err,
-            "roofline": {"bound": bound, "kernel": kname,
-                         "achieved": round(attn_gbs, 1) if bound == "hbm" else round(attn_tflops, 1),
-                         "peak": PEAK_HBM_GBS if bound == "hbm" else PEAK_BF16_TFLOPS,
-                         "unit": "GB/s" if bound == "hbm" else "TFLOP/s",
-                         "frac": round(attn_gbs / PEAK_HBM_GBS if bound == "hbm" else attn_tflops / PEAK_BF16_TFLOPS, 4),
-                         "traffic": traffic, "traffic_source": traffic_src,
-                         "avg_launch_ms": round(attn_s * 1e3 / len(evs), 4),
-                         "bytes_per_step": round(attn_bytes / a.steps / 1e6, 2), "bytes_unit": "MB",
-                         "flop_per_step": round(attn_flop / a.steps / 1e9, 2),
-                         "intensity_flop_per_byte": round(intensity, 1),
-                         "achieved_tflops": round(attn_tflops, 1),
-                         "mfma_frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4),
-                         "bound_note": f"{intensity:.0f} flop/B (keys per {unit_name} / 2: q, k, v read and the output "
-                                       f"written once, 8 B per token x head-dim element) is below the MFMA/HBM ridge "
-                                       f"{PEAK_BF16_TFLOPS / PEAK_HBM_GBS * 1e3:.0f} flop/B, so HBM bounds the kernel",
-                         "timed_on": f"a separate K-step pass on one HIP stream (the headline runs {a.streams}): "
-                                     f"clips/s {a.batch * a.steps * world / dt1:.2f} there",
-                         "mfma_busy": mfma_busy,
-                         "valu_per_mfma": valu_per_mfma, "pmc_source": pmc_src},
+            "logit_err_note": "max |logit - oracle| relative to max(1, max |oracle logit|)" if a.mode == "resnet3d" else None,
+            "roofline": roof,
+            "attention_roofline": attn,
+            "kernel_breakdown": dict(list(table.items())[:12], note=f"3 one-stream steps, HIP events around every "
+                                     f"launch: {instr_ms:.3f} ms per step under that instrumentation"),
             "model_tflops": round(model_tflops, 1), "model_frac_of_peak": round(model_tflops / PEAK_BF16_TFLOPS, 4),
             "cpu_baseline": cpu,
             "build": _build_id(),
@@ -517,7 +571,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--mode", choices=["fwd", "train", "timesformer", "swin"], default="fwd")
+    ap.add_argument("--mode", choices=["fwd", "train", "timesformer", "swin", "resnet3d"], default="fwd")
     ap.add_argument("--batch", type=int, default=None, help="clips per GPU per step (fwd 8, train 4)")
     ap.add_argument("--cpu-clips", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -534,7 +588,7 @@ def main():
     if a.batch is None:
         a.batch = {"fwd": 8, "train": 4}.get(a.mode) or FAMILIES[a.mode][2]
     if a.cpu_clips is None:
-        a.cpu_clips = {"fwd": 2, "timesformer": 3}.get(a.mode, 1)
+        a.cpu_clips = {"fwd": 2, "timesformer": 3, "resnet3d": 2}.get(a.mode, 1)
 
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         sys.exit(_spawn_world(a.gpus))
@@ -618,6 +672,7 @@ def main():
 
     model.concurrent_streams = 1
     breakdown = kernel_breakdown(model, step, a.batch, 1, 3)
+    ktable, instr_ms = op_breakdown(model, step, 3)
 
     clips = a.batch * a.steps * world
     value = clips / dt
@@ -677,6 +732,8 @@ def main():
                          "mfma_busy": mfma_busy, "valu_per_mfma": valu_per_mfma,
                          "pmc_source": pmc_src},
             "kernel_breakdown": breakdown,
+            "kernel_table": dict(ktable, note=f"per kernel instantiation (ops.OpRecorder), 3 one-stream steps with HIP "
+                                 f"events around every launch: {instr_ms:.3f} ms per step under that instrumentation"),
             "build": _build_id(),
             "model_tflops": round(model_tflops, 1),
             "model_frac_of_peak": round(model_tflops / PEAK_BF16_TFLOPS, 4),

@@ -168,6 +168,11 @@ int vc_patch_im2col_h16(const float* pixel_values, int64_t B, int64_t T, int64_t
                         int kt, int kh, int kw, int token_order, int layout, int elem, uint16_t* A, int64_t lda,
                         hipStream_t stream);
 
+/* The tile config (kCfgs index) that vc_gemm_bf16 / vc_gemm_h16 pick with cfg = -1 for this shape,
+ * epilogue and output / aux layout (host-only query: no launch; instrumentation labels launches
+ * with it). */
+int vc_gemm_pick(int64_t M, int64_t N, int64_t K, int epilogue, int64_t ldo, int64_t ldaux, const void* aux);
+
 /* vc_gemm_bf16_cfg with the operand type as an argument: A, W and the 16-bit outputs are `elem`;
  * fp16 supports epilogues 0-4 (the inference forward's), bf16 all of them. */
 int vc_gemm_h16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
