@@ -227,35 +227,42 @@ __device__ __forceinline__ float4 ld_bf16x4(const uint16_t* p) {
                        bf2f((unsigned short)(u.y & 0xffff)), bf2f((unsigned short)(u.y >> 16)));
 }
 
+// Grid: x = 4 clip-layout rows per workgroup, y = clip.  Row indices are wave-uniform (scalar
+// index arithmetic: the per-lane 64-bit divisions of the first version sat in front of every
+// address); NV = float4 per lane (D <= 256 NV), so D = 768 runs 3 straight-line loads per lane
+// for x and y each, all issued before the first add.
+template <int NV>
 __global__ void __launch_bounds__(256) tsf_add_ln_kernel(float* __restrict__ x, int64_t ldx,
-                                                         const uint16_t* __restrict__ y, int64_t ldy, int64_t B, int P,
+                                                         const uint16_t* __restrict__ y, int64_t ldy, int P,
                                                          int T, int D, const float* __restrict__ g,
                                                          const float* __restrict__ be, float eps, int mode,
                                                          uint16_t* __restrict__ h, int64_t ldh) {
     const int lane = threadIdx.x & 63;
-    const int64_t S = 1 + (int64_t)P * T;
-    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= B * S) return;
-    const int64_t b = row / S;
-    const int r = (int)(row - b * S);
-    const int p = (r - 1) / T, t = (r - 1) % T;  // meaningful for r >= 1
+    const int S = 1 + P * T;
+    const int r = (int)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    if (r >= S) return;
+    const int64_t b = blockIdx.y;
+    const int64_t row = b * S + r;
+    const int p = r > 0 ? (r - 1) / T : 0, t = r > 0 ? (r - 1) - p * T : 0;
     const int64_t frow = (b * T + t) * (1 + P) + 1 + p;  // frame-layout row of a patch token
-    float4 v[4];
-    uint2 yv[4];
+    const float* xr = x + row * ldx;
+    const uint16_t* yr = y + (mode == 0 ? row : frow) * ldy;
+    float4 v[NV];
+    uint2 yv[NV];
     float s = 0.f;
     // every load of the row (x and, for patch rows, y) is issued before the first add / store
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NV; ++i) {
         const int n = (i * 64 + lane) * 4;
         v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         yv[i] = make_uint2(0u, 0u);
         if (n < D) {
-            v[i] = *reinterpret_cast<const float4*>(x + row * ldx + n);
-            if (r > 0) yv[i] = *reinterpret_cast<const uint2*>(y + (mode == 0 ? row : frow) * ldy + n);
+            v[i] = *reinterpret_cast<const float4*>(xr + n);
+            if (r > 0) yv[i] = *reinterpret_cast<const uint2*>(yr + n);
         }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NV; ++i) {
         const int n = (i * 64 + lane) * 4;
         if (n < D) {
             float4 a = v[i];
@@ -280,7 +287,7 @@ __global__ void __launch_bounds__(256) tsf_add_ln_kernel(float* __restrict__ x, 
     const float mean = wave_sum(s) / (float)D;
     float q = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NV; ++i) {
         if ((i * 64 + lane) * 4 < D) {
             const float a = v[i].x - mean, bb = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
             q += (a * a + bb * bb) + (c * c + d * d);
@@ -288,7 +295,7 @@ __global__ void __launch_bounds__(256) tsf_add_ln_kernel(float* __restrict__ x, 
     }
     const float rstd = rsqrtf(wave_sum(q) / (float)D + eps);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NV; ++i) {
         const int n = (i * 64 + lane) * 4;
         if (n < D) {
             const float4 gg = *reinterpret_cast<const float4*>(g + n), bb = *reinterpret_cast<const float4*>(be + n);
@@ -349,9 +356,18 @@ int vc_divided_add_layernorm(float* x, int64_t ldx, const uint16_t* y, int64_t l
     if (!x || !y || !gamma || !beta || !h) return fail(VC_ERR_INVALID_ARG, "vc_divided_add_layernorm: null pointer");
     if (D % 4 || D > 1024 || ldx % 4 || ldy % 4 || ldh % 4 || (mode != 0 && mode != 1) || B <= 0 || P <= 0 || T <= 0)
         return fail(VC_ERR_INVALID_ARG, "vc_divided_add_layernorm: bad shape / mode");
-    const int64_t rows = B * (1 + P * T);
-    tsf_add_ln_kernel<<<(unsigned)((rows + 3) / 4), 256, 0, stream>>>(x, ldx, y, ldy, B, (int)P, (int)T, (int)D, gamma,
-                                                                     beta, eps, mode, h, ldh);
+    const int64_t S = 1 + P * T;
+    if (S >= (1LL << 30) || B > 65535) return fail(VC_ERR_INVALID_ARG, "vc_divided_add_layernorm: too many rows");
+    const dim3 grid((unsigned)((S + 3) / 4), (unsigned)B);
+    const int nv = (int)((D + 255) / 256);
+#define VC_TSF_LN(NV_)                                                                                           \
+    tsf_add_ln_kernel<NV_><<<grid, 256, 0, stream>>>(x, ldx, y, ldy, (int)P, (int)T, (int)D, gamma, beta, eps, mode, h, \
+                                                     ldh)
+    if (nv == 1) VC_TSF_LN(1);
+    else if (nv == 2) VC_TSF_LN(2);
+    else if (nv == 3) VC_TSF_LN(3);
+    else VC_TSF_LN(4);
+#undef VC_TSF_LN
     return check_launch("vc_divided_add_layernorm");
 }
 

@@ -765,14 +765,508 @@ gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint
     }
 }
 
+// ---------------------------------------------------------------------------------
+// 256x256 ping-pong kernel (cfg 8).  The two waves that share a SIMD belong to different wave
+// groups (waves 0-3 = output rows 0-127 of the tile, waves 4-7 = rows 128-255; a workgroup's
+// waves 0-3 and 4-7 each cover the 4 SIMDs), and group 1 runs one barrier behind group 0: while
+// one group's 16 MFMAs run, the other group issues its LDS reads and LDS-DMAs and waits for them,
+// so each SIMD's matrix pipe alternates between its two waves instead of both waves stalling on
+// their reads at the same time (cdna_hip_programming.md §5, the 256^2 8-phase template).
+//   * K in 32-deep halves, one LDS ring slot each (A 256 x 32 then W 256 x 32, 64-B rows with
+//     the swz64 chunk swizzle): 4 slots = 128 KiB, one workgroup per CU;
+//   * two phases per K-half u, 16 MFMAs (v_mfma_f32_16x16x32) each:
+//       a(u): read A rows 0-63 of the wave tile + all 4 W fragments, stage W(u+2), MFMA rows 0-63;
+//       b(u): read A rows 64-127, stage A(u+3), vmcnt(6) (retires K-half u+1), MFMA rows 64-127;
+//     phase body: reads | LDS-DMA | [vmcnt] | s_barrier | lgkmcnt(0) | MFMAs | s_barrier;
+//   * RAW: a K-half is retired by every wave's counted vmcnt before the first barrier of phase
+//     b(u) and read from phase a(u+1) on, one barrier later for the lagging group; WAR: a slot is
+//     restaged >= 2 phases after its last read (W(u+2) into W(u-2)'s slot 4 phases after, A(u+3)
+//     into A(u-1)'s slot 2 phases after);
+//   * per phase each wave issues 2 LDS-DMAs (16 KiB per workgroup), 3 phases' DMAs in flight.
+// Epilogue: the shared store_tile16 (all epilogues); a workgroup per output tile with the
+// bijective XCD remap, consecutive tiles of one XCD walking the N tiles of one A row panel.
+// ---------------------------------------------------------------------------------
+// ABL (timing-only ablation, cfg 11): every K-half is staged from k = 0..3 (operands L2-resident,
+// wrong results): the kernel's rate with the memory side taken out.
+template <int EPI, int ET = VC_ELEM_BF16, bool ABL = false>
+__global__ void __launch_bounds__(512, 1)
+gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw, int nbm,
+               int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
+               const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride, int64_t goff) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int BM = 256, BN = 256, BKH = 32, NS = 4;
+    constexpr int SLOT = (BM + BN) * 64;  // 32 KiB
+    constexpr int TM = 128, TN = 64, MI = 8, NI = 4;
+
+    const int nwg = nbm * nbn;
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, xq = nwg >> 3, rr = nwg & 7;
+    const int wgid = (xcd < rr ? xcd * (xq + 1) : rr * (xq + 1) + (xcd - rr) * xq) + (bid >> 3);
+    const int tm = wgid / nbn, tn = wgid % nbn;
+    const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int c16 = lane & 15, q = lane >> 4;
+
+    // staging: wave w fills A rows [32w, 32w + 32) and W rows [32w, 32w + 32), 16 rows per LDS-DMA
+    const int arow = wave * 32 + (lane >> 2);
+    const uint16_t* ag0 = A + (m0 + arow) * lda + swz64(arow, lane & 3) * 8;
+    const uint16_t* ag1 = A + (m0 + arow + 16) * lda + swz64(arow + 16, lane & 3) * 8;
+    const uint16_t* wg0 = W + (n0 + arow) * ldw + swz64(arow, lane & 3) * 8;
+    const uint16_t* wg1 = W + (n0 + arow + 16) * ldw + swz64(arow + 16, lane & 3) * 8;
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
+    auto stage_a = [&](int u) __attribute__((always_inline)) {
+        const uint32_t s = lds0 + (u & (NS - 1)) * SLOT + wave * 32 * 64;
+        const int ku = ABL ? (u & 3) : u;
+        glds16(ag0 + ku * BKH, __builtin_amdgcn_readfirstlane(s));
+        glds16(ag1 + ku * BKH, __builtin_amdgcn_readfirstlane(s + 16 * 64));
+    };
+    auto stage_w = [&](int u) __attribute__((always_inline)) {
+        const uint32_t s = lds0 + (u & (NS - 1)) * SLOT + BM * 64 + wave * 32 * 64;
+        const int ku = ABL ? (u & 3) : u;
+        glds16(wg0 + ku * BKH, __builtin_amdgcn_readfirstlane(s));
+        glds16(wg1 + ku * BKH, __builtin_amdgcn_readfirstlane(s + 16 * 64));
+    };
+    auto read_a = [&](int u, int i0, v8s (&fa)[4]) __attribute__((always_inline)) {
+        const char* At = smem + (u & (NS - 1)) * SLOT;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = lds_frag64(At, wm * TM + i0 + i * 16 + c16, q);
+    };
+    auto read_w = [&](int u, v8s (&fw)[4]) __attribute__((always_inline)) {
+        const char* Wt = smem + (u & (NS - 1)) * SLOT + BM * 64;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fw[j] = lds_frag64(Wt, wn * TN + j * 16 + c16, q);
+    };
+
+    v4f acc[MI][NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+    auto mma = [&](auto I0, const v8s (&fa)[4], const v8s (&fw)[4]) __attribute__((always_inline)) {
+        constexpr int i0 = decltype(I0)::value;
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's fragment reads
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i0 + i][j] = mfma16x32<ET>(fw[j], fa[i], acc[i0 + i][j]);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    using C0 = std::integral_constant<int, 0>;
+    using C4 = std::integral_constant<int, 4>;
+
+    const int nk = K / BKH;  // even, >= 4
+    v8s alo[4], ahi[4], wA[4], wB[4];
+    auto phase_a = [&](int u, v8s (&fw)[4]) __attribute__((always_inline)) {
+        read_a(u, 0, alo);
+        read_w(u, fw);
+        if (u + 2 < nk) stage_w(u + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(C0{}, alo, fw);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto phase_b = [&](int u, const v8s (&fw)[4]) __attribute__((always_inline)) {
+        read_a(u, 64, ahi);
+        if (u + 3 < nk) {
+            stage_a(u + 3);
+            wait_vm<6>();
+        } else if (u + 2 < nk) {
+            wait_vm<4>();
+        } else {
+            wait_vm<0>();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mma(C4{}, ahi, fw);
+        // the lagging group skips its last barrier: both groups then pass the same number
+        if (u + 1 < nk || wm == 0) __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    // prologue: A0 W0 A1 W1 A2 in flight, retire A0 W0, publish; group 1 falls one barrier behind
+    stage_a(0);
+    stage_w(0);
+    stage_a(1);
+    stage_w(1);
+    stage_a(2);
+    wait_vm<6>();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (wm == 1) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+
+    for (int u = 0; u < nk; u += 2) {
+        phase_a(u, wA);
+        phase_b(u, wA);
+        phase_a(u + 1, wB);
+        phase_b(u + 1, wB);
+    }
+    store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bias, out, ldo, aux, ldaux, G, gstride,
+                                  goff);
+}
+
+// ---------------------------------------------------------------------------------
+// 256x128 ping-pong kernel (cfg 9): the cfg 8 schedule on a narrower tile, for N = 768 outputs
+// (o_proj / fc2: 300 tiles per 12800 rows instead of 150).  Waves as 4 (rows) x 2 (cols), wave
+// tile 64 x 64 (4 x 4 blocks), so one K-half is one phase of 16 MFMAs reading 4 A + 4 W
+// fragments; group 0 = waves 0-3 (tile rows 0-127), group 1 = waves 4-7, one barrier behind.
+// Ring of 6 K-half slots (A 256 x 32 + W 128 x 32 = 24 KiB each, 144 KiB): phase u stages
+// K-half u + 4 into the slot read at phase u - 2 (WAR: two phases after its last read) and
+// retires K-half u + 1 with vmcnt(9) before its first barrier (three phases' DMAs in flight).
+// ---------------------------------------------------------------------------------
+template <int EPI, int ET = VC_ELEM_BF16>
+__global__ void __launch_bounds__(512, 1)
+gemm_pp128_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw, int nbm,
+                  int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
+                  const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride, int64_t goff) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int BM = 256, BN = 128, BKH = 32, NS = 6;
+    constexpr int SLOT = (BM + BN) * 64;  // 24 KiB
+    constexpr int TM = 64, TN = 64, MI = 4, NI = 4;
+
+    const int nwg = nbm * nbn;
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, xq = nwg >> 3, rr = nwg & 7;
+    const int wgid = (xcd < rr ? xcd * (xq + 1) : rr * (xq + 1) + (xcd - rr) * xq) + (bid >> 3);
+    const int tm = wgid / nbn, tn = wgid % nbn;
+    const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 1, wn = wave & 1, grp = wave >> 2;
+    const int c16 = lane & 15, q = lane >> 4;
+
+    // staging: wave w fills A rows [32w, 32w + 32) (two DMAs) and W rows [16w, 16w + 16) (one)
+    const int arow = wave * 32 + (lane >> 2), wrow = wave * 16 + (lane >> 2);
+    const uint16_t* ag0 = A + (m0 + arow) * lda + swz64(arow, lane & 3) * 8;
+    const uint16_t* ag1 = A + (m0 + arow + 16) * lda + swz64(arow + 16, lane & 3) * 8;
+    const uint16_t* wg0 = W + (n0 + wrow) * ldw + swz64(wrow, lane & 3) * 8;
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
+    auto stage = [&](int u) __attribute__((always_inline)) {
+        const uint32_t s = lds0 + (u % NS) * SLOT;
+        glds16(ag0 + u * BKH, __builtin_amdgcn_readfirstlane(s + wave * 32 * 64));
+        glds16(ag1 + u * BKH, __builtin_amdgcn_readfirstlane(s + (wave * 32 + 16) * 64));
+        glds16(wg0 + u * BKH, __builtin_amdgcn_readfirstlane(s + BM * 64 + wave * 16 * 64));
+    };
+
+    v4f acc[MI][NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+    const int nk = K / BKH;  // even, >= 4
+    v8s faA[4], fwA[4], faB[4], fwB[4];
+    auto phase = [&](int u, v8s (&fa)[4], v8s (&fw)[4]) __attribute__((always_inline)) {
+        const char* At = smem + (u % NS) * SLOT;
+        const char* Wt = At + BM * 64;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = lds_frag64(At, wm * TM + i * 16 + c16, q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fw[j] = lds_frag64(Wt, wn * TN + j * 16 + c16, q);
+        // retire K-half u + 1 (its younger DMAs: u + 2, u + 3 and, if staged now, u + 4)
+        if (u + 4 < nk) {
+            stage(u + 4);
+            wait_vm<9>();
+        } else if (u + 3 < nk) {
+            wait_vm<6>();
+        } else if (u + 2 < nk) {
+            wait_vm<3>();
+        } else {
+            wait_vm<0>();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's fragment reads
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x32<ET>(fw[j], fa[i], acc[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (u + 1 < nk || grp == 0) __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    stage(0);
+    stage(1);
+    stage(2);
+    stage(3);
+    wait_vm<9>();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (grp == 1) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+
+    for (int u = 0; u < nk; u += 2) {
+        phase(u, faA, fwA);
+        phase(u + 1, faB, fwB);
+    }
+    store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bias, out, ldo, aux, ldaux, G, gstride,
+                                  goff);
+}
+
+// ---------------------------------------------------------------------------------
+// Persistent 256x256 ping-pong kernel (cfg 10) for the 16-bit-output epilogues (q|k|v, fc1):
+// the cfg 8 phase schedule over one continuous sequence of K-halves that runs through all the
+// tiles of a workgroup (one per CU), so the ring never drains between tiles: the next tile's first
+// K-halves are staged during the current tile's last phases, and each group's epilogue (bias from
+// LDS, activation, 16-B stores) runs while the other group's MFMAs of the tile's last (or the
+// next tile's first) phase keep its SIMDs busy.  The epilogue's NST stores per wave are younger
+// than the DMAs of the K-half retired next, so that one wait counts them (vmcnt(6 + NST)).  The
+// first K-half of a tile starts its accumulators from a zero C operand (no 128-register clear).
+// Tile order as cfg 4: in round `it` the 32 workgroups of one XCD take 32 consecutive tiles
+// (row-major, N fastest), so the XCD's L2 holds ~3.5 A row panels and the whole W of q|k|v.
+// ---------------------------------------------------------------------------------
+template <int EPI, int ET = VC_ELEM_BF16>
+__global__ void __launch_bounds__(512, 1)
+gemm_ppp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw, int nbm,
+                int nbn, int K, int N, const float* __restrict__ bias, uint16_t* __restrict__ out, int64_t ldo,
+                uint16_t* __restrict__ pre_out, int64_t ldpre) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int BM = 256, BN = 256, BKH = 32, NS = 4;
+    constexpr int SLOT = (BM + BN) * 64;  // 32 KiB
+    constexpr int TM = 128, TN = 64, MI = 8, NI = 4;
+    constexpr bool SAVE = EPI == VC_EPI_BIAS_GELU_TANH_SAVE;
+    constexpr int NST = MI * (NI / 2) * (SAVE ? 2 : 1);  // 16-B stores per wave per tile epilogue
+    float* bias_lds = reinterpret_cast<float*>(smem + NS * SLOT);
+
+    const int ntiles = nbm * nbn;
+    const int G = gridDim.x;
+    const int b = blockIdx.x;
+    const int lane_slot = (b & 7) * (G >> 3) + (b >> 3);
+    const int mine = lane_slot < ntiles ? (ntiles - 1 - lane_slot) / G + 1 : 0;  // tiles of this workgroup
+    if (mine == 0) return;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int c16 = lane & 15, q = lane >> 4;
+
+    for (int n = tid * 4; n < N; n += 512 * 4)
+        *reinterpret_cast<float4*>(bias_lds + n) = *reinterpret_cast<const float4*>(bias + n);
+    __syncthreads();
+
+    const int nk = K / BKH;  // even, >= 4
+    const int total = mine * nk;  // K-halves of this workgroup, all tiles
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
+    const int arow = wave * 32 + (lane >> 2);
+    const int64_t aoff0 = (int64_t)arow * lda + swz64(arow, lane & 3) * 8;
+    const int64_t aoff1 = (int64_t)(arow + 16) * lda + swz64(arow + 16, lane & 3) * 8;
+    const int64_t woff0 = (int64_t)arow * ldw + swz64(arow, lane & 3) * 8;
+    const int64_t woff1 = (int64_t)(arow + 16) * ldw + swz64(arow + 16, lane & 3) * 8;
+    auto tile_origin = [&](int it, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
+        const int tile = it * G + lane_slot;
+        const int tm = tile / nbn;
+        m0 = (int64_t)tm * BM;
+        n0 = (int64_t)(tile - tm * nbn) * BN;
+    };
+    // staging cursors: the A stream runs 3 K-halves ahead of the phase being computed, the W
+    // stream 2; each walks (tile, k) in order and moves its base pointer at a tile change
+    struct Cursor {
+        int it, u;
+        const uint16_t* p;
+    };
+    auto cursor_at = [&](int U, bool is_a) __attribute__((always_inline)) {
+        Cursor c;
+        c.it = U / nk;
+        c.u = U - c.it * nk;
+        int64_t m0, n0;
+        tile_origin(c.it < mine ? c.it : mine - 1, m0, n0);
+        c.p = is_a ? A + m0 * lda : W + n0 * ldw;
+        return c;
+    };
+    Cursor ca = cursor_at(0, true), cw = cursor_at(0, false);
+    auto advance = [&](Cursor& c, bool is_a) __attribute__((always_inline)) {
+        if (++c.u == nk) {
+            c.u = 0;
+            ++c.it;
+            if (c.it < mine) {
+                int64_t m0, n0;
+                tile_origin(c.it, m0, n0);
+                c.p = is_a ? A + m0 * lda : W + n0 * ldw;
+            }
+        }
+    };
+    auto stage_a = [&](int U) __attribute__((always_inline)) {  // K-half U = (ca.it, ca.u)
+        const uint32_t s = lds0 + (U & (NS - 1)) * SLOT + wave * 32 * 64;
+        glds16(ca.p + aoff0 + ca.u * BKH, __builtin_amdgcn_readfirstlane(s));
+        glds16(ca.p + aoff1 + ca.u * BKH, __builtin_amdgcn_readfirstlane(s + 16 * 64));
+        advance(ca, true);
+    };
+    auto stage_w = [&](int U) __attribute__((always_inline)) {
+        const uint32_t s = lds0 + (U & (NS - 1)) * SLOT + BM * 64 + wave * 32 * 64;
+        glds16(cw.p + woff0 + cw.u * BKH, __builtin_amdgcn_readfirstlane(s));
+        glds16(cw.p + woff1 + cw.u * BKH, __builtin_amdgcn_readfirstlane(s + 16 * 64));
+        advance(cw, false);
+    };
+    auto read_a = [&](int U, int i0, v8s (&fa)[4]) __attribute__((always_inline)) {
+        const char* At = smem + (U & (NS - 1)) * SLOT;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = lds_frag64(At, wm * TM + i0 + i * 16 + c16, q);
+    };
+    auto read_w = [&](int U, v8s (&fw)[4]) __attribute__((always_inline)) {
+        const char* Wt = smem + (U & (NS - 1)) * SLOT + BM * 64;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fw[j] = lds_frag64(Wt, wn * TN + j * 16 + c16, q);
+    };
+
+    v4f acc[MI][NI];
+    auto mma = [&](auto I0, auto FIRST, const v8s (&fa)[4], const v8s (&fw)[4]) __attribute__((always_inline)) {
+        constexpr int i0 = decltype(I0)::value;
+        constexpr bool first = decltype(FIRST)::value;
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i0 + i][j] = mfma16x32<ET>(fw[j], fa[i], first ? v4f{0.f, 0.f, 0.f, 0.f} : acc[i0 + i][j]);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    using C0 = std::integral_constant<int, 0>;
+    using C4 = std::integral_constant<int, 4>;
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+
+    v8s alo[4], ahi[4], wA[4], wB[4];
+    auto phase_a = [&](auto FIRST, int U, v8s (&fw)[4]) __attribute__((always_inline)) {
+        read_a(U, 0, alo);
+        read_w(U, fw);
+        if (U + 2 < total) stage_w(U + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(C0{}, FIRST, alo, fw);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // POST: the first b phase after an epilogue (its NST stores are younger than K-half U + 1)
+    auto phase_b = [&](auto FIRST, auto POST, int U, const v8s (&fw)[4]) __attribute__((always_inline)) {
+        constexpr int X = decltype(POST)::value ? NST : 0;
+        read_a(U, 64, ahi);
+        if (U + 3 < total) {
+            stage_a(U + 3);
+            wait_vm<6 + X>();
+        } else if (U + 2 < total) {
+            wait_vm<4 + X>();
+        } else {
+            wait_vm<0>();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mma(C4{}, FIRST, ahi, fw);
+        if (U + 1 < total || wm == 0) __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    // prologue: A0 W0 A1 W1 A2 of the first tile in flight, retire A0 W0, publish; group 1 one barrier behind
+    stage_a(0);
+    stage_w(0);
+    stage_a(1);
+    stage_w(1);
+    stage_a(2);
+    wait_vm<6>();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (wm == 1) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+
+    using Zero = std::integral_constant<int, 0>;
+    using One = std::integral_constant<int, 1>;
+    int U = 0;
+    for (int it = 0; it < mine; ++it) {
+        int64_t m0, n0;
+        tile_origin(it, m0, n0);
+        phase_a(T_{}, U, wA);
+        if (it == 0) phase_b(T_{}, Zero{}, U, wA);
+        else phase_b(T_{}, One{}, U, wA);
+        phase_a(F_{}, U + 1, wB);
+        phase_b(F_{}, Zero{}, U + 1, wB);
+        for (int u = 2; u < nk; u += 2) {
+            phase_a(F_{}, U + u, wA);
+            phase_b(F_{}, Zero{}, U + u, wA);
+            phase_a(F_{}, U + u + 1, wB);
+            phase_b(F_{}, Zero{}, U + u + 1, wB);
+        }
+        U += nk;
+
+        // epilogue: + bias (LDS), activation, 16-bit, permlane16 pairs -> 16-B row stores
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            const int64_t m = m0 + wm * TM + i * 16 + c16;
+            uint16_t* orow = out + m * ldo;
+            uint16_t* prow = SAVE ? pre_out + m * ldpre : nullptr;
+#pragma unroll
+            for (int jp = 0; jp < NI / 2; ++jp) {
+                unsigned pk[2][2], pp[2][2];
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const int nl = (int)n0 + wn * TN + (2 * jp + s) * 16 + 4 * q;
+                    const float4 bb = *reinterpret_cast<const float4*>(bias_lds + nl);
+                    float v0 = acc[i][2 * jp + s][0] + bb.x, v1 = acc[i][2 * jp + s][1] + bb.y;
+                    float v2 = acc[i][2 * jp + s][2] + bb.z, v3 = acc[i][2 * jp + s][3] + bb.w;
+                    if constexpr (SAVE) {
+                        pp[s][0] = pack2bf(v0, v1);
+                        pp[s][1] = pack2bf(v2, v3);
+                    }
+                    if (EPI == VC_EPI_BIAS_GELU_TANH || SAVE) {
+                        v0 = gelu_tanh(v0); v1 = gelu_tanh(v1); v2 = gelu_tanh(v2); v3 = gelu_tanh(v3);
+                    } else if (EPI == VC_EPI_BIAS_GELU_ERF) {
+                        v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+                    } else if (EPI == VC_EPI_BIAS_RELU_BF16) {
+                        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+                    }
+                    pk[s][0] = pack2<ET>(v0, v1);
+                    pk[s][1] = pack2<ET>(v2, v3);
+                }
+                const int64_t col = n0 + wn * TN + (2 * jp + (q & 1)) * 16 + 4 * (q & 2);
+                auto s0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+                auto s1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+                uint4 v;
+                v.x = s0[0]; v.y = s1[0]; v.z = s0[1]; v.w = s1[1];
+                *reinterpret_cast<uint4*>(orow + col) = v;
+                if constexpr (SAVE) {
+                    auto u0 = __builtin_amdgcn_permlane16_swap(pp[0][0], pp[1][0], false, false);
+                    auto u1 = __builtin_amdgcn_permlane16_swap(pp[0][1], pp[1][1], false, false);
+                    uint4 w;
+                    w.x = u0[0]; w.y = u1[0]; w.z = u0[1]; w.w = u1[1];
+                    *reinterpret_cast<uint4*>(prow + col) = w;
+                }
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
 // Tile configurations (BM, BN); cfg 6 (a ping-pong schedule of the persistent kernel, 23 %
 // slower in round 1) is retired, and with it every timing-only ablation build.
 struct GemmCfg {
     int bm, bn;
 };
 static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}, {128, 128}, {0, 0},
-                                 {64, 128}};
-constexpr int kNumCfgs = 8;
+                                 {64, 128}, {256, 256}, {256, 128}, {256, 256}, {256, 256}};
+constexpr int kNumCfgs = 12;
 
 template <int BM, int BN, int WM, int WN, int E, int ST = 3, int ET = VC_ELEM_BF16>
 static int launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
@@ -805,6 +1299,40 @@ static int launch_big(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t
     }
     gemm_bf16_big_kernel<E, ET><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo,
                                                                      aux, ldaux, G, gs, go);
+    return check_launch("vc_gemm_bf16");
+}
+
+template <int E, int ET, bool ABL = false>
+static int launch_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
+                     const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
+                     int64_t gs, int64_t go, hipStream_t stream) {
+    constexpr int lds = 4 * 512 * 64;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_pp_kernel<E, ET, ABL>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
+        attr_set = true;
+    }
+    gemm_pp_kernel<E, ET, ABL><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out,
+                                                                           ldo, aux, ldaux, G, gs, go);
+    return check_launch("vc_gemm_bf16");
+}
+
+template <int E, int ET>
+static int launch_pp128(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
+                        const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
+                        int64_t gs, int64_t go, hipStream_t stream) {
+    constexpr int lds = 6 * 384 * 64;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_pp128_kernel<E, ET>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
+        attr_set = true;
+    }
+    gemm_pp128_kernel<E, ET><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo,
+                                                                         aux, ldaux, G, gs, go);
     return check_launch("vc_gemm_bf16");
 }
 
@@ -842,6 +1370,26 @@ static int launch_persist(const uint16_t* A, int64_t lda, const uint16_t* W, int
 }
 
 template <int E, int ET>
+static int launch_ppp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K, int N,
+                      const float* bias, void* out, int64_t ldo, hipStream_t stream, const float* aux = nullptr,
+                      int64_t ldaux = 0) {
+    const int lds = 4 * 512 * 64 + N * 4;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_ppp_kernel<E, ET>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
+        attr_set = true;
+    }
+    const int ntiles = nbm * nbn;
+    int grid = num_cus() / 8 * 8;
+    if (grid > (ntiles + 7) / 8 * 8) grid = (ntiles + 7) / 8 * 8;
+    gemm_ppp_kernel<E, ET><<<(unsigned)grid, 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, N, bias, (uint16_t*)out,
+                                                                 ldo, (uint16_t*)const_cast<float*>(aux), ldaux);
+    return check_launch("vc_gemm_bf16");
+}
+
+template <int E, int ET>
 static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int64_t M, int64_t N,
                       int K, const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
                       int64_t gs, int64_t go, hipStream_t s) {
@@ -853,11 +1401,22 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
         case 3: return launch_big<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 5: return launch_cfg<128, 128, 2, 4, E, 2, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 7: return launch_cfg<64, 128, 2, 4, E, 2, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 8: return launch_pp<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 11:
+            if constexpr (E == VC_EPI_BIAS_BF16 && ET == VC_ELEM_BF16)
+                return launch_pp<E, ET, true>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 11 (timing ablation) is bias / bf16 only");
+        case 9: return launch_pp128<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 4:
             if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
                           E == VC_EPI_BIAS_RELU_BF16 || E == VC_EPI_BIAS_GELU_TANH_SAVE)
                 return launch_persist<E, ET>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s, aux, ldaux);
             return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 4 supports bf16-output epilogues only");
+        case 10:
+            if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
+                          E == VC_EPI_BIAS_RELU_BF16 || E == VC_EPI_BIAS_GELU_TANH_SAVE)
+                return launch_ppp<E, ET>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s, aux, ldaux);
+            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 10 supports 16-bit-output epilogues only");
     }
     return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad config");
 }
@@ -927,7 +1486,8 @@ extern "C" int vc_gemm_h16(const uint16_t* A, int64_t lda, const uint16_t* W, in
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: no tile config divides M x N");
     if ((M / kCfgs[cfg].bm) * (N / kCfgs[cfg].bn) > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: grid too large");
     const int k = (int)K;
-    if (cfg == 4 && (K / 32 < 6 || N > 8192 || !st16_ok ||
+    if ((cfg == 8 || cfg == 9 || cfg == 11) && K < 128) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 8 / 9 need K >= 128");
+    if ((cfg == 4 || cfg == 10) && (K / 32 < 6 || N > 8192 || !st16_ok ||
                      (epilogue > VC_EPI_BIAS_GELU_ERF && epilogue != VC_EPI_BIAS_RELU_BF16 &&
                       epilogue != VC_EPI_BIAS_GELU_TANH_SAVE)))
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 4 needs K>=192, N<=8192, ldo%8==0, a 16-bit-output epilogue");

@@ -1,0 +1,85 @@
+"""Ping-pong GEMM (cfg 8) vs the shipped tile configs at the ViViT-B / TimeSformer / Swin shapes:
+bit-identity of the outputs (same MFMA chain per output element), then interleaved HIP-event
+timing in one process (cdna_hip_programming.md rule 24).  One JSON line per case.
+  python tools/r04/pp_check.py [--rounds 5] [--iters 10] [--cfgs 8] [--only name,...]"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from vclip_amd import _lib, ops  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--iters", type=int, default=10)
+ap.add_argument("--cfgs", default="8")
+ap.add_argument("--only", default="")
+a = ap.parse_args()
+new_cfgs = [int(c) for c in a.cfgs.split(",")]
+
+CASES = []
+for M, tag in ((25344, "B8"), (12800, "B4")):
+    CASES += [(f"qkv_{tag}", M, 2304, 768, "bias"), (f"fc1_{tag}", M, 3072, 768, "bias_gelu_tanh"),
+              (f"fc2_{tag}", M, 768, 3072, "bias_resid_f32"), (f"oproj_{tag}", M, 768, 768, "bias_resid_f32")]
+CASES += [("sq4096", 4096, 4096, 4096, "bias"), ("sq8192", 8192, 8192, 8192, "bias"),
+          ("tsf_fc1_B16", 25344, 3072, 768, "bias_gelu_erf")]
+if a.only:
+    keep = set(a.only.split(","))
+    CASES = [c for c in CASES if c[0] in keep]
+
+g = torch.Generator(device="cuda").manual_seed(0)
+E = ops.EPI
+
+
+def operands(M, N, K, epi):
+    A = (torch.rand(M, K, device="cuda", generator=g) * 2 - 1).bfloat16()
+    W = ((torch.rand(N, K, device="cuda", generator=g) * 2 - 1) * 0.05).bfloat16()
+    b = torch.randn(N, device="cuda", generator=g) * 0.1
+    f32 = epi in ("bias_resid_f32", "bias_f32")
+    out = torch.zeros(M, N, device="cuda", dtype=torch.float32 if f32 else torch.bfloat16)
+    return A, W, b, out
+
+
+lib = _lib.load()
+results = []
+for name, M, N, K, epi in CASES:
+    A, W, b, out = operands(M, N, K, epi)
+    base = lib.vc_gemm_pick(M, N, K, E[epi], out.stride(0), 0, None)
+    bf16_out = out.dtype != torch.float32
+    cfgs = [base] + [c for c in new_cfgs if c != base and (c != 11 or epi == "bias") and (c != 10 or bf16_out)]
+    # bit-identity: every config from the same initial out (the residual epilogue accumulates)
+    init = (torch.randn(M, N, device="cuda", generator=g) if out.dtype == torch.float32 else out.clone())
+    ref = None
+    ok = {}
+    for c in cfgs:
+        out.copy_(init)
+        ops.gemm(A, W, b, epi, out, cfg=c)
+        torch.cuda.synchronize()
+        if ref is None:
+            ref = out.clone()
+        ok[c] = bool(torch.equal(out, ref))
+    times = {c: [] for c in cfgs}
+    for c in cfgs:
+        ops.gemm(A, W, b, epi, out, cfg=c)
+    torch.cuda.synchronize()
+    for r in range(a.rounds):
+        for c in cfgs:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                ops.gemm(A, W, b, epi, out, cfg=c)
+            e1.record()
+            e1.synchronize()
+            times[c].append(e0.elapsed_time(e1) / a.iters)
+    line = {"case": name, "M": M, "N": N, "K": K, "epi": epi, "base_cfg": base}
+    for c in cfgs:
+        ts = sorted(times[c])
+        med = ts[len(ts) // 2]
+        line[f"cfg{c}"] = {"us_med": round(med * 1e3, 1), "us_min": round(ts[0] * 1e3, 1),
+                           "tflops": round(2.0 * M * N * K / (med * 1e-3) / 1e12, 1), "bit_identical": ok[c]}
+    print(json.dumps(line), flush=True)
+    del A, W, b, out, init, ref
+    torch.cuda.empty_cache()
