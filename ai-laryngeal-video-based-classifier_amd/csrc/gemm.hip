@@ -399,9 +399,15 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
 // as 2 (rows) x 4 (cols), wave tile 128 x 64 = 4 x 2 blocks of 32x32x16 MFMAs.  Half-tile
 // t+3 is issued while t is computed; the end-of-step wait retires only t+1
 // (vmcnt(8): t+2 and t+3 stay in flight across the barrier).  64-B LDS rows; the chunk
-// swizzle c ^ ((row >> 2) & 3) makes every ds_read_b128 lane group conflict-free.
+// swizzle c ^ ((row >> 2) & 2) makes every ds_read_b128 lane group conflict-free.
 // ---------------------------------------------------------------------------------
-__device__ __forceinline__ int swz64(int r, int c) { return c ^ ((r >> 2) & 3); }
+// Lane (c16, q) of a ds_read_b128 reads row R0 + c16, chunk q; a lane group is {q0: rows 0-3,
+// 12-15; q1: rows 4-11} (or the same with q2 / q3), and its 16 lanes must hit the 16 distinct 16-B
+// slots 4 (row & 3) + chunk of the 256-B bank row.  c ^ ((row >> 2) & 2) does (rows 0-3 / 12-15 of
+// q0 take chunks 0 / 2, rows 4-7 / 8-11 of q1 chunks 1 / 3); the earlier c ^ ((row >> 2) & 3)
+// put rows 0-3 (q0) and 4-7 (q1) on the same chunk: 2-way conflicts on every fragment read
+// (SQ_LDS_BANK_CONFLICT = half of SQ_LDS_IDX_ACTIVE on the 256x256 kernels, round 4).
+__device__ __forceinline__ int swz64(int r, int c) { return c ^ ((r >> 2) & 2); }
 
 __device__ __forceinline__ v8s lds_frag64(const char* tile, int row, int chunk) {
     return *reinterpret_cast<const v8s*>(tile + row * 64 + swz64(row, chunk) * 16);

@@ -218,9 +218,15 @@ static int colsum_launch(const T* in, int64_t ld, int64_t R, int64_t N, float* o
 constexpr int WTILE = 64 * 128 * 2;  // one [64 m][128 cols] bf16 tile = two [64][64] panels
 constexpr int WSLOT = 2 * WTILE;
 
+// 16-B chunk swizzle of the 128-B rows read by ds_read_b64_tr_b16 (two 32-lane groups, 8 B per
+// lane): a group reads rows {0-3, 8-11} (+4 for the second read, +16 for lanes 32-63) at chunks
+// 2cb, 2cb + 1 of each row, so for m = (row >> 1) & 7 the XOR term must differ above bit 0 across
+// m in {0, 1, 4, 5} and across {2, 3, 6, 7}: ((m & 1) << 1) | (m & 4) is conflict-free (the
+// round-3 term ((m & 1) << 2) | (m & 2) | ((m >> 2) & 1) gave rows 0 and 8 the chunk pairs {2cb,
+// 2cb + 1} and {2cb + 1, 2cb}: 2-way conflicts, SQ_LDS_BANK_CONFLICT = 2 cycles per read).
 __device__ __forceinline__ int bswz(int r, int c) {
     const int m = (r >> 1) & 7;
-    return c ^ (((m & 1) << 2) | (m & 2) | ((m >> 2) & 1));
+    return c ^ (((m & 1) << 1) | (m & 4));
 }
 
 __device__ __forceinline__ v8bf tr_frag(const char* tile, int offa, int offb) {

@@ -18,11 +18,16 @@ ap.add_argument("cfgs", nargs="+")
 ap.add_argument("--B", type=int, default=8)
 ap.add_argument("--streams", type=int, default=2)
 ap.add_argument("--rounds", type=int, default=8)
+ap.add_argument("--graph", type=int, default=1, help="replay captured hipGraphs (the bench's default)")
+ap.add_argument("--rows", default=None, help="model.rows ('tight': B*S rows rounded to the tile height)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 pix = torch.from_numpy(make_synthetic_clips(a.B, 32, 224, seed=1)).to(dev)
 m = create_model(num_frames=32, device=dev)
 m.concurrent_streams = a.streams
+m.graph_replay = bool(a.graph)
+if a.rows:
+    m.rows = a.rows
 cfgs = [json.loads(c) for c in a.cfgs]
 outs = []
 for c in cfgs:

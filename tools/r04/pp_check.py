@@ -17,6 +17,7 @@ ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--cfgs", default="8")
 ap.add_argument("--only", default="")
+ap.add_argument("--ksweep", action="store_true", help="q|k|v-shaped cases at K = 768 .. 6144 (per-tile overhead fit)")
 a = ap.parse_args()
 new_cfgs = [int(c) for c in a.cfgs.split(",")]
 
@@ -26,6 +27,8 @@ for M, tag in ((25344, "B8"), (12800, "B4")):
               (f"fc2_{tag}", M, 768, 3072, "bias_resid_f32"), (f"oproj_{tag}", M, 768, 768, "bias_resid_f32")]
 CASES += [("sq4096", 4096, 4096, 4096, "bias"), ("sq8192", 8192, 8192, 8192, "bias"),
           ("tsf_fc1_B16", 25344, 3072, 768, "bias_gelu_erf")]
+if a.ksweep:
+    CASES = [(f"ks_K{K}", 12800, 2304, K, "bias") for K in (768, 1536, 3072, 6144)]
 if a.only:
     keep = set(a.only.split(","))
     CASES = [c for c in CASES if c[0] in keep]
