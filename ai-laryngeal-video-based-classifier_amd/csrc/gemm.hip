@@ -792,9 +792,10 @@ gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint
 // Epilogue: the shared store_tile16 (all epilogues); a workgroup per output tile with the
 // bijective XCD remap, consecutive tiles of one XCD walking the N tiles of one A row panel.
 // ---------------------------------------------------------------------------------
-// ABL (timing-only ablation, cfg 11): every K-half is staged from k = 0..3 (operands L2-resident,
-// wrong results): the kernel's rate with the memory side taken out.
-template <int EPI, int ET = VC_ELEM_BF16, bool ABL = false>
+// ABL (timing-only ablations, wrong results): 1 (cfg 11) every K-half is staged from k = 0..3
+// (operands L2-resident): the kernel's rate with the load side taken out; 2 (cfg 12) no epilogue
+// stores (the accumulators kept live by an empty asm): the cost of the output write.
+template <int EPI, int ET = VC_ELEM_BF16, int ABL = 0>
 __global__ void __launch_bounds__(512, 1)
 gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw, int nbm,
                int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
@@ -825,13 +826,13 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
     auto stage_a = [&](int u) __attribute__((always_inline)) {
         const uint32_t s = lds0 + (u & (NS - 1)) * SLOT + wave * 32 * 64;
-        const int ku = ABL ? (u & 3) : u;
+        const int ku = ABL == 1 ? (u & 3) : u;
         glds16(ag0 + ku * BKH, __builtin_amdgcn_readfirstlane(s));
         glds16(ag1 + ku * BKH, __builtin_amdgcn_readfirstlane(s + 16 * 64));
     };
     auto stage_w = [&](int u) __attribute__((always_inline)) {
         const uint32_t s = lds0 + (u & (NS - 1)) * SLOT + BM * 64 + wave * 32 * 64;
-        const int ku = ABL ? (u & 3) : u;
+        const int ku = ABL == 1 ? (u & 3) : u;
         glds16(wg0 + ku * BKH, __builtin_amdgcn_readfirstlane(s));
         glds16(wg1 + ku * BKH, __builtin_amdgcn_readfirstlane(s + 16 * 64));
     };
@@ -917,6 +918,13 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
         phase_b(u, wA);
         phase_a(u + 1, wB);
         phase_b(u + 1, wB);
+    }
+    if constexpr (ABL == 2) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(acc[i][j]));
+        return;
     }
     store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bias, out, ldo, aux, ldaux, G, gstride,
                                   goff);
@@ -1265,14 +1273,132 @@ gemm_ppp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
     }
 }
 
+// ---------------------------------------------------------------------------------
+// 128x256 dual-workgroup kernel (cfg 13): 4 waves per workgroup, TWO workgroups per CU (72 KiB of
+// LDS each), so one workgroup's prologue and epilogue store burst overlap the other's main loop
+// (round 4: on the 1-workgroup-per-CU 256x256 kernels every CU stores its tile at the same moment;
+// the write burst alone cost ~15 us of a 55 us q|k|v launch at 12800 rows, a timing ablation
+// without the stores).  Wave w: all 128 rows x columns 64w .. 64w + 63 (8 x 4 blocks of
+// v_mfma_f32_16x16x32).  Ring of 3 K-half slots (A 128 x 32 + W 256 x 32 = 24 KiB).  Per K-half u:
+//   first half:  read A rows 64-127 of u | 16 MFMAs on rows 0-63 | vmcnt(6) retires u+1 |
+//                lgkmcnt(0) | s_barrier (publishes u+1, and every wave's last read of slot u)
+//   second half: stage u+3 into slot u | read W and A rows 0-63 of u+1 | 16 MFMAs on rows 64-127
+// so K-half u+1's first fragments are read under u's second MFMA group, and each K-half is staged
+// 1.5 K-halves before its first read.
+// ---------------------------------------------------------------------------------
+template <int EPI, int ET = VC_ELEM_BF16>
+__global__ void __launch_bounds__(256, 2)
+gemm_dual_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw, int nbm,
+                 int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
+                 const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride, int64_t goff) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int BM = 128, BN = 256, BKH = 32, NS = 3;
+    constexpr int SLOT = (BM + BN) * 64;  // 24 KiB
+    constexpr int TM = 128, TN = 64, MI = 8, NI = 4;
+
+    const int nwg = nbm * nbn;
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, xq = nwg >> 3, rr = nwg & 7;
+    const int wgid = (xcd < rr ? xcd * (xq + 1) : rr * (xq + 1) + (xcd - rr) * xq) + (bid >> 3);
+    const int tm = wgid / nbn, tn = wgid % nbn;
+    const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int c16 = lane & 15, q = lane >> 4;
+
+    // staging: wave w fills A rows [32w, 32w + 32) (2 DMAs) and W rows [64w, 64w + 64) (4 DMAs)
+    const int arow = wave * 32 + (lane >> 2);
+    const uint16_t* ag0 = A + (m0 + arow) * lda + swz64(arow, lane & 3) * 8;
+    const uint16_t* ag1 = A + (m0 + arow + 16) * lda + swz64(arow + 16, lane & 3) * 8;
+    const int wrow = wave * 64 + (lane >> 2);
+    const uint16_t* wg[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wg[i] = W + (n0 + wrow + 16 * i) * ldw + swz64(wrow + 16 * i, lane & 3) * 8;
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
+    auto stage = [&](int u) __attribute__((always_inline)) {
+        const uint32_t s = lds0 + (u % NS) * SLOT;
+        glds16(ag0 + u * BKH, __builtin_amdgcn_readfirstlane(s + wave * 32 * 64));
+        glds16(ag1 + u * BKH, __builtin_amdgcn_readfirstlane(s + (wave * 32 + 16) * 64));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            glds16(wg[i] + u * BKH, __builtin_amdgcn_readfirstlane(s + BM * 64 + (wave * 64 + 16 * i) * 64));
+    };
+    auto read_a = [&](int u, int i0, v8s (&fa)[4]) __attribute__((always_inline)) {
+        const char* At = smem + (u % NS) * SLOT;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = lds_frag64(At, i0 + i * 16 + c16, q);
+    };
+    auto read_w = [&](int u, v8s (&fw)[4]) __attribute__((always_inline)) {
+        const char* Wt = smem + (u % NS) * SLOT + BM * 64;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fw[j] = lds_frag64(Wt, wave * TN + j * 16 + c16, q);
+    };
+
+    v4f acc[MI][NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    auto mma = [&](auto I0, const v8s (&fa)[4], const v8s (&fw)[4]) __attribute__((always_inline)) {
+        constexpr int i0 = decltype(I0)::value;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i0 + i][j] = mfma16x32<ET>(fw[j], fa[i], acc[i0 + i][j]);
+    };
+    using C0 = std::integral_constant<int, 0>;
+    using C4 = std::integral_constant<int, 4>;
+
+    const int nk = K / BKH;  // even, >= 4
+    v8s alo[2][4], ahi[4], wf[2][4];
+    // K-half u with its W / A rows 0-63 fragments in set P (compile time: the loop is unrolled by 2)
+    auto khalf = [&](auto P, int u) __attribute__((always_inline)) {
+        constexpr int p = decltype(P)::value;
+        read_a(u, 64, ahi);
+        mma(C0{}, alo[p], wf[p]);
+        if (u + 2 < nk) wait_vm<6>();
+        else wait_vm<0>();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if (u + 3 < nk) stage(u + 3);
+        if (u + 1 < nk) {
+            read_w(u + 1, wf[p ^ 1]);
+            read_a(u + 1, 0, alo[p ^ 1]);
+        }
+        mma(C4{}, ahi, wf[p]);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    stage(0);
+    stage(1);
+    stage(2);
+    wait_vm<12>();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    read_w(0, wf[0]);
+    read_a(0, 0, alo[0]);
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    for (int u = 0; u < nk; u += 2) {
+        khalf(P0{}, u);
+        khalf(P1{}, u + 1);
+    }
+    store_tile16<EPI, MI, NI, ET>(acc, m0, n0 + wave * TN, c16, q, bias, out, ldo, aux, ldaux, G, gstride, goff);
+}
+
 // Tile configurations (BM, BN); cfg 6 (a ping-pong schedule of the persistent kernel, 23 %
 // slower in round 1) is retired, and with it every timing-only ablation build.
 struct GemmCfg {
     int bm, bn;
 };
 static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}, {128, 128}, {0, 0},
-                                 {64, 128}, {256, 256}, {256, 128}, {256, 256}, {256, 256}};
-constexpr int kNumCfgs = 12;
+                                 {64, 128}, {256, 256}, {256, 128}, {256, 256}, {256, 256}, {256, 256}, {128, 256}};
+constexpr int kNumCfgs = 14;
 
 template <int BM, int BN, int WM, int WN, int E, int ST = 3, int ET = VC_ELEM_BF16>
 static int launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
@@ -1308,7 +1434,7 @@ static int launch_big(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t
     return check_launch("vc_gemm_bf16");
 }
 
-template <int E, int ET, bool ABL = false>
+template <int E, int ET, int ABL = 0>
 static int launch_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
                      const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
                      int64_t gs, int64_t go, hipStream_t stream) {
@@ -1339,6 +1465,23 @@ static int launch_pp128(const uint16_t* A, int64_t lda, const uint16_t* W, int64
     }
     gemm_pp128_kernel<E, ET><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo,
                                                                          aux, ldaux, G, gs, go);
+    return check_launch("vc_gemm_bf16");
+}
+
+template <int E, int ET>
+static int launch_dual(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
+                       const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
+                       int64_t gs, int64_t go, hipStream_t stream) {
+    constexpr int lds = 3 * 384 * 64;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_dual_kernel<E, ET>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
+        attr_set = true;
+    }
+    gemm_dual_kernel<E, ET><<<(unsigned)(nbm * nbn), 256, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo,
+                                                                        aux, ldaux, G, gs, go);
     return check_launch("vc_gemm_bf16");
 }
 
@@ -1409,9 +1552,14 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
         case 7: return launch_cfg<64, 128, 2, 4, E, 2, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 8: return launch_pp<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 11:
-            if constexpr (E == VC_EPI_BIAS_BF16 && ET == VC_ELEM_BF16)
-                return launch_pp<E, ET, true>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 11 (timing ablation) is bias / bf16 only");
+        case 12:
+            if constexpr (E == VC_EPI_BIAS_BF16 && ET == VC_ELEM_BF16) {
+                if (cfg == 11)
+                    return launch_pp<E, ET, 1>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+                return launch_pp<E, ET, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+            }
+            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfgs 11 / 12 (timing ablations) are bias / bf16 only");
+        case 13: return launch_dual<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 9: return launch_pp128<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 4:
             if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
@@ -1441,10 +1589,20 @@ static int pick_cfg(int64_t M, int64_t N, int64_t K, int epi) {
     const int64_t t256 = (M / 256) * (N / 256);
     // exact-GELU outputs below ~4 rounds of 256x256 tiles: cfg 5 (Swin-T stages 2-4 fc1,
     // tools/tune_swin_gemm.py: 28 vs 36 us at 12544x1536x384, 46 vs 55 at 6400x3072x768)
+    // (round 4: the ping-pong kernel, cfg 8, where the tiles fill <= 2.5 rounds of CUs: fc1 at 12800 rows
+    // 75.7 vs 78.7 us, q|k|v 50.7 vs 50.5; in the ViViT-B B = 8 two-stream forward +0.3 %)
+    if (bf16_out && M % 256 == 0 && N % 256 == 0 && K % 64 == 0 && K >= 192 && N <= 8192 && t256 >= 64 &&
+        t256 <= 640 && !(epi == VC_EPI_BIAS_GELU_ERF && t256 < 1024))
+        return 8;
     if (bf16_out && M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && K >= 192 && N <= 8192 && t256 >= 64 &&
         !(epi == VC_EPI_BIAS_GELU_ERF && t256 < 1024))
         return 4;
     // (t256 >= 128: Swin-T stage 4 fc2, 6400x768x3072 with 75 tiles, runs 51 us on cfg 5 vs 79 on cfg 3)
+    // round 4: the ping-pong kernel (cfg 8) instead of cfg 3: fc2 at 12800 rows 79.2 vs 87.4 us; in the
+    // ViViT-B B = 8 two-stream forward 957.9 -> 967.8 clips/s (tools/ab_model_cfg.py, interleaved)
+    if (M % 256 == 0 && N % 256 == 0 && K % 64 == 0 && K >= 128 && t256 >= 128 && t256 <= 256 &&
+        !(N <= 768 && K <= 768))
+        return 8;
     if (M % 256 == 0 && N % 256 == 0 && K % 32 == 0 && t256 >= 128 && t256 <= 256 && !(N <= 768 && K <= 768))
         return 3;
     // narrow f32-residual outputs (N <= 384): 64x128 tiles, twice the workgroups to hide the
@@ -1492,7 +1650,7 @@ extern "C" int vc_gemm_h16(const uint16_t* A, int64_t lda, const uint16_t* W, in
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: no tile config divides M x N");
     if ((M / kCfgs[cfg].bm) * (N / kCfgs[cfg].bn) > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: grid too large");
     const int k = (int)K;
-    if ((cfg == 8 || cfg == 9 || cfg == 11) && K < 128) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 8 / 9 need K >= 128");
+    if ((cfg == 8 || cfg == 9 || cfg == 11 || cfg == 12 || cfg == 13) && K < 128) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 8 / 9 need K >= 128");
     if ((cfg == 4 || cfg == 10) && (K / 32 < 6 || N > 8192 || !st16_ok ||
                      (epilogue > VC_EPI_BIAS_GELU_ERF && epilogue != VC_EPI_BIAS_RELU_BF16 &&
                       epilogue != VC_EPI_BIAS_GELU_TANH_SAVE)))
