@@ -1274,27 +1274,37 @@ gemm_ppp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
 }
 
 // ---------------------------------------------------------------------------------
-// 128x256 dual-workgroup kernel (cfg 13): 4 waves per workgroup, TWO workgroups per CU (72 KiB of
-// LDS each), so one workgroup's prologue and epilogue store burst overlap the other's main loop
-// (round 4: on the 1-workgroup-per-CU 256x256 kernels every CU stores its tile at the same moment;
-// the write burst alone cost ~15 us of a 55 us q|k|v launch at 12800 rows, a timing ablation
-// without the stores).  Wave w: all 128 rows x columns 64w .. 64w + 63 (8 x 4 blocks of
-// v_mfma_f32_16x16x32).  Ring of 3 K-half slots (A 128 x 32 + W 256 x 32 = 24 KiB).  Per K-half u:
-//   first half:  read A rows 64-127 of u | 16 MFMAs on rows 0-63 | vmcnt(6) retires u+1 |
-//                lgkmcnt(0) | s_barrier (publishes u+1, and every wave's last read of slot u)
-//   second half: stage u+3 into slot u | read W and A rows 0-63 of u+1 | 16 MFMAs on rows 64-127
-// so K-half u+1's first fragments are read under u's second MFMA group, and each K-half is staged
-// 1.5 K-halves before its first read.
+// Implicit-GEMM 3D convolution on channels-last bf16 activations (ResNet3D conv_a / conv_b /
+// strided branch1; round 4): the cfg 5 machinery (BM x BN x 64 block tile, 8 waves, LDS-DMA
+// ring, two workgroups per CU), with the A operand's rows gathered straight from the input
+// activations: 64-deep k-tile t covers channels c0 .. c0 + 63 of kernel tap `tap` (C % 64 == 0,
+// columns (kt, kh, kw, c) as vc_conv3d_im2col writes them), so the A row of output position m is
+// the 128-B segment of input row in(m, tap) -- or of a 128-B zero row where the tap falls in the
+// padding.  The im2col matrix (up to 9x the activations: 462 MB at ResNet3D stage 1, B = 4) is
+// never written or read back.  Per k-tile the tap decomposition is wave-uniform scalar work; each
+// lane's AL output rows keep their (b, t, h, w) origin in registers.
 // ---------------------------------------------------------------------------------
-template <int EPI, int ET = VC_ELEM_BF16>
-__global__ void __launch_bounds__(256, 2)
-gemm_dual_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw, int nbm,
-                 int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
-                 const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride, int64_t goff) {
+struct ConvGeomG {
+    int Tin, Hin, Win, C;
+    int To, Ho, Wo;
+    int kt, kh, kw;
+    int st, sh, sw;
+    int pt, ph, pw;
+    int64_t M;  // B * To * Ho * Wo
+};
+
+template <int BM, int BN, int WM, int WN, int EPI, int ST = 2>
+__global__ void __launch_bounds__(512, ST == 2 ? 2 : 1)
+conv_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx, ConvGeomG g, const uint16_t* __restrict__ zrow,
+                 const uint16_t* __restrict__ W, int64_t ldw, int nbm, int nbn, int K, const float* __restrict__ bias,
+                 void* __restrict__ out, int64_t ldo, const float* __restrict__ aux, int64_t ldaux) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int BM = 128, BN = 256, BKH = 32, NS = 3;
-    constexpr int SLOT = (BM + BN) * 64;  // 24 KiB
-    constexpr int TM = 128, TN = 64, MI = 8, NI = 4;
+    constexpr int SLOT = (BM + BN) * 128;
+    constexpr int TM = BM / WM, TN = BN / WN;
+    constexpr int MI = TM / 16, NI = TN / 16;
+    constexpr int AL = BM / 64, BL = BN / 64;
+    constexpr int LPT = AL + BL;
+    static_assert(WM * WN == 8 && TM % 16 == 0 && TN % 32 == 0, "8 waves");
 
     const int nwg = nbm * nbn;
     const int bid = blockIdx.x;
@@ -1305,34 +1315,53 @@ gemm_dual_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
 
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WN, wn = wave % WN;
     const int c16 = lane & 15, q = lane >> 4;
 
-    // staging: wave w fills A rows [32w, 32w + 32) (2 DMAs) and W rows [64w, 64w + 64) (4 DMAs)
-    const int arow = wave * 32 + (lane >> 2);
-    const uint16_t* ag0 = A + (m0 + arow) * lda + swz64(arow, lane & 3) * 8;
-    const uint16_t* ag1 = A + (m0 + arow + 16) * lda + swz64(arow + 16, lane & 3) * 8;
-    const int wrow = wave * 64 + (lane >> 2);
-    const uint16_t* wg[4];
+    // this lane's A rows: output position -> batch offset (input rows) and the input origin of the window
+    int64_t rbase[AL];
+    int rt[AL], rh[AL], rw[AL], rch[AL];
+    bool rok[AL];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) wg[i] = W + (n0 + wrow + 16 * i) * ldw + swz64(wrow + 16 * i, lane & 3) * 8;
+    for (int i = 0; i < AL; ++i) {
+        const int row = wave * (BM / 8) + i * 8 + (lane >> 3);
+        const int64_t m = m0 + row;
+        rok[i] = m < g.M;
+        const int64_t mm = rok[i] ? m : 0;
+        const int wo = (int)(mm % g.Wo);
+        const int ho = (int)((mm / g.Wo) % g.Ho);
+        const int to = (int)((mm / ((int64_t)g.Wo * g.Ho)) % g.To);
+        const int64_t b = mm / ((int64_t)g.Wo * g.Ho * g.To);
+        rbase[i] = b * g.Tin * g.Hin * (int64_t)g.Win;
+        rt[i] = to * g.st - g.pt;
+        rh[i] = ho * g.sh - g.ph;
+        rw[i] = wo * g.sw - g.pw;
+        rch[i] = swz(row, lane & 7) * 8;
+    }
+    const uint16_t* bsrc[BL];
+#pragma unroll
+    for (int i = 0; i < BL; ++i) {
+        const int row = wave * (BN / 8) + i * 8 + (lane >> 3);
+        bsrc[i] = W + (n0 + row) * ldw + swz(row, lane & 7) * 8;
+    }
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
-    auto stage = [&](int u) __attribute__((always_inline)) {
-        const uint32_t s = lds0 + (u % NS) * SLOT;
-        glds16(ag0 + u * BKH, __builtin_amdgcn_readfirstlane(s + wave * 32 * 64));
-        glds16(ag1 + u * BKH, __builtin_amdgcn_readfirstlane(s + (wave * 32 + 16) * 64));
+    auto stage = [&](int t, int slot) {
+        const uint32_t s = lds0 + slot * SLOT;
+        const int k0 = t * 64;
+        const int tap = k0 / g.C, c0 = k0 - tap * g.C;  // wave-uniform
+        const int iw = tap % g.kw, ih = (tap / g.kw) % g.kh, it = tap / (g.kw * g.kh);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            glds16(wg[i] + u * BKH, __builtin_amdgcn_readfirstlane(s + BM * 64 + (wave * 64 + 16 * i) * 64));
-    };
-    auto read_a = [&](int u, int i0, v8s (&fa)[4]) __attribute__((always_inline)) {
-        const char* At = smem + (u % NS) * SLOT;
+        for (int i = 0; i < AL; ++i) {
+            const int ti = rt[i] + it, hi = rh[i] + ih, wi = rw[i] + iw;
+            const bool ok = rok[i] && (unsigned)ti < (unsigned)g.Tin && (unsigned)hi < (unsigned)g.Hin &&
+                            (unsigned)wi < (unsigned)g.Win;
+            const uint16_t* src = ok ? X + (rbase[i] + ((int64_t)ti * g.Hin + hi) * g.Win + wi) * ldx + c0 + rch[i]
+                                     : zrow + rch[i];
+            glds16(src, __builtin_amdgcn_readfirstlane(s + (wave * (BM / 8) + i * 8) * 128));
+        }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = lds_frag64(At, i0 + i * 16 + c16, q);
-    };
-    auto read_w = [&](int u, v8s (&fw)[4]) __attribute__((always_inline)) {
-        const char* Wt = smem + (u % NS) * SLOT + BM * 64;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) fw[j] = lds_frag64(Wt, wave * TN + j * 16 + c16, q);
+        for (int i = 0; i < BL; ++i)
+            glds16(bsrc[i] + k0, __builtin_amdgcn_readfirstlane(s + BM * 128 + (wave * (BN / 8) + i * 8) * 128));
     };
 
     v4f acc[MI][NI];
@@ -1340,65 +1369,73 @@ gemm_dual_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
     for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-    auto mma = [&](auto I0, const v8s (&fa)[4], const v8s (&fw)[4]) __attribute__((always_inline)) {
-        constexpr int i0 = decltype(I0)::value;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i0 + i][j] = mfma16x32<ET>(fw[j], fa[i], acc[i0 + i][j]);
-    };
-    using C0 = std::integral_constant<int, 0>;
-    using C4 = std::integral_constant<int, 4>;
 
-    const int nk = K / BKH;  // even, >= 4
-    v8s alo[2][4], ahi[4], wf[2][4];
-    // K-half u with its W / A rows 0-63 fragments in set P (compile time: the loop is unrolled by 2)
-    auto khalf = [&](auto P, int u) __attribute__((always_inline)) {
-        constexpr int p = decltype(P)::value;
-        read_a(u, 64, ahi);
-        mma(C0{}, alo[p], wf[p]);
-        if (u + 2 < nk) wait_vm<6>();
-        else wait_vm<0>();
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        if (u + 3 < nk) stage(u + 3);
-        if (u + 1 < nk) {
-            read_w(u + 1, wf[p ^ 1]);
-            read_a(u + 1, 0, alo[p ^ 1]);
-        }
-        mma(C4{}, ahi, wf[p]);
-        __builtin_amdgcn_sched_barrier(0);
-    };
-
-    stage(0);
-    stage(1);
-    stage(2);
-    wait_vm<12>();
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    read_w(0, wf[0]);
-    read_a(0, 0, alo[0]);
-    using P0 = std::integral_constant<int, 0>;
-    using P1 = std::integral_constant<int, 1>;
-    for (int u = 0; u < nk; u += 2) {
-        khalf(P0{}, u);
-        khalf(P1{}, u + 1);
+    const int nk = K / 64;
+    stage(0, 0);
+    if (ST == 3 && nk > 1) {
+        stage(1, 1);
+        wait_vm<LPT>();
+    } else {
+        wait_vm<0>();
     }
-    store_tile16<EPI, MI, NI, ET>(acc, m0, n0 + wave * TN, c16, q, bias, out, ldo, aux, ldaux, G, gstride, goff);
+    block_sync_lds();
+
+    for (int t = 0; t < nk; ++t) {
+        const int slot = t % ST;
+        if (t + ST - 1 < nk) stage(t + ST - 1, (t + ST - 1) % ST);
+        const char* At = smem + slot * SLOT;
+        const char* Wt = At + BM * 128;
+        v8s af[2][MI], wf[2][NI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) af[0][i] = lds_frag(At, wm * TM + i * 16 + c16, q);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) wf[0][j] = lds_frag(Wt, wn * TN + j * 16 + c16, q);
+#pragma unroll
+        for (int i = 0; i < MI; ++i) af[1][i] = lds_frag(At, wm * TM + i * 16 + c16, 4 + q);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) wf[1][j] = lds_frag(Wt, wn * TN + j * 16 + c16, 4 + q);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+                for (int j = 0; j < NI; ++j) acc[i][j] = mfma16x32<VC_ELEM_BF16>(wf[kk][j], af[kk][i], acc[i][j]);
+        if (ST == 3 && t + 2 < nk) wait_vm<LPT>();
+        else wait_vm<0>();
+        block_sync_lds();
+    }
+    store_tile16<EPI, MI, NI, VC_ELEM_BF16>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bias, out, ldo, aux, ldaux, 1, 0,
+                                            0);
+}
+
+template <int BM, int BN, int WM, int WN, int E>
+static int launch_conv(const uint16_t* X, int64_t ldx, const ConvGeomG& g, const uint16_t* zrow, const uint16_t* W,
+                       int64_t ldw, int nbm, int nbn, int K, const float* bias, void* out, int64_t ldo, const float* aux,
+                       int64_t ldaux, hipStream_t stream) {
+    constexpr int lds = 2 * (BM + BN) * 128;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)conv_gemm_kernel<BM, BN, WM, WN, E, 2>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return fail((int)e, std::string("vc_conv3d_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
+        attr_set = true;
+    }
+    conv_gemm_kernel<BM, BN, WM, WN, E, 2><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(X, ldx, g, zrow, W, ldw, nbm, nbn,
+                                                                                       K, bias, out, ldo, aux, ldaux);
+    return check_launch("vc_conv3d_gemm_bf16");
 }
 
 // Tile configurations (BM, BN); cfg 6 (a ping-pong schedule of the persistent kernel, 23 %
-// slower in round 1) is retired, and with it every timing-only ablation build.
+// slower in round 1) is retired.  Round 4: a 128x256 4-wave kernel at two workgroups per CU (one
+// workgroup's epilogue store burst overlapping the other's main loop) measured slower on every
+// shape (q|k|v 12800 rows 59.9 vs 50.7 us, K = 6144 383 vs 277 us: without the ping-pong the main
+// loop loses more than the overlap gains) and was removed.
 struct GemmCfg {
     int bm, bn;
 };
 static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}, {128, 128}, {0, 0},
-                                 {64, 128}, {256, 256}, {256, 128}, {256, 256}, {256, 256}, {256, 256}, {128, 256}};
-constexpr int kNumCfgs = 14;
+                                 {64, 128}, {256, 256}, {256, 128}, {256, 256}, {256, 256}, {256, 256}};
+constexpr int kNumCfgs = 13;
 
 template <int BM, int BN, int WM, int WN, int E, int ST = 3, int ET = VC_ELEM_BF16>
 static int launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
@@ -1465,23 +1502,6 @@ static int launch_pp128(const uint16_t* A, int64_t lda, const uint16_t* W, int64
     }
     gemm_pp128_kernel<E, ET><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo,
                                                                          aux, ldaux, G, gs, go);
-    return check_launch("vc_gemm_bf16");
-}
-
-template <int E, int ET>
-static int launch_dual(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
-                       const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
-                       int64_t gs, int64_t go, hipStream_t stream) {
-    constexpr int lds = 3 * 384 * 64;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_dual_kernel<E, ET>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
-        attr_set = true;
-    }
-    gemm_dual_kernel<E, ET><<<(unsigned)(nbm * nbn), 256, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo,
-                                                                        aux, ldaux, G, gs, go);
     return check_launch("vc_gemm_bf16");
 }
 
@@ -1559,7 +1579,6 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
                 return launch_pp<E, ET, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
             }
             return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfgs 11 / 12 (timing ablations) are bias / bf16 only");
-        case 13: return launch_dual<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 9: return launch_pp128<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 4:
             if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
@@ -1650,7 +1669,7 @@ extern "C" int vc_gemm_h16(const uint16_t* A, int64_t lda, const uint16_t* W, in
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: no tile config divides M x N");
     if ((M / kCfgs[cfg].bm) * (N / kCfgs[cfg].bn) > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: grid too large");
     const int k = (int)K;
-    if ((cfg == 8 || cfg == 9 || cfg == 11 || cfg == 12 || cfg == 13) && K < 128) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 8 / 9 need K >= 128");
+    if ((cfg == 8 || cfg == 9 || cfg == 11 || cfg == 12) && K < 128) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 8 / 9 need K >= 128");
     if ((cfg == 4 || cfg == 10) && (K / 32 < 6 || N > 8192 || !st16_ok ||
                      (epilogue > VC_EPI_BIAS_GELU_ERF && epilogue != VC_EPI_BIAS_RELU_BF16 &&
                       epilogue != VC_EPI_BIAS_GELU_TANH_SAVE)))
@@ -1677,6 +1696,59 @@ extern "C" int vc_gemm_h16(const uint16_t* A, int64_t lda, const uint16_t* W, in
     }
 #undef VC_GEMM_CASE
     return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad epilogue");
+}
+
+// Implicit-GEMM Conv3d (conv_gemm_kernel): out[m][n] = epilogue(sum_(tap, c) x[in(m, tap)][c] *
+// Wt[n][tap * C + c] + bias[n]); output rows m < B*To*Ho*Wo (rows up to the next multiple of 128
+// are written too: the caller's buffer has them), zero_row: >= 64 zero bf16 (16-B aligned).
+extern "C" int vc_conv3d_gemm_bf16(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_t H, int64_t W,
+                                   int64_t C, const int* kernel, const int* stride, const int* pad,
+                                   const uint16_t* zero_row, const uint16_t* Wt, int64_t ldw, int64_t N,
+                                   const float* bias, int epilogue, void* out, int64_t ldo, const void* aux,
+                                   int64_t ldaux, hipStream_t stream) {
+    if (!x || !kernel || !stride || !pad || !zero_row || !Wt || !bias || !out)
+        return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: null pointer");
+    for (int d = 0; d < 3; ++d)
+        if (kernel[d] <= 0 || stride[d] <= 0 || pad[d] < 0 || kernel[d] > 255)
+            return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: bad kernel / stride / pad");
+    if (B <= 0 || T <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 64 || N <= 0 || N % 128)
+        return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: need C % 64 == 0 and N % 128 == 0");
+    ConvGeomG g;
+    g.Tin = (int)T; g.Hin = (int)H; g.Win = (int)W; g.C = (int)C;
+    g.kt = kernel[0]; g.kh = kernel[1]; g.kw = kernel[2];
+    g.st = stride[0]; g.sh = stride[1]; g.sw = stride[2];
+    g.pt = pad[0]; g.ph = pad[1]; g.pw = pad[2];
+    g.To = (int)((T + 2 * g.pt - g.kt) / g.st + 1);
+    g.Ho = (int)((H + 2 * g.ph - g.kh) / g.sh + 1);
+    g.Wo = (int)((W + 2 * g.pw - g.kw) / g.sw + 1);
+    if (g.To <= 0 || g.Ho <= 0 || g.Wo <= 0) return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: empty output");
+    g.M = B * g.To * g.Ho * (int64_t)g.Wo;
+    const int64_t K = (int64_t)g.kt * g.kh * g.kw * C;
+    if (ldx % 8 || ldx < C || ldw % 8 || ldw < K || ldo < N || K > (1LL << 30))
+        return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: bad leading dimension");
+    if ((((uintptr_t)x) | ((uintptr_t)Wt) | ((uintptr_t)out) | ((uintptr_t)bias) | ((uintptr_t)zero_row)) & 15)
+        return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: pointers must be 16-byte aligned");
+    const int nbm = (int)((g.M + 127) / 128), nbn = (int)(N / 128);
+    if ((int64_t)nbm * nbn > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: grid too large");
+    const float* auxf = reinterpret_cast<const float*>(aux);
+    switch (epilogue) {
+        case VC_EPI_BIAS_BF16:
+            if (ldo % 8) break;
+            return launch_conv<128, 128, 2, 4, VC_EPI_BIAS_BF16>(x, ldx, g, zero_row, Wt, ldw, nbm, nbn, (int)K, bias,
+                                                                  out, ldo, auxf, ldaux, stream);
+        case VC_EPI_BIAS_RELU_BF16:
+            if (ldo % 8) break;
+            return launch_conv<128, 128, 2, 4, VC_EPI_BIAS_RELU_BF16>(x, ldx, g, zero_row, Wt, ldw, nbm, nbn, (int)K,
+                                                                       bias, out, ldo, auxf, ldaux, stream);
+        case VC_EPI_BIAS_RESID_RELU_BF16:
+            if (!aux || ldaux % 4 || ldaux < N || ((uintptr_t)aux & 7)) break;
+            return launch_conv<128, 128, 2, 4, VC_EPI_BIAS_RESID_RELU_BF16>(x, ldx, g, zero_row, Wt, ldw, nbm, nbn,
+                                                                             (int)K, bias, out, ldo, auxf, ldaux, stream);
+        default:
+            break;
+    }
+    return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: epilogue must be bias / bias_relu / bias_resid_relu "
+                                    "(16-B output rows; resid_relu: a bf16 aux with ldaux >= N)");
 }
 
 // the tile config vc_gemm_bf16 / vc_gemm_h16 run with cfg = -1 (host only: no launch, no GPU)

@@ -507,6 +507,46 @@ def conv3d_im2col(x: torch.Tensor, kind: str, B: int, grid, C: int, kernel, stri
     return out
 
 
+_ZERO_ROW = {}
+
+
+def conv3d_gemm(x: torch.Tensor, B: int, grid, C: int, kernel, stride, pad, w: torch.Tensor, bias: torch.Tensor,
+                epilogue: str, out: torch.Tensor, aux: torch.Tensor | None = None, flop: float | None = None,
+                op: str = "conv") -> torch.Tensor:
+    """Implicit-GEMM Conv3d (vc_conv3d_gemm_bf16): x channels-last bf16 rows [>= B*T*H*W, >= C],
+    w bf16 [N, >= kvol*C] (columns (kt, kh, kw, c)), out bf16 [>= roundup(B*To*Ho*Wo, 128), >= N]."""
+    import ctypes
+    _dev(x, w, bias, out)
+    T, H, W = grid
+    To, Ho, Wo = conv_out_size(grid, kernel, stride, pad)
+    kvol = kernel[0] * kernel[1] * kernel[2]
+    M = B * To * Ho * Wo
+    N = w.shape[0]
+    _need(x.dtype == torch.bfloat16 and x.stride(1) == 1 and x.shape[0] >= B * T * H * W and x.shape[1] >= C,
+          "conv3d_gemm x")
+    _need(w.dtype == torch.bfloat16 and w.stride(1) == 1 and w.shape[1] >= kvol * C and bias.numel() == N and
+          bias.dtype == torch.float32, "conv3d_gemm weights")
+    _need(out.dtype == torch.bfloat16 and out.stride(1) == 1 and out.shape[0] >= (M + 127) // 128 * 128 and
+          out.shape[1] >= N, "conv3d_gemm out rows (a multiple of 128)")
+    e = EPI[epilogue]
+    if e == 7:
+        _need(aux is not None and aux.dtype == torch.bfloat16 and aux.stride(1) == 1 and aux.shape[0] >= M and
+              aux.shape[1] >= N, "conv3d_gemm residual")
+    key = x.device
+    if key not in _ZERO_ROW:
+        _ZERO_ROW[key] = torch.zeros(64, dtype=torch.bfloat16, device=x.device)
+    k, s, p = ((ctypes.c_int * 3)(*v) for v in (kernel, stride, pad))
+    rec = _REC[0]
+    e0 = rec.begin() if rec is not None else None
+    _lib.call("vc_conv3d_gemm_bf16", _p(x), x.stride(0), B, T, H, W, C, ctypes.addressof(k), ctypes.addressof(s),
+              ctypes.addressof(p), _p(_ZERO_ROW[key]), _p(w), w.stride(0), N, _p(bias), e, _p(out), out.stride(0),
+              _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0, _stream(x))
+    if rec is not None:
+        rec.end(e0, f"conv_gemm_kernel<128, 128, 2, 4, {e}, 2>", op, 2.0 * M * N * kvol * C if flop is None else flop,
+                "flop")
+    return out
+
+
 def maxpool3d(x: torch.Tensor, B: int, grid, C: int, kernel, stride, pad, out: torch.Tensor) -> torch.Tensor:
     import ctypes
     _dev(x, out)

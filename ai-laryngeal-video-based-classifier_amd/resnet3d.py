@@ -57,6 +57,10 @@ class ResNet3d(torch.nn.Module):
         self.graph_replay = False
         self._graphs = None
         self.head_dropout = True  # train step: the head's Dropout(0.5) (pytorchvideo create_resnet dropout_rate)
+        # inference convolutions other than 1x1x1 stride 1 as implicit GEMMs (vc_conv3d_gemm_bf16: the
+        # A rows gathered from the activations per kernel tap, no im2col buffer); False: im2col + GEMM.
+        # Bit-identical either way (same MFMA chain per output, same column order).
+        self.implicit_conv = True
 
     def state_dict(self, *a, **k):
         return OrderedDict((n, self.params[n.replace(".", "__")].detach()) for n in self._names)
@@ -281,6 +285,7 @@ class ResNet3d(torch.nn.Module):
             if self._graphs is None:
                 self._graphs = GraphReplay()
             key = (video.data_ptr(), tuple(video.shape), tuple(video.stride()), video.dtype, self.concurrent_streams,
+                   self.implicit_conv,
                    str(video.device), self._weights_version())
             return self._graphs.run(key, video, self._forward_eager, keep=lambda: (self._packed, tuple(self._ws_used)))
         return self._forward_eager(video)
@@ -351,6 +356,9 @@ class ResNet3d(torch.nn.Module):
                     fl = 2.0 * vol(g) * dout * cin
                     if stride == (1, 1, 1):
                         ops.gemm(xin, blk["b1"][0], blk["b1"][1], "bias", act["sc"], m=rows(g), flop=fl, op="branch1")
+                    elif self.implicit_conv and cin % 64 == 0:
+                        ops.conv3d_gemm(xin, B, gi, cin, (1, 1, 1), stride, (0, 0, 0), blk["b1"][0], blk["b1"][1], "bias",
+                                        act["sc"], flop=fl, op="branch1")
                     else:
                         A = col(rows(g), cin)
                         tm("conv3d_im2col_kernel", "im2col", (vol(gi) + vol(g)) * cin * 2, "byte", ops.conv3d_im2col,
@@ -363,17 +371,24 @@ class ResNet3d(torch.nn.Module):
                 fl = 2.0 * vol(gi) * inner * cin * ka[0] * ka[1] * ka[2]
                 if tuple(ka) == (1, 1, 1):
                     ops.gemm(xin, blk["a"][0], blk["a"][1], "bias_relu", act["a"], m=rows(gi), flop=fl, op="conv_a")
+                elif self.implicit_conv and cin % 64 == 0:
+                    ops.conv3d_gemm(xin, B, gi, cin, ka, (1, 1, 1), tuple(k // 2 for k in ka), blk["a"][0], blk["a"][1],
+                                    "bias_relu", act["a"], flop=fl, op="conv_a")
                 else:
                     A = col(rows(gi), ka[0] * cin)
                     tm("conv3d_im2col_kernel", "im2col", vol(gi) * cin * 2 * (1 + ka[0]), "byte", ops.conv3d_im2col,
                        xin, "cl_bf16", B, gi, cin, ka, (1, 1, 1), tuple(k // 2 for k in ka), A)
                     ops.gemm(A, blk["a"][0], blk["a"][1], "bias_relu", act["a"], flop=fl, op="conv_a")
                 # conv_b (1,3,3) with the stage stride (+ BN + ReLU)
-                A = col(rows(g), 9 * inner)
-                tm("conv3d_im2col_kernel", "im2col", (vol(gi) + 9 * vol(g)) * inner * 2, "byte", ops.conv3d_im2col,
-                   act["a"], "cl_bf16", B, gi, inner, (1, 3, 3), stride, (0, 1, 1), A)
-                ops.gemm(A, blk["b"][0], blk["b"][1], "bias_relu", act["b"], flop=2.0 * vol(g) * inner * inner * 9,
-                         op="conv_b")
+                if self.implicit_conv and inner % 64 == 0:
+                    ops.conv3d_gemm(act["a"], B, gi, inner, (1, 3, 3), stride, (0, 1, 1), blk["b"][0], blk["b"][1],
+                                    "bias_relu", act["b"], flop=2.0 * vol(g) * inner * inner * 9, op="conv_b")
+                else:
+                    A = col(rows(g), 9 * inner)
+                    tm("conv3d_im2col_kernel", "im2col", (vol(gi) + 9 * vol(g)) * inner * 2, "byte", ops.conv3d_im2col,
+                       act["a"], "cl_bf16", B, gi, inner, (1, 3, 3), stride, (0, 1, 1), A)
+                    ops.gemm(A, blk["b"][0], blk["b"][1], "bias_relu", act["b"], flop=2.0 * vol(g) * inner * inner * 9,
+                             op="conv_b")
                 # conv_c 1x1x1 + BN + skip + ReLU
                 out = act["x"] if xin is not act["x"] else act["x2"]
                 ops.gemm(act["b"][:, :inner], blk["c"][0], blk["c"][1], "bias_resid_relu", out, aux=skip,

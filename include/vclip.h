@@ -306,6 +306,19 @@ int vc_conv3d_im2col(const void* x, int64_t ldx, int input_kind, int64_t B, int6
                      int64_t C, const int* kernel, const int* stride, const int* pad, uint16_t* A, int64_t lda,
                      hipStream_t stream);
 
+/* Implicit-GEMM Conv3d on channels-last bf16 activations (no im2col buffer): out[m][n] =
+ * epilogue(sum over (tap, c) of x[in(m, tap)][c] * Wt[n][tap*C + c] + bias[n]) with the
+ * vc_conv3d_im2col column order (kt, kh, kw, c); epilogue VC_EPI_BIAS_BF16 / _RELU_BF16 /
+ * _RESID_RELU_BF16 (aux = the bf16 residual).  C % 64 == 0, N % 128 == 0 (zero-padded output
+ * channels); `zero_row` points to >= 64 zero bf16 (the padding taps' source); the output rows
+ * up to the next multiple of 128 are written (the caller's buffer holds them).  Replaces
+ * vc_conv3d_im2col + vc_gemm_bf16 for pytorchvideo's conv_a / conv_b / strided branch1
+ * (resnet50-3d-video/video_classifier/models/resnet3d.py:4-48). */
+int vc_conv3d_gemm_bf16(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_t H, int64_t W, int64_t C,
+                        const int* kernel, const int* stride, const int* pad, const uint16_t* zero_row,
+                        const uint16_t* Wt, int64_t ldw, int64_t N, const float* bias, int epilogue, void* out,
+                        int64_t ldo, const void* aux, int64_t ldaux, hipStream_t stream);
+
 /* MaxPool3d on channels-last bf16 (padding counts as -inf): pytorchvideo's stem pool. */
 int vc_maxpool3d(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_t H, int64_t W, int64_t C,
                  const int* kernel, const int* stride, const int* pad, uint16_t* y, int64_t ldy, hipStream_t stream);

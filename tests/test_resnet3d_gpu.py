@@ -113,3 +113,47 @@ def test_resnet3d_batch_invariance():
     full = m(video).clone()
     one = m(video[1:2].contiguous()).clone()
     assert torch.equal(full[1:2], one)
+
+
+@pytest.mark.parametrize("kernel,stride,pad,C,epi", [((1, 3, 3), (1, 2, 2), (0, 1, 1), 64, "bias_relu"),
+                                                      ((1, 3, 3), (1, 1, 1), (0, 1, 1), 128, "bias_relu"),
+                                                      ((3, 1, 1), (1, 1, 1), (1, 0, 0), 64, "bias_relu"),
+                                                      ((1, 1, 1), (1, 2, 2), (0, 0, 0), 128, "bias"),
+                                                      ((1, 3, 3), (1, 1, 1), (0, 1, 1), 64, "bias_resid_relu")])
+def test_conv3d_implicit_gemm_bit_exact(kernel, stride, pad, C, epi):
+    """vc_conv3d_gemm_bf16 (A rows gathered per tap, zero rows for padding taps) == im2col + vc_gemm
+    on the same weights: the same MFMA chain per output element, so bit-identical; odd spatial sizes
+    put padding taps on every border, and 203 output rows leave a partial 128-row tile."""
+    O = ops()
+    g = torch.Generator().manual_seed(C + kernel[0])
+    B, T, H, W = 2, 4, 13, 11
+    N = 128
+    kv = kernel[0] * kernel[1] * kernel[2]
+    x = (torch.randn(B * T * H * W, C, generator=g) * 0.5).bfloat16()
+    xd = torch.zeros(B * T * H * W, C + 64, dtype=torch.bfloat16)  # ldx > C
+    xd[:, :C] = x
+    xd = xd.to(DEV)
+    w = (torch.randn(N, kv * C, generator=g) * 0.05).bfloat16().to(DEV)
+    b = (torch.randn(N, generator=g) * 0.1).to(DEV)
+    To, Ho, Wo = O.conv_out_size((T, H, W), kernel, stride, pad)
+    M = B * To * Ho * Wo
+    Mp = (M + 255) // 256 * 256
+    aux = (torch.randn(Mp, N, generator=g)).bfloat16().to(DEV) if epi == "bias_resid_relu" else None
+    col = torch.zeros(Mp, kv * C, dtype=torch.bfloat16, device=DEV)
+    O.conv3d_im2col(xd, "cl_bf16", B, (T, H, W), C, kernel, stride, pad, col)
+    want = torch.zeros(Mp, N, dtype=torch.bfloat16, device=DEV)
+    O.gemm(col, w, b, epi, want, aux=aux, cfg=5)
+    got = torch.full((Mp, N), 7.0, dtype=torch.bfloat16, device=DEV)
+    O.conv3d_gemm(xd, B, (T, H, W), C, kernel, stride, pad, w, b, epi, got, aux=aux)
+    assert torch.equal(got[:M], want[:M])
+
+
+def test_resnet3d_implicit_conv_matches_im2col_path():
+    """The whole forward with vc_conv3d_gemm_bf16 vs im2col + GEMM: bit-identical logits."""
+    video = torch.from_numpy(make_synthetic_video(2, 8, 224, seed=5)).to(DEV)
+    m = _model()
+    m.implicit_conv = True
+    a = m(video).clone()
+    m.implicit_conv = False
+    b = m(video).clone()
+    assert torch.equal(a, b), (a, b)
