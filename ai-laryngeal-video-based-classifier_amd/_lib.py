@@ -64,6 +64,9 @@ SIGNATURES = {
     "vc_conv3d_im2col": ([c_p, c_i64, c_int, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p], c_int),
     "vc_conv3d_gemm_bf16": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64,
                              c_p, c_int, c_p, c_i64, c_p, c_i64, c_p], c_int),
+    "vc_conv3d_stem_pack": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p], c_int),
+    "vc_conv3d_stem_gemm_bf16": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_int,
+                                  c_p, c_i64, c_p], c_int),
     "vc_maxpool3d": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p], c_int),
     "vc_avgpool_head": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_i64, c_p, c_p, c_p], c_int),
     "vc_col2im_cl": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_i64, c_p], c_int),

@@ -794,7 +794,8 @@ gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint
 // ---------------------------------------------------------------------------------
 // ABL (timing-only ablations, wrong results): 1 (cfg 11) every K-half is staged from k = 0..3
 // (operands L2-resident): the kernel's rate with the load side taken out; 2 (cfg 12) no epilogue
-// stores (the accumulators kept live by an empty asm): the cost of the output write.
+// stores (the accumulators kept live by an empty asm): the cost of the output write; 3 (cfg 13) the
+// same bytes stored as full 128-B row segments per 8 lanes (values scrambled): the store pattern's cost.
 template <int EPI, int ET = VC_ELEM_BF16, int ABL = 0>
 __global__ void __launch_bounds__(512, 1)
 gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw, int nbm,
@@ -924,6 +925,18 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
         for (int i = 0; i < MI; ++i)
 #pragma unroll
             for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(acc[i][j]));
+        return;
+    }
+    if constexpr (ABL == 3) {  // the same bytes as full 128-B row segments per 8 lanes (values scrambled)
+        uint16_t* o16 = reinterpret_cast<uint16_t*>(out);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            const v4f a0 = acc[s >> 1][(s & 1) * 2], a1 = acc[s >> 1][(s & 1) * 2 + 1];
+            uint4 v;
+            v.x = pack2bf(a0[0], a0[1]); v.y = pack2bf(a0[2], a0[3]);
+            v.z = pack2bf(a1[0], a1[1]); v.w = pack2bf(a1[2], a1[3]);
+            *reinterpret_cast<uint4*>(o16 + (m0 + wm * TM + s * 8 + (lane >> 3)) * ldo + n0 + wn * TN + (lane & 7) * 8) = v;
+        }
         return;
     }
     store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bias, out, ldo, aux, ldaux, G, gstride,
@@ -1293,7 +1306,12 @@ struct ConvGeomG {
     int64_t M;  // B * To * Ho * Wo
 };
 
-template <int BM, int BN, int WM, int WN, int EPI, int ST = 2>
+// MODE 1 (the stem, vc_conv3d_stem_gemm_bf16): X is the zero-padded channels-last clip
+// [B][Tp][Hp][Wp][4] bf16 (vc_conv3d_stem_pack: 3 channels + a zero 4th); the K columns are
+// segments of 32 = one (kt, kh) tap row of 8 pixels x 4 channels (kw <= 8), two segments per 64-deep
+// k-tile, so an A row's 16-B chunk is 2 pixels of the padded clip (16-B aligned: the window's first
+// pixel index is even for stride-2 w); segments past kt * kh read the zero row.
+template <int BM, int BN, int WM, int WN, int EPI, int ST = 2, int MODE = 0>
 __global__ void __launch_bounds__(512, ST == 2 ? 2 : 1)
 conv_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx, ConvGeomG g, const uint16_t* __restrict__ zrow,
                  const uint16_t* __restrict__ W, int64_t ldw, int nbm, int nbn, int K, const float* __restrict__ bias,
@@ -1332,12 +1350,17 @@ conv_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx, ConvGeomG g, const
         const int ho = (int)((mm / g.Wo) % g.Ho);
         const int to = (int)((mm / ((int64_t)g.Wo * g.Ho)) % g.To);
         const int64_t b = mm / ((int64_t)g.Wo * g.Ho * g.To);
-        rbase[i] = b * g.Tin * g.Hin * (int64_t)g.Win;
+        if constexpr (MODE == 1) {  // pixel index of the window's first tap in the padded clip
+            rbase[i] = ((b * g.Tin + (int64_t)to * g.st) * g.Hin + (int64_t)ho * g.sh) * g.Win + (int64_t)wo * g.sw;
+        } else {
+            rbase[i] = b * g.Tin * g.Hin * (int64_t)g.Win;
+        }
         rt[i] = to * g.st - g.pt;
         rh[i] = ho * g.sh - g.ph;
         rw[i] = wo * g.sw - g.pw;
         rch[i] = swz(row, lane & 7) * 8;
     }
+
     const uint16_t* bsrc[BL];
 #pragma unroll
     for (int i = 0; i < BL; ++i) {
@@ -1348,16 +1371,29 @@ conv_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx, ConvGeomG g, const
     auto stage = [&](int t, int slot) {
         const uint32_t s = lds0 + slot * SLOT;
         const int k0 = t * 64;
-        const int tap = k0 / g.C, c0 = k0 - tap * g.C;  // wave-uniform
-        const int iw = tap % g.kw, ih = (tap / g.kw) % g.kh, it = tap / (g.kw * g.kh);
+        if constexpr (MODE == 1) {
 #pragma unroll
-        for (int i = 0; i < AL; ++i) {
-            const int ti = rt[i] + it, hi = rh[i] + ih, wi = rw[i] + iw;
-            const bool ok = rok[i] && (unsigned)ti < (unsigned)g.Tin && (unsigned)hi < (unsigned)g.Hin &&
-                            (unsigned)wi < (unsigned)g.Win;
-            const uint16_t* src = ok ? X + (rbase[i] + ((int64_t)ti * g.Hin + hi) * g.Win + wi) * ldx + c0 + rch[i]
-                                     : zrow + rch[i];
-            glds16(src, __builtin_amdgcn_readfirstlane(s + (wave * (BM / 8) + i * 8) * 128));
+            for (int i = 0; i < AL; ++i) {
+                const int lc = rch[i] >> 3;  // this row's logical 16-B chunk (the source side of the swizzle)
+                const int seg = 2 * t + (lc >> 2), sub = lc & 3;
+                const bool sok = seg < g.kt * g.kh;
+                const int it = sok ? seg / g.kh : 0, ih = sok ? seg - it * g.kh : 0;
+                const int64_t soff = ((int64_t)it * g.Hin + ih) * g.Win * 4 + sub * 8;
+                const uint16_t* src = (rok[i] && sok) ? X + rbase[i] * 4 + soff : zrow + rch[i];
+                glds16(src, __builtin_amdgcn_readfirstlane(s + (wave * (BM / 8) + i * 8) * 128));
+            }
+        } else {
+            const int tap = k0 / g.C, c0 = k0 - tap * g.C;  // wave-uniform
+            const int iw = tap % g.kw, ih = (tap / g.kw) % g.kh, it = tap / (g.kw * g.kh);
+#pragma unroll
+            for (int i = 0; i < AL; ++i) {
+                const int ti = rt[i] + it, hi = rh[i] + ih, wi = rw[i] + iw;
+                const bool ok = rok[i] && (unsigned)ti < (unsigned)g.Tin && (unsigned)hi < (unsigned)g.Hin &&
+                                (unsigned)wi < (unsigned)g.Win;
+                const uint16_t* src = ok ? X + (rbase[i] + ((int64_t)ti * g.Hin + hi) * g.Win + wi) * ldx + c0 + rch[i]
+                                         : zrow + rch[i];
+                glds16(src, __builtin_amdgcn_readfirstlane(s + (wave * (BM / 8) + i * 8) * 128));
+            }
         }
 #pragma unroll
         for (int i = 0; i < BL; ++i)
@@ -1408,20 +1444,20 @@ conv_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx, ConvGeomG g, const
                                             0);
 }
 
-template <int BM, int BN, int WM, int WN, int E>
+template <int BM, int BN, int WM, int WN, int E, int MODE = 0>
 static int launch_conv(const uint16_t* X, int64_t ldx, const ConvGeomG& g, const uint16_t* zrow, const uint16_t* W,
                        int64_t ldw, int nbm, int nbn, int K, const float* bias, void* out, int64_t ldo, const float* aux,
                        int64_t ldaux, hipStream_t stream) {
     constexpr int lds = 2 * (BM + BN) * 128;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv_gemm_kernel<BM, BN, WM, WN, E, 2>,
+        hipError_t e = hipFuncSetAttribute((const void*)conv_gemm_kernel<BM, BN, WM, WN, E, 2, MODE>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return fail((int)e, std::string("vc_conv3d_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
         attr_set = true;
     }
-    conv_gemm_kernel<BM, BN, WM, WN, E, 2><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(X, ldx, g, zrow, W, ldw, nbm, nbn,
-                                                                                       K, bias, out, ldo, aux, ldaux);
+    conv_gemm_kernel<BM, BN, WM, WN, E, 2, MODE><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(
+        X, ldx, g, zrow, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux);
     return check_launch("vc_conv3d_gemm_bf16");
 }
 
@@ -1434,8 +1470,8 @@ struct GemmCfg {
     int bm, bn;
 };
 static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}, {128, 128}, {0, 0},
-                                 {64, 128}, {256, 256}, {256, 128}, {256, 256}, {256, 256}, {256, 256}};
-constexpr int kNumCfgs = 13;
+                                 {64, 128}, {256, 256}, {256, 128}, {256, 256}, {256, 256}, {256, 256}, {256, 256}};
+constexpr int kNumCfgs = 14;
 
 template <int BM, int BN, int WM, int WN, int E, int ST = 3, int ET = VC_ELEM_BF16>
 static int launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
@@ -1573,10 +1609,13 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
         case 8: return launch_pp<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 11:
         case 12:
+        case 13:
             if constexpr (E == VC_EPI_BIAS_BF16 && ET == VC_ELEM_BF16) {
                 if (cfg == 11)
                     return launch_pp<E, ET, 1>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-                return launch_pp<E, ET, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+                if (cfg == 12)
+                    return launch_pp<E, ET, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+                return launch_pp<E, ET, 3>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
             }
             return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfgs 11 / 12 (timing ablations) are bias / bf16 only");
         case 9: return launch_pp128<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
@@ -1669,7 +1708,7 @@ extern "C" int vc_gemm_h16(const uint16_t* A, int64_t lda, const uint16_t* W, in
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: no tile config divides M x N");
     if ((M / kCfgs[cfg].bm) * (N / kCfgs[cfg].bn) > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: grid too large");
     const int k = (int)K;
-    if ((cfg == 8 || cfg == 9 || cfg == 11 || cfg == 12) && K < 128) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 8 / 9 need K >= 128");
+    if ((cfg == 8 || cfg == 9 || cfg >= 11) && K < 128) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 8 / 9 need K >= 128");
     if ((cfg == 4 || cfg == 10) && (K / 32 < 6 || N > 8192 || !st16_ok ||
                      (epilogue > VC_EPI_BIAS_GELU_ERF && epilogue != VC_EPI_BIAS_RELU_BF16 &&
                       epilogue != VC_EPI_BIAS_GELU_TANH_SAVE)))
@@ -1711,8 +1750,8 @@ extern "C" int vc_conv3d_gemm_bf16(const uint16_t* x, int64_t ldx, int64_t B, in
     for (int d = 0; d < 3; ++d)
         if (kernel[d] <= 0 || stride[d] <= 0 || pad[d] < 0 || kernel[d] > 255)
             return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: bad kernel / stride / pad");
-    if (B <= 0 || T <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 64 || N <= 0 || N % 128)
-        return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: need C % 64 == 0 and N % 128 == 0");
+    if (B <= 0 || T <= 0 || H <= 0 || W <= 0 || C <= 0 || C % 64 || N <= 0 || N % 64)
+        return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: need C % 64 == 0 and N % 64 == 0");
     ConvGeomG g;
     g.Tin = (int)T; g.Hin = (int)H; g.Win = (int)W; g.C = (int)C;
     g.kt = kernel[0]; g.kh = kernel[1]; g.kw = kernel[2];
@@ -1728,9 +1767,22 @@ extern "C" int vc_conv3d_gemm_bf16(const uint16_t* x, int64_t ldx, int64_t B, in
         return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: bad leading dimension");
     if ((((uintptr_t)x) | ((uintptr_t)Wt) | ((uintptr_t)out) | ((uintptr_t)bias) | ((uintptr_t)zero_row)) & 15)
         return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: pointers must be 16-byte aligned");
+    const float* auxf = reinterpret_cast<const float*>(aux);
+    if (N % 128) {
+        // 64 output channels (ResNet3D stage 1): 256 x 64 tiles (8 waves as 8 x 1), no padded-channel MFMAs
+        const int nbm = (int)((g.M + 255) / 256), nbn = (int)(N / 64);
+        if ((int64_t)nbm * nbn > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: grid too large");
+        if (ldo % 8) return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: ldo % 8");
+        if (epilogue == VC_EPI_BIAS_RELU_BF16)
+            return launch_conv<256, 64, 8, 1, VC_EPI_BIAS_RELU_BF16>(x, ldx, g, zero_row, Wt, ldw, nbm, nbn, (int)K, bias,
+                                                                      out, ldo, auxf, ldaux, stream);
+        if (epilogue == VC_EPI_BIAS_BF16)
+            return launch_conv<256, 64, 8, 1, VC_EPI_BIAS_BF16>(x, ldx, g, zero_row, Wt, ldw, nbm, nbn, (int)K, bias, out,
+                                                                 ldo, auxf, ldaux, stream);
+        return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: N % 128 != 0 supports bias / bias_relu only");
+    }
     const int nbm = (int)((g.M + 127) / 128), nbn = (int)(N / 128);
     if ((int64_t)nbm * nbn > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: grid too large");
-    const float* auxf = reinterpret_cast<const float*>(aux);
     switch (epilogue) {
         case VC_EPI_BIAS_BF16:
             if (ldo % 8) break;
@@ -1749,6 +1801,95 @@ extern "C" int vc_conv3d_gemm_bf16(const uint16_t* x, int64_t ldx, int64_t B, in
     }
     return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: epilogue must be bias / bias_relu / bias_resid_relu "
                                     "(16-B output rows; resid_relu: a bf16 aux with ldaux >= N)");
+}
+
+// Stem input packing for vc_conv3d_stem_gemm_bf16: f32 [B][C][T][H][W] (C <= 4) -> bf16
+// [B][T + 2pt][H + 2ph][W + 2pw][4], zero in the padding and the unused channels.  One thread per
+// padded pixel: C strided f32 reads (coalesced along w), one 8-B store.
+__global__ void __launch_bounds__(256) stem_pack_kernel(const float* __restrict__ x, int C, int T, int H, int W, int pt,
+                                                        int ph, int pw, int Tp, int Hp, int Wp, int64_t total,
+                                                        uint16_t* __restrict__ xp) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= total) return;
+    int64_t r = i;
+    const int wq = (int)(r % Wp);
+    r /= Wp;
+    const int hq = (int)(r % Hp);
+    r /= Hp;
+    const int tq = (int)(r % Tp);
+    const int64_t b = r / Tp;
+    const int t = tq - pt, h = hq - ph, w = wq - pw;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if ((unsigned)t < (unsigned)T && (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
+        const int64_t plane = (int64_t)T * H * W;
+        const float* src = x + b * C * plane + ((int64_t)t * H + h) * W + w;
+        for (int c = 0; c < C; ++c) v[c] = src[c * plane];
+    }
+    uint2 o;
+    o.x = pack2bf(v[0], v[1]);
+    o.y = pack2bf(v[2], v[3]);
+    *reinterpret_cast<uint2*>(xp + i * 4) = o;
+}
+
+extern "C" int vc_conv3d_stem_pack(const float* x, int64_t B, int64_t C, int64_t T, int64_t H, int64_t W,
+                                   const int* pad, uint16_t* xp, hipStream_t stream) {
+    if (!x || !pad || !xp) return fail(VC_ERR_INVALID_ARG, "vc_conv3d_stem_pack: null pointer");
+    if (B <= 0 || C <= 0 || C > 4 || T <= 0 || H <= 0 || W <= 0 || pad[0] < 0 || pad[1] < 0 || pad[2] < 0 ||
+        ((uintptr_t)xp & 7))
+        return fail(VC_ERR_INVALID_ARG, "vc_conv3d_stem_pack: bad shape (C <= 4) / alignment");
+    const int Tp = (int)T + 2 * pad[0], Hp = (int)H + 2 * pad[1], Wp = (int)W + 2 * pad[2];
+    const int64_t total = B * Tp * (int64_t)Hp * Wp;
+    stem_pack_kernel<<<(unsigned)((total + 255) / 256), 256, 0, stream>>>(x, (int)C, (int)T, (int)H, (int)W, pad[0],
+                                                                          pad[1], pad[2], Tp, Hp, Wp, total, xp);
+    return check_launch("vc_conv3d_stem_pack");
+}
+
+// Stem Conv3d as an implicit GEMM over the packed clip (conv_gemm_kernel MODE 1): Wt [N][>= K]
+// with K = 64 * ceil(kt * kh / 2) columns (seg = kt_i * kh + kh_i; column seg * 32 + kw_i * 4 + c),
+// zero where kw_i >= kw or c >= C; the output rows up to the next multiple of 128 are written.
+extern "C" int vc_conv3d_stem_gemm_bf16(const uint16_t* xp, int64_t B, int64_t T, int64_t H, int64_t W,
+                                        const int* kernel, const int* stride, const int* pad, const uint16_t* zero_row,
+                                        const uint16_t* Wt, int64_t ldw, int64_t N, const float* bias, int epilogue,
+                                        void* out, int64_t ldo, hipStream_t stream) {
+    if (!xp || !kernel || !stride || !pad || !zero_row || !Wt || !bias || !out)
+        return fail(VC_ERR_INVALID_ARG, "vc_conv3d_stem_gemm_bf16: null pointer");
+    for (int d = 0; d < 3; ++d)
+        if (kernel[d] <= 0 || stride[d] <= 0 || pad[d] < 0)
+            return fail(VC_ERR_INVALID_ARG, "vc_conv3d_stem_gemm_bf16: bad kernel / stride / pad");
+    if (kernel[2] > 8 || stride[2] % 2 || B <= 0 || N <= 0 || N % 64)
+        return fail(VC_ERR_INVALID_ARG, "vc_conv3d_stem_gemm_bf16: need kw <= 8, an even w stride, N % 64 == 0");
+    ConvGeomG g;
+    g.Tin = (int)T + 2 * pad[0]; g.Hin = (int)H + 2 * pad[1]; g.Win = (int)W + 2 * pad[2]; g.C = 4;
+    g.kt = kernel[0]; g.kh = kernel[1]; g.kw = kernel[2];
+    g.st = stride[0]; g.sh = stride[1]; g.sw = stride[2];
+    g.pt = 0; g.ph = 0; g.pw = 0;
+    g.To = (int)((g.Tin - g.kt) / g.st + 1);
+    g.Ho = (int)((g.Hin - g.kh) / g.sh + 1);
+    g.Wo = (int)((g.Win - g.kw) / g.sw + 1);
+    if (g.To <= 0 || g.Ho <= 0 || g.Wo <= 0 || g.Win % 2) return fail(VC_ERR_INVALID_ARG, "vc_conv3d_stem_gemm_bf16: geometry");
+    g.M = B * g.To * g.Ho * (int64_t)g.Wo;
+    const int64_t K = 64 * ((g.kt * g.kh + 1) / 2);
+    if (ldw % 8 || ldw < K || ldo < N || ldo % 8)
+        return fail(VC_ERR_INVALID_ARG, "vc_conv3d_stem_gemm_bf16: bad leading dimension");
+    if ((((uintptr_t)xp) | ((uintptr_t)Wt) | ((uintptr_t)out) | ((uintptr_t)bias) | ((uintptr_t)zero_row)) & 15)
+        return fail(VC_ERR_INVALID_ARG, "vc_conv3d_stem_gemm_bf16: pointers must be 16-byte aligned");
+    if (N % 128) {
+        const int nbm = (int)((g.M + 255) / 256), nbn = (int)(N / 64);
+        if ((int64_t)nbm * nbn > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_conv3d_stem_gemm_bf16: grid too large");
+        if (epilogue == VC_EPI_BIAS_RELU_BF16)
+            return launch_conv<256, 64, 8, 1, VC_EPI_BIAS_RELU_BF16, 1>(xp, 0, g, zero_row, Wt, ldw, nbm, nbn, (int)K,
+                                                                         bias, out, ldo, nullptr, 0, stream);
+        return fail(VC_ERR_INVALID_ARG, "vc_conv3d_stem_gemm_bf16: N % 128 != 0 supports bias_relu only");
+    }
+    const int nbm = (int)((g.M + 127) / 128), nbn = (int)(N / 128);
+    if ((int64_t)nbm * nbn > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_conv3d_stem_gemm_bf16: grid too large");
+    if (epilogue == VC_EPI_BIAS_RELU_BF16)
+        return launch_conv<128, 128, 2, 4, VC_EPI_BIAS_RELU_BF16, 1>(xp, 0, g, zero_row, Wt, ldw, nbm, nbn, (int)K, bias,
+                                                                      out, ldo, nullptr, 0, stream);
+    if (epilogue == VC_EPI_BIAS_BF16)
+        return launch_conv<128, 128, 2, 4, VC_EPI_BIAS_BF16, 1>(xp, 0, g, zero_row, Wt, ldw, nbm, nbn, (int)K, bias,
+                                                                 out, ldo, nullptr, 0, stream);
+    return fail(VC_ERR_INVALID_ARG, "vc_conv3d_stem_gemm_bf16: epilogue must be bias / bias_relu");
 }
 
 // the tile config vc_gemm_bf16 / vc_gemm_h16 run with cfg = -1 (host only: no launch, no GPU)

@@ -512,22 +512,24 @@ _ZERO_ROW = {}
 
 def conv3d_gemm(x: torch.Tensor, B: int, grid, C: int, kernel, stride, pad, w: torch.Tensor, bias: torch.Tensor,
                 epilogue: str, out: torch.Tensor, aux: torch.Tensor | None = None, flop: float | None = None,
-                op: str = "conv") -> torch.Tensor:
+                op: str = "conv", n: int | None = None) -> torch.Tensor:
     """Implicit-GEMM Conv3d (vc_conv3d_gemm_bf16): x channels-last bf16 rows [>= B*T*H*W, >= C],
-    w bf16 [N, >= kvol*C] (columns (kt, kh, kw, c)), out bf16 [>= roundup(B*To*Ho*Wo, 128), >= N]."""
+    w bf16 [>= N, >= kvol*C] (columns (kt, kh, kw, c)), out bf16 [>= roundup(B*To*Ho*Wo, 128), >= N]
+    (256-row multiples when N % 128 != 0: 256 x 64 tiles); N = n (a multiple of 64) or w's rows."""
     import ctypes
     _dev(x, w, bias, out)
     T, H, W = grid
     To, Ho, Wo = conv_out_size(grid, kernel, stride, pad)
     kvol = kernel[0] * kernel[1] * kernel[2]
     M = B * To * Ho * Wo
-    N = w.shape[0]
+    N = w.shape[0] if n is None else n
+    rt = 128 if N % 128 == 0 else 256
     _need(x.dtype == torch.bfloat16 and x.stride(1) == 1 and x.shape[0] >= B * T * H * W and x.shape[1] >= C,
           "conv3d_gemm x")
-    _need(w.dtype == torch.bfloat16 and w.stride(1) == 1 and w.shape[1] >= kvol * C and bias.numel() == N and
-          bias.dtype == torch.float32, "conv3d_gemm weights")
-    _need(out.dtype == torch.bfloat16 and out.stride(1) == 1 and out.shape[0] >= (M + 127) // 128 * 128 and
-          out.shape[1] >= N, "conv3d_gemm out rows (a multiple of 128)")
+    _need(w.dtype == torch.bfloat16 and w.stride(1) == 1 and w.shape[1] >= kvol * C and w.shape[0] >= N and
+          bias.numel() >= N and bias.dtype == torch.float32, "conv3d_gemm weights")
+    _need(out.dtype == torch.bfloat16 and out.stride(1) == 1 and out.shape[0] >= (M + rt - 1) // rt * rt and
+          out.shape[1] >= N, "conv3d_gemm out rows (a multiple of the tile height)")
     e = EPI[epilogue]
     if e == 7:
         _need(aux is not None and aux.dtype == torch.bfloat16 and aux.stride(1) == 1 and aux.shape[0] >= M and
@@ -542,8 +544,56 @@ def conv3d_gemm(x: torch.Tensor, B: int, grid, C: int, kernel, stride, pad, w: t
               ctypes.addressof(p), _p(_ZERO_ROW[key]), _p(w), w.stride(0), N, _p(bias), e, _p(out), out.stride(0),
               _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0, _stream(x))
     if rec is not None:
-        rec.end(e0, f"conv_gemm_kernel<128, 128, 2, 4, {e}, 2>", op, 2.0 * M * N * kvol * C if flop is None else flop,
-                "flop")
+        tile = "128, 128, 2, 4" if rt == 128 else "256, 64, 8, 1"
+        rec.end(e0, f"conv_gemm_kernel<{tile}, {e}, 2, 0>", op, 2.0 * M * N * kvol * C if flop is None else flop, "flop")
+    return out
+
+
+def conv3d_stem_pack(x: torch.Tensor, pad, out: torch.Tensor) -> torch.Tensor:
+    """f32 clip [B, C<=4, T, H, W] -> zero-padded channels-last bf16 [B, T+2pt, H+2ph, W+2pw, 4] (out, any
+    shape with that many contiguous elements)."""
+    import ctypes
+    _dev(x, out)
+    B, C, T, H, W = x.shape
+    _need(x.dtype == torch.float32 and x.is_contiguous() and C <= 4, "conv3d_stem_pack x")
+    _need(out.dtype == torch.bfloat16 and out.is_contiguous() and
+          out.numel() >= B * (T + 2 * pad[0]) * (H + 2 * pad[1]) * (W + 2 * pad[2]) * 4, "conv3d_stem_pack out")
+    p = (ctypes.c_int * 3)(*pad)
+    _lib.call("vc_conv3d_stem_pack", _p(x), B, C, T, H, W, ctypes.addressof(p), _p(out), _stream(x))
+    return out
+
+
+def conv3d_stem_gemm(xp: torch.Tensor, B: int, grid, kernel, stride, pad, w: torch.Tensor, bias: torch.Tensor,
+                     epilogue: str, out: torch.Tensor, flop: float | None = None, op: str = "stem",
+                     n: int | None = None) -> torch.Tensor:
+    """The stem Conv3d as an implicit GEMM over conv3d_stem_pack's padded clip (vc_conv3d_stem_gemm_bf16);
+    w bf16 [N, >= 64 * ceil(kt*kh/2)] in the segment column order, out bf16 [>= roundup(M, 128), >= N]."""
+    import ctypes
+    _dev(xp, w, bias, out)
+    T, H, W = grid
+    To, Ho, Wo = conv_out_size(grid, kernel, stride, pad)
+    M = B * To * Ho * Wo
+    N = w.shape[0] if n is None else n
+    rt = 128 if N % 128 == 0 else 256
+    K = 64 * ((kernel[0] * kernel[1] + 1) // 2)
+    _need(xp.dtype == torch.bfloat16 and xp.is_contiguous(), "conv3d_stem_gemm xp")
+    _need(w.dtype == torch.bfloat16 and w.stride(1) == 1 and w.shape[1] >= K and w.shape[0] >= N and
+          bias.numel() >= N and bias.dtype == torch.float32, "conv3d_stem_gemm weights")
+    _need(out.dtype == torch.bfloat16 and out.stride(1) == 1 and out.shape[0] >= (M + rt - 1) // rt * rt and
+          out.shape[1] >= N, "conv3d_stem_gemm out")
+    key = xp.device
+    if key not in _ZERO_ROW:
+        _ZERO_ROW[key] = torch.zeros(64, dtype=torch.bfloat16, device=xp.device)
+    k, s, p = ((ctypes.c_int * 3)(*v) for v in (kernel, stride, pad))
+    rec = _REC[0]
+    e0 = rec.begin() if rec is not None else None
+    e = EPI[epilogue]
+    _lib.call("vc_conv3d_stem_gemm_bf16", _p(xp), B, T, H, W, ctypes.addressof(k), ctypes.addressof(s),
+              ctypes.addressof(p), _p(_ZERO_ROW[key]), _p(w), w.stride(0), N, _p(bias), e, _p(out), out.stride(0),
+              _stream(xp))
+    if rec is not None:
+        tile = "128, 128, 2, 4" if rt == 128 else "256, 64, 8, 1"
+        rec.end(e0, f"conv_gemm_kernel<{tile}, {e}, 2, 1>", op, 2.0 * M * N * K if flop is None else flop, "flop")
     return out
 
 

@@ -115,6 +115,18 @@ class ResNet3d(torch.nn.Module):
         pk = {"device": device, "version": ver}
         sk = c.get("stem_kernel", (3, 7, 7))
         pk["stem"] = fold("blocks.0.conv", "blocks.0.norm", channels_last=False, k_pad=_ru(3 * sk[0] * sk[1] * sk[2], 64))
+        if sk[2] <= 8:
+            # the implicit stem GEMM's segment columns: seg = kt_i * kh + kh_i, column seg*32 + kw_i*4 + c
+            w = P("blocks.0.conv.weight")
+            scl = P("blocks.0.norm.weight") / torch.sqrt(P("blocks.0.norm.running_var") + eps)
+            w = w * scl.view(-1, 1, 1, 1, 1)
+            co, ci = w.shape[0], w.shape[1]
+            nseg = sk[0] * sk[1]
+            Wseg = torch.zeros((_ru(co, 128), 64 * ((nseg + 1) // 2)), dtype=torch.float64, device=device)
+            ws_ = torch.zeros((co, sk[0], sk[1], 8, 4), dtype=torch.float64, device=device)
+            ws_[:, :, :, :sk[2], :ci] = w.permute(0, 2, 3, 4, 1)
+            Wseg[:co, :nseg * 32] = ws_.reshape(co, nseg * 32)
+            pk["stem_seg"] = (Wseg.to(torch.bfloat16).contiguous(), pk["stem"][1])
         stages = []
         din, dout = c["stem_dim"], c["stem_dim"] * 4
         for s, depth in enumerate(c["depths"]):
@@ -162,6 +174,8 @@ class ResNet3d(torch.nn.Module):
         rows = lambda g: _ru(B * g[0] * g[1] * g[2], 256)  # noqa: E731
         z = lambda r, cols: torch.zeros((r, cols), dtype=bf, device=device)  # noqa: E731
         ws = {"stem_out": z(rows(stem), 128)}
+        sp = c.get("stem_pad", (1, 3, 3))
+        ws["stem_pad"] = torch.zeros(B * (T + 2 * sp[0]) * (H + 2 * sp[1]) * (W + 2 * sp[2]) * 4, dtype=bf, device=device)
         # im2col scratch: the largest M x K of any convolution
         sk = c.get("stem_kernel", (3, 7, 7))
         big = rows(stem) * _ru(3 * sk[0] * sk[1] * sk[2], 64)
@@ -180,7 +194,10 @@ class ResNet3d(torch.nn.Module):
             din, dout = dout, dout * 2
         ws["x0"] = z(rows(grids[0]), c["stem_dim"])
         ws["acts"] = acts
-        ws["col"] = torch.zeros(big, dtype=bf, device=device)
+        # im2col scratch (1.4 GB at B = 4 for the stem alone): allocated on first use, i.e. only by the
+        # im2col path (implicit_conv = False)
+        ws["col"] = None
+        ws["col_elems"] = big
         ws["head_work"] = torch.zeros(B * T * 2048 * 33, dtype=torch.float32, device=device)
         ws["logits"] = torch.zeros((B, c["num_classes"]), dtype=torch.float32, device=device)
         self._ws[key] = ws
@@ -323,6 +340,8 @@ class ResNet3d(torch.nn.Module):
         rows = lambda g: _ru(B * g[0] * g[1] * g[2], 256)  # noqa: E731
 
         def col(m, k):
+            if ws["col"] is None:
+                ws["col"] = torch.zeros(ws["col_elems"], dtype=torch.bfloat16, device=video.device)
             return ws["col"][: m * k].view(m, k)
 
         # stem: conv (3,7,7)/(1,2,2) + BN + ReLU, then MaxPool (1,3,3)/(1,2,2)
@@ -332,12 +351,21 @@ class ResNet3d(torch.nn.Module):
         vol = lambda g: B * g[0] * g[1] * g[2]  # noqa: E731
         sk = c.get("stem_kernel", (3, 7, 7))
         ks = 3 * sk[0] * sk[1] * sk[2]
-        Kst = pk["stem"][0].shape[1]
-        A = col(rows(stem), Kst)
-        tm("conv3d_im2col_kernel", "im2col", B * 3 * T * H * W * 4 + vol(stem) * ks * 2, "byte", ops.conv3d_im2col,
-           video, "ncthw_f32", B, (T, H, W), 3, sk, (1, 2, 2), c.get("stem_pad", (1, 3, 3)), A)
-        ops.gemm(A, pk["stem"][0], pk["stem"][1], "bias_relu", ws["stem_out"], flop=2.0 * vol(stem) * c["stem_dim"] * ks,
-                 op="stem")
+        spad = c.get("stem_pad", (1, 3, 3))
+        if self.implicit_conv and "stem_seg" in pk:
+            # the clip as zero-padded channels-last bf16 (4 channels), then the implicit stem GEMM
+            tm("stem_pack_kernel", "stem_pack", B * 3 * T * H * W * 4 + ws["stem_pad"].numel() * 2, "byte",
+               ops.conv3d_stem_pack, video, spad, ws["stem_pad"])
+            ops.conv3d_stem_gemm(ws["stem_pad"], B, (T, H, W), sk, (1, 2, 2), spad, pk["stem_seg"][0], pk["stem_seg"][1],
+                                 "bias_relu", ws["stem_out"], flop=2.0 * vol(stem) * c["stem_dim"] * ks, op="stem",
+                                 n=_ru(c["stem_dim"], 64))
+        else:
+            Kst = pk["stem"][0].shape[1]
+            A = col(rows(stem), Kst)
+            tm("conv3d_im2col_kernel", "im2col", B * 3 * T * H * W * 4 + vol(stem) * ks * 2, "byte", ops.conv3d_im2col,
+               video, "ncthw_f32", B, (T, H, W), 3, sk, (1, 2, 2), spad, A)
+            ops.gemm(A, pk["stem"][0], pk["stem"][1], "bias_relu", ws["stem_out"],
+                     flop=2.0 * vol(stem) * c["stem_dim"] * ks, op="stem")
         x = ws["x0"]
         tm("maxpool3d_kernel", "maxpool", (vol(stem) + vol(grids[0])) * c["stem_dim"] * 2, "byte", ops.maxpool3d,
            ws["stem_out"], B, stem, c["stem_dim"], (1, 3, 3), (1, 2, 2), (0, 1, 1), x)
@@ -369,11 +397,15 @@ class ResNet3d(torch.nn.Module):
                     skip = xin
                 # conv_a (+ BN + ReLU) at the block's input resolution
                 fl = 2.0 * vol(gi) * inner * cin * ka[0] * ka[1] * ka[2]
-                if tuple(ka) == (1, 1, 1):
+                if tuple(ka) == (1, 1, 1) and self.implicit_conv and inner % 128 and inner % 64 == 0 and cin % 64 == 0:
+                    # 64 output channels: the 256 x 64 implicit-GEMM tile (no MFMAs on the zero-padded channels)
+                    ops.conv3d_gemm(xin, B, gi, cin, ka, (1, 1, 1), (0, 0, 0), blk["a"][0], blk["a"][1], "bias_relu",
+                                    act["a"], flop=fl, op="conv_a", n=inner)
+                elif tuple(ka) == (1, 1, 1):
                     ops.gemm(xin, blk["a"][0], blk["a"][1], "bias_relu", act["a"], m=rows(gi), flop=fl, op="conv_a")
                 elif self.implicit_conv and cin % 64 == 0:
                     ops.conv3d_gemm(xin, B, gi, cin, ka, (1, 1, 1), tuple(k // 2 for k in ka), blk["a"][0], blk["a"][1],
-                                    "bias_relu", act["a"], flop=fl, op="conv_a")
+                                    "bias_relu", act["a"], flop=fl, op="conv_a", n=_ru(inner, 64))
                 else:
                     A = col(rows(gi), ka[0] * cin)
                     tm("conv3d_im2col_kernel", "im2col", vol(gi) * cin * 2 * (1 + ka[0]), "byte", ops.conv3d_im2col,
@@ -382,7 +414,8 @@ class ResNet3d(torch.nn.Module):
                 # conv_b (1,3,3) with the stage stride (+ BN + ReLU)
                 if self.implicit_conv and inner % 64 == 0:
                     ops.conv3d_gemm(act["a"], B, gi, inner, (1, 3, 3), stride, (0, 1, 1), blk["b"][0], blk["b"][1],
-                                    "bias_relu", act["b"], flop=2.0 * vol(g) * inner * inner * 9, op="conv_b")
+                                    "bias_relu", act["b"], flop=2.0 * vol(g) * inner * inner * 9, op="conv_b",
+                                    n=_ru(inner, 64))
                 else:
                     A = col(rows(g), 9 * inner)
                     tm("conv3d_im2col_kernel", "im2col", (vol(gi) + 9 * vol(g)) * inner * 2, "byte", ops.conv3d_im2col,

@@ -319,6 +319,19 @@ int vc_conv3d_gemm_bf16(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, in
                         const uint16_t* Wt, int64_t ldw, int64_t N, const float* bias, int epilogue, void* out,
                         int64_t ldo, const void* aux, int64_t ldaux, hipStream_t stream);
 
+/* The stem Conv3d (3 input channels, kernel (kt, kh, kw <= 8), even w stride) as an implicit GEMM:
+ * vc_conv3d_stem_pack writes the f32 [B][C][T][H][W] clip (C <= 4) as zero-padded channels-last
+ * bf16 [B][T+2pt][H+2ph][W+2pw][4]; vc_conv3d_stem_gemm_bf16 reads one (kt, kh) tap row of 8
+ * pixels x 4 channels as a 32-column segment, K = 64 * ceil(kt*kh / 2), Wt column
+ * seg*32 + kw_i*4 + c for seg = kt_i*kh + kh_i (zero for kw_i >= kw, c >= C, seg >= kt*kh).
+ * Replaces vc_conv3d_im2col (VC_CONV_IN_NCTHW_F32) + vc_gemm_bf16 for pytorchvideo's stem. */
+int vc_conv3d_stem_pack(const float* x, int64_t B, int64_t C, int64_t T, int64_t H, int64_t W, const int* pad,
+                        uint16_t* xp, hipStream_t stream);
+int vc_conv3d_stem_gemm_bf16(const uint16_t* xp, int64_t B, int64_t T, int64_t H, int64_t W, const int* kernel,
+                             const int* stride, const int* pad, const uint16_t* zero_row, const uint16_t* Wt,
+                             int64_t ldw, int64_t N, const float* bias, int epilogue, void* out, int64_t ldo,
+                             hipStream_t stream);
+
 /* MaxPool3d on channels-last bf16 (padding counts as -inf): pytorchvideo's stem pool. */
 int vc_maxpool3d(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_t H, int64_t W, int64_t C,
                  const int* kernel, const int* stride, const int* pad, uint16_t* y, int64_t ldy, hipStream_t stream);

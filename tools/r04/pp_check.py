@@ -18,6 +18,7 @@ ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--cfgs", default="8")
 ap.add_argument("--only", default="")
 ap.add_argument("--ksweep", action="store_true", help="q|k|v-shaped cases at K = 768 .. 6144 (per-tile overhead fit)")
+ap.add_argument("--swin", action="store_true", help="Video Swin-T B=4 stage-1/2 GEMM shapes (channels padded to 128)")
 a = ap.parse_args()
 new_cfgs = [int(c) for c in a.cfgs.split(",")]
 
@@ -27,6 +28,12 @@ for M, tag in ((25344, "B8"), (12800, "B4")):
               (f"fc2_{tag}", M, 768, 3072, "bias_resid_f32"), (f"oproj_{tag}", M, 768, 768, "bias_resid_f32")]
 CASES += [("sq4096", 4096, 4096, 4096, "bias"), ("sq8192", 8192, 8192, 8192, "bias"),
           ("tsf_fc1_B16", 25344, 3072, 768, "bias_gelu_erf")]
+if a.swin:
+    CASES = []
+    for st, (M, C, Cp) in enumerate(((200704, 96, 128), (50176, 192, 256), (12544, 384, 384), (3136, 768, 768))):
+        q = (3 * C + 127) // 128 * 128
+        CASES += [(f"s{st}_qkv", M, q, Cp, "bias"), (f"s{st}_proj", M, Cp, Cp, "bias_resid_f32"),
+                  (f"s{st}_fc1", M, 4 * C, Cp, "bias_gelu_erf"), (f"s{st}_fc2", M, Cp, 4 * C, "bias_resid_f32")]
 if a.ksweep:
     CASES = [(f"ks_K{K}", 12800, 2304, K, "bias") for K in (768, 1536, 3072, 6144)]
 if a.only:
@@ -52,7 +59,12 @@ for name, M, N, K, epi in CASES:
     A, W, b, out = operands(M, N, K, epi)
     base = lib.vc_gemm_pick(M, N, K, E[epi], out.stride(0), 0, None)
     bf16_out = out.dtype != torch.float32
-    cfgs = [base] + [c for c in new_cfgs if c != base and (c != 11 or epi == "bias") and (c not in (4, 10) or bf16_out)]
+    TILE = {1: (128, 128), 3: (256, 256), 4: (256, 256), 5: (128, 128), 7: (64, 128), 8: (256, 256), 9: (256, 128),
+            10: (256, 256), 11: (256, 256), 12: (256, 256), 13: (256, 256)}
+    ok_shape = lambda c: (c in TILE and M % TILE[c][0] == 0 and N % TILE[c][1] == 0 and K % 64 == 0 and  # noqa: E731
+                          (K >= 192 if c in (4, 10) else K >= 128 if c in (8, 9, 11, 12, 13) else True))
+    cfgs = [base] + [c for c in new_cfgs if c != base and ok_shape(c) and (c not in (11, 12, 13) or epi == "bias") and
+                     (c not in (4, 10) or bf16_out)]
     # bit-identity: every config from the same initial out (the residual epilogue accumulates)
     init = (torch.randn(M, N, device="cuda", generator=g) if out.dtype == torch.float32 else out.clone())
     ref = None
