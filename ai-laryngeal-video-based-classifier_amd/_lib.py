@@ -40,6 +40,10 @@ SIGNATURES = {
     "vc_patch_im2col_h16": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_int, c_int, c_int, c_p,
                              c_i64, c_p], c_int),
     "vc_gemm_pick": ([c_i64, c_i64, c_i64, c_int, c_i64, c_i64, c_p], c_int),
+    "vc_gemm_h16_wrap": ([c_p, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_int, c_p, c_i64, c_p, c_i64,
+                          c_i64, c_i64, c_i64, c_int, c_p], c_int),
+    "vc_patch_im2col_split_h16": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_int, c_int, c_int, c_int, c_int, c_int,
+                                   c_p, c_i64, c_p], c_int),
     "vc_gemm_h16": ([c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_int, c_p, c_i64, c_p, c_i64,
                      c_i64, c_i64, c_i64, c_int, c_int, c_p], c_int),
     "vc_layernorm_f32_h16": ([c_p, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_int, c_p, c_i64, c_p], c_int),

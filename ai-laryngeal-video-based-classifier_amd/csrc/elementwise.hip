@@ -106,10 +106,12 @@ __global__ void __launch_bounds__(256) gather_norm_kernel(const uint8_t* __restr
 // the TimeSformer token order).  One thread converts VEC consecutive pixels of one image
 // row (VEC = 8, or 4 for 4-wide patches such as Swin's 2x4x4).
 // ---------------------------------------------------------------------------------
+// klo > 0 (the split-operand build): the 16-bit rounding residual x - (float)to16(x) also goes to
+// column klo + k, so A = [A_hi | A_lo] (vc_patch_im2col_split_h16).
 template <int VEC, int ET = VC_ELEM_BF16>
 __global__ void __launch_bounds__(256) im2col_kernel(const float* __restrict__ pix, int64_t totalv, int T, int C,
                                                      int H, int W, int kt, int kh, int kw, int order, int layout,
-                                                     uint16_t* __restrict__ A, int64_t lda) {
+                                                     uint16_t* __restrict__ A, int64_t lda, int64_t klo = 0) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= totalv) return;
     const int WV = W / VEC;
@@ -138,6 +140,17 @@ __global__ void __launch_bounds__(256) im2col_kernel(const float* __restrict__ p
         o.z = pack2<ET>(v.x, v.y);
         o.w = pack2<ET>(v.z, v.w);
         *reinterpret_cast<uint4*>(A + m * lda + k) = o;
+        if (klo > 0) {
+            auto lo = [](unsigned p, float a, float b) {
+                return pack2<ET>(a - from16<ET>((unsigned short)(p & 0xffff)), b - from16<ET>((unsigned short)(p >> 16)));
+            };
+            uint4 l;
+            l.x = lo(o.x, u.x, u.y);
+            l.y = lo(o.y, u.z, u.w);
+            l.z = lo(o.z, v.x, v.y);
+            l.w = lo(o.w, v.z, v.w);
+            *reinterpret_cast<uint4*>(A + m * lda + klo + k) = l;
+        }
     } else {
         uint2 o;
         o.x = pack2<ET>(u.x, u.y);
@@ -450,6 +463,32 @@ int vc_patch_im2col_h16(const float* pixel_values, int64_t B, int64_t T, int64_t
                                                     token_order, layout, A, lda);
     }
     return check_launch("vc_patch_im2col");
+}
+
+// A = [A_hi | A_lo] (2 K columns, K = C kt kh kw): the 16-bit operand and its rounding residual, for
+// vc_gemm_h16_wrap with W = [W_hi | W_hi | W_lo] (A_hi W_hi + A_lo W_hi + A_hi W_lo).  8-wide patches.
+int vc_patch_im2col_split_h16(const float* pixel_values, int64_t B, int64_t T, int64_t C, int64_t H, int64_t W,
+                              int kt, int kh, int kw, int token_order, int layout, int elem, uint16_t* A, int64_t lda,
+                              hipStream_t stream) {
+    if (elem != VC_ELEM_BF16 && elem != VC_ELEM_F16) return fail(VC_ERR_INVALID_ARG, "vc_patch_im2col_split: bad elem");
+    if (!pixel_values || !A) return fail(VC_ERR_INVALID_ARG, "vc_patch_im2col_split: null pointer");
+    const int64_t K = C * kt * kh * kw;
+    if (kt <= 0 || kh <= 0 || kw <= 0 || T % kt || H % kh || W % kw || kw % 8 || W % 8 || lda % 8 || lda < 2 * K ||
+        K % 8 || ((uintptr_t)pixel_values & 15) || ((uintptr_t)A & 15))
+        return fail(VC_ERR_INVALID_ARG, "vc_patch_im2col_split: needs 8-wide patches, lda >= 2K, 16-B alignment");
+    if (token_order != VC_TOKENS_TIME_MAJOR && token_order != VC_TOKENS_PATCH_MAJOR)
+        return fail(VC_ERR_INVALID_ARG, "vc_patch_im2col_split: bad token_order");
+    if (layout != VC_VIDEO_BTCHW && layout != VC_VIDEO_BCTHW)
+        return fail(VC_ERR_INVALID_ARG, "vc_patch_im2col_split: bad layout");
+    const int64_t totalv = B * T * C * H * (W / 8);
+    const unsigned nb = (unsigned)((totalv + 255) / 256);
+    if (elem == VC_ELEM_F16)
+        im2col_kernel<8, VC_ELEM_F16><<<nb, 256, 0, stream>>>(pixel_values, totalv, (int)T, (int)C, (int)H, (int)W, kt,
+                                                             kh, kw, token_order, layout, A, lda, K);
+    else
+        im2col_kernel<8><<<nb, 256, 0, stream>>>(pixel_values, totalv, (int)T, (int)C, (int)H, (int)W, kt, kh, kw,
+                                                token_order, layout, A, lda, K);
+    return check_launch("vc_patch_im2col_split");
 }
 
 int vc_patch_im2col(const float* pixel_values, int64_t B, int64_t T, int64_t C, int64_t H, int64_t W, int kt, int kh,

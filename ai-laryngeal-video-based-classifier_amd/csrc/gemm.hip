@@ -800,7 +800,7 @@ template <int EPI, int ET = VC_ELEM_BF16, int ABL = 0>
 __global__ void __launch_bounds__(512, 1)
 gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw, int nbm,
                int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
-               const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride, int64_t goff) {
+               const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride, int64_t goff, int nka) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int BM = 256, BN = 256, BKH = 32, NS = 4;
     constexpr int SLOT = (BM + BN) * 64;  // 32 KiB
@@ -825,9 +825,11 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     const uint16_t* wg0 = W + (n0 + arow) * ldw + swz64(arow, lane & 3) * 8;
     const uint16_t* wg1 = W + (n0 + arow + 16) * ldw + swz64(arow + 16, lane & 3) * 8;
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
+    // nka: K-halves of A; W may be longer (K <= 2 nka): A's columns wrap, so W = [W_hi | W_lo] against
+    // A gives A.W_hi + A.W_lo in one accumulation chain (vc_gemm_h16_wrap, the split-weight fp16 build)
     auto stage_a = [&](int u) __attribute__((always_inline)) {
         const uint32_t s = lds0 + (u & (NS - 1)) * SLOT + wave * 32 * 64;
-        const int ku = ABL == 1 ? (u & 3) : u;
+        const int ku = ABL == 1 ? (u & 3) : (u < nka ? u : u - nka);
         glds16(ag0 + ku * BKH, __builtin_amdgcn_readfirstlane(s));
         glds16(ag1 + ku * BKH, __builtin_amdgcn_readfirstlane(s + 16 * 64));
     };
@@ -1510,7 +1512,7 @@ static int launch_big(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t
 template <int E, int ET, int ABL = 0>
 static int launch_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
                      const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
-                     int64_t gs, int64_t go, hipStream_t stream) {
+                     int64_t gs, int64_t go, hipStream_t stream, int ka = 0) {
     constexpr int lds = 4 * 512 * 64;
     static bool attr_set = false;
     if (!attr_set) {
@@ -1520,7 +1522,8 @@ static int launch_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
         attr_set = true;
     }
     gemm_pp_kernel<E, ET, ABL><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out,
-                                                                           ldo, aux, ldaux, G, gs, go);
+                                                                           ldo, aux, ldaux, G, gs, go,
+                                                                           (ka > 0 ? ka : K) / 32);
     return check_launch("vc_gemm_bf16");
 }
 
@@ -1783,6 +1786,16 @@ extern "C" int vc_conv3d_gemm_bf16(const uint16_t* x, int64_t ldx, int64_t B, in
     }
     const int nbm = (int)((g.M + 127) / 128), nbn = (int)(N / 128);
     if ((int64_t)nbm * nbn > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: grid too large");
+    // fewer 128 x 128 tiles than CUs (ResNet3D stage 4: 49 x 4 at B = 4): 64 x 128 tiles, twice the workgroups
+    if (nbm * nbn < num_cus() && ldo % 8 == 0 &&
+        (epilogue == VC_EPI_BIAS_RELU_BF16 || epilogue == VC_EPI_BIAS_BF16)) {
+        const int nbm64 = (int)((g.M + 63) / 64);
+        if (epilogue == VC_EPI_BIAS_RELU_BF16)
+            return launch_conv<64, 128, 2, 4, VC_EPI_BIAS_RELU_BF16>(x, ldx, g, zero_row, Wt, ldw, nbm64, nbn, (int)K,
+                                                                      bias, out, ldo, auxf, ldaux, stream);
+        return launch_conv<64, 128, 2, 4, VC_EPI_BIAS_BF16>(x, ldx, g, zero_row, Wt, ldw, nbm64, nbn, (int)K, bias, out,
+                                                             ldo, auxf, ldaux, stream);
+    }
     switch (epilogue) {
         case VC_EPI_BIAS_BF16:
             if (ldo % 8) break;
@@ -1890,6 +1903,41 @@ extern "C" int vc_conv3d_stem_gemm_bf16(const uint16_t* xp, int64_t B, int64_t T
         return launch_conv<128, 128, 2, 4, VC_EPI_BIAS_BF16, 1>(xp, 0, g, zero_row, Wt, ldw, nbm, nbn, (int)K, bias,
                                                                  out, ldo, nullptr, 0, stream);
     return fail(VC_ERR_INVALID_ARG, "vc_conv3d_stem_gemm_bf16: epilogue must be bias / bias_relu");
+}
+
+// vc_gemm_h16 on the ping-pong kernel with A's columns wrapping at ka (ka <= K <= 2 ka): W = [W1 | W2]
+// ([N][K]) against A [M][ka] sums A.W1 + A.W2[:, :K - ka] in one fp32 MFMA chain.  With W1 / W2 the
+// fp16 high / low parts of fp32 weights this is the split-weight product (fp16 operands, ~fp32 weights).
+extern "C" int vc_gemm_h16_wrap(const uint16_t* A, int64_t lda, int64_t ka, const uint16_t* W, int64_t ldw, int64_t M,
+                                int64_t N, int64_t K, const float* bias, int epilogue, void* out, int64_t ldo,
+                                const float* aux, int64_t ldaux, int64_t G, int64_t group_stride, int64_t group_offset,
+                                int elem, hipStream_t stream) {
+    if (elem != VC_ELEM_BF16 && elem != VC_ELEM_F16) return fail(VC_ERR_INVALID_ARG, "vc_gemm_h16_wrap: bad elem");
+    if (!A || !W || !bias || !out) return fail(VC_ERR_INVALID_ARG, "vc_gemm_h16_wrap: null pointer");
+    if (M <= 0 || N <= 0 || M % 256 || N % 256 || ka <= 0 || ka % 64 || K % 64 || K < ka || K > 2 * ka || K < 128)
+        return fail(VC_ERR_INVALID_ARG, "vc_gemm_h16_wrap: need M, N % 256 == 0, ka, K % 64 == 0, ka <= K <= 2 ka");
+    if (lda % 8 || ldw % 8 || ldo % 8 || lda < ka || ldw < K || ldo < N)
+        return fail(VC_ERR_INVALID_ARG, "vc_gemm_h16_wrap: bad leading dimension");
+    if ((((uintptr_t)A) | ((uintptr_t)W) | ((uintptr_t)out) | ((uintptr_t)bias)) & 15)
+        return fail(VC_ERR_INVALID_ARG, "vc_gemm_h16_wrap: pointers must be 16-byte aligned");
+    if (epilogue == VC_EPI_EMBED_F32 && (!aux || G <= 0 || ldaux % 4))
+        return fail(VC_ERR_INVALID_ARG, "vc_gemm_h16_wrap: EMBED epilogue needs aux, G > 0");
+    const int nbm = (int)(M / 256), nbn = (int)(N / 256), k = (int)K, kai = (int)ka;
+#define VC_WRAP_CASE(E)                                                                                                \
+    case E:                                                                                                            \
+        return elem == VC_ELEM_F16 ? launch_pp<E, VC_ELEM_F16>(A, lda, W, ldw, nbm, nbn, k, bias, out, ldo, aux, ldaux, G, \
+                                                               group_stride, group_offset, stream, kai)               \
+                                   : launch_pp<E, VC_ELEM_BF16>(A, lda, W, ldw, nbm, nbn, k, bias, out, ldo, aux, ldaux, \
+                                                                G, group_stride, group_offset, stream, kai);
+    switch (epilogue) {
+        VC_WRAP_CASE(VC_EPI_BIAS_BF16)
+        VC_WRAP_CASE(VC_EPI_BIAS_GELU_TANH)
+        VC_WRAP_CASE(VC_EPI_BIAS_GELU_ERF)
+        VC_WRAP_CASE(VC_EPI_BIAS_RESID_F32)
+        VC_WRAP_CASE(VC_EPI_EMBED_F32)
+    }
+#undef VC_WRAP_CASE
+    return fail(VC_ERR_INVALID_ARG, "vc_gemm_h16_wrap: epilogue must be one of the inference epilogues 0-4");
 }
 
 // the tile config vc_gemm_bf16 / vc_gemm_h16 run with cfg = -1 (host only: no launch, no GPU)

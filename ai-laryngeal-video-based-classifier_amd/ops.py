@@ -229,6 +229,49 @@ def _gemm(a, w, bias, epilogue, out, aux, group, group_stride, group_offset, m, 
     return out
 
 
+def gemm_wrap(a: torch.Tensor, ka: int, w: torch.Tensor, bias: torch.Tensor, epilogue: str, out: torch.Tensor,
+              aux: torch.Tensor | None = None, group: int = 0, group_stride: int = 0, group_offset: int = 0,
+              m: int | None = None, flop: float | None = None, op: str = "gemm") -> torch.Tensor:
+    """vc_gemm_h16_wrap: out (+)= epilogue(A . W^T + bias) with A = a[:m, :ka] wrapping along K: W [N, K]
+    with ka <= K <= 2 ka is [W1 | W2] and the product A.W1 + A.W2 (the split-operand fp16 build)."""
+    _dev(a, w, bias, out)
+    M = a.shape[0] if m is None else m
+    N, K = w.shape
+    _need(a.dtype in H16 and w.dtype == a.dtype and bias.dtype == torch.float32 and a.stride(1) == 1 and
+          w.stride(1) == 1 and a.shape[1] >= ka, "gemm_wrap operands")
+    e = EPI[epilogue]
+    _need(e <= 4, "gemm_wrap: inference epilogues only")
+    if e == 4:
+        _need(aux is not None and aux.dtype == torch.float32 and group > 0, "gemm_wrap embed aux")
+    else:
+        _need(out.shape[0] >= M, "gemm_wrap out rows")
+    rec = _REC[0]
+    e0 = rec.begin() if rec is not None else None
+    _lib.call("vc_gemm_h16_wrap", _p(a), a.stride(0), ka, _p(w), w.stride(0), M, N, K, _p(bias), e, _p(out),
+              out.stride(0), _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0, group,
+              group_stride, group_offset, ELEM_F16 if a.dtype == torch.float16 else 0, _stream(a))
+    if rec is not None:
+        rec.end(e0, f"gemm_pp_kernel<{e}, {1 if a.dtype == torch.float16 else 0}, 0>", op,
+                2.0 * M * N * K if flop is None else flop, "flop")
+    return out
+
+
+def patch_im2col_split(pix: torch.Tensor, tubelet, out: torch.Tensor, order: str = "time_major",
+                       layout: str = "btchw") -> torch.Tensor:
+    """[A_hi | A_lo] im2col (vc_patch_im2col_split_h16): out 16-bit [>= tokens, >= 2 K]."""
+    _dev(pix, out)
+    if layout == "btchw":
+        B, T, C, H, W = pix.shape
+    else:
+        B, C, T, H, W = pix.shape
+    kt, kh, kw = tubelet
+    _need(pix.dtype == torch.float32 and pix.is_contiguous() and out.dtype in H16 and out.stride(1) == 1 and
+          out.shape[1] >= 2 * C * kt * kh * kw, "patch_im2col_split")
+    _lib.call("vc_patch_im2col_split_h16", _p(pix), B, T, C, H, W, kt, kh, kw, TOKEN_ORDER[order], VIDEO_LAYOUT[layout],
+              ELEM_F16 if out.dtype == torch.float16 else 0, _p(out), out.stride(0), _stream(pix))
+    return out
+
+
 # tile rows, tile cols and workgroups per CU of the GEMM configs gemm_rounds() composes
 # (csrc/gemm.hip kCfgs; cfg 4 is the persistent 256x256 kernel, one workgroup per CU)
 _GEMM_TILES = {1: (128, 128, 1), 4: (256, 256, 1), 5: (128, 128, 2), 7: (64, 128, 2)}
@@ -544,7 +587,10 @@ def conv3d_gemm(x: torch.Tensor, B: int, grid, C: int, kernel, stride, pad, w: t
               ctypes.addressof(p), _p(_ZERO_ROW[key]), _p(w), w.stride(0), N, _p(bias), e, _p(out), out.stride(0),
               _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0, _stream(x))
     if rec is not None:
-        tile = "128, 128, 2, 4" if rt == 128 else "256, 64, 8, 1"
+        tile = "256, 64, 8, 1"
+        if rt == 128:  # 64 x 128 tiles when the 128 x 128 grid has fewer tiles than CUs (csrc/gemm.hip)
+            small = ((M + 127) // 128) * (N // 128) < _num_cus(x.device) and e in (0, 6)
+            tile = "64, 128, 2, 4" if small else "128, 128, 2, 4"
         rec.end(e0, f"conv_gemm_kernel<{tile}, {e}, 2, 0>", op, 2.0 * M * N * kvol * C if flop is None else flop, "flop")
     return out
 

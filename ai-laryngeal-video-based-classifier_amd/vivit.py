@@ -135,6 +135,12 @@ class VivitForVideoClassification(torch.nn.Module):
         # torch.float16 (same kernels and MFMA rate, logits ~6x closer to the fp32 reference;
         # DESIGN.md §6).  The train step (vivit_train.py) is bf16 either way.
         self.compute_dtype = torch.bfloat16
+        # fp16 build only: the patch embedding and the first `precise_layers` layers' GEMMs take split
+        # operands -- weights as fp16 high + low parts (and the pixels too in the embedding) through
+        # vc_gemm_h16_wrap, A.W_hi + A.W_lo in one fp32 chain.  The fp16 build's logit error is set by
+        # the weight rounding of the first layers (tools/r04/w_probe.py: all weights fp32 3.8e-4, the
+        # embedding + layer 0 4.3e-4, vs 1.25e-3 all fp16 on the bench's 8 clips).
+        self.precise_layers = 0
 
     # ---- state dict in HF naming ---------------------------------------------------
     def hf_state_dict(self):
@@ -255,16 +261,27 @@ class VivitForVideoClassification(torch.nn.Module):
         bf = self.compute_dtype
         if bf not in (torch.bfloat16, torch.float16):
             raise ValueError(f"compute_dtype must be torch.bfloat16 or torch.float16, not {bf}")
+        npre = self.precise_layers if bf == torch.float16 else 0
         if (self._packed is not None and self._packed["device"] == device and self._packed["version"] == ver
-                and self._packed["dtype"] == bf):
+                and self._packed["dtype"] == bf and self._packed["precise"] == npre):
             return self._packed
         c = self.config
         f32 = torch.float32
         P = lambda n: self.P(n).detach().to(device)  # noqa: E731
         D = c.hidden_size
         kt, kh, kw = c.tubelet_size
-        pk = {"device": device, "version": ver, "dtype": bf}
+        pk = {"device": device, "version": ver, "dtype": bf, "precise": npre}
+
+        def split(w, emb=False):
+            # [W_hi | W_lo] (embedding: [W_hi | W_hi | W_lo] against [A_hi | A_lo] with A wrapping)
+            w = w.float()
+            hi = w.to(torch.float16)
+            lo = (w - hi.float()).to(torch.float16)
+            return torch.cat([hi, hi, lo] if emb else [hi, lo], dim=1).contiguous()
+
         pk["w_emb"] = P("vivit.embeddings.patch_embeddings.projection.weight").reshape(D, -1).to(bf).contiguous()
+        if npre > 0:
+            pk["w_emb_split"] = split(P("vivit.embeddings.patch_embeddings.projection.weight").reshape(D, -1), emb=True)
         pk["b_emb"] = P("vivit.embeddings.patch_embeddings.projection.bias").to(f32).contiguous()
         pk["pos"] = P("vivit.embeddings.position_embeddings").reshape(-1, D).to(f32).contiguous()
         pk["cls"] = P("vivit.embeddings.cls_token").reshape(D).to(f32).contiguous()
@@ -289,6 +306,12 @@ class VivitForVideoClassification(torch.nn.Module):
             L["b_1"] = P(p + "mlp.fc1.bias").contiguous()
             L["w_2"] = P(p + "mlp.fc2.weight").to(bf).contiguous()
             L["b_2"] = P(p + "mlp.fc2.bias").contiguous()
+            if i < npre:
+                L["split"] = dict(
+                    w_qkv=split(torch.cat([P(p + "attention.q_proj.weight") * qs, P(p + "attention.k_proj.weight"),
+                                           P(p + "attention.v_proj.weight")])),
+                    w_o=split(P(p + "attention.o_proj.weight")), w_1=split(P(p + "mlp.fc1.weight")),
+                    w_2=split(P(p + "mlp.fc2.weight")))
             layers.append(L)
         pk["layers"] = layers
         pk["lnf_g"] = P("vivit.layernorm.weight").contiguous()
@@ -308,7 +331,7 @@ class VivitForVideoClassification(torch.nn.Module):
         return npatch, S, Mpad, Memb
 
     def _workspace(self, B, device, part: int = 0):
-        key = (B, str(device), part, self.compute_dtype)
+        key = (B, str(device), part, self.compute_dtype, self.precise_layers > 0)
         if key in self._ws:
             ws = self._ws[key]
             if not any(w is ws for w in self._ws_used):
@@ -324,6 +347,8 @@ class VivitForVideoClassification(torch.nn.Module):
         z = lambda *s, dt=bf: torch.zeros(s, dtype=dt, device=device)  # noqa: E731
         ws = dict(A_emb=z(Memb, c.num_channels * kt * kh * kw), X=z(Mpad, D, dt=torch.float32), Y=z(Mpad, D),
                   QKV=z(Mpad, 3 * D), O=z(Mpad, D), Hd=z(Mpad, I), logits=z(B, c.num_labels, dt=torch.float32))
+        if self.precise_layers > 0 and bf == torch.float16 and (B * npatch) % 256 == 0:
+            ws["A_emb_split"] = z(B * npatch, 2 * c.num_channels * kt * kh * kw)
         self._ws[key] = ws
         self._ws_used.append(ws)
         return ws
@@ -366,7 +391,7 @@ class VivitForVideoClassification(torch.nn.Module):
         if self.graph_replay and self.kernel_events is None and not torch.cuda.is_current_stream_capturing():
             key = (pix.data_ptr(), tuple(pix.shape), tuple(pix.stride()), pix.dtype, self.concurrent_streams,
                    self.compute_dtype, self._weights_version(), tuple(sorted(self.gemm_cfg.items())), self.rows,
-                   self.round_split)
+                   self.round_split, self.precise_layers)
             return self._graphs.run(key, pix, self._forward_eager, keep=lambda: (self._packed, tuple(self._ws_used)))
         return self._forward_eager(pix)
 
@@ -435,10 +460,18 @@ class VivitForVideoClassification(torch.nn.Module):
         T_, H_ = c.num_frames, c.image_size
         ln_bytes = M * D * (4 + 2)
         tm = ops.timed
-        run("im2col", tm, "im2col_kernel", "im2col", B * (T_ * c.num_channels * H_ * H_ * 4 + npatch * Kemb * 2), "byte",
-            ops.tubelet_im2col, pix, c.tubelet_size, ws["A_emb"])
-        run("embed", ops.gemm, ws["A_emb"], pk["w_emb"], pk["b_emb"], "embed_f32", X, aux=pk["pos"][1:],
-            group=npatch, group_stride=S, group_offset=1, m=Memb, flop=2.0 * B * npatch * D * Kemb, op="embed")
+        if "A_emb_split" in ws and "w_emb_split" in pk:
+            # split operands: [A_hi | A_lo] against [W_hi | W_hi | W_lo] (A_hi W_hi + A_lo W_hi + A_hi W_lo)
+            run("im2col", tm, "im2col_kernel", "im2col", B * (T_ * c.num_channels * H_ * H_ * 4 + npatch * Kemb * 4),
+                "byte", ops.patch_im2col_split, pix, c.tubelet_size, ws["A_emb_split"])
+            run("embed", ops.gemm_wrap, ws["A_emb_split"], 2 * Kemb, pk["w_emb_split"], pk["b_emb"], "embed_f32", X,
+                aux=pk["pos"][1:], group=npatch, group_stride=S, group_offset=1, m=B * npatch,
+                flop=2.0 * B * npatch * D * Kemb, op="embed")
+        else:
+            run("im2col", tm, "im2col_kernel", "im2col", B * (T_ * c.num_channels * H_ * H_ * 4 + npatch * Kemb * 2),
+                "byte", ops.tubelet_im2col, pix, c.tubelet_size, ws["A_emb"])
+            run("embed", ops.gemm, ws["A_emb"], pk["w_emb"], pk["b_emb"], "embed_f32", X, aux=pk["pos"][1:],
+                group=npatch, group_stride=S, group_offset=1, m=Memb, flop=2.0 * B * npatch * D * Kemb, op="embed")
         ops.cls_init(pk["cls"], pk["pos"], X, B, S)
         act = "bias_gelu_tanh" if c.hidden_act in ("gelu_fast", "gelu_pytorch_tanh", "gelu_new") else "bias_gelu_erf"
         scale = 1.0 / math.sqrt(D // c.num_attention_heads)
@@ -464,19 +497,32 @@ class VivitForVideoClassification(torch.nn.Module):
         Hn = c.num_attention_heads
         attn_flop = 4.0 * S * S * (D // Hn) * Hn * B
         for L in pk["layers"]:
+            sp = L.get("split")  # the split-operand fp16 layers (precise_layers): A wraps against [W_hi | W_lo]
             run("layernorm", tm, "layernorm_kernel", "layernorm", ln_bytes, "byte", ops.layernorm, X, L["ln1_g"],
                 L["ln1_b"], eps, Y, m=m_ln)
-            run("qkv", qkv_gemm, Y, L["w_qkv"], L["b_qkv"], "bias", QKV, m=m_qkv, cfg=c_qkv, flop=2.0 * M * 3 * D * D,
-                op="qkv")
+            if sp is not None:
+                run("qkv", ops.gemm_wrap, Y, D, sp["w_qkv"], L["b_qkv"], "bias", QKV, flop=2.0 * M * 3 * D * D, op="qkv")
+            else:
+                run("qkv", qkv_gemm, Y, L["w_qkv"], L["b_qkv"], "bias", QKV, m=m_qkv, cfg=c_qkv,
+                    flop=2.0 * M * 3 * D * D, op="qkv")
             run("attention", tm, "attn_fwd_d64_kernel", "attention", attn_flop, "flop", ops.attention, QKV, B, S, Hn,
                 scale, O, q_prescaled=True)
-            run("o_proj", ops.gemm, O, L["w_o"], L["b_o"], "bias_resid_f32", X, m=m_o, cfg=c_o, flop=2.0 * M * D * D,
-                op="o_proj")
+            if sp is not None:
+                run("o_proj", ops.gemm_wrap, O, D, sp["w_o"], L["b_o"], "bias_resid_f32", X, flop=2.0 * M * D * D,
+                    op="o_proj")
+            else:
+                run("o_proj", ops.gemm, O, L["w_o"], L["b_o"], "bias_resid_f32", X, m=m_o, cfg=c_o,
+                    flop=2.0 * M * D * D, op="o_proj")
             run("layernorm", tm, "layernorm_kernel", "layernorm", ln_bytes, "byte", ops.layernorm, X, L["ln2_g"],
                 L["ln2_b"], eps, Y, m=m_ln)
-            run("fc1", ops.gemm, Y, L["w_1"], L["b_1"], act, Hd, m=m_1, cfg=c_1, flop=2.0 * M * I * D, op="fc1")
-            run("fc2", fc2_gemm, Hd, L["w_2"], L["b_2"], "bias_resid_f32", X, m=m_2, cfg=c_2, flop=2.0 * M * D * I,
-                op="fc2")
+            if sp is not None:
+                run("fc1", ops.gemm_wrap, Y, D, sp["w_1"], L["b_1"], act, Hd, flop=2.0 * M * I * D, op="fc1")
+                run("fc2", ops.gemm_wrap, Hd, I, sp["w_2"], L["b_2"], "bias_resid_f32", X, flop=2.0 * M * D * I,
+                    op="fc2")
+            else:
+                run("fc1", ops.gemm, Y, L["w_1"], L["b_1"], act, Hd, m=m_1, cfg=c_1, flop=2.0 * M * I * D, op="fc1")
+                run("fc2", fc2_gemm, Hd, L["w_2"], L["b_2"], "bias_resid_f32", X, m=m_2, cfg=c_2,
+                    flop=2.0 * M * D * I, op="fc2")
         return ops.cls_head(X, B, S, pk["lnf_g"], pk["lnf_b"], eps, pk["w_cls"], pk["b_cls"],
                             out=ws["logits"] if out is None else out)
 

@@ -668,6 +668,13 @@ def main():
     evs16 = []
     timed(1, evs16)
     attn_ms16 = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs16]))
+    # ... and with split fp16 operands in the patch embedding and layer 0 (precise_layers = 1: the
+    # weights of the first layers set the fp16 build's logit error)
+    model.precise_layers = 1
+    model.graph_replay = graphed
+    dt16p = timed(a.streams)
+    model.graph_replay = False
+    model.precise_layers = 0
     model.compute_dtype = torch.bfloat16
 
     model.concurrent_streams = 1
@@ -684,7 +691,7 @@ def main():
     out = None
     if rank == 0:
         cpu = None
-        logit_err = logit_err16 = None
+        logit_err = logit_err16 = logit_err16p = None
         traffic, traffic_src = measured_traffic(ATTN_KERNEL, "fwd")
         pmc, pmc_src = measured_pmc(ATTN_KERNEL, "fwd")
         mfma_busy, valu_per_mfma = pmc_rates(pmc)
@@ -692,17 +699,20 @@ def main():
             shape_cfg = dict(cfg.as_shape_cfg(), num_attention_heads=cfg.num_attention_heads,
                              layer_norm_eps=cfg.layer_norm_eps)
 
-            def gpu_logits(dtype):
+            def gpu_logits(dtype, precise=0):
                 def fn(p):
                     model.compute_dtype = dtype
+                    model.precise_layers = precise
                     lg = model.forward_logits(torch.from_numpy(p).to(dev)).cpu().numpy().copy()
                     model.compute_dtype = torch.bfloat16
+                    model.precise_layers = 0
                     return lg
                 return fn
 
             cpu, errs = cpu_baseline(shape_cfg, a.cpu_clips, a.batch,
-                                     {"bf16": gpu_logits(torch.bfloat16), "fp16": gpu_logits(torch.float16)})
-            logit_err, logit_err16 = errs["bf16"], errs["fp16"]
+                                     {"bf16": gpu_logits(torch.bfloat16), "fp16": gpu_logits(torch.float16),
+                                      "fp16_precise": gpu_logits(torch.float16, 1)})
+            logit_err, logit_err16, logit_err16p = errs["bf16"], errs["fp16"], errs["fp16_precise"]
             cpu["lstm_cfg1"] = cpu_lstm_cfg1()
         out = {
             "metric": "clips/sec fwd ViViT-B 32x224^2 bf16",
@@ -742,6 +752,10 @@ def main():
                      "attn_frac": round(ATTN_GFLOP_PER_CLIP_LAYER * launch_clips / (attn_ms16 * 1e-3) / 1e3
                                         / PEAK_BF16_TFLOPS, 4),
                      "note": "same forward with fp16 MFMA operands (VC_ELEM_F16; fp16 dense peak = bf16's)"},
+            "fp16_precise": {"value": round(clips / dt16p, 2), "ms_per_step": round(dt16p / a.steps * 1e3, 3),
+                             "logit_max_abs_err": logit_err16p,
+                             "note": "fp16 build with split operands (fp16 high + low parts: vc_gemm_h16_wrap) in the "
+                                     "patch embedding and layer 0's GEMMs (model.precise_layers = 1)"},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

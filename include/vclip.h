@@ -180,6 +180,22 @@ int vc_gemm_h16(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw,
                 void* out, int64_t ldo, const float* aux, int64_t ldaux,
                 int64_t G, int64_t group_stride, int64_t group_offset, int elem, int cfg, hipStream_t stream);
 
+/* vc_gemm_h16 on the 256x256 ping-pong kernel with A's columns wrapping at ka (ka % 64 == 0,
+ * ka <= K <= 2 ka, M % 256 == N % 256 == 0, epilogues 0-4): W = [W1 | W2] against A [M][ka] sums
+ * A.W1 + A.W2 in one fp32 accumulation chain.  With W1 / W2 the high / low 16-bit parts of fp32
+ * weights (and, for the patch embedding, A = [A_hi | A_lo] from vc_patch_im2col_split_h16 against
+ * W = [W_hi | W_hi | W_lo]) this is the split-operand product of the fp16 build's first layers
+ * (VivitForVideoClassification.precise_layers). */
+int vc_gemm_h16_wrap(const uint16_t* A, int64_t lda, int64_t ka, const uint16_t* W, int64_t ldw, int64_t M,
+                     int64_t N, int64_t K, const float* bias, int epilogue, void* out, int64_t ldo, const float* aux,
+                     int64_t ldaux, int64_t G, int64_t group_stride, int64_t group_offset, int elem,
+                     hipStream_t stream);
+/* vc_patch_im2col_h16 writing [A_hi | A_lo] (2K columns, K = C kt kh kw; 8-wide patches): the 16-bit
+ * pixel values and their rounding residuals. */
+int vc_patch_im2col_split_h16(const float* pixel_values, int64_t B, int64_t T, int64_t C, int64_t H, int64_t W,
+                              int kt, int kh, int kw, int token_order, int layout, int elem, uint16_t* A, int64_t lda,
+                              hipStream_t stream);
+
 /* vc_layernorm_f32_bf16 with the output type as an argument (same widths and kernels). */
 int vc_layernorm_f32_h16(const float* x, int64_t ldx, int64_t M, int64_t D, const float* gamma, const float* beta,
                          float eps, int elem, uint16_t* y, int64_t ldy, hipStream_t stream);

@@ -190,3 +190,48 @@ def test_vivit_tiny_fp16_batch_invariant():
     assert np.abs(lg.cpu().numpy() - g["logits"]).max() < 1e-3
     one = m(pixel_values=pix[:1].contiguous()).logits
     assert torch.equal(lg[:1], one)
+
+
+def test_gemm_wrap_split_weights():
+    """vc_gemm_h16_wrap with W = [W_hi | W_lo] (fp16 high / low parts of fp32 weights) against an
+    fp16 A: the product is A.W to fp32 weight precision -- 10x closer to the fp32-weight reference
+    than the plain fp16 GEMM (whose error is the weight rounding)."""
+    from vclip_amd import ops as O
+    g = torch.Generator().manual_seed(11)
+    M, N, K = 512, 256, 384
+    a = (torch.randn(M, K, generator=g)).to(H)
+    w = torch.randn(N, K, generator=g) * 0.05
+    b = torch.randn(N, generator=g) * 0.1
+    ref = a.float() @ w.T + b
+    hi = w.to(H)
+    lo = (w - hi.float()).to(H)
+    out = torch.zeros(M, N, device=DEV)
+    O.gemm_wrap(a.cuda(), K, torch.cat([hi, lo], 1).cuda(), b.cuda(), "bias_resid_f32", out)
+    err_split = (out.cpu() - ref).abs().max().item()
+    out2 = torch.zeros(M, N, device=DEV)
+    O.gemm(a.cuda(), hi.cuda(), b.cuda(), "bias_resid_f32", out2)
+    err_plain = (out2.cpu() - ref).abs().max().item()
+    assert err_split < 2e-4, err_split
+    assert err_split < 0.1 * err_plain, (err_split, err_plain)
+
+
+def test_vivit_b_precise_layers_fp16():
+    """fp16 build with split operands in the embedding and layer 0 (precise_layers = 1) on 4 clips of the
+    bench's workload: logits within north_star's 1e-3 of the fp32 oracle (run on the GPU in fp32), and
+    closer than the plain fp16 build."""
+    from oracle.vivit_ref import vivit_forward
+    from vclip_amd.weights import make_synthetic_clips, make_vivit_weights
+    cfg = dict(image_size=224, num_frames=32, tubelet_size=[2, 16, 16], num_channels=3, hidden_size=768,
+               num_hidden_layers=12, num_attention_heads=12, intermediate_size=3072, hidden_act="gelu_fast",
+               layer_norm_eps=1e-6, qkv_bias=True)
+    pix = torch.from_numpy(make_synthetic_clips(4, 32, 224, seed=1)).cuda()
+    sd = make_vivit_weights(cfg, seed=0)
+    with torch.no_grad():
+        ref = vivit_forward({k: torch.from_numpy(v).cuda() for k, v in sd.items()}, cfg, pix).cpu().numpy()
+    m = _vivit(cfg, H)
+    plain = np.abs(m(pixel_values=pix).logits.cpu().numpy() - ref).max()
+    m.precise_layers = 1
+    prec = np.abs(m(pixel_values=pix).logits.cpu().numpy() - ref).max()
+    print(f"logit max|err| fp16 {plain:.3e}, fp16 + split embedding / layer 0 {prec:.3e}")
+    assert prec <= 1e-3, prec
+    assert prec < plain, (prec, plain)

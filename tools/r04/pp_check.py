@@ -19,6 +19,7 @@ ap.add_argument("--cfgs", default="8")
 ap.add_argument("--only", default="")
 ap.add_argument("--ksweep", action="store_true", help="q|k|v-shaped cases at K = 768 .. 6144 (per-tile overhead fit)")
 ap.add_argument("--swin", action="store_true", help="Video Swin-T B=4 stage-1/2 GEMM shapes (channels padded to 128)")
+ap.add_argument("--r3d", action="store_true", help="ResNet3D-50 B=4 conv_a / conv_b GEMM shapes (implicit-conv proxies)")
 a = ap.parse_args()
 new_cfgs = [int(c) for c in a.cfgs.split(",")]
 
@@ -34,6 +35,11 @@ if a.swin:
         q = (3 * C + 127) // 128 * 128
         CASES += [(f"s{st}_qkv", M, q, Cp, "bias"), (f"s{st}_proj", M, Cp, Cp, "bias_resid_f32"),
                   (f"s{st}_fc1", M, 4 * C, Cp, "bias_gelu_erf"), (f"s{st}_fc2", M, Cp, 4 * C, "bias_resid_f32")]
+if a.r3d:
+    CASES = [("r3d_s2b", 100352, 128, 1152, "bias_relu"), ("r3d_s3a", 25088, 256, 1536, "bias_relu"),
+             ("r3d_s3b", 25088, 256, 2304, "bias_relu"), ("r3d_s4a", 6400, 512, 3072, "bias_relu"),
+             ("r3d_s4b", 6400, 512, 4608, "bias_relu"), ("r3d_s1c", 401408, 256, 64, "bias_resid_relu"),
+             ("r3d_s2c", 100352, 512, 128, "bias_resid_relu")]
 if a.ksweep:
     CASES = [(f"ks_K{K}", 12800, 2304, K, "bias") for K in (768, 1536, 3072, 6144)]
 if a.only:
@@ -67,25 +73,26 @@ for name, M, N, K, epi in CASES:
                      (c not in (4, 10) or bf16_out)]
     # bit-identity: every config from the same initial out (the residual epilogue accumulates)
     init = (torch.randn(M, N, device="cuda", generator=g) if out.dtype == torch.float32 else out.clone())
+    aux = (torch.randn(M, N, device="cuda", generator=g) * 0.5).bfloat16() if epi == "bias_resid_relu" else None
     ref = None
     ok = {}
     for c in cfgs:
         out.copy_(init)
-        ops.gemm(A, W, b, epi, out, cfg=c)
+        ops.gemm(A, W, b, epi, out, aux=aux, cfg=c)
         torch.cuda.synchronize()
         if ref is None:
             ref = out.clone()
         ok[c] = bool(torch.equal(out, ref))
     times = {c: [] for c in cfgs}
     for c in cfgs:
-        ops.gemm(A, W, b, epi, out, cfg=c)
+        ops.gemm(A, W, b, epi, out, aux=aux, cfg=c)
     torch.cuda.synchronize()
     for r in range(a.rounds):
         for c in cfgs:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(a.iters):
-                ops.gemm(A, W, b, epi, out, cfg=c)
+                ops.gemm(A, W, b, epi, out, aux=aux, cfg=c)
             e1.record()
             e1.synchronize()
             times[c].append(e0.elapsed_time(e1) / a.iters)
@@ -96,5 +103,5 @@ for name, M, N, K, epi in CASES:
         line[f"cfg{c}"] = {"us_med": round(med * 1e3, 1), "us_min": round(ts[0] * 1e3, 1),
                            "tflops": round(2.0 * M * N * K / (med * 1e-3) / 1e12, 1), "bit_identical": ok[c]}
     print(json.dumps(line), flush=True)
-    del A, W, b, out, init, ref
+    del A, W, b, out, init, ref, aux
     torch.cuda.empty_cache()
