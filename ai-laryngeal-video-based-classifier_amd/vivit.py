@@ -133,13 +133,13 @@ class VivitForVideoClassification(torch.nn.Module):
         self.round_split = False
         # 16-bit operand type of the inference forward: bf16 (the benchmarked configuration) or
         # torch.float16 (same kernels and MFMA rate, logits ~6x closer to the fp32 reference;
-        # DESIGN.md §6).  The train step (vivit_train.py) is bf16 either way.
+        # DESIGN.md §5.5).  The train step (vivit_train.py) is bf16 either way.
         self.compute_dtype = torch.bfloat16
         # fp16 build only: the patch embedding and the first `precise_layers` layers' GEMMs take split
         # operands -- weights as fp16 high + low parts (and the pixels too in the embedding) through
         # vc_gemm_h16_wrap, A.W_hi + A.W_lo in one fp32 chain.  The fp16 build's logit error is set by
         # the weight rounding of the first layers (tools/r04/w_probe.py: all weights fp32 3.8e-4, the
-        # embedding + layer 0 4.3e-4, vs 1.25e-3 all fp16 on the bench's 8 clips; DESIGN.md §5c).
+        # embedding + layer 0 4.3e-4, vs 1.25e-3 all fp16 on the bench's 8 clips; DESIGN.md §5.5).
         self.precise_layers = 0
 
     # ---- state dict in HF naming ---------------------------------------------------

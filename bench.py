@@ -669,7 +669,7 @@ def main():
     timed(1, evs16)
     attn_ms16 = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs16]))
     # ... and with split fp16 operands in the patch embedding and layer 0 (precise_layers = 1: the
-    # weights of the first layers set the fp16 build's logit error, DESIGN.md §5c)
+    # weights of the first layers set the fp16 build's logit error, DESIGN.md §5.5)
     model.precise_layers = 1
     model.graph_replay = graphed
     dt16p = timed(a.streams)
