@@ -333,6 +333,19 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
                                                               (m0 + wm * TM + i * 16 + c16) * ldo + n0 + wn * TN +
                                                               j * 16 + 4 * q);
     }
+    // the bf16 residual of the ResNet3D conv_c epilogue likewise: at K = 64 .. 512 (one to eight
+    // k-tiles) its fetch in the epilogue was a second serialized round trip per tile
+    constexpr bool APRE = EPI == VC_EPI_BIAS_RESID_RELU_BF16;
+    uint2 xaux[APRE ? MI : 1][APRE ? NI : 1];
+    if constexpr (APRE) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j)
+                xaux[i][j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(aux) +
+                                                             (m0 + wm * TM + i * 16 + c16) * ldaux + n0 + wn * TN +
+                                                             j * 16 + 4 * q);
+    }
     if (ST == 3 && nk > 1) {
         stage(1, 1);
         wait_vm<LPT>();
@@ -387,6 +400,23 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
                 x.z += acc[i][j][2] + bb.z;
                 x.w += acc[i][j][3] + bb.w;
                 *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + m * ldo + n) = x;
+            }
+    } else if constexpr (APRE) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j) {
+                const int64_t m = m0 + wm * TM + i * 16 + c16, n = n0 + wn * TN + j * 16 + 4 * q;
+                const float4 bb = *reinterpret_cast<const float4*>(bias + n);
+                const uint2 rr = xaux[i][j];
+                const float v0 = fmaxf(acc[i][j][0] + bb.x + bf2f((unsigned short)(rr.x & 0xffff)), 0.f);
+                const float v1 = fmaxf(acc[i][j][1] + bb.y + bf2f((unsigned short)(rr.x >> 16)), 0.f);
+                const float v2 = fmaxf(acc[i][j][2] + bb.z + bf2f((unsigned short)(rr.y & 0xffff)), 0.f);
+                const float v3 = fmaxf(acc[i][j][3] + bb.w + bf2f((unsigned short)(rr.y >> 16)), 0.f);
+                uint2 p;
+                p.x = pack2<ET>(v0, v1);
+                p.y = pack2<ET>(v2, v3);
+                *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + m * ldo + n) = p;
             }
     } else {
         store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bias, out, ldo, aux, ldaux, G, gstride,

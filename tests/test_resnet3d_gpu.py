@@ -207,3 +207,22 @@ def test_conv3d_stem_implicit_gemm_bit_exact(T, H, W):
     ref = torch.nn.functional.pad(x, (3, 3, 3, 3, 1, 1)).permute(0, 2, 3, 4, 1)
     ref = torch.cat([ref, torch.zeros(*ref.shape[:-1], 1)], -1).bfloat16()
     assert torch.equal(xp.view(ref.shape).cpu(), ref)
+
+
+@pytest.mark.parametrize("K,cfg", [(64, 5), (128, 5), (512, 5), (512, 8)])
+def test_gemm_bias_resid_relu_epilogue(K, cfg):
+    """conv_c's epilogue (relu(A.W^T + bias + residual), bf16 residual prefetched before the k loop in
+    the 128x128 kernel) against an fp32 torch reference of the same bf16 operands: <= one bf16 ulp of
+    the output plus f32 summation-order noise."""
+    O = ops()
+    g = torch.Generator().manual_seed(K + cfg)
+    M, N = 1024, 256
+    a = (torch.randn(M, K, generator=g) * 0.5).bfloat16()
+    w = (torch.randn(N, K, generator=g) * 0.05).bfloat16()
+    b = torch.randn(N, generator=g) * 0.1
+    r = torch.randn(M, N, generator=g).bfloat16()
+    want = torch.relu(a.float() @ w.float().T + b + r.float())
+    out = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    O.gemm(a.to(DEV), w.to(DEV), b.to(DEV), "bias_resid_relu", out, aux=r.to(DEV), cfg=cfg)
+    got = out.float().cpu()
+    assert torch.allclose(got, want, rtol=2 ** -7, atol=1e-3), float((got - want).abs().max())

@@ -13,7 +13,7 @@ timeout -k 10 200 python -u tools/r04/pp_check.py --ksweep --rounds 5 --iters 10
 cut -c1-500 $OUT/ksweep.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u tools/r04/pp_check.py --swin --rounds 5 --iters 10 --cfgs 5,7,8,9 > $OUT/swin_gemm.log 2>&1; rc=$?
 cut -c1-600 $OUT/swin_gemm.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u tools/r04/pp_check.py --r3d --rounds 5 --iters 10 --cfgs 5,7,8,9,10 > $OUT/r3d_gemm.log 2>&1; rc=$?
+timeout -k 10 300 python -u tools/r04/pp_check.py --r3d --rounds 5 --iters 10 --cfgs 1,5,7,8,9,10 > $OUT/r3d_gemm.log 2>&1; rc=$?
 cut -c1-600 $OUT/r3d_gemm.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace_train -o run --output-format csv -- \
   python3 bench.py --mode train --steps 10 --warmup 3 --no-cpu-baseline > $OUT/trace_train.log 2>&1

@@ -68,7 +68,7 @@ for name, M, N, K, epi in CASES:
     TILE = {1: (128, 128), 3: (256, 256), 4: (256, 256), 5: (128, 128), 7: (64, 128), 8: (256, 256), 9: (256, 128),
             10: (256, 256), 11: (256, 256), 12: (256, 256), 13: (256, 256)}
     ok_shape = lambda c: (c in TILE and M % TILE[c][0] == 0 and N % TILE[c][1] == 0 and K % 64 == 0 and  # noqa: E731
-                          (K >= 192 if c in (4, 10) else K >= 128 if c in (8, 9, 11, 12, 13) else True))
+                          (K >= 192 if c in (4, 10) else K >= 128 if c in (8, 9, 11, 12, 13) else True))  # cfg 1: 128x128, 3-slot ring
     cfgs = [base] + [c for c in new_cfgs if c != base and ok_shape(c) and (c not in (11, 12, 13) or epi == "bias") and
                      (c not in (4, 10) or bf16_out)]
     # bit-identity: every config from the same initial out (the residual epilogue accumulates)
