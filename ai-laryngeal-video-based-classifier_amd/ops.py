@@ -127,6 +127,24 @@ class OpRecorder:
                       "unit": "TFLOP/s" if a["unit"] == "flop" else "GB/s", "ops": sorted(a["ops"])}
         return dict(sorted(out.items(), key=lambda kv: -kv[1]["share_of_step"]))
 
+    def summary_ops(self, n_steps: int, step_ms: float):
+        """per op label (e.g. ResNet3D's "conv_b.s3": conv_b of res stage 3): launches per step, ms per
+        step, share of the step, achieved rate, the kernels that ran it; sorted by share"""
+        agg = {}
+        for kernel, op, e0, e1, work, unit in self.entries:
+            a = agg.setdefault(op, {"ms": 0.0, "n": 0, "work": 0.0, "unit": unit, "kernels": set()})
+            a["ms"] += e0.elapsed_time(e1)
+            a["n"] += 1
+            a["work"] += work
+            a["kernels"].add(kernel)
+        out = {}
+        for k, a in agg.items():
+            rate = a["work"] / (a["ms"] * 1e-3) / (1e12 if a["unit"] == "flop" else 1e9)
+            out[k] = {"launches_per_step": round(a["n"] / n_steps, 2), "ms_per_step": round(a["ms"] / n_steps, 4),
+                      "share_of_step": round(a["ms"] / n_steps / step_ms, 4), "achieved": round(rate, 1),
+                      "unit": "TFLOP/s" if a["unit"] == "flop" else "GB/s", "kernels": sorted(a["kernels"])}
+        return dict(sorted(out.items(), key=lambda kv: -kv[1]["share_of_step"]))
+
 
 _REC = [None]
 

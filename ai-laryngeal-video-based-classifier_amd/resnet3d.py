@@ -383,15 +383,15 @@ class ResNet3d(torch.nn.Module):
                 if "b1" in blk:
                     fl = 2.0 * vol(g) * dout * cin
                     if stride == (1, 1, 1):
-                        ops.gemm(xin, blk["b1"][0], blk["b1"][1], "bias", act["sc"], m=rows(g), flop=fl, op="branch1")
+                        ops.gemm(xin, blk["b1"][0], blk["b1"][1], "bias", act["sc"], m=rows(g), flop=fl, op=f"branch1.s{s + 2}")
                     elif self.implicit_conv and cin % 64 == 0:
                         ops.conv3d_gemm(xin, B, gi, cin, (1, 1, 1), stride, (0, 0, 0), blk["b1"][0], blk["b1"][1], "bias",
-                                        act["sc"], flop=fl, op="branch1")
+                                        act["sc"], flop=fl, op=f"branch1.s{s + 2}")
                     else:
                         A = col(rows(g), cin)
                         tm("conv3d_im2col_kernel", "im2col", (vol(gi) + vol(g)) * cin * 2, "byte", ops.conv3d_im2col,
                            xin, "cl_bf16", B, gi, cin, (1, 1, 1), stride, (0, 0, 0), A)
-                        ops.gemm(A, blk["b1"][0], blk["b1"][1], "bias", act["sc"], flop=fl, op="branch1")
+                        ops.gemm(A, blk["b1"][0], blk["b1"][1], "bias", act["sc"], flop=fl, op=f"branch1.s{s + 2}")
                     skip = act["sc"]
                 else:
                     skip = xin
@@ -400,32 +400,32 @@ class ResNet3d(torch.nn.Module):
                 if tuple(ka) == (1, 1, 1) and self.implicit_conv and inner % 128 and inner % 64 == 0 and cin % 64 == 0:
                     # 64 output channels: the 256 x 64 implicit-GEMM tile (no MFMAs on the zero-padded channels)
                     ops.conv3d_gemm(xin, B, gi, cin, ka, (1, 1, 1), (0, 0, 0), blk["a"][0], blk["a"][1], "bias_relu",
-                                    act["a"], flop=fl, op="conv_a", n=inner)
+                                    act["a"], flop=fl, op=f"conv_a.s{s + 2}", n=inner)
                 elif tuple(ka) == (1, 1, 1):
-                    ops.gemm(xin, blk["a"][0], blk["a"][1], "bias_relu", act["a"], m=rows(gi), flop=fl, op="conv_a")
+                    ops.gemm(xin, blk["a"][0], blk["a"][1], "bias_relu", act["a"], m=rows(gi), flop=fl, op=f"conv_a.s{s + 2}")
                 elif self.implicit_conv and cin % 64 == 0:
                     ops.conv3d_gemm(xin, B, gi, cin, ka, (1, 1, 1), tuple(k // 2 for k in ka), blk["a"][0], blk["a"][1],
-                                    "bias_relu", act["a"], flop=fl, op="conv_a", n=_ru(inner, 64))
+                                    "bias_relu", act["a"], flop=fl, op=f"conv_a.s{s + 2}", n=_ru(inner, 64))
                 else:
                     A = col(rows(gi), ka[0] * cin)
                     tm("conv3d_im2col_kernel", "im2col", vol(gi) * cin * 2 * (1 + ka[0]), "byte", ops.conv3d_im2col,
                        xin, "cl_bf16", B, gi, cin, ka, (1, 1, 1), tuple(k // 2 for k in ka), A)
-                    ops.gemm(A, blk["a"][0], blk["a"][1], "bias_relu", act["a"], flop=fl, op="conv_a")
+                    ops.gemm(A, blk["a"][0], blk["a"][1], "bias_relu", act["a"], flop=fl, op=f"conv_a.s{s + 2}")
                 # conv_b (1,3,3) with the stage stride (+ BN + ReLU)
                 if self.implicit_conv and inner % 64 == 0:
                     ops.conv3d_gemm(act["a"], B, gi, inner, (1, 3, 3), stride, (0, 1, 1), blk["b"][0], blk["b"][1],
-                                    "bias_relu", act["b"], flop=2.0 * vol(g) * inner * inner * 9, op="conv_b",
+                                    "bias_relu", act["b"], flop=2.0 * vol(g) * inner * inner * 9, op=f"conv_b.s{s + 2}",
                                     n=_ru(inner, 64))
                 else:
                     A = col(rows(g), 9 * inner)
                     tm("conv3d_im2col_kernel", "im2col", (vol(gi) + 9 * vol(g)) * inner * 2, "byte", ops.conv3d_im2col,
                        act["a"], "cl_bf16", B, gi, inner, (1, 3, 3), stride, (0, 1, 1), A)
                     ops.gemm(A, blk["b"][0], blk["b"][1], "bias_relu", act["b"], flop=2.0 * vol(g) * inner * inner * 9,
-                             op="conv_b")
+                             op=f"conv_b.s{s + 2}")
                 # conv_c 1x1x1 + BN + skip + ReLU
                 out = act["x"] if xin is not act["x"] else act["x2"]
                 ops.gemm(act["b"][:, :inner], blk["c"][0], blk["c"][1], "bias_resid_relu", out, aux=skip,
-                         flop=2.0 * vol(g) * dout * inner, op="conv_c")
+                         flop=2.0 * vol(g) * dout * inner, op=f"conv_c.s{s + 2}")
                 x, cin = out, dout
             g_in = g
         return x, B, grids[-1], cin, ws

@@ -336,6 +336,7 @@ def op_breakdown(model, step, n_steps: int):
             step()
     torch.cuda.synchronize()
     step_ms = (time.perf_counter() - t0) / n_steps * 1e3
+    op_breakdown.last_ops = rec.summary_ops(n_steps, step_ms)
     return rec.summary(n_steps, step_ms), step_ms
 
 
@@ -486,6 +487,7 @@ def run_family(a, dist, rank, world, dev):
             "attention_roofline": attn,
             "kernel_breakdown": dict(list(table.items())[:12], note=f"3 one-stream steps, HIP events around every "
                                      f"launch: {instr_ms:.3f} ms per step under that instrumentation"),
+            "op_breakdown": (dict(list(op_breakdown.last_ops.items())[:20]) if a.mode == "resnet3d" else None),
             "model_tflops": round(model_tflops, 1), "model_frac_of_peak": round(model_tflops / PEAK_BF16_TFLOPS, 4),
             "cpu_baseline": cpu,
             "build": _build_id(),
