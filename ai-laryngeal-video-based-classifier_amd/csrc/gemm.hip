@@ -335,16 +335,19 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
     }
     // the bf16 residual of the ResNet3D conv_c epilogue likewise: at K = 64 .. 512 (one to eight
     // k-tiles) its fetch in the epilogue was a second serialized round trip per tile
+    // (G < 0: the cfg-14 timing ablation reads it in the epilogue instead)
     constexpr bool APRE = EPI == VC_EPI_BIAS_RESID_RELU_BF16;
     uint2 xaux[APRE ? MI : 1][APRE ? NI : 1];
     if constexpr (APRE) {
+        if (G >= 0) {
 #pragma unroll
-        for (int i = 0; i < MI; ++i)
+            for (int i = 0; i < MI; ++i)
 #pragma unroll
-            for (int j = 0; j < NI; ++j)
-                xaux[i][j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(aux) +
-                                                             (m0 + wm * TM + i * 16 + c16) * ldaux + n0 + wn * TN +
-                                                             j * 16 + 4 * q);
+                for (int j = 0; j < NI; ++j)
+                    xaux[i][j] = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(aux) +
+                                                                 (m0 + wm * TM + i * 16 + c16) * ldaux + n0 + wn * TN +
+                                                                 j * 16 + 4 * q);
+        }
     }
     if (ST == 3 && nk > 1) {
         stage(1, 1);
@@ -401,26 +404,32 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
                 x.w += acc[i][j][3] + bb.w;
                 *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + m * ldo + n) = x;
             }
-    } else if constexpr (APRE) {
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int j = 0; j < NI; ++j) {
-                const int64_t m = m0 + wm * TM + i * 16 + c16, n = n0 + wn * TN + j * 16 + 4 * q;
-                const float4 bb = *reinterpret_cast<const float4*>(bias + n);
-                const uint2 rr = xaux[i][j];
-                const float v0 = fmaxf(acc[i][j][0] + bb.x + bf2f((unsigned short)(rr.x & 0xffff)), 0.f);
-                const float v1 = fmaxf(acc[i][j][1] + bb.y + bf2f((unsigned short)(rr.x >> 16)), 0.f);
-                const float v2 = fmaxf(acc[i][j][2] + bb.z + bf2f((unsigned short)(rr.y & 0xffff)), 0.f);
-                const float v3 = fmaxf(acc[i][j][3] + bb.w + bf2f((unsigned short)(rr.y >> 16)), 0.f);
-                uint2 p;
-                p.x = pack2<ET>(v0, v1);
-                p.y = pack2<ET>(v2, v3);
-                *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + m * ldo + n) = p;
-            }
     } else {
-        store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bias, out, ldo, aux, ldaux, G, gstride,
-                                      goff);
+        bool done = false;
+        if constexpr (APRE) {
+            if (G >= 0) {
+#pragma unroll
+                for (int i = 0; i < MI; ++i)
+#pragma unroll
+                    for (int j = 0; j < NI; ++j) {
+                        const int64_t m = m0 + wm * TM + i * 16 + c16, n = n0 + wn * TN + j * 16 + 4 * q;
+                        const float4 bb = *reinterpret_cast<const float4*>(bias + n);
+                        const uint2 rr = xaux[i][j];
+                        const float v0 = fmaxf(acc[i][j][0] + bb.x + bf2f((unsigned short)(rr.x & 0xffff)), 0.f);
+                        const float v1 = fmaxf(acc[i][j][1] + bb.y + bf2f((unsigned short)(rr.x >> 16)), 0.f);
+                        const float v2 = fmaxf(acc[i][j][2] + bb.z + bf2f((unsigned short)(rr.y & 0xffff)), 0.f);
+                        const float v3 = fmaxf(acc[i][j][3] + bb.w + bf2f((unsigned short)(rr.y >> 16)), 0.f);
+                        uint2 p;
+                        p.x = pack2<ET>(v0, v1);
+                        p.y = pack2<ET>(v2, v3);
+                        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + m * ldo + n) = p;
+                    }
+                done = true;
+            }
+        }
+        if (!done)
+            store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bias, out, ldo, aux, ldaux, G,
+                                          gstride, goff);
     }
 }
 
@@ -1502,8 +1511,9 @@ struct GemmCfg {
     int bm, bn;
 };
 static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}, {128, 128}, {0, 0},
-                                 {64, 128}, {256, 256}, {256, 128}, {256, 256}, {256, 256}, {256, 256}, {256, 256}};
-constexpr int kNumCfgs = 14;
+                                 {64, 128}, {256, 256}, {256, 128}, {256, 256}, {256, 256}, {256, 256}, {256, 256},
+                                 {128, 128}};
+constexpr int kNumCfgs = 15;
 
 template <int BM, int BN, int WM, int WN, int E, int ST = 3, int ET = VC_ELEM_BF16>
 static int launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
@@ -1651,6 +1661,11 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
                 return launch_pp<E, ET, 3>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
             }
             return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfgs 11 / 12 (timing ablations) are bias / bf16 only");
+        case 14:  // timing ablation: cfg 5 with the bf16 residual read in the epilogue (G < 0), not prefetched
+            if constexpr (E == VC_EPI_BIAS_RESID_RELU_BF16)
+                return launch_cfg<128, 128, 2, 4, E, 2, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, -1, gs,
+                                                            go, s);
+            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 14 (timing ablation) is bias_resid_relu only");
         case 9: return launch_pp128<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 4:
             if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
@@ -1741,7 +1756,7 @@ extern "C" int vc_gemm_h16(const uint16_t* A, int64_t lda, const uint16_t* W, in
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: no tile config divides M x N");
     if ((M / kCfgs[cfg].bm) * (N / kCfgs[cfg].bn) > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: grid too large");
     const int k = (int)K;
-    if ((cfg == 8 || cfg == 9 || cfg >= 11) && K < 128) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 8 / 9 need K >= 128");
+    if ((cfg == 8 || cfg == 9 || (cfg >= 11 && cfg <= 13)) && K < 128) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 8 / 9 need K >= 128");
     if ((cfg == 4 || cfg == 10) && (K / 32 < 6 || N > 8192 || !st16_ok ||
                      (epilogue > VC_EPI_BIAS_GELU_ERF && epilogue != VC_EPI_BIAS_RELU_BF16 &&
                       epilogue != VC_EPI_BIAS_GELU_TANH_SAVE)))

@@ -201,10 +201,10 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: str, ou
     rec = _REC[0]
     if rec is not None:
         M_ = a.shape[0] if m is None else m
+        label = gemm_kernel_name(M_, w.shape[0], a.shape[1], epilogue, out, aux, cfg, a.dtype == torch.float16)
         e0 = rec.begin()
         _gemm(a, w, bias, epilogue, out, aux, group, group_stride, group_offset, m, cfg)
-        rec.end(e0, gemm_kernel_name(M_, w.shape[0], a.shape[1], epilogue, out, aux, cfg, a.dtype == torch.float16), op,
-                2.0 * M_ * w.shape[0] * a.shape[1] if flop is None else flop, "flop")
+        rec.end(e0, label, op, 2.0 * M_ * w.shape[0] * a.shape[1] if flop is None else flop, "flop")
         return out
     return _gemm(a, w, bias, epilogue, out, aux, group, group_stride, group_offset, m, cfg)
 
@@ -600,16 +600,20 @@ def conv3d_gemm(x: torch.Tensor, B: int, grid, C: int, kernel, stride, pad, w: t
         _ZERO_ROW[key] = torch.zeros(64, dtype=torch.bfloat16, device=x.device)
     k, s, p = ((ctypes.c_int * 3)(*v) for v in (kernel, stride, pad))
     rec = _REC[0]
+    if rec is not None:
+        # the label first: nothing but the launch may sit between the two events (a first
+        # get_device_properties inside them once timed as an 8-ms launch)
+        tile = "256, 64, 8, 1"
+        if rt == 128:  # 64 x 128 tiles when the 128 x 128 grid has fewer tiles than CUs (csrc/gemm.hip)
+            small = ((M + 127) // 128) * (N // 128) < _num_cus(x.device) and e in (0, 6)
+            tile = "64, 128, 2, 4" if small else "128, 128, 2, 4"
+        label = f"conv_gemm_kernel<{tile}, {e}, 2, 0>"
     e0 = rec.begin() if rec is not None else None
     _lib.call("vc_conv3d_gemm_bf16", _p(x), x.stride(0), B, T, H, W, C, ctypes.addressof(k), ctypes.addressof(s),
               ctypes.addressof(p), _p(_ZERO_ROW[key]), _p(w), w.stride(0), N, _p(bias), e, _p(out), out.stride(0),
               _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0, _stream(x))
     if rec is not None:
-        tile = "256, 64, 8, 1"
-        if rt == 128:  # 64 x 128 tiles when the 128 x 128 grid has fewer tiles than CUs (csrc/gemm.hip)
-            small = ((M + 127) // 128) * (N // 128) < _num_cus(x.device) and e in (0, 6)
-            tile = "64, 128, 2, 4" if small else "128, 128, 2, 4"
-        rec.end(e0, f"conv_gemm_kernel<{tile}, {e}, 2, 0>", op, 2.0 * M * N * kvol * C if flop is None else flop, "flop")
+        rec.end(e0, label, op, 2.0 * M * N * kvol * C if flop is None else flop, "flop")
     return out
 
 

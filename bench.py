@@ -328,6 +328,8 @@ def op_breakdown(model, step, n_steps: int):
     per kernel instantiation its launches, mean launch time, share of the step and achieved rate on the
     algorithmic work the model states for it.  Returns (table sorted by share, step ms)."""
     from vclip_amd import ops
+    with ops.recording(ops.OpRecorder()):
+        step()  # discarded: one-time host work on the recorder's paths stays out of the table
     rec = ops.OpRecorder()
     torch.cuda.synchronize()
     t0 = time.perf_counter()

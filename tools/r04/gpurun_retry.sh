@@ -2,10 +2,10 @@
 # gpurun with waits while no box is free (exit 3: nothing ran, nothing charged); any other exit is final
 # usage: tools/r04/gpurun_retry.sh <log> <timeout> '<command>'
 LOG=$1; TO=$2; shift 2
-for i in $(seq 1 30); do
+for i in $(seq 1 80); do
   /usr/local/graft/bin/gpurun --timeout $TO -- "$@" > $LOG 2>&1
   rc=$?
   [ $rc -ne 3 ] && { echo "EXIT $rc" >> $LOG; exit $rc; }
-  sleep 60
+  sleep 90
 done
 echo "EXIT 3 (gave up)" >> $LOG

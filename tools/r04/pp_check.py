@@ -20,6 +20,7 @@ ap.add_argument("--only", default="")
 ap.add_argument("--ksweep", action="store_true", help="q|k|v-shaped cases at K = 768 .. 6144 (per-tile overhead fit)")
 ap.add_argument("--swin", action="store_true", help="Video Swin-T B=4 stage-1/2 GEMM shapes (channels padded to 128)")
 ap.add_argument("--r3d", action="store_true", help="ResNet3D-50 B=4 conv_a / conv_b GEMM shapes (implicit-conv proxies)")
+ap.add_argument("--r3dc", action="store_true", help="ResNet3D-50 B=4 conv_c shapes (1x1x1 + bf16 residual + ReLU)")
 a = ap.parse_args()
 new_cfgs = [int(c) for c in a.cfgs.split(",")]
 
@@ -40,6 +41,9 @@ if a.r3d:
              ("r3d_s3b", 25088, 256, 2304, "bias_relu"), ("r3d_s4a", 6400, 512, 3072, "bias_relu"),
              ("r3d_s4b", 6400, 512, 4608, "bias_relu"), ("r3d_s1c", 401408, 256, 64, "bias_resid_relu"),
              ("r3d_s2c", 100352, 512, 128, "bias_resid_relu")]
+if a.r3dc:
+    CASES = [("r3d_s2c", 401408, 256, 64, "bias_resid_relu"), ("r3d_s3c", 100352, 512, 128, "bias_resid_relu"),
+             ("r3d_s4c", 25088, 1024, 256, "bias_resid_relu"), ("r3d_s5c", 6400, 2048, 512, "bias_resid_relu")]
 if a.ksweep:
     CASES = [(f"ks_K{K}", 12800, 2304, K, "bias") for K in (768, 1536, 3072, 6144)]
 if a.only:
@@ -66,10 +70,11 @@ for name, M, N, K, epi in CASES:
     base = lib.vc_gemm_pick(M, N, K, E[epi], out.stride(0), 0, None)
     bf16_out = out.dtype != torch.float32
     TILE = {1: (128, 128), 3: (256, 256), 4: (256, 256), 5: (128, 128), 7: (64, 128), 8: (256, 256), 9: (256, 128),
-            10: (256, 256), 11: (256, 256), 12: (256, 256), 13: (256, 256)}
+            10: (256, 256), 11: (256, 256), 12: (256, 256), 13: (256, 256), 14: (128, 128)}
     ok_shape = lambda c: (c in TILE and M % TILE[c][0] == 0 and N % TILE[c][1] == 0 and K % 64 == 0 and  # noqa: E731
                           (K >= 192 if c in (4, 10) else K >= 128 if c in (8, 9, 11, 12, 13) else True))  # cfg 1: 128x128, 3-slot ring
     cfgs = [base] + [c for c in new_cfgs if c != base and ok_shape(c) and (c not in (11, 12, 13) or epi == "bias") and
+                     (c != 14 or epi == "bias_resid_relu") and
                      (c not in (4, 10) or bf16_out)]
     # bit-identity: every config from the same initial out (the residual epilogue accumulates)
     init = (torch.randn(M, N, device="cuda", generator=g) if out.dtype == torch.float32 else out.clone())
