@@ -333,13 +333,16 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
                                                               (m0 + wm * TM + i * 16 + c16) * ldo + n0 + wn * TN +
                                                               j * 16 + 4 * q);
     }
-    // the bf16 residual of the ResNet3D conv_c epilogue likewise: at K = 64 .. 512 (one to eight
-    // k-tiles) its fetch in the epilogue was a second serialized round trip per tile
-    // (G < 0: the cfg-14 timing ablation reads it in the epilogue instead)
+    // the bf16 residual of the ResNet3D conv_c epilogue likewise, when K is one k-tile (res2's
+    // K = 64: otherwise its fetch in the epilogue is a second serialized round trip per tile;
+    // 138.4 vs 143.1 us at 401408 x 256).  At K >= 128 the early loads delay the operand DMAs
+    // behind them and cost more than they hide (res3 K = 128 67.6 vs 58.4 us, res4 K = 256 43.4 vs
+    // 38.9; cfg 14 = this kernel with the prefetch off, round 4).  G < 0: the cfg-14 ablation.
     constexpr bool APRE = EPI == VC_EPI_BIAS_RESID_RELU_BF16;
+    const bool apre = APRE && G >= 0 && K <= GBK;
     uint2 xaux[APRE ? MI : 1][APRE ? NI : 1];
     if constexpr (APRE) {
-        if (G >= 0) {
+        if (apre) {
 #pragma unroll
             for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -407,7 +410,7 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
     } else {
         bool done = false;
         if constexpr (APRE) {
-            if (G >= 0) {
+            if (apre) {
 #pragma unroll
                 for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -1353,7 +1356,7 @@ struct ConvGeomG {
 // k-tile, so an A row's 16-B chunk is 2 pixels of the padded clip (16-B aligned: the window's first
 // pixel index is even for stride-2 w); segments past kt * kh read the zero row.
 template <int BM, int BN, int WM, int WN, int EPI, int ST = 2, int MODE = 0>
-__global__ void __launch_bounds__(512, ST == 2 ? 2 : 1)
+__global__ void __launch_bounds__(512, (ST == 2 || BM * BN <= 64 * 128) ? 2 : 1)
 conv_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx, ConvGeomG g, const uint16_t* __restrict__ zrow,
                  const uint16_t* __restrict__ W, int64_t ldw, int nbm, int nbn, int K, const float* __restrict__ bias,
                  void* __restrict__ out, int64_t ldo, const float* __restrict__ aux, int64_t ldaux) {
@@ -1485,21 +1488,34 @@ conv_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx, ConvGeomG g, const
                                             0);
 }
 
-template <int BM, int BN, int WM, int WN, int E, int MODE = 0>
-static int launch_conv(const uint16_t* X, int64_t ldx, const ConvGeomG& g, const uint16_t* zrow, const uint16_t* W,
-                       int64_t ldw, int nbm, int nbn, int K, const float* bias, void* out, int64_t ldo, const float* aux,
-                       int64_t ldaux, hipStream_t stream) {
-    constexpr int lds = 2 * (BM + BN) * 128;
+template <int BM, int BN, int WM, int WN, int E, int MODE, int ST>
+static int launch_conv_st(const uint16_t* X, int64_t ldx, const ConvGeomG& g, const uint16_t* zrow, const uint16_t* W,
+                          int64_t ldw, int nbm, int nbn, int K, const float* bias, void* out, int64_t ldo,
+                          const float* aux, int64_t ldaux, hipStream_t stream) {
+    constexpr int lds = ST * (BM + BN) * 128;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv_gemm_kernel<BM, BN, WM, WN, E, 2, MODE>,
+        hipError_t e = hipFuncSetAttribute((const void*)conv_gemm_kernel<BM, BN, WM, WN, E, ST, MODE>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return fail((int)e, std::string("vc_conv3d_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
         attr_set = true;
     }
-    conv_gemm_kernel<BM, BN, WM, WN, E, 2, MODE><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(
+    conv_gemm_kernel<BM, BN, WM, WN, E, ST, MODE><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(
         X, ldx, g, zrow, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux);
     return check_launch("vc_conv3d_gemm_bf16");
+}
+
+// ring: LDS ring depth in k-tiles (2: two workgroups per CU at every tile; 3: one more k-tile in
+// flight, one workgroup per CU except at 64 x 128)
+template <int BM, int BN, int WM, int WN, int E, int MODE = 0>
+static int launch_conv(const uint16_t* X, int64_t ldx, const ConvGeomG& g, const uint16_t* zrow, const uint16_t* W,
+                       int64_t ldw, int nbm, int nbn, int K, const float* bias, void* out, int64_t ldo, const float* aux,
+                       int64_t ldaux, hipStream_t stream, int ring = 2) {
+    if (ring == 3)
+        return launch_conv_st<BM, BN, WM, WN, E, MODE, 3>(X, ldx, g, zrow, W, ldw, nbm, nbn, K, bias, out, ldo, aux,
+                                                          ldaux, stream);
+    return launch_conv_st<BM, BN, WM, WN, E, MODE, 2>(X, ldx, g, zrow, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux,
+                                                      stream);
 }
 
 // Tile configurations (BM, BN); cfg 6 (a ping-pong schedule of the persistent kernel, 23 %
@@ -1788,11 +1804,13 @@ extern "C" int vc_gemm_h16(const uint16_t* A, int64_t lda, const uint16_t* W, in
 // Implicit-GEMM Conv3d (conv_gemm_kernel): out[m][n] = epilogue(sum_(tap, c) x[in(m, tap)][c] *
 // Wt[n][tap * C + c] + bias[n]); output rows m < B*To*Ho*Wo (rows up to the next multiple of 128
 // are written too: the caller's buffer has them), zero_row: >= 64 zero bf16 (16-B aligned).
-extern "C" int vc_conv3d_gemm_bf16(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_t H, int64_t W,
-                                   int64_t C, const int* kernel, const int* stride, const int* pad,
-                                   const uint16_t* zero_row, const uint16_t* Wt, int64_t ldw, int64_t N,
-                                   const float* bias, int epilogue, void* out, int64_t ldo, const void* aux,
-                                   int64_t ldaux, hipStream_t stream) {
+extern "C" int vc_conv3d_gemm_bf16_ring(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_t H, int64_t W,
+                                        int64_t C, const int* kernel, const int* stride, const int* pad,
+                                        const uint16_t* zero_row, const uint16_t* Wt, int64_t ldw, int64_t N,
+                                        const float* bias, int epilogue, void* out, int64_t ldo, const void* aux,
+                                        int64_t ldaux, int ring, hipStream_t stream) {
+    if (ring == 0) ring = 2;
+    if (ring != 2 && ring != 3) return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16_ring: ring must be 0, 2 or 3");
     if (!x || !kernel || !stride || !pad || !zero_row || !Wt || !bias || !out)
         return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: null pointer");
     for (int d = 0; d < 3; ++d)
@@ -1823,10 +1841,10 @@ extern "C" int vc_conv3d_gemm_bf16(const uint16_t* x, int64_t ldx, int64_t B, in
         if (ldo % 8) return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: ldo % 8");
         if (epilogue == VC_EPI_BIAS_RELU_BF16)
             return launch_conv<256, 64, 8, 1, VC_EPI_BIAS_RELU_BF16>(x, ldx, g, zero_row, Wt, ldw, nbm, nbn, (int)K, bias,
-                                                                      out, ldo, auxf, ldaux, stream);
+                                                                      out, ldo, auxf, ldaux, stream, ring);
         if (epilogue == VC_EPI_BIAS_BF16)
             return launch_conv<256, 64, 8, 1, VC_EPI_BIAS_BF16>(x, ldx, g, zero_row, Wt, ldw, nbm, nbn, (int)K, bias, out,
-                                                                 ldo, auxf, ldaux, stream);
+                                                                 ldo, auxf, ldaux, stream, ring);
         return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: N % 128 != 0 supports bias / bias_relu only");
     }
     const int nbm = (int)((g.M + 127) / 128), nbn = (int)(N / 128);
@@ -1837,28 +1855,37 @@ extern "C" int vc_conv3d_gemm_bf16(const uint16_t* x, int64_t ldx, int64_t B, in
         const int nbm64 = (int)((g.M + 63) / 64);
         if (epilogue == VC_EPI_BIAS_RELU_BF16)
             return launch_conv<64, 128, 2, 4, VC_EPI_BIAS_RELU_BF16>(x, ldx, g, zero_row, Wt, ldw, nbm64, nbn, (int)K,
-                                                                      bias, out, ldo, auxf, ldaux, stream);
+                                                                      bias, out, ldo, auxf, ldaux, stream, ring);
         return launch_conv<64, 128, 2, 4, VC_EPI_BIAS_BF16>(x, ldx, g, zero_row, Wt, ldw, nbm64, nbn, (int)K, bias, out,
-                                                             ldo, auxf, ldaux, stream);
+                                                             ldo, auxf, ldaux, stream, ring);
     }
     switch (epilogue) {
         case VC_EPI_BIAS_BF16:
             if (ldo % 8) break;
             return launch_conv<128, 128, 2, 4, VC_EPI_BIAS_BF16>(x, ldx, g, zero_row, Wt, ldw, nbm, nbn, (int)K, bias,
-                                                                  out, ldo, auxf, ldaux, stream);
+                                                                  out, ldo, auxf, ldaux, stream, ring);
         case VC_EPI_BIAS_RELU_BF16:
             if (ldo % 8) break;
             return launch_conv<128, 128, 2, 4, VC_EPI_BIAS_RELU_BF16>(x, ldx, g, zero_row, Wt, ldw, nbm, nbn, (int)K,
-                                                                       bias, out, ldo, auxf, ldaux, stream);
+                                                                       bias, out, ldo, auxf, ldaux, stream, ring);
         case VC_EPI_BIAS_RESID_RELU_BF16:
             if (!aux || ldaux % 4 || ldaux < N || ((uintptr_t)aux & 7)) break;
             return launch_conv<128, 128, 2, 4, VC_EPI_BIAS_RESID_RELU_BF16>(x, ldx, g, zero_row, Wt, ldw, nbm, nbn,
-                                                                             (int)K, bias, out, ldo, auxf, ldaux, stream);
+                                                                             (int)K, bias, out, ldo, auxf, ldaux, stream, ring);
         default:
             break;
     }
     return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: epilogue must be bias / bias_relu / bias_resid_relu "
                                     "(16-B output rows; resid_relu: a bf16 aux with ldaux >= N)");
+}
+
+extern "C" int vc_conv3d_gemm_bf16(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_t H, int64_t W,
+                                   int64_t C, const int* kernel, const int* stride, const int* pad,
+                                   const uint16_t* zero_row, const uint16_t* Wt, int64_t ldw, int64_t N,
+                                   const float* bias, int epilogue, void* out, int64_t ldo, const void* aux,
+                                   int64_t ldaux, hipStream_t stream) {
+    return vc_conv3d_gemm_bf16_ring(x, ldx, B, T, H, W, C, kernel, stride, pad, zero_row, Wt, ldw, N, bias, epilogue, out,
+                                    ldo, aux, ldaux, 0, stream);
 }
 
 // Stem input packing for vc_conv3d_stem_gemm_bf16: f32 [B][C][T][H][W] (C <= 4) -> bf16

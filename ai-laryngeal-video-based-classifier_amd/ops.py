@@ -573,7 +573,7 @@ _ZERO_ROW = {}
 
 def conv3d_gemm(x: torch.Tensor, B: int, grid, C: int, kernel, stride, pad, w: torch.Tensor, bias: torch.Tensor,
                 epilogue: str, out: torch.Tensor, aux: torch.Tensor | None = None, flop: float | None = None,
-                op: str = "conv", n: int | None = None) -> torch.Tensor:
+                op: str = "conv", n: int | None = None, ring: int = 0) -> torch.Tensor:
     """Implicit-GEMM Conv3d (vc_conv3d_gemm_bf16): x channels-last bf16 rows [>= B*T*H*W, >= C],
     w bf16 [>= N, >= kvol*C] (columns (kt, kh, kw, c)), out bf16 [>= roundup(B*To*Ho*Wo, 128), >= N]
     (256-row multiples when N % 128 != 0: 256 x 64 tiles); N = n (a multiple of 64) or w's rows."""
@@ -607,11 +607,11 @@ def conv3d_gemm(x: torch.Tensor, B: int, grid, C: int, kernel, stride, pad, w: t
         if rt == 128:  # 64 x 128 tiles when the 128 x 128 grid has fewer tiles than CUs (csrc/gemm.hip)
             small = ((M + 127) // 128) * (N // 128) < _num_cus(x.device) and e in (0, 6)
             tile = "64, 128, 2, 4" if small else "128, 128, 2, 4"
-        label = f"conv_gemm_kernel<{tile}, {e}, 2, 0>"
+        label = f"conv_gemm_kernel<{tile}, {e}, {3 if ring == 3 else 2}, 0>"
     e0 = rec.begin() if rec is not None else None
-    _lib.call("vc_conv3d_gemm_bf16", _p(x), x.stride(0), B, T, H, W, C, ctypes.addressof(k), ctypes.addressof(s),
+    _lib.call("vc_conv3d_gemm_bf16_ring", _p(x), x.stride(0), B, T, H, W, C, ctypes.addressof(k), ctypes.addressof(s),
               ctypes.addressof(p), _p(_ZERO_ROW[key]), _p(w), w.stride(0), N, _p(bias), e, _p(out), out.stride(0),
-              _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0, _stream(x))
+              _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0, ring, _stream(x))
     if rec is not None:
         rec.end(e0, label, op, 2.0 * M * N * kvol * C if flop is None else flop, "flop")
     return out

@@ -61,6 +61,9 @@ class ResNet3d(torch.nn.Module):
         # A rows gathered from the activations per kernel tap, no im2col buffer); False: im2col + GEMM.
         # Bit-identical either way (same MFMA chain per output, same column order).
         self.implicit_conv = True
+        # LDS ring depth of the implicit convolutions per res stage ("s2" .. "s5" -> 2 or 3;
+        # vc_conv3d_gemm_bf16_ring), default 2 (bit-identical for any setting)
+        self.conv_ring = {}
 
     def state_dict(self, *a, **k):
         return OrderedDict((n, self.params[n.replace(".", "__")].detach()) for n in self._names)
@@ -302,7 +305,7 @@ class ResNet3d(torch.nn.Module):
             if self._graphs is None:
                 self._graphs = GraphReplay()
             key = (video.data_ptr(), tuple(video.shape), tuple(video.stride()), video.dtype, self.concurrent_streams,
-                   self.implicit_conv,
+                   self.implicit_conv, tuple(sorted(self.conv_ring.items())),
                    str(video.device), self._weights_version())
             return self._graphs.run(key, video, self._forward_eager, keep=lambda: (self._packed, tuple(self._ws_used)))
         return self._forward_eager(video)
@@ -386,7 +389,7 @@ class ResNet3d(torch.nn.Module):
                         ops.gemm(xin, blk["b1"][0], blk["b1"][1], "bias", act["sc"], m=rows(g), flop=fl, op=f"branch1.s{s + 2}")
                     elif self.implicit_conv and cin % 64 == 0:
                         ops.conv3d_gemm(xin, B, gi, cin, (1, 1, 1), stride, (0, 0, 0), blk["b1"][0], blk["b1"][1], "bias",
-                                        act["sc"], flop=fl, op=f"branch1.s{s + 2}")
+                                        act["sc"], flop=fl, op=f"branch1.s{s + 2}", ring=self.conv_ring.get(f"s{s + 2}", 0))
                     else:
                         A = col(rows(g), cin)
                         tm("conv3d_im2col_kernel", "im2col", (vol(gi) + vol(g)) * cin * 2, "byte", ops.conv3d_im2col,
@@ -400,12 +403,12 @@ class ResNet3d(torch.nn.Module):
                 if tuple(ka) == (1, 1, 1) and self.implicit_conv and inner % 128 and inner % 64 == 0 and cin % 64 == 0:
                     # 64 output channels: the 256 x 64 implicit-GEMM tile (no MFMAs on the zero-padded channels)
                     ops.conv3d_gemm(xin, B, gi, cin, ka, (1, 1, 1), (0, 0, 0), blk["a"][0], blk["a"][1], "bias_relu",
-                                    act["a"], flop=fl, op=f"conv_a.s{s + 2}", n=inner)
+                                    act["a"], flop=fl, op=f"conv_a.s{s + 2}", n=inner, ring=self.conv_ring.get(f"s{s + 2}", 0))
                 elif tuple(ka) == (1, 1, 1):
                     ops.gemm(xin, blk["a"][0], blk["a"][1], "bias_relu", act["a"], m=rows(gi), flop=fl, op=f"conv_a.s{s + 2}")
                 elif self.implicit_conv and cin % 64 == 0:
                     ops.conv3d_gemm(xin, B, gi, cin, ka, (1, 1, 1), tuple(k // 2 for k in ka), blk["a"][0], blk["a"][1],
-                                    "bias_relu", act["a"], flop=fl, op=f"conv_a.s{s + 2}", n=_ru(inner, 64))
+                                    "bias_relu", act["a"], flop=fl, op=f"conv_a.s{s + 2}", n=_ru(inner, 64), ring=self.conv_ring.get(f"s{s + 2}", 0))
                 else:
                     A = col(rows(gi), ka[0] * cin)
                     tm("conv3d_im2col_kernel", "im2col", vol(gi) * cin * 2 * (1 + ka[0]), "byte", ops.conv3d_im2col,
@@ -415,7 +418,7 @@ class ResNet3d(torch.nn.Module):
                 if self.implicit_conv and inner % 64 == 0:
                     ops.conv3d_gemm(act["a"], B, gi, inner, (1, 3, 3), stride, (0, 1, 1), blk["b"][0], blk["b"][1],
                                     "bias_relu", act["b"], flop=2.0 * vol(g) * inner * inner * 9, op=f"conv_b.s{s + 2}",
-                                    n=_ru(inner, 64))
+                                    n=_ru(inner, 64), ring=self.conv_ring.get(f"s{s + 2}", 0))
                 else:
                     A = col(rows(g), 9 * inner)
                     tm("conv3d_im2col_kernel", "im2col", (vol(gi) + 9 * vol(g)) * inner * 2, "byte", ops.conv3d_im2col,

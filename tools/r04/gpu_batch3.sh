@@ -4,7 +4,7 @@ set -o pipefail
 T=${TAG:-r04_b3}
 OUT=gpurun_out/$T
 mkdir -p $OUT
-timeout -k 10 200 python -u tools/r04/pp_check.py --r3dc --rounds 7 --iters 10 --cfgs 1,5,14 > $OUT/r3dc_gemm.log 2>&1; rc=$?
+timeout -k 10 200 python -u tools/r04/pp_check.py --r3dc --rounds 7 --iters 10 --cfgs 1,5,7,14 > $OUT/r3dc_gemm.log 2>&1; rc=$?
 cut -c1-600 $OUT/r3dc_gemm.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u tools/r04/pp_check.py --r3d --rounds 5 --iters 10 --cfgs 1,5,7,8,9,10 > $OUT/r3d_gemm.log 2>&1; rc=$?
 cut -c1-600 $OUT/r3d_gemm.log; [ $rc -eq 0 ] || exit $rc
