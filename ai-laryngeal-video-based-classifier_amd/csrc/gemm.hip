@@ -1809,8 +1809,12 @@ extern "C" int vc_conv3d_gemm_bf16_ring(const uint16_t* x, int64_t ldx, int64_t 
                                         const uint16_t* zero_row, const uint16_t* Wt, int64_t ldw, int64_t N,
                                         const float* bias, int epilogue, void* out, int64_t ldo, const void* aux,
                                         int64_t ldaux, int ring, hipStream_t stream) {
-    if (ring == 0) ring = 2;
-    if (ring != 2 && ring != 3) return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16_ring: ring must be 0, 2 or 3");
+    if (ring != 0 && ring != 2 && ring != 3)
+        return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16_ring: ring must be 0, 2 or 3");
+    // ring 0 (automatic): a 3-deep ring when the grid has fewer tiles than two per CU (the workgroups
+    // are few, so each one's DMA latency is exposed; ResNet3D res4 / res5 at B = 4: +1.1 / +1.5 % of
+    // the forward each), else 2 (res2 / res3: -3.7 / -2.5 %), tools/r04/ab_resnet3d_ring.py, round 4
+    auto pick_ring = [&](int64_t tiles) { return ring ? ring : (tiles < 2 * (int64_t)num_cus() ? 3 : 2); };
     if (!x || !kernel || !stride || !pad || !zero_row || !Wt || !bias || !out)
         return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: null pointer");
     for (int d = 0; d < 3; ++d)
@@ -1839,6 +1843,7 @@ extern "C" int vc_conv3d_gemm_bf16_ring(const uint16_t* x, int64_t ldx, int64_t 
         const int nbm = (int)((g.M + 255) / 256), nbn = (int)(N / 64);
         if ((int64_t)nbm * nbn > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: grid too large");
         if (ldo % 8) return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: ldo % 8");
+        ring = pick_ring((int64_t)nbm * nbn);
         if (epilogue == VC_EPI_BIAS_RELU_BF16)
             return launch_conv<256, 64, 8, 1, VC_EPI_BIAS_RELU_BF16>(x, ldx, g, zero_row, Wt, ldw, nbm, nbn, (int)K, bias,
                                                                       out, ldo, auxf, ldaux, stream, ring);
@@ -1853,12 +1858,14 @@ extern "C" int vc_conv3d_gemm_bf16_ring(const uint16_t* x, int64_t ldx, int64_t 
     if (nbm * nbn < num_cus() && ldo % 8 == 0 &&
         (epilogue == VC_EPI_BIAS_RELU_BF16 || epilogue == VC_EPI_BIAS_BF16)) {
         const int nbm64 = (int)((g.M + 63) / 64);
+        ring = pick_ring((int64_t)nbm64 * nbn);
         if (epilogue == VC_EPI_BIAS_RELU_BF16)
             return launch_conv<64, 128, 2, 4, VC_EPI_BIAS_RELU_BF16>(x, ldx, g, zero_row, Wt, ldw, nbm64, nbn, (int)K,
                                                                       bias, out, ldo, auxf, ldaux, stream, ring);
         return launch_conv<64, 128, 2, 4, VC_EPI_BIAS_BF16>(x, ldx, g, zero_row, Wt, ldw, nbm64, nbn, (int)K, bias, out,
                                                              ldo, auxf, ldaux, stream, ring);
     }
+    ring = pick_ring((int64_t)nbm * nbn);
     switch (epilogue) {
         case VC_EPI_BIAS_BF16:
             if (ldo % 8) break;

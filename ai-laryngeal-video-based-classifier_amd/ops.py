@@ -607,7 +607,10 @@ def conv3d_gemm(x: torch.Tensor, B: int, grid, C: int, kernel, stride, pad, w: t
         if rt == 128:  # 64 x 128 tiles when the 128 x 128 grid has fewer tiles than CUs (csrc/gemm.hip)
             small = ((M + 127) // 128) * (N // 128) < _num_cus(x.device) and e in (0, 6)
             tile = "64, 128, 2, 4" if small else "128, 128, 2, 4"
-        label = f"conv_gemm_kernel<{tile}, {e}, {3 if ring == 3 else 2}, 0>"
+        nt = (((M + 127) // 128) * (N // 128) if tile == "128, 128, 2, 4" else ((M + 63) // 64) * (N // 128)
+              if tile == "64, 128, 2, 4" else ((M + 255) // 256) * (N // 64))
+        st = ring if ring else (3 if nt < 2 * _num_cus(x.device) else 2)  # csrc/gemm.hip pick_ring
+        label = f"conv_gemm_kernel<{tile}, {e}, {st}, 0>"
     e0 = rec.begin() if rec is not None else None
     _lib.call("vc_conv3d_gemm_bf16_ring", _p(x), x.stride(0), B, T, H, W, C, ctypes.addressof(k), ctypes.addressof(s),
               ctypes.addressof(p), _p(_ZERO_ROW[key]), _p(w), w.stride(0), N, _p(bias), e, _p(out), out.stride(0),

@@ -62,7 +62,7 @@ class ResNet3d(torch.nn.Module):
         # Bit-identical either way (same MFMA chain per output, same column order).
         self.implicit_conv = True
         # LDS ring depth of the implicit convolutions per res stage ("s2" .. "s5" -> 2 or 3;
-        # vc_conv3d_gemm_bf16_ring), default 2 (bit-identical for any setting)
+        # vc_conv3d_gemm_bf16_ring), absent = automatic by grid size (bit-identical for any setting)
         self.conv_ring = {}
 
     def state_dict(self, *a, **k):

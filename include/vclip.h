@@ -335,8 +335,9 @@ int vc_conv3d_gemm_bf16(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, in
                         const uint16_t* Wt, int64_t ldw, int64_t N, const float* bias, int epilogue, void* out,
                         int64_t ldo, const void* aux, int64_t ldaux, hipStream_t stream);
 /* The same with the LDS ring depth chosen by the caller (a tuning entry, as vc_gemm_bf16_cfg):
- * ring 0 = the default (2 k-tiles), 2, or 3 (one more k-tile in flight, one workgroup per CU
- * except at 64 x 128 tiles).  Results are bit-identical for every ring. */
+ * ring 0 = automatic (what vc_conv3d_gemm_bf16 runs: 3 k-tiles when the grid has fewer than two
+ * tiles per CU, else 2), 2, or 3 (one more k-tile in flight, one workgroup per CU except at 64 x 128
+ * tiles).  Results are bit-identical for every ring. */
 int vc_conv3d_gemm_bf16_ring(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_t H, int64_t W, int64_t C,
                              const int* kernel, const int* stride, const int* pad, const uint16_t* zero_row,
                              const uint16_t* Wt, int64_t ldw, int64_t N, const float* bias, int epilogue, void* out,
