@@ -138,7 +138,7 @@ class VivitForVideoClassification(torch.nn.Module):
         # fp16 build only: the patch embedding and the first `precise_layers` layers' GEMMs take split
         # operands -- weights as fp16 high + low parts (and the pixels too in the embedding) through
         # vc_gemm_h16_wrap, A.W_hi + A.W_lo in one fp32 chain.  The fp16 build's logit error is set by
-        # the weight rounding of the first layers (tools/r04/w_probe.py: all weights fp32 3.8e-4, the
+        # the weight rounding of the first layers (tests/analysis/w_probe.py: all weights fp32 3.8e-4, the
         # embedding + layer 0 4.3e-4, vs 1.25e-3 all fp16 on the bench's 8 clips).
         self.precise_layers = 0
 

@@ -1,4 +1,4 @@
-"""[tools experiment, outside the product suite: python -m pytest tools/lstm_gpu/check_lstm.py after
+"""[tools experiment, outside the product suite: python -m pytest tests/analysis/check_lstm.py after
 python tools/lstm_gpu/build.py]  ResNet50-LSTM on the GPU vs oracle/lstm_ref.py (torch's own nn.LSTM for the recurrence; the
 ResNet-50 part restates torchvision, which is absent: UNPINNED there).  Logit tolerance 1e-2."""
 import os
@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "tools", "lstm_gpu"))
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import lstm_model  # noqa: E402
 

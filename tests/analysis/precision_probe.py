@@ -9,7 +9,7 @@ stays fp32.  Rounding points of the HIP forward:
   hid   GELU output (fc2 A operand)
 Reports max |logit - fp32 logit| per configuration on B clips of ViViT-B/16x2 32x224^2.
 
-  python tools/precision_probe.py [--clips 2] [--layers 12]
+  python tests/analysis/precision_probe.py [--clips 2] [--layers 12]
 """
 import argparse
 import itertools
@@ -20,7 +20,7 @@ import time
 import numpy as np
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from oracle.vivit_ref import gelu_fast, layer_norm  # noqa: E402
 from vclip_amd.weights import make_synthetic_clips, make_vivit_weights  # noqa: E402
 

@@ -1,6 +1,6 @@
-"""Which weights set the fp16-operand ViViT-B logit error?  CPU emulation (tools/precision_probe.py's
+"""Which weights set the fp16-operand ViViT-B logit error?  CPU emulation (tests/analysis/precision_probe.py's
 forward): every rounding point fp16, then one weight group at a time kept fp32.
-  python tools/r04/w_probe.py [--clips 8]"""
+  python tests/analysis/w_probe.py [--clips 8]"""
 import argparse
 import os
 import sys
@@ -8,7 +8,7 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "tools"))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import precision_probe as pp  # noqa: E402
 from vclip_amd.weights import make_synthetic_clips, make_vivit_weights  # noqa: E402
 
