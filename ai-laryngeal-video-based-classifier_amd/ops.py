@@ -193,18 +193,23 @@ def gemm_kernel_name(M, N, K, epilogue: str, out, aux=None, cfg: int = -1, f16: 
 
 def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: str, out: torch.Tensor,
          aux: torch.Tensor | None = None, group: int = 0, group_stride: int = 0, group_offset: int = 0,
-         m: int | None = None, cfg: int = -1, flop: float | None = None, op: str = "gemm") -> torch.Tensor:
+         m: int | None = None, cfg: int = -1, flop: float | None = None, op: str = "gemm",
+         nbytes: float | None = None) -> torch.Tensor:
     """out (+)= epilogue(a[:m] @ w.T + bias).  a bf16 [M,K], w bf16 [N,K], bias f32 [N]; or a, w (and the
     16-bit out) fp16 for the inference epilogues (bias / gelu / resid_f32 / embed_f32).  `flop` / `op`:
     the algorithmic work and op name an installed OpRecorder files this launch under (default
-    2 M N K of the operand shapes)."""
+    2 M N K of the operand shapes); `nbytes` instead: the launch is HBM-bound (intensity below the
+    ridge) and is filed under its algorithmic bytes."""
     rec = _REC[0]
     if rec is not None:
         M_ = a.shape[0] if m is None else m
         label = gemm_kernel_name(M_, w.shape[0], a.shape[1], epilogue, out, aux, cfg, a.dtype == torch.float16)
         e0 = rec.begin()
         _gemm(a, w, bias, epilogue, out, aux, group, group_stride, group_offset, m, cfg)
-        rec.end(e0, label, op, 2.0 * M_ * w.shape[0] * a.shape[1] if flop is None else flop, "flop")
+        if nbytes is not None:
+            rec.end(e0, label, op, nbytes, "byte")
+        else:
+            rec.end(e0, label, op, 2.0 * M_ * w.shape[0] * a.shape[1] if flop is None else flop, "flop")
         return out
     return _gemm(a, w, bias, epilogue, out, aux, group, group_stride, group_offset, m, cfg)
 

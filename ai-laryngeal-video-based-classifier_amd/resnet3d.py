@@ -427,8 +427,10 @@ class ResNet3d(torch.nn.Module):
                              op=f"conv_b.s{s + 2}")
                 # conv_c 1x1x1 + BN + skip + ReLU
                 out = act["x"] if xin is not act["x"] else act["x2"]
+                # HBM-bound at every stage (K = inner = 64 .. 512 against a bf16 residual in and a bf16
+                # output: 28 .. 229 flop/B, below the 312 flop/B ridge): filed under its bytes
                 ops.gemm(act["b"][:, :inner], blk["c"][0], blk["c"][1], "bias_resid_relu", out, aux=skip,
-                         flop=2.0 * vol(g) * dout * inner, op=f"conv_c.s{s + 2}")
+                         op=f"conv_c.s{s + 2}", nbytes=2.0 * (vol(g) * (inner + 2 * dout) + dout * inner))
                 x, cin = out, dout
             g_in = g
         return x, B, grids[-1], cin, ws
