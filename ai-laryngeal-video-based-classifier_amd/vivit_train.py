@@ -119,7 +119,8 @@ class TrainEngine:
         self.logits = z(B, c.num_labels, dt=f32)
         # backward scratch
         self.dX = z(Mpad, D, dt=f32)
-        self.dXb = z(Mpad, D)
+        self.dXb = z(Mpad, D)    # bf16 gradient at a block's input (head / layernorm_before backward)
+        self.dXb2 = z(Mpad, D)   # bf16 gradient between the attention and MLP blocks (layernorm_after backward)
         self.dY = z(Mpad, D, dt=f32)
         self.dH = z(Mpad, I)
         self.dO = z(Mpad, D)
@@ -127,6 +128,12 @@ class TrainEngine:
         self.delta = z(B * H * S, dt=f32)
         self.demb = z(Memb, D)
         self.work = z(max(16 * max(I, 3 * D) * D, (512 + 16) * 2 * D, 256 * max(I, 3 * D)), dt=f32)
+        # weight / bias gradients on a side stream, beside the data-gradient chain (split-K tails, the
+        # partial reductions and the column sums fill what the dgrad GEMMs and the attention backward
+        # leave idle); its own split-K scratch.  False: everything on the caller's stream.
+        self.side_wgrad = True
+        self.side = None
+        self.work_side = torch.zeros_like(self.work)
         self.zeros = z(max(I, 3 * D, self.Kemb), dt=f32)
         # packed bf16 weights (forward operand W [N, K] and dgrad operand W^T [K, N]) + packed q|k|v bias
         self.W = [dict(qkv=z(3 * D, D), qkvT=z(D, 3 * D), o=z(D, D), oT=z(D, D), f1=z(I, D), f1T=z(D, I),
@@ -195,29 +202,57 @@ class TrainEngine:
         G = lambda n, shape=None: lay.view(gflat, n, shape)  # noqa: E731
         ready = ready or (lambda *a: None)
         stages = {s[0]: s for s in lay.stages}
-        dX, dXb, dY, dH, dO, dQKV = self.dX, self.dXb, self.dY, self.dH, self.dO, self.dQKV
+        dX, dXa, dXb, dY, dH, dO, dQKV = self.dX, self.dXb, self.dXb2, self.dY, self.dH, self.dO, self.dQKV
+        main = torch.cuda.current_stream(self.device)
+        side_on = self.side_wgrad
+        if side_on and self.side is None:
+            self.side = torch.cuda.Stream(device=self.device)
+        ws = self.work_side if side_on else self.work
+
+        def on_side(fn):
+            """fn() (weight / bias gradients whose operands main has produced by now) on the side
+            stream; returns the event main waits on before it overwrites those operands"""
+            if not side_on:
+                fn()
+                return None
+            self.side.wait_stream(main)
+            with torch.cuda.stream(self.side):
+                fn()
+            e = torch.cuda.Event()
+            e.record(self.side)
+            return e
+
+        def wait(e):
+            if e is not None:
+                main.wait_event(e)
+
         dX.zero_()
-        dXb.zero_()
+        dXa.zero_()
         ops.cls_head_bwd(self.R[2 * self.L], B, S, P("vivit.layernorm.weight"), P("vivit.layernorm.bias"), eps,
-                         P("classifier.weight"), dlogits, dX, dXb, G("classifier.weight"), G("classifier.bias"),
+                         P("classifier.weight"), dlogits, dX, dXa, G("classifier.weight"), G("classifier.bias"),
                          G("vivit.layernorm.weight"), G("vivit.layernorm.bias"))
         ready(*stages["head"])
+        ev_fc1 = ev_o = ev_qkv = None  # the previous (deeper) layer's side work on dH / dXb / dQKV
+        pending = None                 # (side event, stage) of a layer whose gradients are complete there
         for i in reversed(range(self.L)):
             p = f"vivit.layers.{i}."
             W = self.W[i]
             # MLP block: out = R1 + fc2(gelu(fc1(LN2(R1))))
-            ops.gemm(dXb, W["f2T"], self.zeros[:I], "dgelu_tanh", dH, aux=self.Hpre[i])
-            ops.wgrad(dXb, self.Hd[i], G(p + "mlp.fc2.weight"), self.work)
+            wait(ev_fc1)  # dH was read by the previous layer's fc1 weight / bias gradients
+            ops.gemm(dXa, W["f2T"], self.zeros[:I], "dgelu_tanh", dH, aux=self.Hpre[i])
+            ev_fc2 = on_side(lambda: ops.wgrad(dXa, self.Hd[i], G(p + "mlp.fc2.weight"), ws))
             ops.gemm(dH, W["f1T"], self.zeros[:D], "bias_f32", dY)
-            ops.wgrad(dH, self.Y2[i], G(p + "mlp.fc1.weight"), self.work)
-            ops.colsum(dH, G(p + "mlp.fc1.bias"), self.work)
+            ev_fc1 = on_side(lambda: (ops.wgrad(dH, self.Y2[i], G(p + "mlp.fc1.weight"), ws),
+                                      ops.colsum(dH, G(p + "mlp.fc1.bias"), ws)))
             # + the fc2 / o_proj bias gradients: column sums of dX before / after this update
+            wait(ev_o)  # dXb was read by the previous layer's o_proj weight gradient
             ops.layernorm_bwd(dY, self.R[2 * i + 1], P(p + "layernorm_after.weight"), eps, dX, dXb,
                               G(p + "layernorm_after.weight"), G(p + "layernorm_after.bias"), self.work, m=B * S,
                               dsum_in=G(p + "mlp.fc2.bias"), dsum_out=G(p + "attention.o_proj.bias"))
             # attention block: R1 = R0 + o_proj(attn(qkv(LN1(R0))))
             ops.gemm(dXb, W["oT"], self.zeros[:D], "bias", dO)
-            ops.wgrad(dXb, self.O[i], G(p + "attention.o_proj.weight"), self.work)
+            ev_o = on_side(lambda: ops.wgrad(dXb, self.O[i], G(p + "attention.o_proj.weight"), ws))
+            wait(ev_qkv)  # dQKV was read by the previous layer's q|k|v weight / bias gradients
             ev = self.kernel_events  # optional HIP-event timing of the attention backward (bench.py)
             if ev is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -227,13 +262,24 @@ class TrainEngine:
                 e1.record()
                 ev.append((e0, e1))
             ops.gemm(dQKV, W["qkvT"], self.zeros[:D], "bias_f32", dY)
-            ops.wgrad(dQKV, self.Y1[i], lay.span(gflat, p + "attention.q_proj.weight", 3 * D * D, (3 * D, D)),
-                      self.work, nscaled=D, scale=qs)
-            ops.colsum(dQKV, lay.span(gflat, p + "attention.q_proj.bias", 3 * D, (3 * D,)), self.work,
-                       nscaled=D, scale=qs)
-            ops.layernorm_bwd(dY, self.R[2 * i], P(p + "layernorm_before.weight"), eps, dX, dXb,
+            ev_qkv = on_side(lambda: (
+                ops.wgrad(dQKV, self.Y1[i], lay.span(gflat, p + "attention.q_proj.weight", 3 * D * D, (3 * D, D)),
+                          ws, nscaled=D, scale=qs),
+                ops.colsum(dQKV, lay.span(gflat, p + "attention.q_proj.bias", 3 * D, (3 * D,)), ws,
+                           nscaled=D, scale=qs)))
+            wait(ev_fc2)  # dXa was read by this layer's fc2 weight gradient
+            ops.layernorm_bwd(dY, self.R[2 * i], P(p + "layernorm_before.weight"), eps, dX, dXa,
                               G(p + "layernorm_before.weight"), G(p + "layernorm_before.bias"), self.work, m=B * S)
-            ready(*stages[f"layer{i}"])
+            # a layer's gradients are announced one layer later, when its side work has long finished
+            if pending is not None:
+                wait(pending[0])
+                ready(*pending[1])
+            pending = (ev_qkv, stages[f"layer{i}"])
+        if pending is not None:
+            wait(pending[0])
+            ready(*pending[1])
+        if side_on:
+            main.wait_stream(self.side)
         gpos = G("vivit.embeddings.position_embeddings").view(S, D)
         ops.embed_bwd(dX, B, S, gpos, G("vivit.embeddings.cls_token").view(D), self.demb)
         ops.wgrad(self.demb, self.A_emb, G("vivit.embeddings.patch_embeddings.projection.weight", (D, self.Kemb)),

@@ -155,6 +155,26 @@ def test_train_step_deterministic():
     assert torch.equal(gs[0], gs[1])
 
 
+def test_train_step_side_stream_wgrad_bit_identical():
+    """Weight / bias gradients on the side stream (the default) == everything on one stream: the same
+    kernels on the same operands, so bit-identical gradients; run twice so the side stream's event
+    waits are exercised across steps too."""
+    model, sd, pix, labels = _setup(SMALL, 2)
+    x, y = pix.to(DEV), labels.to(DEV)
+    gs = {}
+    for side in (False, True, True):
+        model.zero_grad(set_to_none=True)
+        model(pixel_values=x)  # the engine exists after one forward
+        eng = model._train_engine(x.shape[0], x.device)
+        eng.side_wgrad = side
+        model.zero_grad(set_to_none=True)
+        torch.nn.functional.cross_entropy(model(pixel_values=x).logits, y).backward()
+        torch.cuda.synchronize()
+        gs.setdefault(side, []).append(model._gflat.clone())
+    assert torch.equal(gs[False][0], gs[True][0])
+    assert torch.equal(gs[True][0], gs[True][1])
+
+
 # BASELINE configs[4]'s own geometry: ViViT-B/16x2 (12 layers, S = 3137, D = 768, 12 heads), 32x224^2,
 # 4 clips per GPU (the reference CLI's --batch_size 4, vivit_transformer/main.py:47)
 VIVIT_B = dict(WIDE, num_hidden_layers=12)
