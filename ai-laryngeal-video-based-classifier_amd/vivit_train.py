@@ -134,6 +134,9 @@ class TrainEngine:
         self.side_wgrad = True
         self.side = None
         self.work_side = torch.zeros_like(self.work)
+        # cap on the split-K factor of the side-stream weight gradients (None: vc_wgrad_bf16's own
+        # ~one-workgroup-per-CU choice); the scratch handed over bounds the splits
+        self.wgrad_max_splits = None
         self.zeros = z(max(I, 3 * D, self.Kemb), dt=f32)
         # packed bf16 weights (forward operand W [N, K] and dgrad operand W^T [K, N]) + packed q|k|v bias
         self.W = [dict(qkv=z(3 * D, D), qkvT=z(D, 3 * D), o=z(D, D), oT=z(D, D), f1=z(I, D), f1T=z(D, I),
@@ -207,7 +210,19 @@ class TrainEngine:
         side_on = self.side_wgrad
         if side_on and self.side is None:
             self.side = torch.cuda.Stream(device=self.device)
-        ws = self.work_side if side_on else self.work
+        ws0 = self.work_side if side_on else self.work
+
+        class _WS:  # the split-K scratch of one weight gradient, capped at wgrad_max_splits partials
+            def __init__(s2, cap):
+                s2.cap = cap
+
+            def __call__(s2, out):
+                if s2.cap is None:
+                    return ws0
+                return ws0[: min(ws0.numel(), max(2, s2.cap) * out.numel())]
+
+        wsf = _WS(self.wgrad_max_splits)
+        ws = ws0
 
         def on_side(fn):
             """fn() (weight / bias gradients whose operands main has produced by now) on the side
@@ -240,9 +255,9 @@ class TrainEngine:
             # MLP block: out = R1 + fc2(gelu(fc1(LN2(R1))))
             wait(ev_fc1)  # dH was read by the previous layer's fc1 weight / bias gradients
             ops.gemm(dXa, W["f2T"], self.zeros[:I], "dgelu_tanh", dH, aux=self.Hpre[i])
-            ev_fc2 = on_side(lambda: ops.wgrad(dXa, self.Hd[i], G(p + "mlp.fc2.weight"), ws))
+            ev_fc2 = on_side(lambda: ops.wgrad(dXa, self.Hd[i], G(p + "mlp.fc2.weight"), wsf(G(p + "mlp.fc2.weight"))))
             ops.gemm(dH, W["f1T"], self.zeros[:D], "bias_f32", dY)
-            ev_fc1 = on_side(lambda: (ops.wgrad(dH, self.Y2[i], G(p + "mlp.fc1.weight"), ws),
+            ev_fc1 = on_side(lambda: (ops.wgrad(dH, self.Y2[i], G(p + "mlp.fc1.weight"), wsf(G(p + "mlp.fc1.weight"))),
                                       ops.colsum(dH, G(p + "mlp.fc1.bias"), ws)))
             # + the fc2 / o_proj bias gradients: column sums of dX before / after this update
             wait(ev_o)  # dXb was read by the previous layer's o_proj weight gradient
@@ -251,7 +266,7 @@ class TrainEngine:
                               dsum_in=G(p + "mlp.fc2.bias"), dsum_out=G(p + "attention.o_proj.bias"))
             # attention block: R1 = R0 + o_proj(attn(qkv(LN1(R0))))
             ops.gemm(dXb, W["oT"], self.zeros[:D], "bias", dO)
-            ev_o = on_side(lambda: ops.wgrad(dXb, self.O[i], G(p + "attention.o_proj.weight"), ws))
+            ev_o = on_side(lambda: ops.wgrad(dXb, self.O[i], G(p + "attention.o_proj.weight"), wsf(G(p + "attention.o_proj.weight"))))
             wait(ev_qkv)  # dQKV was read by the previous layer's q|k|v weight / bias gradients
             ev = self.kernel_events  # optional HIP-event timing of the attention backward (bench.py)
             if ev is not None:
@@ -264,7 +279,8 @@ class TrainEngine:
             ops.gemm(dQKV, W["qkvT"], self.zeros[:D], "bias_f32", dY)
             ev_qkv = on_side(lambda: (
                 ops.wgrad(dQKV, self.Y1[i], lay.span(gflat, p + "attention.q_proj.weight", 3 * D * D, (3 * D, D)),
-                          ws, nscaled=D, scale=qs),
+                          wsf(lay.span(gflat, p + "attention.q_proj.weight", 3 * D * D, (3 * D, D))), nscaled=D,
+                          scale=qs),
                 ops.colsum(dQKV, lay.span(gflat, p + "attention.q_proj.bias", 3 * D, (3 * D,)), ws,
                            nscaled=D, scale=qs)))
             wait(ev_fc2)  # dXa was read by this layer's fc2 weight gradient

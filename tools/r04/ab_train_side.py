@@ -1,7 +1,10 @@
-"""Interleaved A/B of the ViViT-B train step (32x224^2, B clips, the reference loop with vclip AdamW):
-weight / bias gradients on a side stream (TrainEngine.side_wgrad) vs one stream, in one process.
-  python tools/r04/ab_train_side.py [--B 4] [--rounds 6] [--steps 5]"""
+"""Interleaved A/B of the ViViT-B train step (32x224^2, B clips, the reference loop with vclip AdamW)
+over TrainEngine settings, in one process; default arms: weight / bias gradients on a side stream
+(side_wgrad) vs one stream.
+  python tools/r04/ab_train_side.py ['{"side_wgrad": false}' '{"side_wgrad": true, "wgrad_max_splits": 4}' ...]
+                                    [--B 4] [--rounds 6] [--steps 5]"""
 import argparse
+import json
 import os
 import sys
 import time
@@ -15,6 +18,7 @@ from vclip_amd.vivit import create_model  # noqa: E402
 from vclip_amd.weights import make_synthetic_clips  # noqa: E402
 
 ap = argparse.ArgumentParser()
+ap.add_argument("arms", nargs="*", default=['{"side_wgrad": false}', '{"side_wgrad": true}'])
 ap.add_argument("--B", type=int, default=4)
 ap.add_argument("--rounds", type=int, default=6)
 ap.add_argument("--steps", type=int, default=5)
@@ -36,17 +40,19 @@ def step():
 
 step()
 eng = model._engine
-res = {False: [], True: []}
+arms = [json.loads(x) for x in a.arms]
+res = [[] for _ in arms]
 for r in range(a.rounds):
-    for side in ((False, True) if r % 2 == 0 else (True, False)):
-        eng.side_wgrad = side
+    for i in (range(len(arms)) if r % 2 == 0 else reversed(range(len(arms)))):
+        for k, v in arms[i].items():
+            setattr(eng, k, v)
         step()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(a.steps):
             step()
         torch.cuda.synchronize()
-        res[side].append((time.perf_counter() - t0) / a.steps * 1e3)
-for side, t in res.items():
-    print(f"side_wgrad={side}: median {np.median(t):.3f} ms/step  min {min(t):.3f}  ({a.B / np.median(t) * 1e3:.1f} clips/s)",
+        res[i].append((time.perf_counter() - t0) / a.steps * 1e3)
+for arm, t in zip(a.arms, res):
+    print(f"{arm}: median {np.median(t):.3f} ms/step  min {min(t):.3f}  ({a.B / np.median(t) * 1e3:.1f} clips/s)",
           flush=True)
