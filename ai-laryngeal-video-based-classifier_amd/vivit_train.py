@@ -134,9 +134,11 @@ class TrainEngine:
         self.side_wgrad = True
         self.side = None
         self.work_side = torch.zeros_like(self.work)
-        # cap on the split-K factor of the side-stream weight gradients (None: vc_wgrad_bf16's own
-        # ~one-workgroup-per-CU choice); the scratch handed over bounds the splits
-        self.wgrad_max_splits = None
+        # cap on the split-K factor of the weight gradients (None: vc_wgrad_bf16's own ~one-workgroup-
+        # per-CU choice, 10 - 28 partials here); the scratch handed over bounds the splits.  Beside the
+        # data-gradient chain fewer, longer workgroups win: 4 -> 214.3 clips/s vs 205.7 uncapped, 208.1
+        # at 8, 206.4 at 2 (tools/r04/ab_train_side.py, one process, round 4)
+        self.wgrad_max_splits = 4
         self.zeros = z(max(I, 3 * D, self.Kemb), dt=f32)
         # packed bf16 weights (forward operand W [N, K] and dgrad operand W^T [K, N]) + packed q|k|v bias
         self.W = [dict(qkv=z(3 * D, D), qkvT=z(D, 3 * D), o=z(D, D), oT=z(D, D), f1=z(I, D), f1T=z(D, I),
