@@ -97,6 +97,8 @@ SIGNATURES = {
     "vc_attention_fwd_lse": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_int, c_p, c_i64, c_p, c_p], c_int),
     "vc_attention_bwd": ([c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p],
                          c_int),
+    "vc_attention_bwd_2s": ([c_p, c_i64, c_p, c_i64, c_p, c_i64, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p,
+                             c_p], c_int),
     "vc_layernorm_bwd": ([c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_f, c_p, c_i64, c_p, c_i64, c_p, c_p, c_p, c_p,
                           c_p, c_i64, c_p], c_int),
     "vc_colsum": ([c_p, c_int, c_i64, c_i64, c_i64, c_i64, c_f, c_p, c_p, c_i64, c_p], c_int),

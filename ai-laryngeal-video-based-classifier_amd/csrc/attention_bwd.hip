@@ -439,6 +439,11 @@ attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const uint16_t*
 using namespace vc;
 using namespace vc::abwd;
 
+extern "C" int vc_attention_bwd_2s(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ldo,
+                                   const uint16_t* dout, int64_t lddo, const float* lse, float* delta, int64_t B,
+                                   int64_t S, int64_t H, int64_t head_dim, uint16_t* dqkv, int64_t lddq,
+                                   hipStream_t stream, hipStream_t stream2);
+
 extern "C" int vc_attention_bwd(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ldo, const uint16_t* dout,
                                 int64_t lddo, const float* lse, float* delta, int64_t B, int64_t S, int64_t H,
                                 int64_t head_dim, uint16_t* dqkv, int64_t lddq, hipStream_t stream) {
@@ -451,10 +456,50 @@ extern "C" int vc_attention_bwd(const uint16_t* qkv, int64_t ld, const uint16_t*
          ((uintptr_t)delta)) & 15)
         return fail(VC_ERR_INVALID_ARG, "vc_attention_bwd: pointers must be 16-byte aligned");
     if (B * H > 65535 || S > (1 << 24)) return fail(VC_ERR_INVALID_ARG, "vc_attention_bwd: grid too large");
+    return vc_attention_bwd_2s(qkv, ld, out, ldo, dout, lddo, lse, delta, B, S, H, head_dim, dqkv, lddq, stream, nullptr);
+}
+
+// dK/dV and dQ write disjoint column ranges of dqkv from the same inputs: with a second stream the
+// dQ kernel runs beside dK/dV (its workgroups fill the other's last partial round), and `stream`
+// waits for it before returning
+extern "C" int vc_attention_bwd_2s(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ldo,
+                                   const uint16_t* dout, int64_t lddo, const float* lse, float* delta, int64_t B,
+                                   int64_t S, int64_t H, int64_t head_dim, uint16_t* dqkv, int64_t lddq,
+                                   hipStream_t stream, hipStream_t stream2) {
+    if (!qkv || !out || !dout || !lse || !delta || !dqkv) return fail(VC_ERR_INVALID_ARG, "vc_attention_bwd: null pointer");
+    if (head_dim != 64) return fail(VC_ERR_UNSUPPORTED, "vc_attention_bwd: head_dim must be 64");
+    if (B <= 0 || S <= 0 || H <= 0 || ld < 3 * H * 64 || lddq < 3 * H * 64 || ldo < H * 64 || lddo < H * 64 ||
+        ld % 8 || ldo % 8 || lddo % 8 || lddq % 8)
+        return fail(VC_ERR_INVALID_ARG, "vc_attention_bwd: bad shape / leading dimension");
+    if ((((uintptr_t)qkv) | ((uintptr_t)out) | ((uintptr_t)dout) | ((uintptr_t)dqkv) | ((uintptr_t)lse) |
+         ((uintptr_t)delta)) & 15)
+        return fail(VC_ERR_INVALID_ARG, "vc_attention_bwd: pointers must be 16-byte aligned");
+    if (B * H > 65535 || S > (1 << 24)) return fail(VC_ERR_INVALID_ARG, "vc_attention_bwd: grid too large");
     const int64_t n = B * S * H;
     attn_bwd_prep_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(dout, lddo, out, ldo, n, (int)S, (int)H, delta);
     const dim3 grid((unsigned)((S + 127) / 128), (unsigned)(B * H));
+    const bool two = stream2 != nullptr && stream2 != stream;
+    hipEvent_t e_prep = nullptr, e_dq = nullptr;
+    if (two) {
+        hipError_t e = hipEventCreateWithFlags(&e_prep, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&e_dq, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventRecord(e_prep, stream);
+        if (e == hipSuccess) e = hipStreamWaitEvent(stream2, e_prep, 0);
+        if (e != hipSuccess) {
+            if (e_prep) (void)hipEventDestroy(e_prep);
+            if (e_dq) (void)hipEventDestroy(e_dq);
+            return fail((int)e, std::string("vc_attention_bwd_2s: event: ") + hipGetErrorString(e));
+        }
+    }
     attn_bwd_dkdv_kernel<<<grid, 256, 0, stream>>>(qkv, ld, dout, lddo, lse, delta, (int)S, (int)H, dqkv, lddq);
-    attn_bwd_dq_kernel<<<grid, 256, 0, stream>>>(qkv, ld, dout, lddo, lse, delta, (int)S, (int)H, dqkv, lddq);
+    attn_bwd_dq_kernel<<<grid, 256, 0, two ? stream2 : stream>>>(qkv, ld, dout, lddo, lse, delta, (int)S, (int)H, dqkv,
+                                                                 lddq);
+    if (two) {
+        hipError_t e = hipEventRecord(e_dq, stream2);
+        if (e == hipSuccess) e = hipStreamWaitEvent(stream, e_dq, 0);
+        (void)hipEventDestroy(e_prep);  // released once complete
+        (void)hipEventDestroy(e_dq);
+        if (e != hipSuccess) return fail((int)e, std::string("vc_attention_bwd_2s: event: ") + hipGetErrorString(e));
+    }
     return check_launch("vc_attention_bwd");
 }

@@ -719,8 +719,10 @@ def attention_fwd_lse(qkv: torch.Tensor, B: int, S: int, H: int, out: torch.Tens
 
 
 def attention_bwd(qkv: torch.Tensor, out: torch.Tensor, dout: torch.Tensor, lse: torch.Tensor, delta: torch.Tensor,
-                  B: int, S: int, H: int, dqkv: torch.Tensor) -> torch.Tensor:
-    """dqkv (q part = dL/dq' of the stored pre-scaled q', then dk, dv) of the joint attention."""
+                  B: int, S: int, H: int, dqkv: torch.Tensor, stream2: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """dqkv (q part = dL/dq' of the stored pre-scaled q', then dk, dv) of the joint attention.
+    `stream2`: the dQ kernel runs there beside dK/dV (vc_attention_bwd_2s); the current stream waits
+    for it before anything enqueued after this call."""
     _dev(qkv, out, dout, lse, delta, dqkv)
     for t, nm in ((qkv, "qkv"), (out, "out"), (dout, "dout"), (dqkv, "dqkv")):
         _need(t.dtype == torch.bfloat16 and t.stride(1) == 1, f"attention_bwd: {nm} bf16 with unit column stride")
@@ -731,6 +733,10 @@ def attention_bwd(qkv: torch.Tensor, out: torch.Tensor, dout: torch.Tensor, lse:
     _need(out.shape[0] >= B * S and dqkv.shape[0] >= B * S, "attention_bwd rows")
     _need(qkv.shape[1] >= 3 * H * 64 and dqkv.shape[1] >= 3 * H * 64 and out.shape[1] >= H * 64 and
           dout.shape[1] >= H * 64, "attention_bwd columns")
+    if stream2 is not None:
+        _lib.call("vc_attention_bwd_2s", _p(qkv), qkv.stride(0), _p(out), out.stride(0), _p(dout), dout.stride(0),
+                  _p(lse), _p(delta), B, S, H, 64, _p(dqkv), dqkv.stride(0), _stream(qkv), stream2.cuda_stream)
+        return dqkv
     _lib.call("vc_attention_bwd", _p(qkv), qkv.stride(0), _p(out), out.stride(0), _p(dout), dout.stride(0), _p(lse),
               _p(delta), B, S, H, 64, _p(dqkv), dqkv.stride(0), _stream(qkv))
     return dqkv

@@ -139,6 +139,9 @@ class TrainEngine:
         # data-gradient chain fewer, longer workgroups win: 4 -> 214.3 clips/s vs 205.7 uncapped, 208.1
         # at 8, 206.4 at 2 (tools/r04/ab_train_side.py, one process, round 4)
         self.wgrad_max_splits = 4
+        # the attention backward's dQ kernel on a stream of its own beside dK/dV (vc_attention_bwd_2s)
+        self.attn_bwd_2s = True
+        self.side_dq = None
         self.zeros = z(max(I, 3 * D, self.Kemb), dt=f32)
         # packed bf16 weights (forward operand W [N, K] and dgrad operand W^T [K, N]) + packed q|k|v bias
         self.W = [dict(qkv=z(3 * D, D), qkvT=z(D, 3 * D), o=z(D, D), oT=z(D, D), f1=z(I, D), f1T=z(D, I),
@@ -274,7 +277,10 @@ class TrainEngine:
             if ev is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-            ops.attention_bwd(self.QKV[i], self.O[i], dO, self.LSE[i], self.delta, B, S, H, dQKV)
+            if self.attn_bwd_2s and self.side_dq is None:
+                self.side_dq = torch.cuda.Stream(device=self.device)
+            ops.attention_bwd(self.QKV[i], self.O[i], dO, self.LSE[i], self.delta, B, S, H, dQKV,
+                              stream2=self.side_dq if self.attn_bwd_2s else None)
             if ev is not None:
                 e1.record()
                 ev.append((e0, e1))

@@ -516,6 +516,12 @@ int vc_attention_fwd_lse(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, 
 int vc_attention_bwd(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ldo, const uint16_t* dout,
                      int64_t lddo, const float* lse, float* delta, int64_t B, int64_t S, int64_t H, int64_t head_dim,
                      uint16_t* dqkv, int64_t lddq, hipStream_t stream);
+/* The same with the dQ kernel on a second stream beside dK/dV (disjoint outputs, same inputs);
+ * `stream` waits for it before the call returns, so later work on `stream` sees all of dqkv.
+ * stream2 NULL or == stream: vc_attention_bwd. */
+int vc_attention_bwd_2s(const uint16_t* qkv, int64_t ld, const uint16_t* out, int64_t ldo, const uint16_t* dout,
+                        int64_t lddo, const float* lse, float* delta, int64_t B, int64_t S, int64_t H,
+                        int64_t head_dim, uint16_t* dqkv, int64_t lddq, hipStream_t stream, hipStream_t stream2);
 
 /*
  * LayerNorm backward fused with the residual-gradient add (nn.LayerNorm layernorm_before /

@@ -156,7 +156,8 @@ def test_train_step_deterministic():
 
 
 def test_train_step_side_stream_wgrad_bit_identical():
-    """Weight / bias gradients on the side stream (the default) == everything on one stream: the same
+    """Weight / bias gradients on the side stream and the attention backward's dQ on a third (the
+    defaults) == everything on one stream: the same
     kernels on the same operands, so bit-identical gradients; run twice so the side stream's event
     waits are exercised across steps too."""
     model, sd, pix, labels = _setup(SMALL, 2)
@@ -167,6 +168,7 @@ def test_train_step_side_stream_wgrad_bit_identical():
         model(pixel_values=x)  # the engine exists after one forward
         eng = model._train_engine(x.shape[0], x.device)
         eng.side_wgrad = side
+        eng.attn_bwd_2s = side  # the dQ kernel on its own stream (vc_attention_bwd_2s)
         model.zero_grad(set_to_none=True)
         torch.nn.functional.cross_entropy(model(pixel_values=x).logits, y).backward()
         torch.cuda.synchronize()
