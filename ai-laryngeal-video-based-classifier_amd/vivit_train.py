@@ -142,6 +142,9 @@ class TrainEngine:
         # the attention backward's dQ kernel on a stream of its own beside dK/dV (vc_attention_bwd_2s)
         self.attn_bwd_2s = True
         self.side_dq = None
+        # tile-configuration overrides of the backward's data-gradient GEMMs (vc_gemm_bf16_cfg; name ->
+        # cfg): "dgelu" (fc2^T with the gelu' epilogue), "dfc1" (fc1^T), "do" (o_proj^T), "dqkv" (q|k|v^T)
+        self.gemm_cfg = {}
         self.zeros = z(max(I, 3 * D, self.Kemb), dt=f32)
         # packed bf16 weights (forward operand W [N, K] and dgrad operand W^T [K, N]) + packed q|k|v bias
         self.W = [dict(qkv=z(3 * D, D), qkvT=z(D, 3 * D), o=z(D, D), oT=z(D, D), f1=z(I, D), f1T=z(D, I),
@@ -246,6 +249,8 @@ class TrainEngine:
             if e is not None:
                 main.wait_event(e)
 
+        gc = lambda name: self.gemm_cfg.get(name, -1)  # noqa: E731
+
         dX.zero_()
         dXa.zero_()
         ops.cls_head_bwd(self.R[2 * self.L], B, S, P("vivit.layernorm.weight"), P("vivit.layernorm.bias"), eps,
@@ -259,9 +264,9 @@ class TrainEngine:
             W = self.W[i]
             # MLP block: out = R1 + fc2(gelu(fc1(LN2(R1))))
             wait(ev_fc1)  # dH was read by the previous layer's fc1 weight / bias gradients
-            ops.gemm(dXa, W["f2T"], self.zeros[:I], "dgelu_tanh", dH, aux=self.Hpre[i])
+            ops.gemm(dXa, W["f2T"], self.zeros[:I], "dgelu_tanh", dH, aux=self.Hpre[i], cfg=gc("dgelu"))
             ev_fc2 = on_side(lambda: ops.wgrad(dXa, self.Hd[i], G(p + "mlp.fc2.weight"), wsf(G(p + "mlp.fc2.weight"))))
-            ops.gemm(dH, W["f1T"], self.zeros[:D], "bias_f32", dY)
+            ops.gemm(dH, W["f1T"], self.zeros[:D], "bias_f32", dY, cfg=gc("dfc1"))
             ev_fc1 = on_side(lambda: (ops.wgrad(dH, self.Y2[i], G(p + "mlp.fc1.weight"), wsf(G(p + "mlp.fc1.weight"))),
                                       ops.colsum(dH, G(p + "mlp.fc1.bias"), ws)))
             # + the fc2 / o_proj bias gradients: column sums of dX before / after this update
@@ -270,7 +275,7 @@ class TrainEngine:
                               G(p + "layernorm_after.weight"), G(p + "layernorm_after.bias"), self.work, m=B * S,
                               dsum_in=G(p + "mlp.fc2.bias"), dsum_out=G(p + "attention.o_proj.bias"))
             # attention block: R1 = R0 + o_proj(attn(qkv(LN1(R0))))
-            ops.gemm(dXb, W["oT"], self.zeros[:D], "bias", dO)
+            ops.gemm(dXb, W["oT"], self.zeros[:D], "bias", dO, cfg=gc("do"))
             ev_o = on_side(lambda: ops.wgrad(dXb, self.O[i], G(p + "attention.o_proj.weight"), wsf(G(p + "attention.o_proj.weight"))))
             wait(ev_qkv)  # dQKV was read by the previous layer's q|k|v weight / bias gradients
             ev = self.kernel_events  # optional HIP-event timing of the attention backward (bench.py)
@@ -284,7 +289,7 @@ class TrainEngine:
             if ev is not None:
                 e1.record()
                 ev.append((e0, e1))
-            ops.gemm(dQKV, W["qkvT"], self.zeros[:D], "bias_f32", dY)
+            ops.gemm(dQKV, W["qkvT"], self.zeros[:D], "bias_f32", dY, cfg=gc("dqkv"))
             ev_qkv = on_side(lambda: (
                 ops.wgrad(dQKV, self.Y1[i], lay.span(gflat, p + "attention.q_proj.weight", 3 * D * D, (3 * D, D)),
                           wsf(lay.span(gflat, p + "attention.q_proj.weight", 3 * D * D, (3 * D, D))), nscaled=D,
