@@ -222,12 +222,13 @@ class TrainEngine:
 
         class _WS:  # the split-K scratch of one weight gradient, capped at wgrad_max_splits partials
             def __init__(s2, cap):
-                s2.cap = cap
+                s2.cap = cap  # int, or {"fc2" | "fc1" | "o" | "qkv": int} (absent: 4)
 
-            def __call__(s2, out):
-                if s2.cap is None:
+            def __call__(s2, out, name):
+                cap = s2.cap.get(name, 4) if isinstance(s2.cap, dict) else s2.cap
+                if cap is None:
                     return ws0
-                return ws0[: min(ws0.numel(), max(2, s2.cap) * out.numel())]
+                return ws0[: min(ws0.numel(), max(2, cap) * out.numel())]
 
         wsf = _WS(self.wgrad_max_splits)
         ws = ws0
@@ -265,9 +266,9 @@ class TrainEngine:
             # MLP block: out = R1 + fc2(gelu(fc1(LN2(R1))))
             wait(ev_fc1)  # dH was read by the previous layer's fc1 weight / bias gradients
             ops.gemm(dXa, W["f2T"], self.zeros[:I], "dgelu_tanh", dH, aux=self.Hpre[i], cfg=gc("dgelu"))
-            ev_fc2 = on_side(lambda: ops.wgrad(dXa, self.Hd[i], G(p + "mlp.fc2.weight"), wsf(G(p + "mlp.fc2.weight"))))
+            ev_fc2 = on_side(lambda: ops.wgrad(dXa, self.Hd[i], G(p + "mlp.fc2.weight"), wsf(G(p + "mlp.fc2.weight"), "fc2")))
             ops.gemm(dH, W["f1T"], self.zeros[:D], "bias_f32", dY, cfg=gc("dfc1"))
-            ev_fc1 = on_side(lambda: (ops.wgrad(dH, self.Y2[i], G(p + "mlp.fc1.weight"), wsf(G(p + "mlp.fc1.weight"))),
+            ev_fc1 = on_side(lambda: (ops.wgrad(dH, self.Y2[i], G(p + "mlp.fc1.weight"), wsf(G(p + "mlp.fc1.weight"), "fc1")),
                                       ops.colsum(dH, G(p + "mlp.fc1.bias"), ws)))
             # + the fc2 / o_proj bias gradients: column sums of dX before / after this update
             wait(ev_o)  # dXb was read by the previous layer's o_proj weight gradient
@@ -276,7 +277,7 @@ class TrainEngine:
                               dsum_in=G(p + "mlp.fc2.bias"), dsum_out=G(p + "attention.o_proj.bias"))
             # attention block: R1 = R0 + o_proj(attn(qkv(LN1(R0))))
             ops.gemm(dXb, W["oT"], self.zeros[:D], "bias", dO, cfg=gc("do"))
-            ev_o = on_side(lambda: ops.wgrad(dXb, self.O[i], G(p + "attention.o_proj.weight"), wsf(G(p + "attention.o_proj.weight"))))
+            ev_o = on_side(lambda: ops.wgrad(dXb, self.O[i], G(p + "attention.o_proj.weight"), wsf(G(p + "attention.o_proj.weight"), "o")))
             wait(ev_qkv)  # dQKV was read by the previous layer's q|k|v weight / bias gradients
             ev = self.kernel_events  # optional HIP-event timing of the attention backward (bench.py)
             if ev is not None:
@@ -292,7 +293,7 @@ class TrainEngine:
             ops.gemm(dQKV, W["qkvT"], self.zeros[:D], "bias_f32", dY, cfg=gc("dqkv"))
             ev_qkv = on_side(lambda: (
                 ops.wgrad(dQKV, self.Y1[i], lay.span(gflat, p + "attention.q_proj.weight", 3 * D * D, (3 * D, D)),
-                          wsf(lay.span(gflat, p + "attention.q_proj.weight", 3 * D * D, (3 * D, D))), nscaled=D,
+                          wsf(lay.span(gflat, p + "attention.q_proj.weight", 3 * D * D, (3 * D, D)), "qkv"), nscaled=D,
                           scale=qs),
                 ops.colsum(dQKV, lay.span(gflat, p + "attention.q_proj.bias", 3 * D, (3 * D,)), ws,
                            nscaled=D, scale=qs)))
