@@ -1813,7 +1813,7 @@ extern "C" int vc_conv3d_gemm_bf16_ring(const uint16_t* x, int64_t ldx, int64_t 
         return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16_ring: ring must be 0, 2 or 3");
     // ring 0 (automatic): a 3-deep ring when the grid has fewer tiles than two per CU (the workgroups
     // are few, so each one's DMA latency is exposed; ResNet3D res4 / res5 at B = 4: +1.1 / +1.5 % of
-    // the forward each), else 2 (res2 / res3: -3.7 / -2.5 %), tools/r04/ab_resnet3d_ring.py, round 4
+    // the forward each), else 2 (res2 / res3: -3.7 / -2.5 %), tools/ab_resnet3d_ring.py, round 4
     auto pick_ring = [&](int64_t tiles) { return ring ? ring : (tiles < 2 * (int64_t)num_cus() ? 3 : 2); };
     if (!x || !kernel || !stride || !pad || !zero_row || !Wt || !bias || !out)
         return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: null pointer");

@@ -576,6 +576,20 @@ def conv3d_im2col(x: torch.Tensor, kind: str, B: int, grid, C: int, kernel, stri
 _ZERO_ROW = {}
 
 
+def zero_row(device) -> torch.Tensor:
+    """The shared 64-element zero bf16 row the implicit convolutions read for padding taps (one per
+    device).  Created once, on the caller's stream, which is then waited for: a split forward's parts
+    read it from side streams that are ordered only after the caller's stream, so a zero-fill queued on
+    one part's stream could still be pending when another part's first conv reads it."""
+    z = _ZERO_ROW.get(device)
+    if z is None:
+        z = torch.zeros(64, dtype=torch.bfloat16, device=device)
+        if not torch.cuda.is_current_stream_capturing():
+            torch.cuda.current_stream(device).synchronize()
+        _ZERO_ROW[device] = z
+    return z
+
+
 def conv3d_gemm(x: torch.Tensor, B: int, grid, C: int, kernel, stride, pad, w: torch.Tensor, bias: torch.Tensor,
                 epilogue: str, out: torch.Tensor, aux: torch.Tensor | None = None, flop: float | None = None,
                 op: str = "conv", n: int | None = None, ring: int = 0) -> torch.Tensor:
@@ -598,11 +612,11 @@ def conv3d_gemm(x: torch.Tensor, B: int, grid, C: int, kernel, stride, pad, w: t
           out.shape[1] >= N, "conv3d_gemm out rows (a multiple of the tile height)")
     e = EPI[epilogue]
     if e == 7:
-        _need(aux is not None and aux.dtype == torch.bfloat16 and aux.stride(1) == 1 and aux.shape[0] >= M and
-              aux.shape[1] >= N, "conv3d_gemm residual")
-    key = x.device
-    if key not in _ZERO_ROW:
-        _ZERO_ROW[key] = torch.zeros(64, dtype=torch.bfloat16, device=x.device)
+        # the tile epilogue reads the residual for every row of the padded tile
+        _need(aux is not None and aux.dtype == torch.bfloat16 and aux.stride(1) == 1 and
+              aux.shape[0] >= (M + rt - 1) // rt * rt and aux.shape[1] >= N,
+              "conv3d_gemm residual (rows up to the tile-height multiple of the output rows)")
+    zrow = zero_row(x.device)
     k, s, p = ((ctypes.c_int * 3)(*v) for v in (kernel, stride, pad))
     rec = _REC[0]
     if rec is not None:
@@ -618,7 +632,7 @@ def conv3d_gemm(x: torch.Tensor, B: int, grid, C: int, kernel, stride, pad, w: t
         label = f"conv_gemm_kernel<{tile}, {e}, {st}, 0>"
     e0 = rec.begin() if rec is not None else None
     _lib.call("vc_conv3d_gemm_bf16_ring", _p(x), x.stride(0), B, T, H, W, C, ctypes.addressof(k), ctypes.addressof(s),
-              ctypes.addressof(p), _p(_ZERO_ROW[key]), _p(w), w.stride(0), N, _p(bias), e, _p(out), out.stride(0),
+              ctypes.addressof(p), _p(zrow), _p(w), w.stride(0), N, _p(bias), e, _p(out), out.stride(0),
               _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0, ring, _stream(x))
     if rec is not None:
         rec.end(e0, label, op, 2.0 * M * N * kvol * C if flop is None else flop, "flop")
@@ -657,15 +671,13 @@ def conv3d_stem_gemm(xp: torch.Tensor, B: int, grid, kernel, stride, pad, w: tor
           bias.numel() >= N and bias.dtype == torch.float32, "conv3d_stem_gemm weights")
     _need(out.dtype == torch.bfloat16 and out.stride(1) == 1 and out.shape[0] >= (M + rt - 1) // rt * rt and
           out.shape[1] >= N, "conv3d_stem_gemm out")
-    key = xp.device
-    if key not in _ZERO_ROW:
-        _ZERO_ROW[key] = torch.zeros(64, dtype=torch.bfloat16, device=xp.device)
+    zrow = zero_row(xp.device)
     k, s, p = ((ctypes.c_int * 3)(*v) for v in (kernel, stride, pad))
     rec = _REC[0]
     e0 = rec.begin() if rec is not None else None
     e = EPI[epilogue]
     _lib.call("vc_conv3d_stem_gemm_bf16", _p(xp), B, T, H, W, ctypes.addressof(k), ctypes.addressof(s),
-              ctypes.addressof(p), _p(_ZERO_ROW[key]), _p(w), w.stride(0), N, _p(bias), e, _p(out), out.stride(0),
+              ctypes.addressof(p), _p(zrow), _p(w), w.stride(0), N, _p(bias), e, _p(out), out.stride(0),
               _stream(xp))
     if rec is not None:
         tile = "128, 128, 2, 4" if rt == 128 else "256, 64, 8, 1"
@@ -808,8 +820,15 @@ def wgrad(g: torch.Tensor, x: torch.Tensor, out: torch.Tensor, work: torch.Tenso
     _need(g.stride(1) == 1 and x.stride(1) == 1 and out.stride(1) == 1 and g.shape[1] >= N1 and x.shape[1] >= N2 and
           g.shape[0] >= M and x.shape[0] >= M, "wgrad shapes")
     wp, wn = (_p(work), work.numel()) if work is not None else (None, 0)
+    rec = _REC[0]
+    if rec is not None:  # one entry per vc_wgrad_bf16 call: the split-K kernel plus its partial reduction
+        big = N1 % 256 == 0 and N2 % 256 == 0
+        label = "trn::wgrad_big_kernel (+ wgrad_reduce_kernel)" if big else "trn::wgrad_kernel (+ wgrad_reduce_kernel)"
+        e0 = rec.begin()
     _lib.call("vc_wgrad_bf16", _p(g), g.stride(0), _p(x), x.stride(0), M, N1, N2, nscaled, scale, _p(out),
               out.stride(0), wp, wn, _stream(g))
+    if rec is not None:
+        rec.end(e0, label, "wgrad", 2.0 * M * N1 * N2, "flop")
     return out
 
 

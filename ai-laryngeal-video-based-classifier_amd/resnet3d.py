@@ -59,7 +59,9 @@ class ResNet3d(torch.nn.Module):
         self.head_dropout = True  # train step: the head's Dropout(0.5) (pytorchvideo create_resnet dropout_rate)
         # inference convolutions other than 1x1x1 stride 1 as implicit GEMMs (vc_conv3d_gemm_bf16: the
         # A rows gathered from the activations per kernel tap, no im2col buffer); False: im2col + GEMM.
-        # Bit-identical either way (same MFMA chain per output, same column order).
+        # The bottleneck convolutions are bit-identical either way (same MFMA chain per output, same
+        # column order); the implicit stem sums its 441 products in another k order, so the stem (and
+        # the logits) agree with the im2col path to bf16 rounding.
         self.implicit_conv = True
         # LDS ring depth of the implicit convolutions per res stage ("s2" .. "s5" -> 2 or 3;
         # vc_conv3d_gemm_bf16_ring), absent = automatic by grid size (bit-identical for any setting)
@@ -97,6 +99,7 @@ class ResNet3d(torch.nn.Module):
         ver = self._weights_version()  # the fused AdamW updates in place without bumping _version
         if self._packed is not None and self._packed["device"] == device and self._packed["version"] == ver:
             return self._packed
+        ops.zero_row(device)  # the implicit convs' padding row, zeroed on the caller's stream before any fork
         c = self.cfg
         eps = c["bn_eps"]
         P = lambda n: self.params[n.replace(".", "__")].detach().to(device=device, dtype=torch.float64)  # noqa: E731
@@ -178,7 +181,10 @@ class ResNet3d(torch.nn.Module):
         z = lambda r, cols: torch.zeros((r, cols), dtype=bf, device=device)  # noqa: E731
         ws = {"stem_out": z(rows(stem), 128)}
         sp = c.get("stem_pad", (1, 3, 3))
-        ws["stem_pad"] = torch.zeros(B * (T + 2 * sp[0]) * (H + 2 * sp[1]) * (W + 2 * sp[2]) * 4, dtype=bf, device=device)
+        # + 8 pixels x 4 channels of slack: the implicit stem reads 8 pixels per tap row, so with kw < 8 the
+        # last output window of the last row reads up to 8 - kw pixels past the packed clip (zero weights)
+        ws["stem_pad"] = torch.zeros(B * (T + 2 * sp[0]) * (H + 2 * sp[1]) * (W + 2 * sp[2]) * 4 + 32, dtype=bf,
+                                     device=device)
         # im2col scratch: the largest M x K of any convolution
         sk = c.get("stem_kernel", (3, 7, 7))
         big = rows(stem) * _ru(3 * sk[0] * sk[1] * sk[2], 64)
@@ -355,7 +361,8 @@ class ResNet3d(torch.nn.Module):
         sk = c.get("stem_kernel", (3, 7, 7))
         ks = 3 * sk[0] * sk[1] * sk[2]
         spad = c.get("stem_pad", (1, 3, 3))
-        if self.implicit_conv and "stem_seg" in pk:
+        # (the implicit stem reads 16-B aligned 8-pixel rows of the padded clip: its padded width must be even)
+        if self.implicit_conv and "stem_seg" in pk and (W + 2 * spad[2]) % 2 == 0:
             # the clip as zero-padded channels-last bf16 (4 channels), then the implicit stem GEMM
             tm("stem_pack_kernel", "stem_pack", B * 3 * T * H * W * 4 + ws["stem_pad"].numel() * 2, "byte",
                ops.conv3d_stem_pack, video, spad, ws["stem_pad"])

@@ -7,7 +7,28 @@ kernels (ViViT-B B = 8: 840 -> 916 clips/s with 2 streams, tools/exp_streams.py,
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
+
+# instrumentation switch (bench.py's per-kernel tables): every part of a split forward runs on the
+# CALLER's stream, one after the other -- the headline's launches (same part sizes, kernels and
+# workspaces) without the overlap, so HIP events around a launch time that launch alone
+_SERIAL = [False]
+
+
+@contextlib.contextmanager
+def serial_parts(on: bool = True):
+    prev = _SERIAL[0]
+    _SERIAL[0] = bool(on)
+    try:
+        yield
+    finally:
+        _SERIAL[0] = prev
+
+
+def serial() -> bool:
+    return _SERIAL[0]
 
 
 def run_split(owner, x: torch.Tensor, ns: int, part_fn, num_labels: int, prepare=None) -> torch.Tensor:
@@ -31,6 +52,10 @@ def run_split(owner, x: torch.Tensor, ns: int, part_fn, num_labels: int, prepare
     logits = owner._split_out[key]
     cur = torch.cuda.current_stream(dev)
     bounds = [B * i // ns for i in range(ns + 1)]
+    if _SERIAL[0]:
+        for i in range(ns):
+            part_fn(x[bounds[i]:bounds[i + 1]], i, out=logits[bounds[i]:bounds[i + 1]])
+        return logits
     for i in range(ns):
         st = owner._streams[i]
         st.wait_stream(cur)

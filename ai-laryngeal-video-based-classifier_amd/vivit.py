@@ -25,7 +25,7 @@ from collections import OrderedDict
 import numpy as np
 import torch
 
-from . import ops
+from . import ops, streams
 from .streams import GraphReplay
 from .vivit_train import FlatLayout, TrainEngine, VivitTrainFn
 from .weights import vivit_param_shapes
@@ -388,7 +388,8 @@ class VivitForVideoClassification(torch.nn.Module):
         if T != c.num_frames or H != c.image_size or W != c.image_size or C != c.num_channels:
             raise ValueError(f"pixel_values {tuple(pix.shape)} do not match config "
                              f"(T={c.num_frames}, C={c.num_channels}, {c.image_size}^2)")
-        if self.graph_replay and self.kernel_events is None and not torch.cuda.is_current_stream_capturing():
+        if (self.graph_replay and self.kernel_events is None and not streams.serial()
+                and not torch.cuda.is_current_stream_capturing()):
             key = (pix.data_ptr(), tuple(pix.shape), tuple(pix.stride()), pix.dtype, self.concurrent_streams,
                    self.compute_dtype, self._weights_version(), tuple(sorted(self.gemm_cfg.items())), self.rows,
                    self.round_split, self.precise_layers)
@@ -416,6 +417,10 @@ class VivitForVideoClassification(torch.nn.Module):
         # (streams.run_split's rule): packed inside part 0 they would race parts 1..n-1
         self._pack(dev)
         bounds = [B * i // ns for i in range(ns + 1)]
+        if streams.serial():  # instrumentation: the parts one after the other on the caller's stream
+            for i in range(ns):
+                self._forward_part(pix[bounds[i]:bounds[i + 1]], i, out=logits[bounds[i]:bounds[i + 1]])
+            return logits
         sts = self._streams[:ns]
         # whole parts enqueued one after the other (measured, tools/exp_streams.py: enqueueing the
         # parts layer by layer round robin ran 725 vs 911 clips/s, chaining their attention launches

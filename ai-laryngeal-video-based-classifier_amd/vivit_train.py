@@ -137,7 +137,7 @@ class TrainEngine:
         # cap on the split-K factor of the weight gradients (None: vc_wgrad_bf16's own ~one-workgroup-
         # per-CU choice, 10 - 28 partials here); the scratch handed over bounds the splits.  Beside the
         # data-gradient chain fewer, longer workgroups win: 4 -> 214.3 clips/s vs 205.7 uncapped, 208.1
-        # at 8, 206.4 at 2 (tools/r04/ab_train_side.py, one process, round 4)
+        # at 8, 206.4 at 2 (tools/ab_train_side.py, one process, round 4)
         self.wgrad_max_splits = 4
         # the attention backward's dQ kernel on a stream of its own beside dK/dV (vc_attention_bwd_2s)
         self.attn_bwd_2s = True

@@ -29,6 +29,8 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from vclip_amd import streams as vstreams  # noqa: E402
+
 ATTN_GFLOP_PER_CLIP_LAYER = 4.0 * 3137 * 3137 * 64 * 12 / 1e9  # QK^T + PV, 30.23 GF
 VIVIT_GFLOP_PER_CLIP = 903.05   # measured with torch.utils.flop_counter on the HF model
 ATTN_GFLOP_PER_CLIP = 362.77
@@ -54,7 +56,12 @@ def _same_build(pattern: str, mode: str):
     import re
     me = _build_id()
     fs = []
-    for f in glob.glob(os.path.join(ROOT, "profiles", pattern)):
+    dirs = [os.path.join(ROOT, "profiles")] + [d for d in os.environ.get("VCLIP_PROFILES", "").split(":") if d]
+    seen = set()
+    for f in sorted(f for d in dirs for f in glob.glob(os.path.join(d, pattern))):
+        if os.path.basename(f) in seen:
+            continue
+        seen.add(os.path.basename(f))
         try:
             with open(f) as fh:
                 d = json.load(fh)
@@ -68,8 +75,14 @@ def _same_build(pattern: str, mode: str):
     best = max(key(fd) for fd in fs)
     top = [fd for fd in fs if key(fd) == best]
     if len(top) > 1:
-        return None, "ambiguous: " + ", ".join(sorted(os.path.relpath(f, ROOT) for f, _ in top))
+        return None, "ambiguous: " + ", ".join(sorted(_cite(f) for f, _ in top))
     return top[0]
+
+
+def _cite(f: str) -> str:
+    """how a line cites a summary: profiles/<name> (a session's own summaries are collected into
+    profiles/ under the same name: tools/profile_round.sh, tools/collect_profiles.py)"""
+    return "profiles/" + os.path.basename(f)
 
 
 def measured_traffic(kernels, mode: str = "fwd"):
@@ -82,8 +95,8 @@ def measured_traffic(kernels, mode: str = "fwd"):
         return None, d
     ks = [kernels] if isinstance(kernels, str) else list(kernels)
     if any(k not in d["kernels"] for k in ks):
-        return None, f"{os.path.relpath(f, ROOT)} has no entry for {ks}"
-    return sum(d["kernels"][k]["hbm_bytes_per_launch"] for k in ks), os.path.relpath(f, ROOT)
+        return None, f"{_cite(f)} has no entry for {ks}"
+    return sum(d["kernels"][k]["hbm_bytes_per_launch"] for k in ks), _cite(f)
 
 
 def measured_pmc(kernel: str, mode: str = "fwd"):
@@ -93,8 +106,8 @@ def measured_pmc(kernel: str, mode: str = "fwd"):
     if not f:
         return None, d
     if kernel not in d.get("kernels", {}):
-        return None, f"{os.path.relpath(f, ROOT)} has no entry for {kernel}"
-    return d["kernels"][kernel], os.path.relpath(f, ROOT)
+        return None, f"{_cite(f)} has no entry for {kernel}"
+    return d["kernels"][kernel], _cite(f)
 
 
 def pmc_rates(pmc):
@@ -206,8 +219,9 @@ def kernel_breakdown(model, step, clips, streams, n_steps):
         out[name] = {"launches_per_step": len(ms) // n_steps, "avg_launch_ms": round(avg, 4),
                      "share_of_step": round(sum(ms) / n_steps / step_ms, 4), "bound": bound,
                      "achieved": round(rate, 1), "unit": unit, "peak": peak, "frac": round(rate / peak, 4)}
-    out["note"] = (f"{n_steps} extra untimed steps with HIP events around every launch; step {step_ms:.3f} ms "
-                   "under that instrumentation; algorithmic work (M = clips x 3137 rows, no padding)")
+    out["note"] = (f"{n_steps} extra untimed steps with HIP events around every launch ({clips:g} clips per launch: "
+                   f"the headline's {streams}-part split serialised on one stream); step {step_ms:.3f} ms under that "
+                   "instrumentation; algorithmic work (M = clips x 3137 rows, no padding)")
     return out
 
 
@@ -324,7 +338,7 @@ PROF_NAME = {"attn_short_d64_kernel": "ashort::attn_short_d64_kernel<0, 7>",
 
 
 def op_breakdown(model, step, n_steps: int):
-    """`n_steps` extra (untimed) one-stream steps with HIP events around EVERY launch (ops.OpRecorder):
+    """`n_steps` extra (untimed) steps with HIP events around EVERY launch (ops.OpRecorder):
     per kernel instantiation its launches, mean launch time, share of the step and achieved rate on the
     algorithmic work the model states for it.  Returns (table sorted by share, step ms)."""
     from vclip_amd import ops
@@ -358,8 +372,9 @@ def dominant_roofline(table, mode):
             "share_of_step": row["share_of_step"], "avg_launch_ms": row["avg_launch_ms"],
             "launches_per_step": row["launches_per_step"], "traffic": traffic, "traffic_source": traffic_src,
             "mfma_busy": mfma_busy, "valu_per_mfma": valu_per_mfma, "pmc_source": pmc_src,
-            "timed_on": "HIP events around every launch of 3 extra one-stream steps (ops.OpRecorder); algorithmic "
-                        "work = real token rows and channels (no padding)"}
+            "timed_on": "HIP events around every launch of 3 extra steps of the headline's split, its parts "
+                        "serialised on one stream (ops.OpRecorder); algorithmic work = real token rows and channels "
+                        "(no padding)"}
 
 
 def cpu_family_baseline(mode, n_clips, gpu_logits_fn):
@@ -441,7 +456,10 @@ def run_family(a, dist, rank, world, dev):
     dt = timed(a.streams)
     model.graph_replay = False  # the passes below are event-instrumented or one-off calls
     dt1 = timed(1)
-    table, instr_ms = op_breakdown(model, step, 3)
+    # the per-kernel table on the headline's own launches: its split, the parts serialised on one stream
+    model.concurrent_streams = a.streams
+    with vstreams.serial_parts():
+        table, instr_ms = op_breakdown(model, step, 3)
     model.concurrent_streams = 1
     value = a.batch * a.steps * world / dt
     ms_per_step = dt / a.steps * 1e3
@@ -487,8 +505,9 @@ def run_family(a, dist, rank, world, dev):
             "logit_err_note": "max |logit - oracle| relative to max(1, max |oracle logit|)" if a.mode == "resnet3d" else None,
             "roofline": roof,
             "attention_roofline": attn,
-            "kernel_breakdown": dict(list(table.items())[:12], note=f"3 one-stream steps, HIP events around every "
-                                     f"launch: {instr_ms:.3f} ms per step under that instrumentation"),
+            "kernel_breakdown": dict(list(table.items())[:12], note=f"3 steps of the headline's {a.streams}-part split "
+                                     "serialised on one stream, HIP events around every launch: "
+                                     f"{instr_ms:.3f} ms per step under that instrumentation"),
             "op_breakdown": (dict(list(op_breakdown.last_ops.items())[:20]) if a.mode == "resnet3d" else None),
             "model_tflops": round(model_tflops, 1), "model_frac_of_peak": round(model_tflops / PEAK_BF16_TFLOPS, 4),
             "cpu_baseline": cpu,
@@ -496,6 +515,28 @@ def run_family(a, dist, rank, world, dev):
         }
         print(json.dumps(out), flush=True)
     return out
+
+
+WGRAD_LABEL = "trn::wgrad_big_kernel (+ wgrad_reduce_kernel)"
+
+
+def wgrad_line(ktable, instr_ms):
+    """the weight-gradient row of the train step's per-kernel table against the bf16 peak, with the
+    wgrad_big_kernel counters of this build's train profile (when present)"""
+    row = ktable.get(WGRAD_LABEL)
+    if row is None:
+        return None
+    traffic, traffic_src = measured_traffic(["trn::wgrad_big_kernel", "trn::wgrad_reduce_kernel"], "train")
+    pmc, pmc_src = measured_pmc("trn::wgrad_big_kernel", "train")
+    mfma_busy, valu_per_mfma = pmc_rates(pmc)
+    return {"bound": "mfma", "kernel": WGRAD_LABEL, "achieved": row["achieved"], "peak": PEAK_BF16_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(row["achieved"] / PEAK_BF16_TFLOPS, 4),
+            "avg_launch_ms": row["avg_launch_ms"], "launches_per_step": row["launches_per_step"],
+            "share_of_step": row["share_of_step"], "traffic": traffic, "traffic_source": traffic_src,
+            "mfma_busy": mfma_busy, "valu_per_mfma": valu_per_mfma, "pmc_source": pmc_src,
+            "timed_on": f"2 extra steps, weight gradients on the chain's stream (the timed step runs them on a side "
+                        f"stream), HIP events around each vc_wgrad_bf16 call: {instr_ms:.3f} ms per step there; work "
+                        "2 M N1 N2 per call (M = the rows the call reduces over: the padded rows of the activations, 12800 at B = 4 for 12548 tokens)"}
 
 
 def run_train(a, dist, rank, world, dev):
@@ -532,6 +573,24 @@ def run_train(a, dist, rank, world, dev):
     dt = timed_loop(step, a.steps, 0, dist, torch.cuda.synchronize)
     model._engine.kernel_events = None
     attn_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    # the step's largest kernel by GPU time, the weight gradients (vc_wgrad_bf16: trn::wgrad_big_kernel +
+    # its split-K reduction): 2 extra steps with HIP events around every GEMM / weight-gradient launch, the
+    # weight gradients on the chain's own stream for that pass (side_wgrad off) so each event times its
+    # launch alone
+    from vclip_amd import ops
+    eng = model._engine
+    side = eng.side_wgrad
+    eng.side_wgrad = False
+    rec = ops.OpRecorder()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with ops.recording(rec):
+        for _ in range(2):
+            step()
+    torch.cuda.synchronize()
+    instr_ms = (time.perf_counter() - t0) / 2 * 1e3
+    eng.side_wgrad = side
+    ktable = rec.summary(2, instr_ms)
     clips = a.batch * a.steps * world
     value = clips / dt
     ms_per_step = dt / a.steps * 1e3
@@ -563,6 +622,11 @@ def run_train(a, dist, rank, world, dev):
                          "mfma_busy_dkdv": mfma_busy, "valu_per_mfma_dkdv": valu_per_mfma, "pmc_source": pmc_src,
                          "flop_per_launch": f"{TRAIN_ATTN_GFLOP_PER_CLIP_LAYER:.2f} GF/clip x {a.batch} clips"},
             "step_tflops": round(step_tflops, 1), "step_frac_of_peak": round(step_tflops / PEAK_BF16_TFLOPS, 4),
+            "wgrad_roofline": wgrad_line(ktable, instr_ms),
+            "kernel_table": dict(list(ktable.items())[:10], note="2 extra steps, weight gradients on the chain's "
+                                 "stream, HIP events around every GEMM / weight-gradient launch (ops.OpRecorder): "
+                                 f"{instr_ms:.3f} ms per step under that instrumentation; the attention backward "
+                                 "is timed separately (roofline)"),
             "cpu_baseline": cpu,
             "build": _build_id(),
         }
@@ -655,13 +719,19 @@ def main():
     streams = model.last_streams
     graphed = model.graph_replay
     model.graph_replay = False  # the event-instrumented passes and one-off calls below run eagerly
-    # the kernel roofline: the same K steps on ONE stream with HIP events around every attention
-    # launch, so a launch's event time is its own execution (under two streams it would include time
-    # shared with the other stream's kernels) and matches the rocprofv3 kernel trace of
-    # `bench.py --streams 1` (tools/profile_round.sh)
+    # the kernel roofline on the headline's OWN launches: the same split (batch / streams clips per launch,
+    # the same kernels and workspaces) with the parts one after the other on one stream and HIP events
+    # around every attention launch, so a launch's event time is its own execution (under two concurrent
+    # streams it would include time shared with the other part's kernels); rocprofv3 of
+    # `tools/headline.py --serial 1` times the same launches (tools/profile_round.sh)
     evs = []
-    dt1 = timed(1, evs)
+    with vstreams.serial_parts():
+        dts = timed(a.streams, evs)
     attn_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    # ... and the whole batch as ONE launch per op on one stream (round-4's roofline pass), for reference
+    evs1 = []
+    dt1 = timed(1, evs1)
+    attn_ms1 = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs1]))
 
     # the fp16-operand build of the same forward (VC_ELEM_F16: same kernels, same MFMA rate,
     # logits within 1e-3), timed the same way after the bf16 headline; reported beside it
@@ -670,7 +740,8 @@ def main():
     dt16 = timed(a.streams)
     model.graph_replay = False
     evs16 = []
-    timed(1, evs16)
+    with vstreams.serial_parts():
+        timed(a.streams, evs16)
     attn_ms16 = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs16]))
     # ... and with split fp16 operands in the patch embedding and layer 0 (precise_layers = 1: the
     # weights of the first layers set the fp16 build's logit error)
@@ -681,15 +752,20 @@ def main():
     model.precise_layers = 0
     model.compute_dtype = torch.bfloat16
 
+    # per-op and per-kernel tables of the headline's own launches (its split, serialised on one stream)
+    model.concurrent_streams = streams
+    part_clips = a.batch // streams if a.batch % streams == 0 else a.batch / streams
+    with vstreams.serial_parts():
+        breakdown = kernel_breakdown(model, step, part_clips, streams, 3)
+        ktable, instr_ms = op_breakdown(model, step, 3)
     model.concurrent_streams = 1
-    breakdown = kernel_breakdown(model, step, a.batch, 1, 3)
-    ktable, instr_ms = op_breakdown(model, step, 3)
 
     clips = a.batch * a.steps * world
     value = clips / dt
     ms_per_step = dt / a.steps * 1e3
-    launch_clips = a.batch  # the roofline pass runs the whole batch on one stream
+    launch_clips = part_clips  # the roofline pass times the headline's launches: batch / streams clips each
     attn_tflops = ATTN_GFLOP_PER_CLIP_LAYER * launch_clips / (attn_ms * 1e-3) / 1e3
+    attn_tflops1 = ATTN_GFLOP_PER_CLIP_LAYER * a.batch / (attn_ms1 * 1e-3) / 1e3
     model_tflops = VIVIT_GFLOP_PER_CLIP * a.batch / (ms_per_step * 1e-3) / 1e3
 
     out = None
@@ -741,13 +817,19 @@ def main():
                          "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes": ATTN_IO_BYTES_PER_CLIP * launch_clips, "avg_launch_ms": round(attn_ms, 4),
                          "flop_per_launch": f"{ATTN_GFLOP_PER_CLIP_LAYER:.2f} GF/clip x {launch_clips:g} clips",
-                         "timed_on": "a separate K-step pass on one HIP stream (the headline runs "
-                                     f"{streams}): clips/s {a.batch * a.steps * world / dt1:.2f} there",
+                         "timed_on": f"the headline's own launches ({launch_clips:g} clips each: its {streams}-stream "
+                                     "split) run one after the other on one HIP stream, HIP events around every "
+                                     f"attention launch: clips/s {a.batch * a.steps * world / dts:.2f} there",
+                         "whole_batch_launch": {"clips": a.batch, "avg_launch_ms": round(attn_ms1, 4),
+                                                "achieved": round(attn_tflops1, 1),
+                                                "frac": round(attn_tflops1 / PEAK_BF16_TFLOPS, 4),
+                                                "one_stream_clips_s": round(a.batch * a.steps * world / dt1, 2)},
                          "mfma_busy": mfma_busy, "valu_per_mfma": valu_per_mfma,
                          "pmc_source": pmc_src},
             "kernel_breakdown": breakdown,
-            "kernel_table": dict(ktable, note=f"per kernel instantiation (ops.OpRecorder), 3 one-stream steps with HIP "
-                                 f"events around every launch: {instr_ms:.3f} ms per step under that instrumentation"),
+            "kernel_table": dict(ktable, note=f"per kernel instantiation (ops.OpRecorder), 3 steps of the headline's "
+                                 f"{streams}-part split serialised on one stream, HIP events around every launch: "
+                                 f"{instr_ms:.3f} ms per step under that instrumentation"),
             "build": _build_id(),
             "model_tflops": round(model_tflops, 1),
             "model_frac_of_peak": round(model_tflops / PEAK_BF16_TFLOPS, 4),

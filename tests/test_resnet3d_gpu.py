@@ -115,6 +115,32 @@ def test_resnet3d_batch_invariance():
     assert torch.equal(full[1:2], one)
 
 
+def test_resnet3d_b4_bench_path_graphed():
+    """bench.py --mode resnet3d's timed configuration: B = 4 32x224^2 clips over 2 concurrent HIP streams,
+    replayed from the captured hipGraph.  A FRESH model's first call (packing, workspaces, the padding
+    row) goes straight into the split + capture; its logits and a second input tensor's (served by the
+    static-buffer capture) must equal the one-stream eager forward bit for bit, and the oracle within
+    the file's relative bar."""
+    video = torch.from_numpy(make_synthetic_video(4, 32, 224, seed=3)).to(DEV)
+    video2 = torch.flip(video, dims=[0]).contiguous()
+    m = _model()
+    m.concurrent_streams = 2
+    m.graph_replay = True
+    got = m.forward_logits(video).clone()
+    got2 = m.forward_logits(video2.clone()).clone()
+    again = m.forward_logits(video).clone()
+    eager_m = _model()
+    want = eager_m.forward_logits(video).clone()
+    want2 = eager_m.forward_logits(video2).clone()
+    assert torch.equal(got, want) and torch.equal(again, want)
+    assert torch.equal(got2, want2)
+    sd = {k: torch.from_numpy(v) for k, v in make_resnet3d_weights(ref.RESNET3D_50, seed=0).items()}
+    with torch.no_grad():
+        r = ref.resnet3d_forward(sd, ref.RESNET3D_50, video[:1].cpu()).numpy()
+    err = np.abs(got[:1].cpu().numpy() - r).max()
+    assert err < 1e-2 * max(1.0, np.abs(r).max()), (err, got[:1], r)
+
+
 @pytest.mark.parametrize("kernel,stride,pad,C,epi", [((1, 3, 3), (1, 2, 2), (0, 1, 1), 64, "bias_relu"),
                                                       ((1, 3, 3), (1, 1, 1), (0, 1, 1), 128, "bias_relu"),
                                                       ((3, 1, 1), (1, 1, 1), (1, 0, 0), 64, "bias_relu"),
@@ -173,7 +199,7 @@ def test_resnet3d_implicit_conv_matches_im2col_path():
 
 
 @pytest.mark.parametrize("T,H,W", [(4, 20, 18), (3, 17, 22)])
-def test_conv3d_stem_implicit_gemm_bit_exact(T, H, W):
+def test_conv3d_stem_implicit_gemm_matches_im2col(T, H, W):
     """The implicit stem (vc_conv3d_stem_pack + vc_conv3d_stem_gemm_bf16, one 32-column segment per
     (kt, kh) tap row) == im2col (NCTHW f32) + GEMM on the same BN-folded weights: each output is the
     same products in a different k order, so the comparison is to fp32 of the bf16 operands (both

@@ -216,3 +216,35 @@ def test_vivit_weight_update_then_split_forward():
     fresh.load_state_dict(make_vivit_weights(cfg, seed=7))
     fresh = fresh.cuda().eval()
     assert torch.equal(got, fresh.forward_logits(pix))
+
+
+def test_vivit_b_batch8_headline_path_graphed():
+    """The exact configuration bench.py times (BASELINE configs[1]): ViViT-B/16x2, 32x224^2, B = 8 over
+    2 concurrent HIP streams, replayed from the captured hipGraph.  Bit-identical to the one-stream
+    eager forward (and to the split run serially, the bench's per-kernel pass), and within north_star's
+    bf16 bar 1e-2 of transformers' VivitForVideoClassification (tests/golden/vivit_b8.json); a second
+    input tensor of the same shape is served by the static-buffer capture, bit-exact too."""
+    from vclip_amd import streams
+    from vclip_amd.vivit import create_model
+    with open(os.path.join(GD, "vivit_b8.json")) as f:
+        g = json.load(f)
+    cfg = g["config"]
+    pix = torch.from_numpy(make_synthetic_clips(g["batch"], cfg["num_frames"], cfg["image_size"],
+                                                seed=g["input_seed"])).cuda()
+    m = create_model(num_frames=32, device="cuda")
+    m.concurrent_streams = 1
+    eager = m.forward_logits(pix).clone()
+    pix2 = torch.flip(pix, dims=[0]).contiguous()
+    eager2 = m.forward_logits(pix2).clone()
+    m.concurrent_streams = 2
+    with streams.serial_parts():
+        assert torch.equal(m.forward_logits(pix), eager)
+    m.graph_replay = True
+    for _ in range(2):
+        got = m.forward_logits(pix).clone()
+        assert m.last_streams == 2
+        assert torch.equal(got, eager)
+    assert torch.equal(m.forward_logits(pix2.clone()), eager2)
+    err = float(np.abs(got.cpu().numpy() - np.array(g["logits"])).max())
+    print("ViViT-B B=8 two-stream graph replay: max |logit - HF golden|", err)
+    assert err < 1e-2, err

@@ -58,18 +58,37 @@ def main():
     tag = sys.argv[1]
     src = os.path.join(ROOT, "gpurun_out", tag)
     dst = os.path.join(ROOT, "profiles")
-    bench = json.loads(open(os.path.join(src, "bench.json")).read())
-    build = bench.get("build")
+    if "--dst" in sys.argv:  # on the GPU box: the session's own summaries, for its bench line (VCLIP_PROFILES)
+        dst = sys.argv[sys.argv.index("--dst") + 1]
+        os.makedirs(dst, exist_ok=True)
+    bf = os.path.join(src, "bench.json")
+    bench = json.loads(open(bf).read()) if os.path.exists(bf) else None
+    if bench is not None:
+        build = bench.get("build")
+    else:  # a session without its bench line (NO_BENCH=1): the tree's own build
+        sys.path.insert(0, ROOT)
+        from vclip_amd.build import source_hash
+        build = source_hash()
     cf = os.path.join(src, "pmc_command.txt")
     if not os.path.exists(cf):
         raise SystemExit(f"{cf} missing: profile with tools/profile_round.sh, which records the command")
     command = open(cf).read().strip()
     mode = bench_mode(command)
-    with open(os.path.join(dst, f"{tag}_bench.json"), "w") as f:
-        json.dump(bench, f, indent=1)
+    if bench is not None:
+        with open(os.path.join(dst, f"{tag}_bench.json"), "w") as f:
+            json.dump(bench, f, indent=1)
+    tl = os.path.join(src, "timeline.json")
+    if os.path.exists(tl):
+        d = json.load(open(tl))
+        with open(os.path.join(dst, f"{tag}_timeline.json"), "w") as f:
+            json.dump({"build": build, "mode": mode, "note": "the concurrent headline (tools/headline.py: "
+                       "its streams, graph replay), rocprofv3 --kernel-trace", **d}, f, indent=1)
     stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
         shutil.copy(stats[0], os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    hstats = glob.glob(os.path.join(src, "htrace", "**", "*kernel_stats.csv"), recursive=True)
+    if hstats:
+        shutil.copy(hstats[0], os.path.join(dst, f"{tag}_headline_kernel_stats.csv"))
     fe, wr = per_kernel(os.path.join(src, "pmc_FETCH_SIZE")), per_kernel(os.path.join(src, "pmc_WRITE_SIZE"))
     if fe and wr:
         out = {"build": build, "mode": mode, "command": command,
