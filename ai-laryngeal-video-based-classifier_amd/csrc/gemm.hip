@@ -44,6 +44,15 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_addr) {
                  : "memory", "m0");
 }
 
+// the saddr form: wave-uniform 64-bit base in SGPRs + a 32-bit per-lane byte offset (one VGPR per
+// source stream instead of a 64-bit address pair)
+__device__ __forceinline__ void glds16s(const void* sbase, uint32_t voff, uint32_t lds_addr) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+                 :
+                 : "v"(voff), "s"(sbase), "s"(lds_addr)
+                 : "memory", "m0");
+}
+
 __device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
@@ -557,6 +566,164 @@ gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
     read_frags(nk - 1, fa1, fw1);
     mfmas(fa1, fw1);
     store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bias, out, ldo, aux, ldaux, G, gstride, goff);
+}
+
+// ---------------------------------------------------------------------------------
+// 160x256 ping-pong kernel (cfg 17) -- the cfg 8 schedule on 160-row tiles, for the grids that 256-row
+// tiles quantise badly at the ViViT-B two-stream split (4 clips = 12800 padded rows = 80 x 160): fc2 /
+// o_proj 150 tiles of 256 x 256 fill 150 of 256 CUs for one tile-time, 240 tiles of 160 x 256 fill 240
+// for 0.625 of it; fc1 600 -> 960 tiles (3 rounds of 1.0 -> 4 of 0.625), q|k|v 450 -> 720 (2 -> 3 x 0.625).
+//   * 8 waves as 2 (rows) x 4 (cols), wave tile 80 x 64 = 5 x 4 blocks of v_mfma_f32_16x16x32;
+//     group 0 = waves 0-3 (tile rows 0-79), group 1 = waves 4-7 (rows 80-159), one barrier behind;
+//   * phases split by COLUMNS (10 MFMAs each, balanced): a(u) reads the wave's 5 A fragments and W
+//     blocks 0-1, stages W(u+2), MFMAs on column blocks 0-1; b(u) reads W blocks 2-3 (the A fragments
+//     stay in registers), stages A(u+3), retires K-half u+1, MFMAs on column blocks 2-3;
+//   * ring of 4 K-half slots (A 160 x 32 then W 256 x 32, 64-B rows, swz64): 104 KiB.  A is 10 LDS-DMA
+//     pieces per K-half: waves 0-4 stage two each, waves 5-7 none, so their counted waits differ
+//     (vmcnt(6) / vmcnt(2): the DMAs younger than W(u+1) are A(u+2), W(u+2), A(u+3) vs W(u+2) alone);
+//   * WAR: W(u+2) overwrites W(u-2), last read in b(u-2), A(u+3) overwrites A(u-1), last read in
+//     a(u-1): both >= 3 barriers after the lagging group's reads completed.
+// Same K order and MFMA chain per output as every other config: bit-identical.  Epilogue: store_tile16
+// (every epilogue, incl. the f32 residual).
+// ---------------------------------------------------------------------------------
+template <int EPI, int ET = VC_ELEM_BF16>
+__global__ void __launch_bounds__(512, 1)
+gemm_pp160_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw, int nbm,
+                  int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
+                  const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride, int64_t goff) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int BM = 160, BN = 256, BKH = 32, NS = 4;
+    constexpr int SLOT = (BM + BN) * 64;  // 26 KiB
+    constexpr int TM = 80, TN = 64, MI = 5, NI = 4;
+
+    const int nwg = nbm * nbn;
+    const int bid = blockIdx.x;
+    const int xcd = bid & 7, xq = nwg >> 3, rr = nwg & 7;
+    const int wgid = (xcd < rr ? xcd * (xq + 1) : rr * (xq + 1) + (xcd - rr) * xq) + (bid >> 3);
+    const int tm = wgid / nbn, tn = wgid % nbn;
+    const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int c16 = lane & 15, q = lane >> 4;
+    const bool astager = wave < 5;  // waves 0-4 stage A rows [32w, 32w + 32)
+
+    // staging sources (byte offsets from the wave-uniform panel bases)
+    const int srow = wave * 32 + (lane >> 2);
+    const int arow = astager ? srow : 0;
+    const uint32_t aoff0 = (uint32_t)(arow * lda + swz64(arow, lane & 3) * 8) * 2;
+    const uint32_t aoff1 = (uint32_t)((arow + 16) * lda + swz64(arow + 16, lane & 3) * 8) * 2;
+    const uint32_t woff0 = (uint32_t)(srow * ldw + swz64(srow, lane & 3) * 8) * 2;
+    const uint32_t woff1 = (uint32_t)((srow + 16) * ldw + swz64(srow + 16, lane & 3) * 8) * 2;
+    const uint16_t* Ap = A + m0 * lda;
+    const uint16_t* Wp = W + n0 * ldw;
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
+    auto stage_a = [&](int u) __attribute__((always_inline)) {
+        const uint32_t s = lds0 + (u & (NS - 1)) * SLOT + wave * 32 * 64;
+        glds16s(Ap + u * BKH, aoff0, __builtin_amdgcn_readfirstlane(s));
+        glds16s(Ap + u * BKH, aoff1, __builtin_amdgcn_readfirstlane(s + 16 * 64));
+    };
+    auto stage_w = [&](int u) __attribute__((always_inline)) {
+        const uint32_t s = lds0 + (u & (NS - 1)) * SLOT + BM * 64 + wave * 32 * 64;
+        glds16s(Wp + u * BKH, woff0, __builtin_amdgcn_readfirstlane(s));
+        glds16s(Wp + u * BKH, woff1, __builtin_amdgcn_readfirstlane(s + 16 * 64));
+    };
+    auto read_a = [&](int u, v8s (&fa)[MI]) __attribute__((always_inline)) {
+        const char* At = smem + (u & (NS - 1)) * SLOT;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) fa[i] = lds_frag64(At, wm * TM + i * 16 + c16, q);
+    };
+    auto read_w = [&](int u, int j0, v8s (&fw)[2]) __attribute__((always_inline)) {
+        const char* Wt = smem + (u & (NS - 1)) * SLOT + BM * 64;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fw[j] = lds_frag64(Wt, wn * TN + (j0 + j) * 16 + c16, q);
+    };
+
+    v4f acc[MI][NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+    auto mma = [&](auto J0, const v8s (&fa)[MI], const v8s (&fw)[2]) __attribute__((always_inline)) {
+        constexpr int j0 = decltype(J0)::value;
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's fragment reads
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[i][j0 + j] = mfma16x32<ET>(fw[j], fa[i], acc[i][j0 + j]);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    using C0 = std::integral_constant<int, 0>;
+    using C2 = std::integral_constant<int, 2>;
+
+    const int nk = K / BKH;  // even, >= 4
+    v8s fa[MI], fw[2];
+    auto phase_a = [&](int u) __attribute__((always_inline)) {
+        read_a(u, fa);
+        read_w(u, 0, fw);
+        if (u + 2 < nk) stage_w(u + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(C0{}, fa, fw);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto phase_b = [&](int u) __attribute__((always_inline)) {
+        read_w(u, 2, fw);
+        if (astager) {
+            if (u + 3 < nk) {
+                stage_a(u + 3);
+                wait_vm<6>();
+            } else if (u + 2 < nk) {
+                wait_vm<4>();
+            } else {
+                wait_vm<0>();
+            }
+        } else {
+            if (u + 2 < nk) wait_vm<2>();
+            else wait_vm<0>();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mma(C2{}, fa, fw);
+        // the lagging group skips its last barrier: both groups then pass the same number
+        if (u + 1 < nk || wm == 0) __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    // prologue: A0 W0 A1 W1 A2 in flight (waves 5-7: W0 W1), retire K-half 0, publish; group 1 one
+    // barrier behind
+    if (astager) {
+        stage_a(0);
+        stage_w(0);
+        stage_a(1);
+        stage_w(1);
+        stage_a(2);
+        wait_vm<6>();
+    } else {
+        stage_w(0);
+        stage_w(1);
+        wait_vm<2>();
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (wm == 1) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+
+    for (int u = 0; u < nk; ++u) {
+        phase_a(u);
+        phase_b(u);
+    }
+    store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bias, out, ldo, aux, ldaux, G, gstride,
+                                  goff);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1331,6 +1498,319 @@ gemm_ppp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
 }
 
 // ---------------------------------------------------------------------------------
+// Persistent 256x256 ping-pong kernel with DEFERRED epilogue stores (cfg 15; q|k|v, fc1 at K >= 640).
+// What bounded the K = 768 launches was not the main loop but the output write:
+// every CU stores its 128-KiB tile at the same moment -- a 32-MB burst at ~4 TB/s with the matrix
+// pipes idle -- and the in-order vmcnt makes the DMAs issued after a store wait for it.  Here a
+// tile's epilogue only computes (bias from LDS, activation, 16-bit pack, permlane16 pairing) into 16
+// packed 16-B row pieces per wave held in registers, and the stores go out during the NEXT tile, one
+// per K-half in phase b for its first 16 K-halves: the chip's write stream is spread over the main
+// loop (~3 TB/s) instead of bursting between tiles.  Each store is younger than the DMAs of the
+// K-half it retires next, so the counted wait of phase b(u) allows the stores of phases b(u - 1) and
+// b(u) on top of the 6 DMAs (vmcnt(6 + NY)); a store issued two phases earlier must have completed.
+// The last tile of a workgroup stores its pieces at once.  Same K order and MFMA chain per output as
+// cfgs 4 / 8 / 10: bit-identical.  One fragment register set per role (A rows, W columns) -- the
+// ping-pong's reads of a phase come after the previous phase's MFMAs issued -- which leaves room for
+// the 64 pending registers next to the 128 accumulators.
+// ---------------------------------------------------------------------------------
+template <int EPI, int ET = VC_ELEM_BF16, int NDEF = 16>
+__global__ void __launch_bounds__(512, 1)
+gemm_ppd_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw, int nbm,
+                int nbn, int K, int N, const float* __restrict__ bias, uint16_t* __restrict__ out, int64_t ldo) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    constexpr int BM = 256, BN = 256, BKH = 32, NS = 4;
+    constexpr int SLOT = (BM + BN) * 64;  // 32 KiB
+    constexpr int TM = 128, TN = 64, MI = 8, NI = 4;
+    constexpr int NST = MI * (NI / 2);  // 16-B row pieces per wave per tile
+    constexpr int P0 = NST - NDEF;      // pieces stored at once at the end of a tile (the rest deferred)
+    static_assert(NDEF >= 1 && NDEF <= 16, "deferred pieces");
+    static_assert(EPI == VC_EPI_BIAS_BF16 || EPI == VC_EPI_BIAS_GELU_TANH || EPI == VC_EPI_BIAS_GELU_ERF ||
+                      EPI == VC_EPI_BIAS_RELU_BF16,
+                  "16-bit-output epilogues without a second output");
+    float* bias_lds = reinterpret_cast<float*>(smem + NS * SLOT);
+
+    const int ntiles = nbm * nbn;
+    const int G = gridDim.x;
+    const int b = blockIdx.x;
+    const int lane_slot = (b & 7) * (G >> 3) + (b >> 3);
+    const int mine = lane_slot < ntiles ? (ntiles - 1 - lane_slot) / G + 1 : 0;  // tiles of this workgroup
+    if (mine == 0) return;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int c16 = lane & 15, q = lane >> 4;
+
+    for (int n = tid * 4; n < N; n += 512 * 4)
+        *reinterpret_cast<float4*>(bias_lds + n) = *reinterpret_cast<const float4*>(bias + n);
+    __syncthreads();
+
+    const int nk = K / BKH;  // even, >= 20
+    const int total = mine * nk;
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
+    const int arow = wave * 32 + (lane >> 2);
+    // per-lane BYTE offsets from the wave-uniform panel base (32-bit: a 256-row panel is < 4 GiB)
+    const uint32_t aoff0 = (uint32_t)(arow * lda + swz64(arow, lane & 3) * 8) * 2;
+    const uint32_t aoff1 = (uint32_t)((arow + 16) * lda + swz64(arow + 16, lane & 3) * 8) * 2;
+    const uint32_t woff0 = (uint32_t)(arow * ldw + swz64(arow, lane & 3) * 8) * 2;
+    const uint32_t woff1 = (uint32_t)((arow + 16) * ldw + swz64(arow + 16, lane & 3) * 8) * 2;
+    auto tile_origin = [&](int it, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
+        const int tile = it * G + lane_slot;
+        const int tm = tile / nbn;
+        m0 = (int64_t)tm * BM;
+        n0 = (int64_t)(tile - tm * nbn) * BN;
+    };
+    struct Cursor {
+        int it, u;
+        const uint16_t* p;
+    };
+    auto cursor_at = [&](bool is_a) __attribute__((always_inline)) {
+        Cursor c;
+        c.it = 0;
+        c.u = 0;
+        int64_t m0, n0;
+        tile_origin(0, m0, n0);
+        c.p = is_a ? A + m0 * lda : W + n0 * ldw;
+        return c;
+    };
+    Cursor ca = cursor_at(true), cw = cursor_at(false);
+    auto advance = [&](Cursor& c, bool is_a) __attribute__((always_inline)) {
+        if (++c.u == nk) {
+            c.u = 0;
+            ++c.it;
+            if (c.it < mine) {
+                int64_t m0, n0;
+                tile_origin(c.it, m0, n0);
+                c.p = is_a ? A + m0 * lda : W + n0 * ldw;
+            }
+        }
+    };
+    auto stage_a = [&](int U) __attribute__((always_inline)) {
+        const uint32_t s = lds0 + (U & (NS - 1)) * SLOT + wave * 32 * 64;
+        glds16s(ca.p + ca.u * BKH, aoff0, __builtin_amdgcn_readfirstlane(s));
+        glds16s(ca.p + ca.u * BKH, aoff1, __builtin_amdgcn_readfirstlane(s + 16 * 64));
+        advance(ca, true);
+    };
+    auto stage_w = [&](int U) __attribute__((always_inline)) {
+        const uint32_t s = lds0 + (U & (NS - 1)) * SLOT + BM * 64 + wave * 32 * 64;
+        glds16s(cw.p + cw.u * BKH, woff0, __builtin_amdgcn_readfirstlane(s));
+        glds16s(cw.p + cw.u * BKH, woff1, __builtin_amdgcn_readfirstlane(s + 16 * 64));
+        advance(cw, false);
+    };
+    auto read_a = [&](int U, int i0, v8s (&fa)[4]) __attribute__((always_inline)) {
+        const char* At = smem + (U & (NS - 1)) * SLOT;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = lds_frag64(At, wm * TM + i0 + i * 16 + c16, q);
+    };
+    auto read_w = [&](int U, v8s (&fw)[4]) __attribute__((always_inline)) {
+        const char* Wt = smem + (U & (NS - 1)) * SLOT + BM * 64;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fw[j] = lds_frag64(Wt, wn * TN + j * 16 + c16, q);
+    };
+
+    v4f acc[MI][NI];
+    uint4 pend[NST];      // the previous tile's packed output pieces (P0 .. NST - 1 stored during this tile)
+    int64_t pm0 = 0, pn0 = 0;  // ... and that tile's origin
+    auto mma = [&](auto I0, auto FIRST, const v8s (&fa)[4], const v8s (&fw)[4]) __attribute__((always_inline)) {
+        constexpr int i0 = decltype(I0)::value;
+        constexpr bool first = decltype(FIRST)::value;
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i0 + i][j] = mfma16x32<ET>(fw[j], fa[i], first ? v4f{0.f, 0.f, 0.f, 0.f} : acc[i0 + i][j]);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // piece s of the pending tile: rows i = s / 2 (16-row block of the wave tile), column pair jp = s % 2
+    // (wave-uniform base of the piece's 16-row block + one loop-invariant per-lane byte offset)
+    const uint32_t soff = (uint32_t)(c16 * ldo + (q & 1) * 16 + 4 * (q & 2)) * 2;
+    auto store_piece = [&](auto S) __attribute__((always_inline)) {
+        constexpr int sI = decltype(S)::value;
+        constexpr int i = sI >> 1, jp = sI & 1;
+        const uint16_t* base = out + (pm0 + wm * TM + i * 16) * ldo + pn0 + wn * TN + jp * 32;
+        *reinterpret_cast<uint4*>(reinterpret_cast<char*>(const_cast<uint16_t*>(base)) + soff) = pend[sI];
+    };
+    // pieces s .. P0 - 1, at once (recursion over compile-time indices)
+    auto store_first = [&](auto S) __attribute__((always_inline)) {
+        auto rec = [&](auto self, auto T) __attribute__((always_inline)) {
+            constexpr int t = decltype(T)::value;
+            if constexpr (t < P0) {
+                store_piece(std::integral_constant<int, t>{});
+                self(self, std::integral_constant<int, t + 1>{});
+            }
+        };
+        rec(rec, S);
+    };
+    using C0 = std::integral_constant<int, 0>;
+    using C4 = std::integral_constant<int, 4>;
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+
+    v8s fa[4], fw[4];
+    auto phase_a = [&](auto FIRST, int U) __attribute__((always_inline)) {
+        read_a(U, 0, fa);
+        read_w(U, fw);
+        if (U + 2 < total) stage_w(U + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(C0{}, FIRST, fa, fw);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // ST: the pending piece stored in this phase (-1: none); NY: stores younger than K-half U + 1's DMAs
+    auto phase_b = [&](auto FIRST, auto ST, auto NY, int U) __attribute__((always_inline)) {
+        constexpr int st = decltype(ST)::value, ny = decltype(NY)::value;
+        read_a(U, 64, fa);
+        if (U + 3 < total) {
+            stage_a(U + 3);
+            if constexpr (st >= 0) store_piece(std::integral_constant<int, st >= 0 ? st : 0>{});
+            wait_vm<6 + ny>();
+        } else if (U + 2 < total) {
+            if constexpr (st >= 0) store_piece(std::integral_constant<int, st >= 0 ? st : 0>{});
+            wait_vm<4 + ny>();
+        } else {
+            if constexpr (st >= 0) store_piece(std::integral_constant<int, st >= 0 ? st : 0>{});
+            wait_vm<0>();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mma(C4{}, FIRST, fa, fw);
+        if (U + 1 < total || wm == 0) __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // one tile's K-halves; STORES: the previous tile's pieces go out in phase b of K-halves 0 .. 15
+    // (nk >= 20, so the ring's drain at the end of the last tile never meets a store phase)
+    auto run_tile = [&](auto STORES, int U) __attribute__((always_inline)) {
+        constexpr bool stores = decltype(STORES)::value;
+        using N0 = std::integral_constant<int, 0>;
+        using NO = std::integral_constant<int, -1>;
+        if constexpr (stores) {
+            // K-half 0 .. NDEF - 1 store piece P0 + u in phase b; NY counts the stores of b(u - 1), b(u)
+            phase_a(T_{}, U);
+            phase_b(T_{}, std::integral_constant<int, P0>{}, std::integral_constant<int, 1>{}, U);
+            auto body = [&](auto S) __attribute__((always_inline)) {
+                constexpr int sI = decltype(S)::value;
+                if constexpr (sI < NDEF) {
+                    phase_a(F_{}, U + sI);
+                    phase_b(F_{}, std::integral_constant<int, P0 + sI>{}, std::integral_constant<int, 2>{}, U + sI);
+                }
+            };
+            body(std::integral_constant<int, 1>{});
+            body(std::integral_constant<int, 2>{});
+            body(std::integral_constant<int, 3>{});
+            body(std::integral_constant<int, 4>{});
+            body(std::integral_constant<int, 5>{});
+            body(std::integral_constant<int, 6>{});
+            body(std::integral_constant<int, 7>{});
+            body(std::integral_constant<int, 8>{});
+            body(std::integral_constant<int, 9>{});
+            body(std::integral_constant<int, 10>{});
+            body(std::integral_constant<int, 11>{});
+            body(std::integral_constant<int, 12>{});
+            body(std::integral_constant<int, 13>{});
+            body(std::integral_constant<int, 14>{});
+            body(std::integral_constant<int, 15>{});
+            phase_a(F_{}, U + NDEF);
+            phase_b(F_{}, NO{}, std::integral_constant<int, 1>{}, U + NDEF);
+            int u = NDEF + 1;
+            if constexpr (NDEF % 2 == 0) {
+                phase_a(F_{}, U + u);
+                phase_b(F_{}, NO{}, N0{}, U + u);
+                ++u;
+            }
+            for (; u < nk; u += 2) {
+                phase_a(F_{}, U + u);
+                phase_b(F_{}, NO{}, N0{}, U + u);
+                phase_a(F_{}, U + u + 1);
+                phase_b(F_{}, NO{}, N0{}, U + u + 1);
+            }
+        } else {
+            phase_a(T_{}, U);
+            phase_b(T_{}, NO{}, N0{}, U);
+            phase_a(F_{}, U + 1);
+            phase_b(F_{}, NO{}, N0{}, U + 1);
+            for (int u = 2; u < nk; u += 2) {
+                phase_a(F_{}, U + u);
+                phase_b(F_{}, NO{}, N0{}, U + u);
+                phase_a(F_{}, U + u + 1);
+                phase_b(F_{}, NO{}, N0{}, U + u + 1);
+            }
+        }
+    };
+    // epilogue arithmetic of the tile just finished into pend: + bias (LDS), activation, 16-bit,
+    // permlane16 pairs (even q: block 2jp, columns 4q .. 4q+7; odd q: block 2jp+1)
+    auto finish = [&](int64_t m0, int64_t n0) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+#pragma unroll
+            for (int jp = 0; jp < NI / 2; ++jp) {
+                unsigned pk[2][2];
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int nl = (int)n0 + wn * TN + (2 * jp + s2) * 16 + 4 * q;
+                    const float4 bb = *reinterpret_cast<const float4*>(bias_lds + nl);
+                    float v0 = acc[i][2 * jp + s2][0] + bb.x, v1 = acc[i][2 * jp + s2][1] + bb.y;
+                    float v2 = acc[i][2 * jp + s2][2] + bb.z, v3 = acc[i][2 * jp + s2][3] + bb.w;
+                    if (EPI == VC_EPI_BIAS_GELU_TANH) {
+                        v0 = gelu_tanh(v0); v1 = gelu_tanh(v1); v2 = gelu_tanh(v2); v3 = gelu_tanh(v3);
+                    } else if (EPI == VC_EPI_BIAS_GELU_ERF) {
+                        v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
+                    } else if (EPI == VC_EPI_BIAS_RELU_BF16) {
+                        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+                    }
+                    pk[s2][0] = pack2<ET>(v0, v1);
+                    pk[s2][1] = pack2<ET>(v2, v3);
+                }
+                auto s0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+                auto s1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+                pend[2 * i + jp] = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+            }
+        }
+        pm0 = m0;
+        pn0 = n0;
+        __builtin_amdgcn_sched_barrier(0);
+        store_first(std::integral_constant<int, 0>{});
+    };
+
+    // prologue: A0 W0 A1 W1 A2 of the first tile in flight, retire A0 W0, publish; group 1 one barrier behind
+    stage_a(0);
+    stage_w(0);
+    stage_a(1);
+    stage_w(1);
+    stage_a(2);
+    wait_vm<6>();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (wm == 1) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+
+    int64_t m0, n0;
+    tile_origin(0, m0, n0);
+    run_tile(F_{}, 0);
+    finish(m0, n0);
+    for (int it = 1; it < mine; ++it) {
+        tile_origin(it, m0, n0);
+        run_tile(T_{}, it * nk);
+        finish(m0, n0);
+    }
+    auto store_rest = [&](auto self, auto T) __attribute__((always_inline)) {
+        constexpr int t = decltype(T)::value;
+        if constexpr (t < NST) {
+            store_piece(std::integral_constant<int, t>{});
+            self(self, std::integral_constant<int, t + 1>{});
+        }
+    };
+    store_rest(store_rest, std::integral_constant<int, P0>{});
+}
+
+// ---------------------------------------------------------------------------------
 // Implicit-GEMM 3D convolution on channels-last bf16 activations (ResNet3D conv_a / conv_b /
 // strided branch1; round 4): the cfg 5 machinery (BM x BN x 64 block tile, 8 waves, LDS-DMA
 // ring, two workgroups per CU), with the A operand's rows gathered straight from the input
@@ -1528,8 +2008,8 @@ struct GemmCfg {
 };
 static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}, {128, 128}, {0, 0},
                                  {64, 128}, {256, 256}, {256, 128}, {256, 256}, {256, 256}, {256, 256}, {256, 256},
-                                 {128, 128}};
-constexpr int kNumCfgs = 15;
+                                 {128, 128}, {256, 256}, {256, 256}, {160, 256}};
+constexpr int kNumCfgs = 18;
 
 template <int BM, int BN, int WM, int WN, int E, int ST = 3, int ET = VC_ELEM_BF16>
 static int launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
@@ -1580,6 +2060,23 @@ static int launch_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t 
     gemm_pp_kernel<E, ET, ABL><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out,
                                                                            ldo, aux, ldaux, G, gs, go,
                                                                            (ka > 0 ? ka : K) / 32);
+    return check_launch("vc_gemm_bf16");
+}
+
+template <int E, int ET>
+static int launch_pp160(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
+                        const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
+                        int64_t gs, int64_t go, hipStream_t stream) {
+    constexpr int lds = 4 * (160 + 256) * 64;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_pp160_kernel<E, ET>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
+        attr_set = true;
+    }
+    gemm_pp160_kernel<E, ET><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo,
+                                                                          aux, ldaux, G, gs, go);
     return check_launch("vc_gemm_bf16");
 }
 
@@ -1653,6 +2150,25 @@ static int launch_ppp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t
     return check_launch("vc_gemm_bf16");
 }
 
+template <int E, int ET, int NDEF>
+static int launch_ppd(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K, int N,
+                      const float* bias, void* out, int64_t ldo, hipStream_t stream) {
+    const int lds = 4 * 512 * 64 + N * 4;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_ppd_kernel<E, ET, NDEF>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
+        attr_set = true;
+    }
+    const int ntiles = nbm * nbn;
+    int grid = num_cus() / 8 * 8;
+    if (grid > (ntiles + 7) / 8 * 8) grid = (ntiles + 7) / 8 * 8;
+    gemm_ppd_kernel<E, ET, NDEF><<<(unsigned)grid, 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, N, bias,
+                                                                       (uint16_t*)out, ldo);
+    return check_launch("vc_gemm_bf16");
+}
+
 template <int E, int ET>
 static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int64_t M, int64_t N,
                       int K, const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
@@ -1683,6 +2199,7 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
                                                             go, s);
             return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 14 (timing ablation) is bias_resid_relu only");
         case 9: return launch_pp128<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 17: return launch_pp160<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 4:
             if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
                           E == VC_EPI_BIAS_RELU_BF16 || E == VC_EPI_BIAS_GELU_TANH_SAVE)
@@ -1693,6 +2210,14 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
                           E == VC_EPI_BIAS_RELU_BF16 || E == VC_EPI_BIAS_GELU_TANH_SAVE)
                 return launch_ppp<E, ET>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s, aux, ldaux);
             return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 10 supports 16-bit-output epilogues only");
+        case 15:
+        case 16:  // cfg 16: half the pieces deferred, half stored at the end of the tile (A/B)
+            if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
+                          E == VC_EPI_BIAS_RELU_BF16) {
+                if (cfg == 16) return launch_ppd<E, ET, 8>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
+                return launch_ppd<E, ET, 16>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
+            }
+            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfgs 15 / 16 support the plain 16-bit-output epilogues only");
     }
     return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad config");
 }
@@ -1746,8 +2271,8 @@ extern "C" int vc_gemm_h16(const uint16_t* A, int64_t lda, const uint16_t* W, in
     if (elem == VC_ELEM_F16 && epilogue > VC_EPI_EMBED_F32)
         return fail(VC_ERR_UNSUPPORTED, "vc_gemm: fp16 operands support epilogues 0-4 (the inference forward) only");
     if (!A || !W || !bias || !out) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: null pointer");
-    if (M <= 0 || N <= 0 || K <= 0 || M % 128 || N % 128 || K % GBK)
-        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: need M%128==0, N%128==0, K%64==0 (got M=" +
+    if (M <= 0 || N <= 0 || K <= 0 || (M % 128 && M % 160) || N % 128 || K % GBK)
+        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: need M % 128 == 0 (or M % 160 == 0 for cfg 17), N % 128 == 0, K % 64 == 0 (got M=" +
                                             std::to_string(M) + " N=" + std::to_string(N) + " K=" + std::to_string(K) + ")");
     if (lda % 8 || ldw % 8 || ldo % 4 || lda < K || ldw < K || ldo < N)
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad leading dimension");
@@ -1772,7 +2297,10 @@ extern "C" int vc_gemm_h16(const uint16_t* A, int64_t lda, const uint16_t* W, in
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: no tile config divides M x N");
     if ((M / kCfgs[cfg].bm) * (N / kCfgs[cfg].bn) > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: grid too large");
     const int k = (int)K;
-    if ((cfg == 8 || cfg == 9 || (cfg >= 11 && cfg <= 13)) && K < 128) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 8 / 9 need K >= 128");
+    if ((cfg == 8 || cfg == 9 || cfg == 17 || (cfg >= 11 && cfg <= 13)) && K < 128)
+        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfgs 8 / 9 / 17 need K >= 128");
+    if ((cfg == 15 || cfg == 16) && (K < 640 || K % 64 || N > 8192 || ldo % 8 || ((uintptr_t)out & 15)))
+        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfgs 15 / 16 need K >= 640, K % 64 == 0, N <= 8192, 16-B output rows");
     if ((cfg == 4 || cfg == 10) && (K / 32 < 6 || N > 8192 || !st16_ok ||
                      (epilogue > VC_EPI_BIAS_GELU_ERF && epilogue != VC_EPI_BIAS_RELU_BF16 &&
                       epilogue != VC_EPI_BIAS_GELU_TANH_SAVE)))

@@ -180,7 +180,9 @@ GEMM_KERNEL = {0: "gemm_bf16_kernel<256, 128, 4, 2, {E}, 3, {ET}>", 1: "gemm_bf1
                2: "gemm_bf16_kernel<128, 256, 2, 4, {E}, 3, {ET}>", 3: "gemm_bf16_big_kernel<{E}, {ET}>",
                4: "gemm_bf16_persist_kernel<{E}, {ET}>", 5: "gemm_bf16_kernel<128, 128, 2, 4, {E}, 2, {ET}>",
                7: "gemm_bf16_kernel<64, 128, 2, 4, {E}, 2, {ET}>", 8: "gemm_pp_kernel<{E}, {ET}, 0>",
-               9: "gemm_pp128_kernel<{E}, {ET}>", 10: "gemm_ppp_kernel<{E}, {ET}>"}
+               9: "gemm_pp128_kernel<{E}, {ET}>", 10: "gemm_ppp_kernel<{E}, {ET}>",
+               15: "gemm_ppd_kernel<{E}, {ET}, 16>", 16: "gemm_ppd_kernel<{E}, {ET}, 8>",
+               17: "gemm_pp160_kernel<{E}, {ET}>"}
 
 
 def gemm_kernel_name(M, N, K, epilogue: str, out, aux=None, cfg: int = -1, f16: bool = False) -> str:
