@@ -209,9 +209,18 @@ __device__ __forceinline__ void store_tile(const v16f (&acc)[MI][NI], int64_t mb
 // Epilogue of the 16x16x32 kernels: acc[i][j] holds D[n][m] of a 16x16 block, lane (c16, q) ->
 // m = mb + 16i + c16, reg e -> n = nb + 16j + 4q + e.  Plain 16-bit outputs pair blocks j, j+1
 // with v_permlane16_swap so each lane stores 8 consecutive columns (16 B).
+// bias[nb + 16j + 4q .. + 3] for the NI column blocks of a lane: loaded at kernel entry, so the epilogue
+// does not open with NI dependent global loads (a ping-pong tile's epilogue took 3.3 us to issue with
+// them, 1/6 of its K = 768 main loop: tools/gemm_stamps.py, round 5)
+template <int NI>
+__device__ __forceinline__ void load_bias16(const float* __restrict__ bias, int64_t nb, int q, float4 (&bb)[NI]) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) bb[j] = *reinterpret_cast<const float4*>(bias + nb + j * 16 + 4 * q);
+}
+
 template <int EPI, int MI, int NI, int ET = VC_ELEM_BF16>
 __device__ __forceinline__ void store_tile16(const v4f (&acc)[MI][NI], int64_t mb, int64_t nb, int c16, int q,
-                                             const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
+                                             const float4 (&bq)[NI], void* __restrict__ out, int64_t ldo,
                                              const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride,
                                              int64_t goff) {
     constexpr bool PLAIN16 = EPI == VC_EPI_BIAS_BF16 || EPI == VC_EPI_BIAS_GELU_TANH || EPI == VC_EPI_BIAS_GELU_ERF ||
@@ -226,7 +235,7 @@ __device__ __forceinline__ void store_tile16(const v4f (&acc)[MI][NI], int64_t m
                     unsigned pk[2][2];
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
-                        const float4 bb = *reinterpret_cast<const float4*>(bias + nb + (2 * jp + s) * 16 + 4 * q);
+                        const float4 bb = bq[2 * jp + s];
                         float v0 = acc[i][2 * jp + s][0] + bb.x, v1 = acc[i][2 * jp + s][1] + bb.y;
                         float v2 = acc[i][2 * jp + s][2] + bb.z, v3 = acc[i][2 * jp + s][3] + bb.w;
                         if (EPI == VC_EPI_BIAS_GELU_TANH) {
@@ -255,7 +264,7 @@ __device__ __forceinline__ void store_tile16(const v4f (&acc)[MI][NI], int64_t m
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
             const int64_t m = mb + i * 16 + c16, n = nb + j * 16 + 4 * q;
-            const float4 bb = *reinterpret_cast<const float4*>(bias + n);
+            const float4 bb = bq[j];
             store4<EPI, ET>(m, n, acc[i][j][0] + bb.x, acc[i][j][1] + bb.y, acc[i][j][2] + bb.z, acc[i][j][3] + bb.w,
                             out, ldo, aux, ldaux, G, gstride, goff);
         }
@@ -296,6 +305,8 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave % WN;
     const int c16 = lane & 15, q = lane >> 4;
+    float4 bq[NI];  // this lane's bias columns, loaded now (their latency hides under the main loop)
+    load_bias16<NI>(bias, n0 + wn * TN, q, bq);
 
     // per-lane staging sources (k offset added per tile)
     const uint16_t* asrc[AL];
@@ -408,7 +419,7 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
             for (int j = 0; j < NI; ++j)
             {
                 const int64_t m = m0 + wm * TM + i * 16 + c16, n = n0 + wn * TN + j * 16 + 4 * q;
-                const float4 bb = *reinterpret_cast<const float4*>(bias + n);
+                const float4 bb = bq[j];
                 float4 x = xres[i][j];
                 x.x += acc[i][j][0] + bb.x;
                 x.y += acc[i][j][1] + bb.y;
@@ -425,7 +436,7 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
 #pragma unroll
                     for (int j = 0; j < NI; ++j) {
                         const int64_t m = m0 + wm * TM + i * 16 + c16, n = n0 + wn * TN + j * 16 + 4 * q;
-                        const float4 bb = *reinterpret_cast<const float4*>(bias + n);
+                        const float4 bb = bq[j];
                         const uint2 rr = xaux[i][j];
                         const float v0 = fmaxf(acc[i][j][0] + bb.x + bf2f((unsigned short)(rr.x & 0xffff)), 0.f);
                         const float v1 = fmaxf(acc[i][j][1] + bb.y + bf2f((unsigned short)(rr.x >> 16)), 0.f);
@@ -440,7 +451,7 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
             }
         }
         if (!done)
-            store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bias, out, ldo, aux, ldaux, G,
+            store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bq, out, ldo, aux, ldaux, G,
                                           gstride, goff);
     }
 }
@@ -485,6 +496,8 @@ gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
     const int c16 = lane & 15, q = lane >> 4;
+    float4 bq[NI];  // this lane's bias columns, loaded now (their latency hides under the main loop)
+    load_bias16<NI>(bias, n0 + wn * TN, q, bq);
 
     // staging: wave w fills A rows [32w, 32w+32) and W rows [32w, 32w+32), 16 rows per glds
     const uint16_t* asrc[2];
@@ -565,7 +578,7 @@ gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
     block_sync_lds();
     read_frags(nk - 1, fa1, fw1);
     mfmas(fa1, fw1);
-    store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bias, out, ldo, aux, ldaux, G, gstride, goff);
+    store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bq, out, ldo, aux, ldaux, G, gstride, goff);
 }
 
 // ---------------------------------------------------------------------------------
@@ -607,6 +620,8 @@ gemm_pp160_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* _
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
     const int c16 = lane & 15, q = lane >> 4;
+    float4 bq[NI];  // this lane's bias columns, loaded now (their latency hides under the main loop)
+    load_bias16<NI>(bias, n0 + wn * TN, q, bq);
     const bool astager = wave < 5;  // waves 0-4 stage A rows [32w, 32w + 32)
 
     // staging sources (byte offsets from the wave-uniform panel bases)
@@ -722,7 +737,7 @@ gemm_pp160_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* _
         phase_a(u);
         phase_b(u);
     }
-    store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bias, out, ldo, aux, ldaux, G, gstride,
+    store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bq, out, ldo, aux, ldaux, G, gstride,
                                   goff);
 }
 
@@ -1026,6 +1041,8 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 2, wn = wave & 3;
     const int c16 = lane & 15, q = lane >> 4;
+    float4 bq[NI];  // this lane's bias columns, loaded now (their latency hides under the main loop)
+    load_bias16<NI>(bias, n0 + wn * TN, q, bq);
 
     // staging: wave w fills A rows [32w, 32w + 32) and W rows [32w, 32w + 32), 16 rows per LDS-DMA
     const int arow = wave * 32 + (lane >> 2);
@@ -1111,6 +1128,14 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
         __builtin_amdgcn_sched_barrier(0);
     };
 
+    // ABL 4 (cfg 18, diagnostics): wave 0 and wave 4 stamp s_memrealtime (100 MHz, chip-wide) and
+    // s_memtime (shader clock) at entry, after the prologue wait, after the main loop, after issuing the
+    // epilogue stores and after they drained; aux = u64 [nwg][2 waves][8], results as with cfg 8
+    unsigned long long st_r[5], st_c[2];
+    if constexpr (ABL == 4) {
+        st_r[0] = __builtin_amdgcn_s_memrealtime();
+        st_c[0] = __builtin_amdgcn_s_memtime();
+    }
     // prologue: A0 W0 A1 W1 A2 in flight, retire A0 W0, publish; group 1 falls one barrier behind
     stage_a(0);
     stage_w(0);
@@ -1119,6 +1144,7 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     stage_a(2);
     wait_vm<6>();
     __builtin_amdgcn_s_waitcnt(0xC07F);
+    if constexpr (ABL == 4) st_r[1] = __builtin_amdgcn_s_memrealtime();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -1130,6 +1156,23 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
         phase_b(u, wA);
         phase_a(u + 1, wB);
         phase_b(u + 1, wB);
+    }
+    if constexpr (ABL == 4) {
+        st_r[2] = __builtin_amdgcn_s_memrealtime();
+        store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bq, out, ldo, nullptr, 0, 0, 0, 0);
+        st_r[3] = __builtin_amdgcn_s_memrealtime();
+        __builtin_amdgcn_s_waitcnt(0);
+        st_r[4] = __builtin_amdgcn_s_memrealtime();
+        st_c[1] = __builtin_amdgcn_s_memtime();
+        if ((wave & 3) == 0 && lane == 0) {
+            unsigned long long* o = reinterpret_cast<unsigned long long*>(const_cast<float*>(aux)) +
+                                    ((int64_t)wgid * 2 + (wave >> 2)) * 8;
+            o[0] = st_r[0]; o[1] = st_r[1]; o[2] = st_r[2]; o[3] = st_r[3]; o[4] = st_r[4];
+            o[5] = st_c[1] - st_c[0];
+            o[6] = (unsigned long long)xcd;
+            o[7] = (unsigned long long)bid;
+        }
+        return;
     }
     if constexpr (ABL == 2) {
 #pragma unroll
@@ -1150,7 +1193,7 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
         }
         return;
     }
-    store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bias, out, ldo, aux, ldaux, G, gstride,
+    store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bq, out, ldo, aux, ldaux, G, gstride,
                                   goff);
 }
 
@@ -1184,6 +1227,8 @@ gemm_pp128_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* _
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave >> 1, wn = wave & 1, grp = wave >> 2;
     const int c16 = lane & 15, q = lane >> 4;
+    float4 bq[NI];  // this lane's bias columns, loaded now (their latency hides under the main loop)
+    load_bias16<NI>(bias, n0 + wn * TN, q, bq);
 
     // staging: wave w fills A rows [32w, 32w + 32) (two DMAs) and W rows [16w, 16w + 16) (one)
     const int arow = wave * 32 + (lane >> 2), wrow = wave * 16 + (lane >> 2);
@@ -1256,7 +1301,7 @@ gemm_pp128_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* _
         phase(u, faA, fwA);
         phase(u + 1, faB, fwB);
     }
-    store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bias, out, ldo, aux, ldaux, G, gstride,
+    store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bq, out, ldo, aux, ldaux, G, gstride,
                                   goff);
 }
 
@@ -1516,7 +1561,8 @@ gemm_ppp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
 template <int EPI, int ET = VC_ELEM_BF16, int NDEF = 16>
 __global__ void __launch_bounds__(512, 1)
 gemm_ppd_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw, int nbm,
-                int nbn, int K, int N, const float* __restrict__ bias, uint16_t* __restrict__ out, int64_t ldo) {
+                int nbn, int K, int N, const float* __restrict__ bias, uint16_t* __restrict__ out, int64_t ldo,
+                unsigned long long* __restrict__ stamps) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int BM = 256, BN = 256, BKH = 32, NS = 4;
     constexpr int SLOT = (BM + BN) * 64;  // 32 KiB
@@ -1791,13 +1837,19 @@ gemm_ppd_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
     if (wm == 1) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
 
+    // diagnostics (tools/gemm_stamps.py --ppd): s_memrealtime at entry and after each tile's main loop,
+    // wave 0 of each workgroup, into stamps[b][16] (entry, tiles 0 .. 13, end)
+    const bool stamp = stamps != nullptr && tid == 0;
+    if (stamp) stamps[b * 16] = __builtin_amdgcn_s_memrealtime();
     int64_t m0, n0;
     tile_origin(0, m0, n0);
     run_tile(F_{}, 0);
+    if (stamp) stamps[b * 16 + 1] = __builtin_amdgcn_s_memrealtime();
     finish(m0, n0);
     for (int it = 1; it < mine; ++it) {
         tile_origin(it, m0, n0);
         run_tile(T_{}, it * nk);
+        if (stamp && it < 14) stamps[b * 16 + 1 + it] = __builtin_amdgcn_s_memrealtime();
         finish(m0, n0);
     }
     auto store_rest = [&](auto self, auto T) __attribute__((always_inline)) {
@@ -1808,6 +1860,10 @@ gemm_ppd_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
         }
     };
     store_rest(store_rest, std::integral_constant<int, P0>{});
+    if (stamp) {
+        __builtin_amdgcn_s_waitcnt(0);
+        stamps[b * 16 + 15] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1859,6 +1915,8 @@ conv_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx, ConvGeomG g, const
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave % WN;
     const int c16 = lane & 15, q = lane >> 4;
+    float4 bq[NI];  // this lane's bias columns, loaded now (their latency hides under the main loop)
+    load_bias16<NI>(bias, n0 + wn * TN, q, bq);
 
     // this lane's A rows: output position -> batch offset (input rows) and the input origin of the window
     int64_t rbase[AL];
@@ -1964,7 +2022,7 @@ conv_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx, ConvGeomG g, const
         else wait_vm<0>();
         block_sync_lds();
     }
-    store_tile16<EPI, MI, NI, VC_ELEM_BF16>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bias, out, ldo, aux, ldaux, 1, 0,
+    store_tile16<EPI, MI, NI, VC_ELEM_BF16>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bq, out, ldo, aux, ldaux, 1, 0,
                                             0);
 }
 
@@ -2008,8 +2066,8 @@ struct GemmCfg {
 };
 static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}, {128, 128}, {0, 0},
                                  {64, 128}, {256, 256}, {256, 128}, {256, 256}, {256, 256}, {256, 256}, {256, 256},
-                                 {128, 128}, {256, 256}, {256, 256}, {160, 256}};
-constexpr int kNumCfgs = 18;
+                                 {128, 128}, {256, 256}, {256, 256}, {160, 256}, {256, 256}, {256, 256}};
+constexpr int kNumCfgs = 20;
 
 template <int BM, int BN, int WM, int WN, int E, int ST = 3, int ET = VC_ELEM_BF16>
 static int launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
@@ -2152,7 +2210,8 @@ static int launch_ppp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t
 
 template <int E, int ET, int NDEF>
 static int launch_ppd(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K, int N,
-                      const float* bias, void* out, int64_t ldo, hipStream_t stream) {
+                      const float* bias, void* out, int64_t ldo, hipStream_t stream,
+                      unsigned long long* stamps = nullptr) {
     const int lds = 4 * 512 * 64 + N * 4;
     static bool attr_set = false;
     if (!attr_set) {
@@ -2165,7 +2224,7 @@ static int launch_ppd(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t
     int grid = num_cus() / 8 * 8;
     if (grid > (ntiles + 7) / 8 * 8) grid = (ntiles + 7) / 8 * 8;
     gemm_ppd_kernel<E, ET, NDEF><<<(unsigned)grid, 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, N, bias,
-                                                                       (uint16_t*)out, ldo);
+                                                                       (uint16_t*)out, ldo, stamps);
     return check_launch("vc_gemm_bf16");
 }
 
@@ -2185,6 +2244,12 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
         case 11:
         case 12:
         case 13:
+        case 18:
+            if constexpr ((E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_RESID_F32) &&
+                          ET == VC_ELEM_BF16) {
+                if (cfg == 18)  // diagnostics: cfg 8 with per-workgroup time stamps into aux (ABL 4)
+                    return launch_pp<E, ET, 4>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+            }
             if constexpr (E == VC_EPI_BIAS_BF16 && ET == VC_ELEM_BF16) {
                 if (cfg == 11)
                     return launch_pp<E, ET, 1>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
@@ -2192,7 +2257,7 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
                     return launch_pp<E, ET, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
                 return launch_pp<E, ET, 3>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
             }
-            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfgs 11 / 12 (timing ablations) are bias / bf16 only");
+            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfgs 11 / 12 / 13 / 18 (timing ablations) are bias / bf16 only");
         case 14:  // timing ablation: cfg 5 with the bf16 residual read in the epilogue (G < 0), not prefetched
             if constexpr (E == VC_EPI_BIAS_RESID_RELU_BF16)
                 return launch_cfg<128, 128, 2, 4, E, 2, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, -1, gs,
@@ -2212,12 +2277,14 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
             return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 10 supports 16-bit-output epilogues only");
         case 15:
         case 16:  // cfg 16: half the pieces deferred, half stored at the end of the tile (A/B)
+        case 19:  // diagnostics: cfg 15 writing per-tile time stamps into aux (u64 [grid][16])
             if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
                           E == VC_EPI_BIAS_RELU_BF16) {
                 if (cfg == 16) return launch_ppd<E, ET, 8>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
-                return launch_ppd<E, ET, 16>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
+                auto* st = cfg == 19 ? reinterpret_cast<unsigned long long*>(const_cast<float*>(aux)) : nullptr;
+                return launch_ppd<E, ET, 16>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s, st);
             }
-            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfgs 15 / 16 support the plain 16-bit-output epilogues only");
+            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfgs 15 / 16 / 19 support the plain 16-bit-output epilogues only");
     }
     return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad config");
 }
@@ -2234,6 +2301,13 @@ static int pick_cfg(int64_t M, int64_t N, int64_t K, int epi) {
     const bool bf16_out = epi == VC_EPI_BIAS_BF16 || epi == VC_EPI_BIAS_GELU_TANH || epi == VC_EPI_BIAS_GELU_ERF ||
                           epi == VC_EPI_BIAS_RELU_BF16 || epi == VC_EPI_BIAS_GELU_TANH_SAVE;
     const int64_t t256 = (M / 256) * (N / 256);
+    // round 5: plain-bias outputs with at least a round of 256 x 256 tiles on the persistent kernel with
+    // deferred stores (cfg 15): q|k|v 12800 x 2304 x 768 49.9 vs 52.6 us (cfg 8), 25344 rows 92.8 vs 97.7
+    // (cfg 4); per tile after the first 21.2 vs 23.3 us (tools/gemm_stamps.py).  Not with a GELU: its
+    // epilogue arithmetic at the tile boundary is serial there (fc1 81.0 vs 75.9 us)
+    if (epi == VC_EPI_BIAS_BF16 && M % 256 == 0 && N % 256 == 0 && K % 64 == 0 && K >= 640 && N <= 8192 &&
+        t256 >= 256)
+        return 15;
     // exact-GELU outputs below ~4 rounds of 256x256 tiles: cfg 5 (Swin-T stages 2-4 fc1,
     // tools/tune_swin_gemm.py: 28 vs 36 us at 12544x1536x384, 46 vs 55 at 6400x3072x768)
     // (round 4: the ping-pong kernel, cfg 8, where the tiles fill <= 2.5 rounds of CUs: fc1 at 12800 rows
@@ -2291,15 +2365,15 @@ extern "C" int vc_gemm_h16(const uint16_t* A, int64_t lda, const uint16_t* W, in
     const bool st16_ok = ldo % 8 == 0 && (epilogue != VC_EPI_BIAS_GELU_TANH_SAVE || (ldaux % 8 == 0 && !((uintptr_t)aux & 15)));
     if (cfg < 0) {
         cfg = pick_cfg(M, N, K, epilogue);
-        if (cfg == 4 && !st16_ok) cfg = 5;
+        if ((cfg == 4 || cfg == 15) && (!st16_ok || ((uintptr_t)out & 15))) cfg = 5;
     }
     if (cfg < 0 || cfg >= kNumCfgs || kCfgs[cfg].bm == 0 || M % kCfgs[cfg].bm || N % kCfgs[cfg].bn)
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: no tile config divides M x N");
     if ((M / kCfgs[cfg].bm) * (N / kCfgs[cfg].bn) > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: grid too large");
     const int k = (int)K;
-    if ((cfg == 8 || cfg == 9 || cfg == 17 || (cfg >= 11 && cfg <= 13)) && K < 128)
+    if ((cfg == 8 || cfg == 9 || cfg == 17 || cfg == 18 || (cfg >= 11 && cfg <= 13)) && K < 128)
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfgs 8 / 9 / 17 need K >= 128");
-    if ((cfg == 15 || cfg == 16) && (K < 640 || K % 64 || N > 8192 || ldo % 8 || ((uintptr_t)out & 15)))
+    if ((cfg == 15 || cfg == 16 || cfg == 19) && (K < 640 || K % 64 || N > 8192 || ldo % 8 || ((uintptr_t)out & 15)))
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfgs 15 / 16 need K >= 640, K % 64 == 0, N <= 8192, 16-B output rows");
     if ((cfg == 4 || cfg == 10) && (K / 32 < 6 || N > 8192 || !st16_ok ||
                      (epilogue > VC_EPI_BIAS_GELU_ERF && epilogue != VC_EPI_BIAS_RELU_BF16 &&
@@ -2553,7 +2627,7 @@ extern "C" int vc_gemm_pick(int64_t M, int64_t N, int64_t K, int epilogue, int64
     const bool st16_ok =
         ldo % 8 == 0 && (epilogue != VC_EPI_BIAS_GELU_TANH_SAVE || (ldaux % 8 == 0 && !((uintptr_t)aux & 15)));
     int cfg = pick_cfg(M, N, K, epilogue);
-    if (cfg == 4 && !st16_ok) cfg = 5;
+    if ((cfg == 4 || cfg == 15) && !st16_ok) cfg = 5;
     return cfg;
 }
 

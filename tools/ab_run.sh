@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU A/B session: targeted parity tests of the changed kernels, then the in-tree library vs
-# abl/base/libvclip.so (tools/ab_build.sh of the previous revision) per model family,
+# ab/base/libvclip.so (tools/ab_build.sh of the previous revision) per model family,
 # alternating builds in separate processes (tools/ab_lib.py).
 set -o pipefail
 mkdir -p gpurun_out
@@ -11,9 +11,9 @@ if [ -n "$BENCH" ]; then
   tail -1 gpurun_out/ab_bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], {k: v['avg_launch_ms'] for k, v in d['kernel_breakdown'].items() if k != 'note'})"
 fi
 NEW=ai-laryngeal-video-based-classifier_amd/libvclip.so
-OLD=abl/base/libvclip.so
+OLD=ab/base/libvclip.so
 for mode in ${MODES:-fwd timesformer swin}; do
-  for lib in $NEW $OLD $OLD $NEW; do
+  for lib in $NEW $OLD $OLD $NEW $NEW $OLD; do
     timeout -k 10 120 python tools/ab_lib.py $lib $mode 30 2>&1 | grep -v amdgpu.ids || exit 1
   done
 done
