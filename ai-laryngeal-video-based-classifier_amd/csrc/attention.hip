@@ -42,6 +42,23 @@ constexpr int KV_SLOT = 2 * KV_TILE_BYTES;  // K then V
 constexpr int NSLOT = 4;
 constexpr float LIM = 256.0f;  // WLSE: partial row-sum bound (P <= 2^8) before the running max is re-based
 
+// Experiment hook (round 5, tools/ab_attn.sh -DVC_ATTN_SWEXP=k): the first k of every 32 exp2 of a
+// wave-tile on the VALU instead of v_exp_f32 -- round to nearest by the 1.5 * 2^23 trick, a cubic on
+// [-1/2, 1/2] (rel. error 1e-4, below bf16's 2^-9), the integer part added into the exponent bits:
+// 9 plain VALU ops (4 issue cycles each) for one 8-cycle transcendental.
+#ifndef VC_ATTN_SWEXP
+#define VC_ATTN_SWEXP 0
+#endif
+__device__ __forceinline__ float sw_exp2(float x) {
+    x = fmaxf(x, -126.0f);
+    const float t = x + 12582912.0f;
+    const float f = x - (t - 12582912.0f);
+    float p = __builtin_fmaf(f, 0.0550292665f, 0.2422569819f);
+    p = __builtin_fmaf(f, p, 0.6932530550f);
+    p = __builtin_fmaf(f, p, 0.9999513387f);
+    return __builtin_bit_cast(float, __builtin_bit_cast(unsigned, p) + (__builtin_bit_cast(unsigned, t) << 23));
+}
+
 __device__ __forceinline__ int kswz(int r, int c) { return c ^ ((r >> 1) & 7); }
 __device__ __forceinline__ int vswz(int r, int c) { return c ^ (((r >> 1) & 1) << 2); }
 
@@ -383,7 +400,10 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
             if constexpr (PIPE) {
                 // exp2 of tile t's scores in 16-key-step order (step g = regs 8 (g & 1) .. of key block
                 // g >> 1), so step g's P can be packed as soon as its 8 exp2 are done
-                auto ex = [&](int i) { scur[0][i >> 4][i & 15] = __builtin_amdgcn_exp2f(scur[0][i >> 4][i & 15]); };
+                auto ex = [&](int i) {
+                    if (i < VC_ATTN_SWEXP) scur[0][i >> 4][i & 15] = sw_exp2(scur[0][i >> 4][i & 15]);
+                    else scur[0][i >> 4][i & 15] = __builtin_amdgcn_exp2f(scur[0][i >> 4][i & 15]);
+                };
                 v8s ka = *reinterpret_cast<const v8s*>(nslot + koff[0]);
                 v8s kb = *reinterpret_cast<const v8s*>(nslot + koff[0] + 4096);
                 ex(0); ex(1); ex(2); ex(3);
