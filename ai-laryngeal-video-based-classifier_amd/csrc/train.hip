@@ -8,6 +8,8 @@
 // bit-identical run to run and across data-parallel replicas fed the same shard.
 #include "common.hpp"
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cmath>
 
@@ -499,6 +501,170 @@ wgrad_big_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __
     }
 }
 
+// ---------------------------------------------------------------------------------
+// The weight gradient on the forward GEMM's ping-pong schedule (gemm.hip gemm_pp_kernel; round 5):
+// wgrad_big_kernel's tile (256 n1 x 256 n2, 8 waves as 2 (n2) x 4 (n1), wave tile 128 x 64), its
+// slot layout and transposed fragment reads, but the two waves of each SIMD belong to groups one
+// barrier apart (waves 0-3: n2 0-127, waves 4-7: n2 128-255), so one group's 16 MFMAs run while the
+// other issues its fragment reads and LDS-DMAs.  Per 32-row half-tile u: phase a reads X blocks 0-3
+// of the wave and all 4 G blocks, stages G(u+2), MFMAs; phase b reads X blocks 4-7, stages X(u+3),
+// retires half-tile u+1 (vmcnt(6)), MFMAs with the same G fragments.  WAR: G(u+2) overwrites G(u-2),
+// last read in a(u-2); X(u+3) overwrites X(u-1), last read in b(u-1): both after the lagging group's
+// reads completed (the gemm_pp_kernel argument).  Same MFMA chain per output as wgrad_big_kernel:
+// bit-identical.  Needs >= 3 half-tiles per split.
+// ---------------------------------------------------------------------------------
+__global__ void __launch_bounds__(512, 1)
+wgrad_pp_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __restrict__ X, int64_t ldx, int64_t M,
+                int nJ, int64_t mchunk, float* __restrict__ out, int64_t ldo, int64_t split_stride, int64_t nscaled,
+                float scale) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int ntiles = gridDim.x;
+    const int L = blockIdx.x;
+    const int xq = ntiles >> 3, xr = ntiles & 7, xcd = L & 7;
+    const int tile = (xcd < xr ? xcd * (xq + 1) : xr * (xq + 1) + (xcd - xr) * xq) + (L >> 3);
+    const int ti = tile / nJ, tj = tile % nJ;
+    const int64_t n1_0 = (int64_t)ti * 256, n2_0 = (int64_t)tj * 256;
+    const int64_t mb = (int64_t)blockIdx.y * mchunk;
+    const int64_t me = mb + mchunk < M ? mb + mchunk : M;
+    const int nk = (int)((me - mb) / 32);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int w2 = wave >> 2, w1 = wave & 3;
+
+    // staging: wave w DMAs pieces q = 2w, 2w+1 of each operand (piece = 8 rows of one [32][64] panel);
+    // per-lane byte offsets from the wave-uniform half-tile bases
+    uint32_t goff[2], xoff[2], ldst[2];
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+        const int q = 2 * wave + pp, panel = q >> 2, row = (q & 3) * 8 + (lane >> 3);
+        const int lch = bswz(row, lane & 7);
+        goff[pp] = (uint32_t)(row * ldg + panel * 64 + lch * 8) * 2;
+        xoff[pp] = (uint32_t)(row * ldx + panel * 64 + lch * 8) * 2;
+        ldst[pp] = panel * WPANEL + (q & 3) * 8 * 128;
+    }
+    const uint16_t* Gp = G + mb * ldg + n1_0;
+    const uint16_t* Xp = X + mb * ldx + n2_0;
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem);
+    auto dma = [&](const void* base, uint32_t voff, uint32_t l) __attribute__((always_inline)) {
+        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1"
+                     :
+                     : "v"(voff), "s"(base), "s"(l)
+                     : "memory", "m0");
+    };
+    auto stage_g = [&](int u) __attribute__((always_inline)) {
+        const uint32_t sl = lds0 + (u % WBNS) * WBSLOT;
+        const uint16_t* b = Gp + (int64_t)u * 32 * ldg;
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) dma(b, goff[pp], __builtin_amdgcn_readfirstlane(sl + ldst[pp]));
+    };
+    auto stage_x = [&](int u) __attribute__((always_inline)) {
+        const uint32_t sl = lds0 + (u % WBNS) * WBSLOT + WOPND;
+        const uint16_t* b = Xp + (int64_t)u * 32 * ldx;
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) dma(b, xoff[pp], __builtin_amdgcn_readfirstlane(sl + ldst[pp]));
+    };
+
+    const int gq = (lane & 15) >> 2, gp = lane & 3, gg = lane >> 4;
+    int off1[4], off2[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+        const int col = cb * 16 + gp * 4;
+        const int r1 = 8 * gg + gq, r2 = r1 + 4;
+        off1[cb] = r1 * 128 + bswz(r1, col >> 3) * 16 + (col & 7) * 2;
+        off2[cb] = r2 * 128 + bswz(r2, col >> 3) * 16 + (col & 7) * 2;
+    }
+    constexpr int MI = 8, NI = 4;
+    v4f acc[MI][NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    v8bf fa[4], fb[NI];
+    // X blocks i0 .. i0 + 3 of the wave (panel 2 w2 + i0 / 4)
+    auto read_x = [&](int u, int i0) __attribute__((always_inline)) {
+        const char* pn = smem + (u % WBNS) * WBSLOT + WOPND + (2 * w2 + (i0 >> 2)) * WPANEL;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = tr_frag(pn, off1[i], off2[i]);
+    };
+    auto read_g = [&](int u) __attribute__((always_inline)) {
+        const char* pn = smem + (u % WBNS) * WBSLOT + w1 * WPANEL;
+#pragma unroll
+        for (int j = 0; j < NI; ++j) fb[j] = tr_frag(pn, off1[j], off2[j]);
+    };
+    auto mma = [&](int i0) __attribute__((always_inline)) {
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's fragment reads
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j)
+                acc[i0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i0 + i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto phase_a = [&](int u) __attribute__((always_inline)) {
+        read_x(u, 0);
+        read_g(u);
+        if (u + 2 < nk) stage_g(u + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(0);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto phase_b = [&](int u) __attribute__((always_inline)) {
+        read_x(u, 4);
+        if (u + 3 < nk) {
+            stage_x(u + 3);
+            wg_wait_vm<6>();
+        } else if (u + 2 < nk) {
+            wg_wait_vm<4>();
+        } else {
+            wg_wait_vm<0>();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        mma(4);
+        // the lagging group skips its last barrier: both groups then pass the same number
+        if (u + 1 < nk || w2 == 0) __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    // prologue: X0 G0 X1 G1 X2 in flight, retire X0 G0, publish; group 1 one barrier behind
+    stage_x(0);
+    stage_g(0);
+    stage_x(1);
+    stage_g(1);
+    stage_x(2);
+    wg_wait_vm<6>();
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (w2 == 1) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    for (int u = 0; u < nk; ++u) {
+        phase_a(u);
+        phase_b(u);
+    }
+
+    float* o = out + (int64_t)blockIdx.y * split_stride;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+        const int64_t n1 = n1_0 + w1 * 64 + j * 16 + (lane & 15);
+        const float sc = n1 < nscaled ? scale : 1.0f;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            const int64_t n2 = n2_0 + w2 * 128 + i * 16 + 4 * gg;
+            *reinterpret_cast<float4*>(o + n1 * ldo + n2) =
+                make_float4(acc[i][j][0] * sc, acc[i][j][1] * sc, acc[i][j][2] * sc, acc[i][j][3] * sc);
+        }
+    }
+}
+
 // out[n1][n2] = sum_z ws[z][n1][n2] (the scale was applied per split)
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, int64_t n4, int splits,
                                                            int64_t N2, float* __restrict__ out, int64_t ldo) {
@@ -803,6 +969,17 @@ int vc_colsum(const void* in, int dtype, int64_t ld, int64_t R, int64_t N, int64
     return check_launch("vc_colsum");
 }
 
+// VCLIP_WGRAD_PP=0 in the environment: the weight gradients on wgrad_big_kernel (A/B of the schedules;
+// read once per process)
+static bool wgrad_pp_enabled() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("VCLIP_WGRAD_PP");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v == 1;
+}
+
 int vc_wgrad_bf16(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, int64_t M, int64_t N1, int64_t N2,
                   int64_t nscaled, float scale, float* out, int64_t ldo, float* work, int64_t work_elems,
                   hipStream_t stream) {
@@ -830,15 +1007,21 @@ int vc_wgrad_bf16(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx
         if (!attr) {
             hipError_t e = hipFuncSetAttribute((const void*)wgrad_big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                WBNS * WBSLOT);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void*)wgrad_pp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        WBNS * WBSLOT);
             if (e != hipSuccess) return fail((int)e, std::string("vc_wgrad_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
             attr = true;
         }
+        // the ping-pong schedule when every split has >= 3 half-tiles (the last split is the shortest)
+        const bool pp = (M - (sp - 1) * mch) / 32 >= 3 && wgrad_pp_enabled();
+        auto kern = pp ? wgrad_pp_kernel : wgrad_big_kernel;
         if (sp == 1) {
-            wgrad_big_kernel<<<dim3((unsigned)nt2, 1), 512, WBNS * WBSLOT, stream>>>(G, ldg, X, ldx, M, nJ2, mch, out, ldo,
-                                                                                     0, nscaled, scale);
+            kern<<<dim3((unsigned)nt2, 1), 512, WBNS * WBSLOT, stream>>>(G, ldg, X, ldx, M, nJ2, mch, out, ldo, 0, nscaled,
+                                                                         scale);
         } else {
-            wgrad_big_kernel<<<dim3((unsigned)nt2, (unsigned)sp), 512, WBNS * WBSLOT, stream>>>(
-                G, ldg, X, ldx, M, nJ2, mch, work, N2, N1 * N2, nscaled, scale);
+            kern<<<dim3((unsigned)nt2, (unsigned)sp), 512, WBNS * WBSLOT, stream>>>(G, ldg, X, ldx, M, nJ2, mch, work, N2,
+                                                                                    N1 * N2, nscaled, scale);
             const int64_t n4 = N1 * N2 / 4;
             wgrad_reduce_kernel<<<(unsigned)((n4 + 255) / 256), 256, 0, stream>>>(work, n4, (int)sp, N2, out, ldo);
         }

@@ -316,3 +316,39 @@ def test_adamw_multi_matches_per_tensor():
     torch.cuda.synchronize()
     for (rp, rm, rv), p, m, v in zip(ref, ps, ms, vs):
         assert torch.equal(p, rp) and torch.equal(m, rm) and torch.equal(v, rv)
+
+
+def test_wgrad_pp_bit_identical_to_big(tmp_path):
+    """The ping-pong weight-gradient kernel (wgrad_pp_kernel, the default) runs wgrad_big_kernel's MFMA
+    chain per output: a child process with VCLIP_WGRAD_PP=0 (the big kernel) must give the same bits,
+    with and without split-K partials."""
+    import subprocess
+    import sys
+    O = ops()
+    g = torch.Generator().manual_seed(11)
+    cases = [(12800, 768, 3072, True), (3200, 2304, 768, False), (4096, 768, 768, True)]
+    data = {}
+    for i, (M, N1, N2, split) in enumerate(cases):
+        gg = torch.randn(M, N1, generator=g).bfloat16()
+        xx = torch.randn(M, N2, generator=g).bfloat16()
+        out = torch.zeros(N1, N2, device=DEV)
+        work = torch.empty(4 * N1 * N2, device=DEV) if split else None
+        O.wgrad(gg.to(DEV), xx.to(DEV), out, work, nscaled=N1 // 3, scale=0.3)
+        data[f"g{i}"], data[f"x{i}"], data[f"o{i}"] = gg, xx, out.cpu()
+    torch.save(data, tmp_path / "in.pt")
+    root = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+    code = (
+        "import sys, torch; sys.path.insert(0, %r)\n"
+        "from vclip_amd import ops as O\n"
+        "d = torch.load(%r, weights_only=True); r = {}\n"
+        "for i, (M, N1, N2, split) in enumerate(%r):\n"
+        "    out = torch.zeros(N1, N2, device='cuda')\n"
+        "    work = torch.empty(4 * N1 * N2, device='cuda') if split else None\n"
+        "    O.wgrad(d[f'g{i}'].cuda(), d[f'x{i}'].cuda(), out, work, nscaled=N1 // 3, scale=0.3)\n"
+        "    r[f'o{i}'] = out.cpu()\n"
+        "torch.save(r, %r)\n" % (root, str(tmp_path / "in.pt"), cases, str(tmp_path / "out.pt")))
+    env = dict(__import__("os").environ, VCLIP_WGRAD_PP="0")
+    subprocess.run([sys.executable, "-c", code], env=env, check=True, timeout=300)
+    big = torch.load(tmp_path / "out.pt", weights_only=True)
+    for i in range(len(cases)):
+        assert torch.equal(data[f"o{i}"], big[f"o{i}"]), i
