@@ -812,6 +812,27 @@ def wgrad_work(M: int, N1: int, N2: int, device) -> torch.Tensor:
     return torch.empty(max(2, sp) * N1 * N2, dtype=torch.float32, device=device)
 
 
+def wgrad_kernel_name(M: int, N1: int, N2: int, work_elems: int) -> str:
+    """The rocprofv3 name of the kernel vc_wgrad_bf16 runs for this call (csrc/train.hip's dispatch:
+    the split count it derives from the scratch size, then the ping-pong kernel when every split has
+    >= 3 32-row half-tiles, unless VCLIP_WGRAD_PP=0)"""
+    import os
+    if N1 % 256 or N2 % 256:
+        return "trn::wgrad_kernel"
+    nt2 = (N1 // 256) * (N2 // 256)
+    kt2 = M // 32
+    sp = min(-(-256 // nt2), kt2 // 4)
+    if work_elems < 2 * N1 * N2:
+        sp = 1
+    elif sp * N1 * N2 > work_elems:
+        sp = work_elems // (N1 * N2)
+    sp = max(sp, 1)
+    mch = -(-kt2 // sp) * 32
+    sp = -(-M // mch)
+    pp = (M - (sp - 1) * mch) // 32 >= 3 and os.environ.get("VCLIP_WGRAD_PP", "1")[:1] != "0"
+    return "trn::wgrad_pp_kernel" if pp else "trn::wgrad_big_kernel"
+
+
 def wgrad(g: torch.Tensor, x: torch.Tensor, out: torch.Tensor, work: torch.Tensor | None = None,
           nscaled: int = 0, scale: float = 1.0, m: int | None = None) -> torch.Tensor:
     """out[n1][n2] = s(n1) * sum_m g[m][n1] x[m][n2]  (g bf16 [M, N1], x bf16 [M, N2], out f32 [N1, N2])."""
@@ -824,8 +845,7 @@ def wgrad(g: torch.Tensor, x: torch.Tensor, out: torch.Tensor, work: torch.Tenso
     wp, wn = (_p(work), work.numel()) if work is not None else (None, 0)
     rec = _REC[0]
     if rec is not None:  # one entry per vc_wgrad_bf16 call: the split-K kernel plus its partial reduction
-        big = N1 % 256 == 0 and N2 % 256 == 0
-        label = "trn::wgrad_big_kernel (+ wgrad_reduce_kernel)" if big else "trn::wgrad_kernel (+ wgrad_reduce_kernel)"
+        label = wgrad_kernel_name(M, N1, N2, wn) + " (+ wgrad_reduce_kernel)"
         e0 = rec.begin()
     _lib.call("vc_wgrad_bf16", _p(g), g.stride(0), _p(x), x.stride(0), M, N1, N2, nscaled, scale, _p(out),
               out.stride(0), wp, wn, _stream(g))

@@ -483,15 +483,15 @@ class Swin3d(torch.nn.Module):
                 shift_full = [0 if i % 2 == 0 else k // 2 for k in c["window_size"]]
                 window, shift = window_and_shift((t, h, w), c["window_size"], shift_full)
                 biasT = self._biasT(s, i, window, video.device)
-                tm("layernorm_grp_kernel", "layernorm", ntok * C * 6, "byte", ops.layernorm, X, blk["ln1"][0],
+                tm("layernorm_grp_kernel", f"layernorm.s{s}", ntok * C * 6, "byte", ops.layernorm, X, blk["ln1"][0],
                    blk["ln1"][1], eps, Y, m=ntok)
-                ops.gemm(Y, blk["w_qkv"], blk["b_qkv"], "bias", QKV, flop=2.0 * ntok * 3 * C * C, op="qkv")
+                ops.gemm(Y, blk["w_qkv"], blk["b_qkv"], "bias", QKV, flop=2.0 * ntok * 3 * C * C, op=f"qkv.s{s}")
                 ev = self.kernel_events
                 if ev is not None:  # recorded on the current stream, the one the kernel runs on
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record()
                 n = window[0] * window[1] * window[2]
-                tm("window_attn_mb_d32_kernel", "window_attention", 4.0 * ntok * n * 32 * st["heads"], "flop",
+                tm("window_attn_mb_d32_kernel", f"window_attention.s{s}", 4.0 * ntok * n * 32 * st["heads"], "flop",
                    ops.window_attention3d, QKV, B, (t, h, w), st["heads"], window, shift, biasT, O)
                 if ev is not None:
                     e1.record()
@@ -499,11 +499,11 @@ class Swin3d(torch.nn.Module):
                     # algorithmic bytes: q, k, v read and the output written once (4 x 32 x 2 B per
                     # token-head)
                     ev.append((e0, e1, 4.0 * ntok * n * 32 * st["heads"], 256.0 * ntok * st["heads"]))
-                ops.gemm(O, blk["w_proj"], blk["b_proj"], "bias_resid_f32", X, flop=2.0 * ntok * C * C, op="proj")
-                tm("layernorm_grp_kernel", "layernorm", ntok * C * 6, "byte", ops.layernorm, X, blk["ln2"][0],
+                ops.gemm(O, blk["w_proj"], blk["b_proj"], "bias_resid_f32", X, flop=2.0 * ntok * C * C, op=f"proj.s{s}")
+                tm("layernorm_grp_kernel", f"layernorm.s{s}", ntok * C * 6, "byte", ops.layernorm, X, blk["ln2"][0],
                    blk["ln2"][1], eps, Y, m=ntok)
-                ops.gemm(Y, blk["w_1"], blk["b_1"], "bias_gelu_erf", Hd, flop=2.0 * ntok * hid * C, op="fc1")
-                ops.gemm(Hd, blk["w_2"], blk["b_2"], "bias_resid_f32", X, flop=2.0 * ntok * C * hid, op="fc2")
+                ops.gemm(Y, blk["w_1"], blk["b_1"], "bias_gelu_erf", Hd, flop=2.0 * ntok * hid * C, op=f"fc1.s{s}")
+                ops.gemm(Hd, blk["w_2"], blk["b_2"], "bias_resid_f32", X, flop=2.0 * ntok * C * hid, op=f"fc2.s{s}")
             if s < len(grids) - 1:
                 nxt = ws["stages"][s + 1]
                 t2, h2, w2 = grids[s + 1]

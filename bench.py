@@ -508,7 +508,7 @@ def run_family(a, dist, rank, world, dev):
             "kernel_breakdown": dict(list(table.items())[:12], note=f"3 steps of the headline's {a.streams}-part split "
                                      "serialised on one stream, HIP events around every launch: "
                                      f"{instr_ms:.3f} ms per step under that instrumentation"),
-            "op_breakdown": (dict(list(op_breakdown.last_ops.items())[:20]) if a.mode == "resnet3d" else None),
+            "op_breakdown": dict(list(op_breakdown.last_ops.items())[:24]),
             "model_tflops": round(model_tflops, 1), "model_frac_of_peak": round(model_tflops / PEAK_BF16_TFLOPS, 4),
             "cpu_baseline": cpu,
             "build": _build_id(),
@@ -517,19 +517,21 @@ def run_family(a, dist, rank, world, dev):
     return out
 
 
-WGRAD_LABEL = "trn::wgrad_big_kernel (+ wgrad_reduce_kernel)"
+WGRAD_KERNELS = ("trn::wgrad_pp_kernel", "trn::wgrad_big_kernel")
 
 
 def wgrad_line(ktable, instr_ms):
     """the weight-gradient row of the train step's per-kernel table against the bf16 peak, with the
-    wgrad_big_kernel counters of this build's train profile (when present)"""
-    row = ktable.get(WGRAD_LABEL)
-    if row is None:
+    weight-gradient kernel's counters of this build's train profile (when present)"""
+    kern = next((k for k in WGRAD_KERNELS if f"{k} (+ wgrad_reduce_kernel)" in ktable), None)
+    if kern is None:
         return None
-    traffic, traffic_src = measured_traffic(["trn::wgrad_big_kernel", "trn::wgrad_reduce_kernel"], "train")
-    pmc, pmc_src = measured_pmc("trn::wgrad_big_kernel", "train")
+    label = f"{kern} (+ wgrad_reduce_kernel)"
+    row = ktable[label]
+    traffic, traffic_src = measured_traffic([kern, "trn::wgrad_reduce_kernel"], "train")
+    pmc, pmc_src = measured_pmc(kern, "train")
     mfma_busy, valu_per_mfma = pmc_rates(pmc)
-    return {"bound": "mfma", "kernel": WGRAD_LABEL, "achieved": row["achieved"], "peak": PEAK_BF16_TFLOPS,
+    return {"bound": "mfma", "kernel": label, "achieved": row["achieved"], "peak": PEAK_BF16_TFLOPS,
             "unit": "TFLOP/s", "frac": round(row["achieved"] / PEAK_BF16_TFLOPS, 4),
             "avg_launch_ms": row["avg_launch_ms"], "launches_per_step": row["launches_per_step"],
             "share_of_step": row["share_of_step"], "traffic": traffic, "traffic_source": traffic_src,
