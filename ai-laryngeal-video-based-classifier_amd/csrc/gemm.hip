@@ -742,6 +742,187 @@ gemm_pp160_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* _
 }
 
 // ---------------------------------------------------------------------------------
+// Streaming 1x1x1-conv kernel for the ResNet3D conv_c (cfg 20; round 5): out = relu(A.W^T + b + res),
+// bf16 residual, K in {64, 128}.  At K = 64 / 128 the launch is HBM-bound (res2: 461 MB per launch for
+// 26 GFLOP): the 128 x 128 two-workgroups-per-CU kernel loaded, computed and stored each tile in turn
+// and moved 3.4 TB/s (0.43 of peak).  Here one 512-thread workgroup per CU keeps its 128 x 256 tile
+// column (n) fixed -- W [256][K] staged into LDS once -- and walks the m tiles r, r + R, ...; while tile
+// i is computed and stored, tile i+1's A rows (registers -> the other LDS buffer) and its residual
+// (registers) are in flight.  Those loads are inline asm with explicit vmcnt waits: compiler-visible
+// loads were re-ordered behind the stores and waited for with vmcnt(0-3) before the epilogue, which
+// serialised the pipeline again.  vmcnt counts loads and stores in issue order; per step: ACH A
+// loads, 8 residual loads, 8 stores.  Residual and output move as 16-B lanes (v_permlane16_swap pairs
+// blocks 2jp, 2jp+1: 64-B row segments instead of 32-B ones).  Workgroups of one m tile (same r,
+// different n tiles) sit R apart in block id, R % 8 == 0: same XCD.  Same k order, MFMA chain and
+// epilogue arithmetic per output as cfg 5: bit-identical.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ void gld16_asm(v4u& r, const void* p) {
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p));
+}
+template <int N>
+__device__ __forceinline__ void vm_wait_asm() {
+    static_assert(N >= 0 && N < 64, "vmcnt immediate");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+template <class T>
+__device__ __forceinline__ void vtie(T& r) {
+    asm volatile("" : "+v"(r));
+}
+
+template <int KD>
+__global__ void __launch_bounds__(512, 1)
+conv_c_stream_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
+                     int nbm, int R, const float* __restrict__ bias, uint16_t* __restrict__ out, int64_t ldo,
+                     const uint16_t* __restrict__ res, int64_t ldres) {
+    static_assert(KD == 64 || KD == 128, "K of one or two 64-deep k-tiles");
+    constexpr int BM = 128, BN = 256, NKT = KD / 64, TM = 64, TN = 64, MI = 4, NI = 4, NP = NI / 2;
+    constexpr int ACH = BM * 8 * NKT / 512;  // 16-B chunks of the A tile per thread
+    constexpr int NRES = MI * NP;            // 16-B residual loads (and output stores) per thread per tile
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* Ws = smem;                      // NKT x [256 rows][128 B]
+    char* As = smem + NKT * BN * 128;     // 2 buffers x NKT x [128 rows][128 B]
+    constexpr int ABUF = NKT * BM * 128;
+
+    const int tn = blockIdx.x / R, r0 = blockIdx.x - tn * R;
+    if (r0 >= nbm) return;
+    const int64_t n0 = (int64_t)tn * BN;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave >> 2, wn = wave & 3;
+    const int c16 = lane & 15, q = lane >> 4;
+    float4 bq[NI];
+    load_bias16<NI>(bias, n0 + wn * TN, q, bq);
+
+    // W [256][KD] -> LDS (row-swizzled 16-B chunks), once
+#pragma unroll
+    for (int s = 0; s < BN * 8 * NKT / 512; ++s) {
+        const int c = tid + 512 * s, kt = c / (BN * 8), rw = (c >> 3) & (BN - 1), ch = c & 7;
+        const uint4 v = *reinterpret_cast<const uint4*>(W + (n0 + rw) * ldw + kt * 64 + ch * 8);
+        *reinterpret_cast<uint4*>(Ws + kt * BN * 128 + rw * 128 + swz(rw, ch) * 16) = v;
+    }
+    // a lane's 16-B row segment of column-block pair jp (as store_tile16's PLAIN16 layout)
+    const int64_t ncol = n0 + wn * TN + (q & 1) * 16 + 4 * (q & 2);
+    v4u areg[ACH];
+    auto load_a = [&](int mt) __attribute__((always_inline)) {
+        const int64_t m0 = (int64_t)mt * BM;
+#pragma unroll
+        for (int s = 0; s < ACH; ++s) {
+            const int c = tid + 512 * s, kt = c / (BM * 8), rw = (c >> 3) & (BM - 1), ch = c & 7;
+            gld16_asm(areg[s], A + (m0 + rw) * lda + kt * 64 + ch * 8);
+        }
+    };
+    auto store_a = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+        for (int s = 0; s < ACH; ++s) {
+            const int c = tid + 512 * s, kt = c / (BM * 8), rw = (c >> 3) & (BM - 1), ch = c & 7;
+            *reinterpret_cast<v4u*>(As + buf * ABUF + kt * BM * 128 + rw * 128 + swz(rw, ch) * 16) = areg[s];
+        }
+    };
+    auto load_res = [&](int mt, v4u (&rr)[NRES]) __attribute__((always_inline)) {
+        const int64_t m0 = (int64_t)mt * BM;
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int jp = 0; jp < NP; ++jp)
+                gld16_asm(rr[i * NP + jp], res + (m0 + wm * TM + i * 16 + c16) * ldres + ncol + jp * 32);
+    };
+    // one m tile: issue tile `nm`'s loads, compute `mt` from LDS buffer `buf`, epilogue with rc
+    // (loaded one step earlier), then stage nm's A rows into buffer buf ^ 1
+    auto step = [&](int mt, int buf, v4u (&rc)[NRES], v4u (&rn)[NRES]) __attribute__((always_inline)) -> bool {
+        const int nxt = mt + R;
+        const bool more = nxt < nbm;
+        const int nm = more ? nxt : mt;  // the last step re-reads its own tile (uniform vmcnt accounting)
+        load_a(nm);
+        load_res(nm, rn);
+        v4f acc[MI][NI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kt = 0; kt < NKT; ++kt) {
+            const char* At = As + buf * ABUF + kt * BM * 128;
+            const char* Wt = Ws + kt * BN * 128;
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                v8s af[MI];
+#pragma unroll
+                for (int i = 0; i < MI; ++i) af[i] = lds_frag(At, wm * TM + i * 16 + c16, 4 * kk + q);
+#pragma unroll
+                for (int j = 0; j < NI; ++j) {  // one W fragment live at a time (register budget)
+                    const v8s wf = lds_frag(Wt, wn * TN + j * 16 + c16, 4 * kk + q);
+#pragma unroll
+                    for (int i = 0; i < MI; ++i) acc[i][j] = mfma16x32<VC_ELEM_BF16>(wf, af[i], acc[i][j]);
+                }
+            }
+        }
+        // rc landed: younger than its loads are the previous step's NRES stores and this step's loads
+        vm_wait_asm<NRES + ACH + NRES>();
+#pragma unroll
+        for (int u = 0; u < NRES; ++u) vtie(rc[u]);
+        const int64_t m0 = (int64_t)mt * BM;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            uint16_t* orow = out + (m0 + wm * TM + i * 16 + c16) * ldo + ncol;
+#pragma unroll
+            for (int jp = 0; jp < NP; ++jp) {
+                // residual back into the accumulator layout: the inverse of the output's lane swap
+                const v4u r = rc[i * NP + jp];
+                const auto t0 = __builtin_amdgcn_permlane16_swap(r.x, r.z, false, false);
+                const auto t1 = __builtin_amdgcn_permlane16_swap(r.y, r.w, false, false);
+                const unsigned rw[2][2] = {{t0[0], t1[0]}, {t0[1], t1[1]}};
+                unsigned pk[2][2];
+#pragma unroll
+                for (int sb = 0; sb < 2; ++sb) {
+                    const int j = 2 * jp + sb;
+                    const float4 bb = bq[j];
+                    float v0 = acc[i][j][0] + bb.x, v1 = acc[i][j][1] + bb.y, v2 = acc[i][j][2] + bb.z,
+                          v3 = acc[i][j][3] + bb.w;
+                    v0 += bf2f((unsigned short)(rw[sb][0] & 0xffff)); v1 += bf2f((unsigned short)(rw[sb][0] >> 16));
+                    v2 += bf2f((unsigned short)(rw[sb][1] & 0xffff)); v3 += bf2f((unsigned short)(rw[sb][1] >> 16));
+                    pk[sb][0] = pack2<VC_ELEM_BF16>(fmaxf(v0, 0.f), fmaxf(v1, 0.f));
+                    pk[sb][1] = pack2<VC_ELEM_BF16>(fmaxf(v2, 0.f), fmaxf(v3, 0.f));
+                }
+                const auto s0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+                const auto s1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+                v4u v;
+                v.x = s0[0]; v.y = s1[0]; v.z = s0[1]; v.w = s1[1];
+                *reinterpret_cast<v4u*>(orow + jp * 32) = v;
+            }
+        }
+        if (!more) {
+            vm_wait_asm<0>();
+            return false;
+        }
+        // nm's A rows landed: younger are its NRES residual loads and this step's NRES stores
+        vm_wait_asm<NRES + NRES>();
+#pragma unroll
+        for (int s = 0; s < ACH; ++s) vtie(areg[s]);
+        store_a(buf ^ 1);
+        block_sync_lds();
+        return true;
+    };
+
+    v4u r0b[NRES], r1b[NRES];
+    int mt = r0;
+    load_a(mt);
+    load_res(mt, r0b);
+    vm_wait_asm<0>();
+#pragma unroll
+    for (int s = 0; s < ACH; ++s) vtie(areg[s]);
+#pragma unroll
+    for (int u = 0; u < NRES; ++u) vtie(r0b[u]);
+    store_a(0);
+    block_sync_lds();
+    for (;;) {  // two steps per trip: the residual registers alternate without copies
+        if (!step(mt, 0, r0b, r1b)) break;
+        mt += R;
+        if (!step(mt, 1, r1b, r0b)) break;
+        mt += R;
+    }
+}
+
+// ---------------------------------------------------------------------------------
 // Persistent 256x256 kernel for the 16-bit-output epilogues (q|k|v, fc1; cfg 4): one workgroup
 // per CU walks its tiles; the next tile's first three half-tiles (BK = 32, 4-slot LDS ring,
 // counted vmcnt, one barrier per half-tile) go in flight BEFORE the current tile's epilogue,
@@ -2066,8 +2247,8 @@ struct GemmCfg {
 };
 static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}, {128, 128}, {0, 0},
                                  {64, 128}, {256, 256}, {256, 128}, {256, 256}, {256, 256}, {256, 256}, {256, 256},
-                                 {128, 128}, {256, 256}, {256, 256}, {160, 256}, {256, 256}, {256, 256}};
-constexpr int kNumCfgs = 20;
+                                 {128, 128}, {256, 256}, {256, 256}, {160, 256}, {256, 256}, {256, 256}, {128, 256}};
+constexpr int kNumCfgs = 21;
 
 template <int BM, int BN, int WM, int WN, int E, int ST = 3, int ET = VC_ELEM_BF16>
 static int launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
@@ -2228,6 +2409,28 @@ static int launch_ppd(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t
     return check_launch("vc_gemm_bf16");
 }
 
+template <int KD>
+static int launch_conv_c_stream(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int64_t M, int64_t N,
+                                const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux,
+                                hipStream_t stream) {
+    constexpr int lds = (KD / 64) * 256 * 128 + 2 * (KD / 64) * 128 * 128;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)conv_c_stream_kernel<KD>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
+        attr_set = true;
+    }
+    const int nbm = (int)(M / 128), nbn = (int)(N / 256);
+    // about one workgroup per CU over all n tiles; R a multiple of 8 (the n tiles of one m tile share an XCD)
+    int R = (num_cus() + nbn - 1) / nbn;
+    R = (R + 7) / 8 * 8;
+    if (R > (nbm + 7) / 8 * 8) R = (nbm + 7) / 8 * 8;
+    conv_c_stream_kernel<KD><<<(unsigned)(R * nbn), 512, lds, stream>>>(
+        A, lda, W, ldw, nbm, R, bias, (uint16_t*)out, ldo, reinterpret_cast<const uint16_t*>(aux), ldaux);
+    return check_launch("vc_gemm_bf16");
+}
+
 template <int E, int ET>
 static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int64_t M, int64_t N,
                       int K, const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
@@ -2265,6 +2468,12 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
             return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 14 (timing ablation) is bias_resid_relu only");
         case 9: return launch_pp128<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 17: return launch_pp160<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 20:  // streaming 1x1x1 conv with the bf16 residual (ResNet3D conv_c), K 64 / 128, N % 256
+            if constexpr (E == VC_EPI_BIAS_RESID_RELU_BF16 && ET == VC_ELEM_BF16) {
+                if (K == 64) return launch_conv_c_stream<64>(A, lda, W, ldw, M, N, bias, out, ldo, aux, ldaux, s);
+                if (K == 128) return launch_conv_c_stream<128>(A, lda, W, ldw, M, N, bias, out, ldo, aux, ldaux, s);
+            }
+            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 20 is bias_resid_relu with K 64 / 128 only");
         case 4:
             if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
                           E == VC_EPI_BIAS_RELU_BF16 || E == VC_EPI_BIAS_GELU_TANH_SAVE)
@@ -2308,6 +2517,8 @@ static int pick_cfg(int64_t M, int64_t N, int64_t K, int epi) {
     if (epi == VC_EPI_BIAS_BF16 && M % 256 == 0 && N % 256 == 0 && K % 64 == 0 && K >= 640 && N <= 8192 &&
         t256 >= 256)
         return 15;
+    // round 5: the ResNet3D conv_c at K = 64 / 128 (HBM-bound) on the streaming kernel
+    if (epi == VC_EPI_BIAS_RESID_RELU_BF16 && (K == 64 || K == 128) && M % 128 == 0 && N % 256 == 0) return 20;
     // exact-GELU outputs below ~4 rounds of 256x256 tiles: cfg 5 (Swin-T stages 2-4 fc1,
     // tools/tune_swin_gemm.py: 28 vs 36 us at 12544x1536x384, 46 vs 55 at 6400x3072x768)
     // (round 4: the ping-pong kernel, cfg 8, where the tiles fill <= 2.5 rounds of CUs: fc1 at 12800 rows

@@ -257,3 +257,32 @@ def test_gemm_bias_resid_relu_epilogue(K, cfg):
     O.gemm(a.to(DEV), w.to(DEV), b.to(DEV), "bias_resid_relu", out, aux=r.to(DEV), cfg=cfg)
     got = out.float().cpu()
     assert torch.allclose(got, want, rtol=2 ** -7, atol=1e-3), float((got - want).abs().max())
+
+
+@pytest.mark.parametrize("M,N,K,lda,ldr", [(1024, 256, 64, 64, 256), (8192, 512, 128, 256, 512),
+                                           (401408, 256, 64, 64, 256), (100352, 512, 128, 128, 512),
+                                           (25600, 768, 64, 192, 1024)])
+def test_conv_c_stream_bit_identical(M, N, K, lda, ldr):
+    """The streaming conv_c kernel (cfg 20: W tile resident in LDS, the next m tile's A rows and
+    residual in flight under the current tile) against the 128x128 kernel (cfg 5): same MFMA chain and
+    epilogue order per output -> bit-identical; strided A (a column slice of a wider buffer, as
+    resnet3d passes act["b"][:, :inner]), padded residual rows, fewer m tiles than workgroups and the
+    res2 / res3 full sizes."""
+    O = ops()
+    g = torch.Generator(device=DEV).manual_seed(M + K)
+    abuf = (torch.randn(M, lda, device=DEV, generator=g) * 0.5).bfloat16()
+    a = abuf[:, :K]
+    w = (torch.randn(N, K, device=DEV, generator=g) * 0.05).bfloat16()
+    b = torch.randn(N, device=DEV, generator=g) * 0.1
+    rbuf = torch.randn(M, ldr, device=DEV, generator=g).bfloat16()
+    r = rbuf[:, :N]
+    want = torch.full((M, N), 7.0, dtype=torch.bfloat16, device=DEV)
+    assert O.gemm_kernel_name(M, N, K, "bias_resid_relu", want, r) == f"conv_c_stream_kernel<{K}>"
+    got = want.clone()
+    O.gemm(a, w, b, "bias_resid_relu", want, aux=r, cfg=5)
+    O.gemm(a, w, b, "bias_resid_relu", got, aux=r)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want), int((got != want).sum())
+    if M <= 8192:  # and the fp32 torch reference
+        ref = torch.relu(a.float() @ w.float().T + b + r.float())
+        assert torch.allclose(got.float(), ref, rtol=2 ** -7, atol=1e-3)
