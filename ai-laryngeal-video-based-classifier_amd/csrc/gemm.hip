@@ -69,6 +69,20 @@ __device__ __forceinline__ void wait_vm() {
     __builtin_amdgcn_s_waitcnt((NW & 15) | ((NW >> 4) << 14) | 0x0F70);  // vmcnt(NW) only
 }
 
+// wait until at most min(n, MAXT) tiles of LPT loads each are outstanding (n uniform; n < 0 -> 0)
+template <int LPT, int MAXT>
+__device__ __forceinline__ void wait_tiles(int n) {
+    if constexpr (MAXT > 0) {
+        if (n >= MAXT) {
+            wait_vm<LPT * MAXT>();
+            return;
+        }
+        wait_tiles<LPT, MAXT - 1>(n);
+    } else {
+        wait_vm<0>();
+    }
+}
+
 __device__ __forceinline__ void block_sync_lds() {
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
@@ -286,7 +300,7 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
                  int nbm, int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
                  const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride, int64_t goff) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    static_assert(ST == 2 || ST == 3, "ring depth");
+    static_assert(ST >= 2 && ST <= 8, "ring depth");
     constexpr int SLOT = (BM + BN) * 128;       // bytes per ring slot (A then W, 128-B rows)
     constexpr int TM = BM / WM, TN = BN / WN;   // wave tile
     constexpr int MI = TM / 16, NI = TN / 16;
@@ -372,12 +386,11 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
                                                                  j * 16 + 4 * q);
         }
     }
-    if (ST == 3 && nk > 1) {
-        stage(1, 1);
-        wait_vm<LPT>();
-    } else {
-        wait_vm<0>();
-    }
+    // tiles 1 .. ST-2 in flight too; then retire tile 0 (the tiles issued after it may stay in flight)
+#pragma unroll
+    for (int u = 1; u < ST - 1; ++u)
+        if (u < nk) stage(u, u);
+    wait_tiles<LPT, ST - 2>(nk - 1);
     block_sync_lds();
 
     for (int t = 0; t < nk; ++t) {
@@ -406,9 +419,8 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
                     for (int j = 0; j < NI; ++j)
                         acc[i][j] = mfma16x32<ET>(wf[kk][j], af[kk][i], acc[i][j]);
         }
-        // retire tile t+1 (with ST = 3, tile t+2 may stay in flight), then all waves pass the barrier
-        if (ST == 3 && t + 2 < nk) wait_vm<LPT>();
-        else wait_vm<0>();
+        // retire tile t+1 (tiles t+2 .. t+ST-1 may stay in flight), then all waves pass the barrier
+        wait_tiles<LPT, ST - 2>(nk - 2 - t);
         block_sync_lds();
     }
 
@@ -2171,12 +2183,11 @@ conv_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx, ConvGeomG g, const
 
     const int nk = K / 64;
     stage(0, 0);
-    if (ST == 3 && nk > 1) {
-        stage(1, 1);
-        wait_vm<LPT>();
-    } else {
-        wait_vm<0>();
-    }
+    // tiles 1 .. ST-2 in flight too; then retire tile 0 (the tiles issued after it may stay in flight)
+#pragma unroll
+    for (int u = 1; u < ST - 1; ++u)
+        if (u < nk) stage(u, u);
+    wait_tiles<LPT, ST - 2>(nk - 1);
     block_sync_lds();
 
     for (int t = 0; t < nk; ++t) {
@@ -2247,8 +2258,9 @@ struct GemmCfg {
 };
 static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}, {128, 128}, {0, 0},
                                  {64, 128}, {256, 256}, {256, 128}, {256, 256}, {256, 256}, {256, 256}, {256, 256},
-                                 {128, 128}, {256, 256}, {256, 256}, {160, 256}, {256, 256}, {256, 256}, {128, 256}};
-constexpr int kNumCfgs = 21;
+                                 {128, 128}, {256, 256}, {256, 256}, {160, 256}, {256, 256}, {256, 256}, {128, 256},
+                                 {64, 128}, {64, 128}, {128, 128}};
+constexpr int kNumCfgs = 24;
 
 template <int BM, int BN, int WM, int WN, int E, int ST = 3, int ET = VC_ELEM_BF16>
 static int launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
@@ -2443,6 +2455,10 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
         case 3: return launch_big<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 5: return launch_cfg<128, 128, 2, 4, E, 2, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 7: return launch_cfg<64, 128, 2, 4, E, 2, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        // round 5: deeper rings for the latency-bound small launches (Swin-T's per-stream parts)
+        case 21: return launch_cfg<64, 128, 2, 4, E, 4, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 22: return launch_cfg<64, 128, 2, 4, E, 6, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 23: return launch_cfg<128, 128, 2, 4, E, 4, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 8: return launch_pp<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 11:
         case 12:
@@ -2519,6 +2535,20 @@ static int pick_cfg(int64_t M, int64_t N, int64_t K, int epi) {
         return 15;
     // round 5: the ResNet3D conv_c at K = 64 / 128 (HBM-bound) on the streaming kernel
     if (epi == VC_EPI_BIAS_RESID_RELU_BF16 && (K == 64 || K == 128) && M % 128 == 0 && N % 256 == 0) return 20;
+    // round 5, Swin-T's per-stream parts (B = 1 of the 4-stream headline; tools/pp_check.py --swinpart
+    // --graph, hipGraph-timed): the 64x128 tile where 128x128 tiles are under ~2.5 rounds of CUs and N is
+    // wide (stage 2 fc1 3328x1536x384 10.7 vs 11.7 us, stage 3 q|k|v 1024x2304x768 9.6 vs 10.8, stage 1
+    // fc1 12544x768x256 13.4 vs 14.9); the f32-residual GEMMs below a round of 128x128 tiles likewise
+    // (stage 3 proj 1024x768x768 8.4 vs 12.0), and with a 4-deep ring when K is long (stage 3 fc2
+    // 1024x768x3072: 48 k-tiles per workgroup, latency-bound: 21.0 vs 38.1)
+    const int64_t t128 = (M / 128) * (N / 128);
+    if ((epi == VC_EPI_BIAS_BF16 || epi == VC_EPI_BIAS_GELU_ERF) && M % 64 == 0 && N % 128 == 0 && N >= 768 &&
+        t128 < 640 && !(M % 256 == 0 && N % 256 == 0 && t256 >= 64 && epi == VC_EPI_BIAS_BF16 && K >= 192))
+        return 7;
+    if (epi == VC_EPI_BIAS_RESID_F32 && M % 64 == 0 && N % 128 == 0 && t128 < 256) {
+        if (K >= 2048 && (M / 64) * (N / 128) < 128) return 21;
+        return 7;
+    }
     // exact-GELU outputs below ~4 rounds of 256x256 tiles: cfg 5 (Swin-T stages 2-4 fc1,
     // tools/tune_swin_gemm.py: 28 vs 36 us at 12544x1536x384, 46 vs 55 at 6400x3072x768)
     // (round 4: the ping-pong kernel, cfg 8, where the tiles fill <= 2.5 rounds of CUs: fc1 at 12800 rows

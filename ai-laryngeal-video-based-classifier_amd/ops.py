@@ -182,7 +182,9 @@ GEMM_KERNEL = {0: "gemm_bf16_kernel<256, 128, 4, 2, {E}, 3, {ET}>", 1: "gemm_bf1
                7: "gemm_bf16_kernel<64, 128, 2, 4, {E}, 2, {ET}>", 8: "gemm_pp_kernel<{E}, {ET}, 0>",
                9: "gemm_pp128_kernel<{E}, {ET}>", 10: "gemm_ppp_kernel<{E}, {ET}>",
                15: "gemm_ppd_kernel<{E}, {ET}, 16>", 16: "gemm_ppd_kernel<{E}, {ET}, 8>",
-               17: "gemm_pp160_kernel<{E}, {ET}>", 20: "conv_c_stream_kernel<{K}>"}
+               17: "gemm_pp160_kernel<{E}, {ET}>", 20: "conv_c_stream_kernel<{K}>",
+               21: "gemm_bf16_kernel<64, 128, 2, 4, {E}, 4, {ET}>", 22: "gemm_bf16_kernel<64, 128, 2, 4, {E}, 6, {ET}>",
+               23: "gemm_bf16_kernel<128, 128, 2, 4, {E}, 4, {ET}>"}
 
 
 def gemm_kernel_name(M, N, K, epilogue: str, out, aux=None, cfg: int = -1, f16: bool = False) -> str:

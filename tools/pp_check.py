@@ -17,8 +17,10 @@ ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--cfgs", default="8")
 ap.add_argument("--only", default="")
+ap.add_argument("--graph", action="store_true", help="time hipGraph replays of the iters launches (small shapes: no host launch cost)")
 ap.add_argument("--ksweep", action="store_true", help="q|k|v-shaped cases at K = 768 .. 6144 (per-tile overhead fit)")
 ap.add_argument("--swin", action="store_true", help="Video Swin-T B=4 stage-1/2 GEMM shapes (channels padded to 128)")
+ap.add_argument("--swinpart", action="store_true", help="--swin at one stream's part of the B=4 headline (B=1, rows padded to 256)")
 ap.add_argument("--r3d", action="store_true", help="ResNet3D-50 B=4 conv_a / conv_b GEMM shapes (implicit-conv proxies)")
 ap.add_argument("--r3dc", action="store_true", help="ResNet3D-50 B=4 conv_c shapes (1x1x1 + bf16 residual + ReLU)")
 a = ap.parse_args()
@@ -30,9 +32,12 @@ for M, tag in ((25344, "B8"), (12800, "B4")):
               (f"fc2_{tag}", M, 768, 3072, "bias_resid_f32"), (f"oproj_{tag}", M, 768, 768, "bias_resid_f32")]
 CASES += [("sq4096", 4096, 4096, 4096, "bias"), ("sq8192", 8192, 8192, 8192, "bias"),
           ("tsf_fc1_B16", 25344, 3072, 768, "bias_gelu_erf")]
-if a.swin:
+if a.swin or a.swinpart:
     CASES = []
-    for st, (M, C, Cp) in enumerate(((200704, 96, 128), (50176, 192, 256), (12544, 384, 384), (3136, 768, 768))):
+    geo = ((200704, 96, 128), (50176, 192, 256), (12544, 384, 384), (3136, 768, 768))
+    if a.swinpart:
+        geo = tuple(((M // 4 + 255) // 256 * 256, C, Cp) for M, C, Cp in geo)
+    for st, (M, C, Cp) in enumerate(geo):
         q = (3 * C + 127) // 128 * 128
         CASES += [(f"s{st}_qkv", M, q, Cp, "bias"), (f"s{st}_proj", M, Cp, Cp, "bias_resid_f32"),
                   (f"s{st}_fc1", M, 4 * C, Cp, "bias_gelu_erf"), (f"s{st}_fc2", M, Cp, 4 * C, "bias_resid_f32")]
@@ -70,7 +75,7 @@ for name, M, N, K, epi in CASES:
     base = lib.vc_gemm_pick(M, N, K, E[epi], out.stride(0), 0, None)
     bf16_out = out.dtype != torch.float32
     TILE = {1: (128, 128), 3: (256, 256), 4: (256, 256), 5: (128, 128), 7: (64, 128), 8: (256, 256), 9: (256, 128),
-            10: (256, 256), 11: (256, 256), 12: (256, 256), 13: (256, 256), 14: (128, 128), 15: (256, 256), 16: (256, 256), 17: (160, 256), 20: (128, 256)}
+            10: (256, 256), 11: (256, 256), 12: (256, 256), 13: (256, 256), 14: (128, 128), 15: (256, 256), 16: (256, 256), 17: (160, 256), 20: (128, 256), 21: (64, 128), 22: (64, 128), 23: (128, 128)}
     ok_shape = lambda c: (c in TILE and M % TILE[c][0] == 0 and N % TILE[c][1] == 0 and K % 64 == 0 and  # noqa: E731
                           (K >= 192 if c in (4, 10) else K >= 640 if c in (15, 16) else K >= 128 if c in (8, 9, 11, 12, 13, 17) else True))  # cfg 1: 128x128, 3-slot ring
     cfgs = [base] + [c for c in new_cfgs if c != base and ok_shape(c) and (c not in (11, 12, 13) or epi == "bias") and
@@ -92,12 +97,25 @@ for name, M, N, K, epi in CASES:
     for c in cfgs:
         ops.gemm(A, W, b, epi, out, aux=aux, cfg=c)
     torch.cuda.synchronize()
+    graphs = {}
+    if a.graph:
+        s = torch.cuda.Stream()
+        for c in cfgs:
+            g_ = torch.cuda.CUDAGraph()
+            with torch.cuda.stream(s), torch.cuda.graph(g_, stream=s):
+                for _ in range(a.iters):
+                    ops.gemm(A, W, b, epi, out, aux=aux, cfg=c)
+            graphs[c] = g_
+        torch.cuda.synchronize()
     for r in range(a.rounds):
         for c in cfgs:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            for _ in range(a.iters):
-                ops.gemm(A, W, b, epi, out, aux=aux, cfg=c)
+            if a.graph:
+                graphs[c].replay()
+            else:
+                for _ in range(a.iters):
+                    ops.gemm(A, W, b, epi, out, aux=aux, cfg=c)
             e1.record()
             e1.synchronize()
             times[c].append(e0.elapsed_time(e1) / a.iters)
@@ -110,5 +128,5 @@ for name, M, N, K, epi in CASES:
         if epi == "bias_resid_relu":  # HBM-bound: A + residual in, output out (+ W)
             line[f"cfg{c}"]["tb_s"] = round(2.0 * (M * K + 2 * M * N + N * K) / (med * 1e-3) / 1e12, 2)
     print(json.dumps(line), flush=True)
-    del A, W, b, out, init, ref, aux
+    del A, W, b, out, init, ref, aux, graphs
     torch.cuda.empty_cache()
