@@ -100,6 +100,13 @@ __device__ __forceinline__ void store_rows(uint16_t* row, const v16f (&acc)[2], 
         }
 }
 
+// s_waitcnt vmcnt(0) through the builtin, so the compiler's wait-count scoreboard sees it.
+// Round 5: registers loaded ahead of a main loop and first used inside it make hipcc put that wait
+// INSIDE the loop (at the first use), where it also drains the next tile's prefetch loads every
+// iteration -- the prefetch then hides nothing (the dQ kernel waited vmcnt(0) before its first MFMAs
+// each tile; dK/dV negated its prefetched -lse right after the load, same effect)
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 // bijective XCD-aware remap of the linear workgroup id (as the forward kernel)
 __device__ __forceinline__ int xcd_remap(int L, int nwg) {
     const int xq = nwg >> 3, xr = nwg & 7, xcd = L & 7;
@@ -186,7 +193,7 @@ attn_bwd_dkdv_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const uint16_
     const int nt = (S + 63) / 64;
     // tile prefetch lives in plain registers (a struct captured by lambdas ended up in scratch)
     uint4 pq0, pq1, pd0, pd1;
-    float tf = 0.f;
+    float tf = 0.f;  // the raw lse (threads 0-63) / Delta (64-127) of the prefetched tile
     const int sr0 = tid >> 3, sc = tid & 7;
     const int so0 = sr0 * 128 + bswz(sr0, sc) * 16, so1 = (sr0 + 32) * 128 + bswz(sr0 + 32, sc) * 16;
     // LDS holds -lse and -Delta: they initialise the S and dP accumulators (so the MFMAs emit
@@ -199,22 +206,25 @@ attn_bwd_dkdv_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const uint16_
         pq1 = *reinterpret_cast<const uint4*>(qs + 32 * ld);                                            \
         pd0 = *reinterpret_cast<const uint4*>(ds);                                                      \
         pd1 = *reinterpret_cast<const uint4*>(ds + 32 * lddo);                                          \
-        if (tid < 128) {                                                                                \
+        {   /* every thread loads (no branch); used only at ABWD_STORE_A, after the tile's compute */   \
             const int q = (t) * 64 + (tid & 63);                                                        \
             const int qc = q < S ? q : S - 1;                                                           \
-            tf = tid < 64 ? (q < S ? -lseb[qc] : -INFINITY) : -delb[qc];                                \
+            tf = ((tid >> 6) & 1) ? delb[qc] : lseb[qc];                                                \
         }                                                                                               \
     }
-#define ABWD_STORE_A(slot)                                                                              \
+#define ABWD_STORE_A(slot, t)                                                                           \
     {                                                                                                   \
         *reinterpret_cast<uint4*>((slot) + so0) = pq0;                                                  \
         *reinterpret_cast<uint4*>((slot) + so1) = pq1;                                                  \
         *reinterpret_cast<uint4*>((slot) + TILE_BYTES + so0) = pd0;                                     \
         *reinterpret_cast<uint4*>((slot) + TILE_BYTES + so1) = pd1;                                     \
-        if (tid < 128) reinterpret_cast<float*>((slot) + 2 * TILE_BYTES)[tid] = tf;                     \
+        if (tid < 128)                                                                                  \
+            reinterpret_cast<float*>((slot) + 2 * TILE_BYTES)[tid] =                                    \
+                (tid < 64 && (t) * 64 + tid >= S) ? -INFINITY : -tf;                                    \
     }
     ABWD_LOAD_A(0);
-    ABWD_STORE_A(smem);
+    ABWD_STORE_A(smem, 0);
+    vm_drain();
     __syncthreads();
 
     for (int t = 0; t < nt; ++t) {
@@ -288,7 +298,7 @@ attn_bwd_dkdv_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const uint16_
         __builtin_amdgcn_sched_barrier(0);
         dv_mfma(1, s1);
         dk_mfma(1, dp1);
-        if (t + 1 < nt) ABWD_STORE_A(smem + ((t + 1) & 1) * SLOT_A);
+        if (t + 1 < nt) ABWD_STORE_A(smem + ((t + 1) & 1) * SLOT_A, t + 1);
         __syncthreads();
     }
 #undef ABWD_LOAD_A
@@ -379,6 +389,10 @@ attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv, int64_t ld, const uint16_t*
         negL[e] = -lq;
         negD[e] = -dq_delta;
     }
+    // qf / df landed before the loop (see vm_drain): the empty asm "uses" them here, so hipcc waits for
+    // their loads at this point and not inside the loop
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) asm volatile("" : "+v"(qf[kk]), "+v"(df[kk]));
     auto dq_mfma = [&](const char* ki, int kb, const v16f& ds) {
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
