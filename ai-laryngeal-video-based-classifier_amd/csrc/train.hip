@@ -996,8 +996,23 @@ int vc_wgrad_bf16(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx
         const int nJ2 = (int)(N2 / 256);
         const int nt2 = (int)(N1 / 256) * nJ2;
         const int64_t kt2 = M / 32;
-        int64_t sp = (256 + nt2 - 1) / nt2;
-        if (sp > kt2 / 4) sp = kt2 / 4;
+        // split count: fewest (workgroup rounds x half-tiles per workgroup) over 1 .. ceil(256 / tiles)
+        // splits (one workgroup per CU).  round 5: ceil(256 / tiles) alone gave 270 / 261 / 288
+        // workgroups for the ViViT-B q|k|v / o_proj / fc1 weights -- a second round of 14 / 5 / 32
+        // (floor: 243 / 252 / 252 workgroups in one round)
+        static int ncu_s = 0;
+        if (!ncu_s) {
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            if (hipDeviceGetAttribute(&ncu_s, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu_s <= 0)
+                ncu_s = 256;
+        }
+        const int64_t ncu = ncu_s;
+        int64_t sp = 1, best = -1;
+        for (int64_t c = 1; c <= (ncu + nt2 - 1) / nt2 && c <= (kt2 / 4 > 0 ? kt2 / 4 : 1); ++c) {
+            const int64_t cost = ((nt2 * c + ncu - 1) / ncu) * ((kt2 + c - 1) / c);
+            if (best < 0 || cost <= best) { best = cost; sp = c; }
+        }
         if (!work || work_elems < 2 * N1 * N2) sp = 1;
         else if (sp * N1 * N2 > work_elems) sp = work_elems / (N1 * N2);
         if (sp < 1) sp = 1;

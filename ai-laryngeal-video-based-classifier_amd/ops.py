@@ -114,6 +114,8 @@ class OpRecorder:
         GB/s of algorithmic work), the ops that ran it; sorted by share"""
         agg = {}
         for kernel, op, e0, e1, work, unit in self.entries:
+            if kernel in agg and agg[kernel]["unit"] != unit:  # one kernel, launches on both sides of the ridge
+                kernel = f"{kernel} [{'HBM' if unit == 'byte' else 'MFMA'}-bound launches]"
             a = agg.setdefault(kernel, {"ms": [], "work": 0.0, "unit": unit, "ops": set()})
             a["ms"].append(e0.elapsed_time(e1))
             a["work"] += work
@@ -132,6 +134,8 @@ class OpRecorder:
         step, share of the step, achieved rate, the kernels that ran it; sorted by share"""
         agg = {}
         for kernel, op, e0, e1, work, unit in self.entries:
+            if op in agg and agg[op]["unit"] != unit:
+                op = f"{op} [{'HBM' if unit == 'byte' else 'MFMA'}-bound launches]"
             a = agg.setdefault(op, {"ms": 0.0, "n": 0, "work": 0.0, "unit": unit, "kernels": set()})
             a["ms"] += e0.elapsed_time(e1)
             a["n"] += 1
@@ -187,6 +191,22 @@ GEMM_KERNEL = {0: "gemm_bf16_kernel<256, 128, 4, 2, {E}, 3, {ET}>", 1: "gemm_bf1
                23: "gemm_bf16_kernel<128, 128, 2, 4, {E}, 4, {ET}>"}
 
 
+# roofline ridge of the bf16 matrix pipe against HBM (MI355X_MICROARCH.md: 2.5 PFLOP/s dense, 8 TB/s):
+# a launch whose algorithmic FLOP per byte falls below it is bounded by HBM, and its table row is
+# filed under its bytes (GB/s vs 8 TB/s) instead of its FLOP
+RIDGE_FLOP_PER_BYTE = 2500e12 / 8e12
+# bytes per output element an epilogue moves (output written, plus the residual / aux it reads)
+_EPI_OUT_BYTES = {"bias": 2, "bias_gelu_tanh": 2, "bias_gelu_erf": 2, "bias_resid_f32": 8, "embed_f32": 8,
+                  "bias_f32": 4, "bias_relu": 2, "bias_resid_relu": 4, "bias_add_f32": 8, "bias_gelu_tanh_save": 4,
+                  "dgelu_tanh": 4}
+
+
+def gemm_bytes(M: int, N: int, K: int, epilogue: str, esize: int = 2) -> float:
+    """algorithmic HBM bytes of one GEMM launch: A and W read once, the epilogue's output (and residual /
+    aux operand) once"""
+    return float(M * K * esize + N * K * esize + M * N * _EPI_OUT_BYTES[epilogue])
+
+
 def gemm_kernel_name(M, N, K, epilogue: str, out, aux=None, cfg: int = -1, f16: bool = False) -> str:
     e = EPI[epilogue]
     if cfg < 0:
@@ -202,18 +222,25 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: str, ou
     """out (+)= epilogue(a[:m] @ w.T + bias).  a bf16 [M,K], w bf16 [N,K], bias f32 [N]; or a, w (and the
     16-bit out) fp16 for the inference epilogues (bias / gelu / resid_f32 / embed_f32).  `flop` / `op`:
     the algorithmic work and op name an installed OpRecorder files this launch under (default
-    2 M N K of the operand shapes); `nbytes` instead: the launch is HBM-bound (intensity below the
-    ridge) and is filed under its algorithmic bytes."""
+    2 M N K of the operand shapes); `nbytes` (default: gemm_bytes of the operand shapes when `flop` is
+    not given either) its algorithmic bytes: the launch is filed under whichever bounds it -- bytes
+    when flop / bytes is below RIDGE_FLOP_PER_BYTE (or when only `nbytes` is given), FLOP otherwise."""
     rec = _REC[0]
     if rec is not None:
         M_ = a.shape[0] if m is None else m
         label = gemm_kernel_name(M_, w.shape[0], a.shape[1], epilogue, out, aux, cfg, a.dtype == torch.float16)
         e0 = rec.begin()
         _gemm(a, w, bias, epilogue, out, aux, group, group_stride, group_offset, m, cfg)
-        if nbytes is not None:
+        if nbytes is not None and flop is None:
             rec.end(e0, label, op, nbytes, "byte")
         else:
-            rec.end(e0, label, op, 2.0 * M_ * w.shape[0] * a.shape[1] if flop is None else flop, "flop")
+            fl = 2.0 * M_ * w.shape[0] * a.shape[1] if flop is None else flop
+            nb = nbytes if nbytes is not None else (
+                gemm_bytes(M_, w.shape[0], a.shape[1], epilogue, a.element_size()) if flop is None else None)
+            if nb is not None and fl / nb < RIDGE_FLOP_PER_BYTE:
+                rec.end(e0, label, op, nb, "byte")
+            else:
+                rec.end(e0, label, op, fl, "flop")
         return out
     return _gemm(a, w, bias, epilogue, out, aux, group, group_stride, group_offset, m, cfg)
 

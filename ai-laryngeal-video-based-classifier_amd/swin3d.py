@@ -485,7 +485,8 @@ class Swin3d(torch.nn.Module):
                 biasT = self._biasT(s, i, window, video.device)
                 tm("layernorm_grp_kernel", f"layernorm.s{s}", ntok * C * 6, "byte", ops.layernorm, X, blk["ln1"][0],
                    blk["ln1"][1], eps, Y, m=ntok)
-                ops.gemm(Y, blk["w_qkv"], blk["b_qkv"], "bias", QKV, flop=2.0 * ntok * 3 * C * C, op=f"qkv.s{s}")
+                ops.gemm(Y, blk["w_qkv"], blk["b_qkv"], "bias", QKV, flop=2.0 * ntok * 3 * C * C, op=f"qkv.s{s}",
+                         nbytes=ops.gemm_bytes(ntok, 3 * C, C, "bias"))
                 ev = self.kernel_events
                 if ev is not None:  # recorded on the current stream, the one the kernel runs on
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -499,11 +500,14 @@ class Swin3d(torch.nn.Module):
                     # algorithmic bytes: q, k, v read and the output written once (4 x 32 x 2 B per
                     # token-head)
                     ev.append((e0, e1, 4.0 * ntok * n * 32 * st["heads"], 256.0 * ntok * st["heads"]))
-                ops.gemm(O, blk["w_proj"], blk["b_proj"], "bias_resid_f32", X, flop=2.0 * ntok * C * C, op=f"proj.s{s}")
+                ops.gemm(O, blk["w_proj"], blk["b_proj"], "bias_resid_f32", X, flop=2.0 * ntok * C * C, op=f"proj.s{s}",
+                         nbytes=ops.gemm_bytes(ntok, C, C, "bias_resid_f32"))
                 tm("layernorm_grp_kernel", f"layernorm.s{s}", ntok * C * 6, "byte", ops.layernorm, X, blk["ln2"][0],
                    blk["ln2"][1], eps, Y, m=ntok)
-                ops.gemm(Y, blk["w_1"], blk["b_1"], "bias_gelu_erf", Hd, flop=2.0 * ntok * hid * C, op=f"fc1.s{s}")
-                ops.gemm(Hd, blk["w_2"], blk["b_2"], "bias_resid_f32", X, flop=2.0 * ntok * C * hid, op=f"fc2.s{s}")
+                ops.gemm(Y, blk["w_1"], blk["b_1"], "bias_gelu_erf", Hd, flop=2.0 * ntok * hid * C, op=f"fc1.s{s}",
+                         nbytes=ops.gemm_bytes(ntok, hid, C, "bias_gelu_erf"))
+                ops.gemm(Hd, blk["w_2"], blk["b_2"], "bias_resid_f32", X, flop=2.0 * ntok * C * hid, op=f"fc2.s{s}",
+                         nbytes=ops.gemm_bytes(ntok, C, hid, "bias_resid_f32"))
             if s < len(grids) - 1:
                 nxt = ws["stages"][s + 1]
                 t2, h2, w2 = grids[s + 1]

@@ -374,7 +374,10 @@ def dominant_roofline(table, mode):
             "mfma_busy": mfma_busy, "valu_per_mfma": valu_per_mfma, "pmc_source": pmc_src,
             "timed_on": "HIP events around every launch of 3 extra steps of the headline's split, its parts "
                         "serialised on one stream (ops.OpRecorder); algorithmic work = real token rows and channels "
-                        "(no padding)"}
+                        "(no padding)",
+            "bound_rule": "per launch: HBM (algorithmic bytes: operands read once, the epilogue's output / residual "
+                          "once) when its algorithmic flop per byte is below the 312.5 flop/B ridge (2.5 PFLOP/s bf16 "
+                          "/ 8 TB/s), else the bf16 MFMA peak (ops.RIDGE_FLOP_PER_BYTE)"}
 
 
 def cpu_family_baseline(mode, n_clips, gpu_logits_fn):
