@@ -781,18 +781,21 @@ __device__ __forceinline__ void vtie(T& r) {
     asm volatile("" : "+v"(r));
 }
 
-template <int KD>
+template <int KD, int BN>
 __global__ void __launch_bounds__(512, 1)
 conv_c_stream_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw,
                      int nbm, int R, const float* __restrict__ bias, uint16_t* __restrict__ out, int64_t ldo,
                      const uint16_t* __restrict__ res, int64_t ldres) {
-    static_assert(KD == 64 || KD == 128, "K of one or two 64-deep k-tiles");
-    constexpr int BM = 128, BN = 256, NKT = KD / 64, TM = 64, TN = 64, MI = 4, NI = 4, NP = NI / 2;
+    static_assert((KD == 64 || KD == 128) ? BN == 256 : (KD == 256 && BN == 128), "K 64 / 128 (N tile 256) or 256 (128)");
+    constexpr int BM = 128, NKT = KD / 64, TM = 64, TN = BN / 4, MI = 4, NI = TN / 16, NP = NI / 2;
+    // K <= 128: two A buffers in LDS; K = 256: one (W 64 KiB + A 64 KiB), the next tile's rows waiting
+    // in registers until every wave is done with the current one (a second barrier per tile)
+    constexpr bool DBUF = KD <= 128;
     constexpr int ACH = BM * 8 * NKT / 512;  // 16-B chunks of the A tile per thread
     constexpr int NRES = MI * NP;            // 16-B residual loads (and output stores) per thread per tile
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    char* Ws = smem;                      // NKT x [256 rows][128 B]
-    char* As = smem + NKT * BN * 128;     // 2 buffers x NKT x [128 rows][128 B]
+    char* Ws = smem;                      // NKT x [BN rows][128 B]
+    char* As = smem + NKT * BN * 128;     // (2 buffers x) NKT x [128 rows][128 B]
     constexpr int ABUF = NKT * BM * 128;
 
     const int tn = blockIdx.x / R, r0 = blockIdx.x - tn * R;
@@ -805,7 +808,7 @@ conv_c_stream_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
     float4 bq[NI];
     load_bias16<NI>(bias, n0 + wn * TN, q, bq);
 
-    // W [256][KD] -> LDS (row-swizzled 16-B chunks), once
+    // W [BN][KD] -> LDS (row-swizzled 16-B chunks), once
 #pragma unroll
     for (int s = 0; s < BN * 8 * NKT / 512; ++s) {
         const int c = tid + 512 * s, kt = c / (BN * 8), rw = (c >> 3) & (BN - 1), ch = c & 7;
@@ -910,7 +913,8 @@ conv_c_stream_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
         vm_wait_asm<NRES + NRES>();
 #pragma unroll
         for (int s = 0; s < ACH; ++s) vtie(areg[s]);
-        store_a(buf ^ 1);
+        if constexpr (!DBUF) block_sync_lds();  // every wave done reading the one A buffer
+        store_a(DBUF ? buf ^ 1 : 0);
         block_sync_lds();
         return true;
     };
@@ -929,7 +933,7 @@ conv_c_stream_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
     for (;;) {  // two steps per trip: the residual registers alternate without copies
         if (!step(mt, 0, r0b, r1b)) break;
         mt += R;
-        if (!step(mt, 1, r1b, r0b)) break;
+        if (!step(mt, DBUF ? 1 : 0, r1b, r0b)) break;
         mt += R;
     }
 }
@@ -2258,7 +2262,7 @@ struct GemmCfg {
 };
 static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}, {128, 128}, {0, 0},
                                  {64, 128}, {256, 256}, {256, 128}, {256, 256}, {256, 256}, {256, 256}, {256, 256},
-                                 {128, 128}, {256, 256}, {256, 256}, {160, 256}, {256, 256}, {256, 256}, {128, 256},
+                                 {128, 128}, {256, 256}, {256, 256}, {160, 256}, {256, 256}, {256, 256}, {128, 128},
                                  {64, 128}, {64, 128}, {128, 128}};
 constexpr int kNumCfgs = 24;
 
@@ -2421,24 +2425,24 @@ static int launch_ppd(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t
     return check_launch("vc_gemm_bf16");
 }
 
-template <int KD>
+template <int KD, int BN>
 static int launch_conv_c_stream(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int64_t M, int64_t N,
                                 const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux,
                                 hipStream_t stream) {
-    constexpr int lds = (KD / 64) * 256 * 128 + 2 * (KD / 64) * 128 * 128;
+    constexpr int lds = (KD / 64) * BN * 128 + (KD <= 128 ? 2 : 1) * (KD / 64) * 128 * 128;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)conv_c_stream_kernel<KD>,
+        hipError_t e = hipFuncSetAttribute((const void*)conv_c_stream_kernel<KD, BN>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
         attr_set = true;
     }
-    const int nbm = (int)(M / 128), nbn = (int)(N / 256);
+    const int nbm = (int)(M / 128), nbn = (int)(N / BN);
     // about one workgroup per CU over all n tiles; R a multiple of 8 (the n tiles of one m tile share an XCD)
     int R = (num_cus() + nbn - 1) / nbn;
     R = (R + 7) / 8 * 8;
     if (R > (nbm + 7) / 8 * 8) R = (nbm + 7) / 8 * 8;
-    conv_c_stream_kernel<KD><<<(unsigned)(R * nbn), 512, lds, stream>>>(
+    conv_c_stream_kernel<KD, BN><<<(unsigned)(R * nbn), 512, lds, stream>>>(
         A, lda, W, ldw, nbm, R, bias, (uint16_t*)out, ldo, reinterpret_cast<const uint16_t*>(aux), ldaux);
     return check_launch("vc_gemm_bf16");
 }
@@ -2484,12 +2488,15 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
             return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 14 (timing ablation) is bias_resid_relu only");
         case 9: return launch_pp128<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 17: return launch_pp160<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-        case 20:  // streaming 1x1x1 conv with the bf16 residual (ResNet3D conv_c), K 64 / 128, N % 256
+        case 20:  // streaming 1x1x1 conv with the bf16 residual (ResNet3D conv_c), K 64 / 128 (N % 256), 256
             if constexpr (E == VC_EPI_BIAS_RESID_RELU_BF16 && ET == VC_ELEM_BF16) {
-                if (K == 64) return launch_conv_c_stream<64>(A, lda, W, ldw, M, N, bias, out, ldo, aux, ldaux, s);
-                if (K == 128) return launch_conv_c_stream<128>(A, lda, W, ldw, M, N, bias, out, ldo, aux, ldaux, s);
+                if (K == 64 && N % 256 == 0)
+                    return launch_conv_c_stream<64, 256>(A, lda, W, ldw, M, N, bias, out, ldo, aux, ldaux, s);
+                if (K == 128 && N % 256 == 0)
+                    return launch_conv_c_stream<128, 256>(A, lda, W, ldw, M, N, bias, out, ldo, aux, ldaux, s);
+                if (K == 256) return launch_conv_c_stream<256, 128>(A, lda, W, ldw, M, N, bias, out, ldo, aux, ldaux, s);
             }
-            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 20 is bias_resid_relu with K 64 / 128 only");
+            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 20 is bias_resid_relu with K 64 / 128 (N % 256) or 256");
         case 4:
             if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
                           E == VC_EPI_BIAS_RELU_BF16 || E == VC_EPI_BIAS_GELU_TANH_SAVE)
@@ -2534,7 +2541,10 @@ static int pick_cfg(int64_t M, int64_t N, int64_t K, int epi) {
         t256 >= 256)
         return 15;
     // round 5: the ResNet3D conv_c at K = 64 / 128 (HBM-bound) on the streaming kernel
-    if (epi == VC_EPI_BIAS_RESID_RELU_BF16 && (K == 64 || K == 128) && M % 128 == 0 && N % 256 == 0) return 20;
+    // (K = 256 on 128-column tiles, one A buffer: res4 25088x1024x256 27.4 vs 43.7 us, 4.24 TB/s)
+    if (epi == VC_EPI_BIAS_RESID_RELU_BF16 && M % 128 == 0 &&
+        (((K == 64 || K == 128) && N % 256 == 0) || (K == 256 && N % 128 == 0)))
+        return 20;
     // round 5, Swin-T's per-stream parts (B = 1 of the 4-stream headline; tools/pp_check.py --swinpart
     // --graph, hipGraph-timed): the 64x128 tile where 128x128 tiles are under ~2.5 rounds of CUs and N is
     // wide (stage 2 fc1 3328x1536x384 10.7 vs 11.7 us, stage 3 q|k|v 1024x2304x768 9.6 vs 10.8, stage 1

@@ -186,7 +186,7 @@ GEMM_KERNEL = {0: "gemm_bf16_kernel<256, 128, 4, 2, {E}, 3, {ET}>", 1: "gemm_bf1
                7: "gemm_bf16_kernel<64, 128, 2, 4, {E}, 2, {ET}>", 8: "gemm_pp_kernel<{E}, {ET}, 0>",
                9: "gemm_pp128_kernel<{E}, {ET}>", 10: "gemm_ppp_kernel<{E}, {ET}>",
                15: "gemm_ppd_kernel<{E}, {ET}, 16>", 16: "gemm_ppd_kernel<{E}, {ET}, 8>",
-               17: "gemm_pp160_kernel<{E}, {ET}>", 20: "conv_c_stream_kernel<{K}>",
+               17: "gemm_pp160_kernel<{E}, {ET}>", 20: "conv_c_stream_kernel<{K}, {BN}>",
                21: "gemm_bf16_kernel<64, 128, 2, 4, {E}, 4, {ET}>", 22: "gemm_bf16_kernel<64, 128, 2, 4, {E}, 6, {ET}>",
                23: "gemm_bf16_kernel<128, 128, 2, 4, {E}, 4, {ET}>"}
 
@@ -212,7 +212,7 @@ def gemm_kernel_name(M, N, K, epilogue: str, out, aux=None, cfg: int = -1, f16: 
     if cfg < 0:
         cfg = _lib.load().vc_gemm_pick(M, N, K, e, out.stride(0), aux.stride(0) if aux is not None else 0,
                                        _p(aux) if aux is not None else None)
-    return GEMM_KERNEL.get(cfg, f"gemm cfg {cfg}").format(E=e, ET=1 if f16 else 0, K=K)
+    return GEMM_KERNEL.get(cfg, f"gemm cfg {cfg}").format(E=e, ET=1 if f16 else 0, K=K, BN=256 if K <= 128 else 128)
 
 
 def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: str, out: torch.Tensor,

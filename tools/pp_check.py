@@ -75,11 +75,11 @@ for name, M, N, K, epi in CASES:
     base = lib.vc_gemm_pick(M, N, K, E[epi], out.stride(0), 0, None)
     bf16_out = out.dtype != torch.float32
     TILE = {1: (128, 128), 3: (256, 256), 4: (256, 256), 5: (128, 128), 7: (64, 128), 8: (256, 256), 9: (256, 128),
-            10: (256, 256), 11: (256, 256), 12: (256, 256), 13: (256, 256), 14: (128, 128), 15: (256, 256), 16: (256, 256), 17: (160, 256), 20: (128, 256), 21: (64, 128), 22: (64, 128), 23: (128, 128)}
+            10: (256, 256), 11: (256, 256), 12: (256, 256), 13: (256, 256), 14: (128, 128), 15: (256, 256), 16: (256, 256), 17: (160, 256), 20: (128, 128), 21: (64, 128), 22: (64, 128), 23: (128, 128)}
     ok_shape = lambda c: (c in TILE and M % TILE[c][0] == 0 and N % TILE[c][1] == 0 and K % 64 == 0 and  # noqa: E731
                           (K >= 192 if c in (4, 10) else K >= 640 if c in (15, 16) else K >= 128 if c in (8, 9, 11, 12, 13, 17) else True))  # cfg 1: 128x128, 3-slot ring
     cfgs = [base] + [c for c in new_cfgs if c != base and ok_shape(c) and (c not in (11, 12, 13) or epi == "bias") and
-                     (c != 14 or epi == "bias_resid_relu") and (c != 20 or (epi == "bias_resid_relu" and K in (64, 128))) and
+                     (c != 14 or epi == "bias_resid_relu") and (c != 20 or (epi == "bias_resid_relu" and K in (64, 128, 256))) and
                      (c not in (4, 10, 15, 16) or bf16_out) and (c not in (15, 16) or epi in ("bias", "bias_gelu_tanh", "bias_gelu_erf"))]
     # bit-identity: every config from the same initial out (the residual epilogue accumulates)
     init = (torch.randn(M, N, device="cuda", generator=g) if out.dtype == torch.float32 else out.clone())
