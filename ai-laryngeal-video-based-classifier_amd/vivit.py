@@ -141,6 +141,12 @@ class VivitForVideoClassification(torch.nn.Module):
         # the weight rounding of the first layers (tests/analysis/w_probe.py: all weights fp32 3.8e-4, the
         # embedding + layer 0 4.3e-4, vs 1.25e-3 all fp16 on the bench's 8 clips).
         self.precise_layers = 0
+        # ... and which GEMMs: "embed" (pixels and weights split: three products) or "embed_w" (weights
+        # only: A.W_hi + A.W_lo), and layer 0's "qkv" / "o_proj" / "fc1" / "fc2".  Default: the
+        # embedding's weights and layer 0's q|k|v -- logit error 6.3e-4 on 4 of the bench's clips vs 6.7e-4
+        # with the pixels and all of layer 0 split too, at less than half the extra MFMA work (957 vs 926
+        # clips/s, bf16 982: tests/test_fp16_gpu.py, profiles/r05_fp16_clock.json)
+        self.precise_ops = ("embed_w", "qkv")
 
     # ---- state dict in HF naming ---------------------------------------------------
     def hf_state_dict(self):
@@ -262,15 +268,18 @@ class VivitForVideoClassification(torch.nn.Module):
         if bf not in (torch.bfloat16, torch.float16):
             raise ValueError(f"compute_dtype must be torch.bfloat16 or torch.float16, not {bf}")
         npre = self.precise_layers if bf == torch.float16 else 0
+        pops = tuple(sorted(self.precise_ops)) if npre > 0 else ()
+        if not set(pops) <= {"embed", "embed_w", "qkv", "o_proj", "fc1", "fc2"} or {"embed", "embed_w"} <= set(pops):
+            raise ValueError(f"precise_ops must name embed | embed_w and q|k|v / o_proj / fc1 / fc2, not {self.precise_ops}")
         if (self._packed is not None and self._packed["device"] == device and self._packed["version"] == ver
-                and self._packed["dtype"] == bf and self._packed["precise"] == npre):
+                and self._packed["dtype"] == bf and self._packed["precise"] == npre and self._packed["pops"] == pops):
             return self._packed
         c = self.config
         f32 = torch.float32
         P = lambda n: self.P(n).detach().to(device)  # noqa: E731
         D = c.hidden_size
         kt, kh, kw = c.tubelet_size
-        pk = {"device": device, "version": ver, "dtype": bf, "precise": npre}
+        pk = {"device": device, "version": ver, "dtype": bf, "precise": npre, "pops": pops}
 
         def split(w, emb=False):
             # [W_hi | W_lo] (embedding: [W_hi | W_hi | W_lo] against [A_hi | A_lo] with A wrapping)
@@ -280,8 +289,9 @@ class VivitForVideoClassification(torch.nn.Module):
             return torch.cat([hi, hi, lo] if emb else [hi, lo], dim=1).contiguous()
 
         pk["w_emb"] = P("vivit.embeddings.patch_embeddings.projection.weight").reshape(D, -1).to(bf).contiguous()
-        if npre > 0:
-            pk["w_emb_split"] = split(P("vivit.embeddings.patch_embeddings.projection.weight").reshape(D, -1), emb=True)
+        if "embed" in pops or "embed_w" in pops:
+            pk["w_emb_split"] = split(P("vivit.embeddings.patch_embeddings.projection.weight").reshape(D, -1),
+                                      emb="embed" in pops)
         pk["b_emb"] = P("vivit.embeddings.patch_embeddings.projection.bias").to(f32).contiguous()
         pk["pos"] = P("vivit.embeddings.position_embeddings").reshape(-1, D).to(f32).contiguous()
         pk["cls"] = P("vivit.embeddings.cls_token").reshape(D).to(f32).contiguous()
@@ -307,11 +317,17 @@ class VivitForVideoClassification(torch.nn.Module):
             L["w_2"] = P(p + "mlp.fc2.weight").to(bf).contiguous()
             L["b_2"] = P(p + "mlp.fc2.bias").contiguous()
             if i < npre:
-                L["split"] = dict(
-                    w_qkv=split(torch.cat([P(p + "attention.q_proj.weight") * qs, P(p + "attention.k_proj.weight"),
-                                           P(p + "attention.v_proj.weight")])),
-                    w_o=split(P(p + "attention.o_proj.weight")), w_1=split(P(p + "mlp.fc1.weight")),
-                    w_2=split(P(p + "mlp.fc2.weight")))
+                sp = {}
+                if "qkv" in pops:
+                    sp["w_qkv"] = split(torch.cat([P(p + "attention.q_proj.weight") * qs,
+                                                   P(p + "attention.k_proj.weight"), P(p + "attention.v_proj.weight")]))
+                if "o_proj" in pops:
+                    sp["w_o"] = split(P(p + "attention.o_proj.weight"))
+                if "fc1" in pops:
+                    sp["w_1"] = split(P(p + "mlp.fc1.weight"))
+                if "fc2" in pops:
+                    sp["w_2"] = split(P(p + "mlp.fc2.weight"))
+                L["split"] = sp
             layers.append(L)
         pk["layers"] = layers
         pk["lnf_g"] = P("vivit.layernorm.weight").contiguous()
@@ -392,7 +408,7 @@ class VivitForVideoClassification(torch.nn.Module):
                 and not torch.cuda.is_current_stream_capturing()):
             key = (pix.data_ptr(), tuple(pix.shape), tuple(pix.stride()), pix.dtype, self.concurrent_streams,
                    self.compute_dtype, self._weights_version(), tuple(sorted(self.gemm_cfg.items())), self.rows,
-                   self.round_split, self.precise_layers)
+                   self.round_split, self.precise_layers, tuple(sorted(self.precise_ops)))
             return self._graphs.run(key, pix, self._forward_eager, keep=lambda: (self._packed, tuple(self._ws_used)))
         return self._forward_eager(pix)
 
@@ -465,7 +481,14 @@ class VivitForVideoClassification(torch.nn.Module):
         T_, H_ = c.num_frames, c.image_size
         ln_bytes = M * D * (4 + 2)
         tm = ops.timed
-        if "A_emb_split" in ws and "w_emb_split" in pk:
+        if "A_emb_split" in ws and "w_emb_split" in pk and "embed_w" in pk["pops"]:
+            # split weights only: A (plain fp16 im2col) wrapping against [W_hi | W_lo]
+            run("im2col", tm, "im2col_kernel", "im2col", B * (T_ * c.num_channels * H_ * H_ * 4 + npatch * Kemb * 2),
+                "byte", ops.tubelet_im2col, pix, c.tubelet_size, ws["A_emb"])
+            run("embed", ops.gemm_wrap, ws["A_emb"], Kemb, pk["w_emb_split"], pk["b_emb"], "embed_f32", X,
+                aux=pk["pos"][1:], group=npatch, group_stride=S, group_offset=1, m=B * npatch,
+                flop=2.0 * B * npatch * D * Kemb, op="embed")
+        elif "A_emb_split" in ws and "w_emb_split" in pk:
             # split operands: [A_hi | A_lo] against [W_hi | W_hi | W_lo] (A_hi W_hi + A_lo W_hi + A_hi W_lo)
             run("im2col", tm, "im2col_kernel", "im2col", B * (T_ * c.num_channels * H_ * H_ * 4 + npatch * Kemb * 4),
                 "byte", ops.patch_im2col_split, pix, c.tubelet_size, ws["A_emb_split"])
@@ -502,17 +525,17 @@ class VivitForVideoClassification(torch.nn.Module):
         Hn = c.num_attention_heads
         attn_flop = 4.0 * S * S * (D // Hn) * Hn * B
         for L in pk["layers"]:
-            sp = L.get("split")  # the split-operand fp16 layers (precise_layers): A wraps against [W_hi | W_lo]
+            sp = L.get("split", {})  # the split-operand fp16 GEMMs (precise_layers / precise_ops): A wraps against [W_hi | W_lo]
             run("layernorm", tm, "layernorm_kernel", "layernorm", ln_bytes, "byte", ops.layernorm, X, L["ln1_g"],
                 L["ln1_b"], eps, Y, m=m_ln)
-            if sp is not None:
+            if "w_qkv" in sp:
                 run("qkv", ops.gemm_wrap, Y, D, sp["w_qkv"], L["b_qkv"], "bias", QKV, flop=2.0 * M * 3 * D * D, op="qkv")
             else:
                 run("qkv", qkv_gemm, Y, L["w_qkv"], L["b_qkv"], "bias", QKV, m=m_qkv, cfg=c_qkv,
                     flop=2.0 * M * 3 * D * D, op="qkv")
             run("attention", tm, "attn_fwd_d64_kernel", "attention", attn_flop, "flop", ops.attention, QKV, B, S, Hn,
                 scale, O, q_prescaled=True)
-            if sp is not None:
+            if "w_o" in sp:
                 run("o_proj", ops.gemm_wrap, O, D, sp["w_o"], L["b_o"], "bias_resid_f32", X, flop=2.0 * M * D * D,
                     op="o_proj")
             else:
@@ -520,12 +543,14 @@ class VivitForVideoClassification(torch.nn.Module):
                     flop=2.0 * M * D * D, op="o_proj")
             run("layernorm", tm, "layernorm_kernel", "layernorm", ln_bytes, "byte", ops.layernorm, X, L["ln2_g"],
                 L["ln2_b"], eps, Y, m=m_ln)
-            if sp is not None:
+            if "w_1" in sp:
                 run("fc1", ops.gemm_wrap, Y, D, sp["w_1"], L["b_1"], act, Hd, flop=2.0 * M * I * D, op="fc1")
+            else:
+                run("fc1", ops.gemm, Y, L["w_1"], L["b_1"], act, Hd, m=m_1, cfg=c_1, flop=2.0 * M * I * D, op="fc1")
+            if "w_2" in sp:
                 run("fc2", ops.gemm_wrap, Hd, I, sp["w_2"], L["b_2"], "bias_resid_f32", X, flop=2.0 * M * D * I,
                     op="fc2")
             else:
-                run("fc1", ops.gemm, Y, L["w_1"], L["b_1"], act, Hd, m=m_1, cfg=c_1, flop=2.0 * M * I * D, op="fc1")
                 run("fc2", fc2_gemm, Hd, L["w_2"], L["b_2"], "bias_resid_f32", X, m=m_2, cfg=c_2,
                     flop=2.0 * M * D * I, op="fc2")
         return ops.cls_head(X, B, S, pk["lnf_g"], pk["lnf_b"], eps, pk["w_cls"], pk["b_cls"],

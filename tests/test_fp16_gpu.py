@@ -231,7 +231,15 @@ def test_vivit_b_precise_layers_fp16():
     m = _vivit(cfg, H)
     plain = np.abs(m(pixel_values=pix).logits.cpu().numpy() - ref).max()
     m.precise_layers = 1
+    m.precise_ops = ("embed", "qkv", "o_proj", "fc1", "fc2")  # pixels and weights, all of layer 0
     prec = np.abs(m(pixel_values=pix).logits.cpu().numpy() - ref).max()
-    print(f"logit max|err| fp16 {plain:.3e}, fp16 + split embedding / layer 0 {prec:.3e}")
+    m.precise_ops = ("embed", "qkv")  # the split on the embedding and layer 0's q|k|v only
+    prec_qkv = np.abs(m(pixel_values=pix).logits.cpu().numpy() - ref).max()
+    m.precise_ops = ("embed_w", "qkv")  # ... with the embedding's pixels unsplit (the default)
+    prec_w = np.abs(m(pixel_values=pix).logits.cpu().numpy() - ref).max()
+    print(f"logit max|err| fp16 {plain:.3e}, fp16 + split embedding / layer 0 {prec:.3e}, "
+          f"embedding / layer-0 q|k|v {prec_qkv:.3e}, embedding weights / layer-0 q|k|v {prec_w:.3e}")
     assert prec <= 1e-3, prec
     assert prec < plain, (prec, plain)
+    assert prec_qkv <= 1e-3, prec_qkv
+    assert prec_qkv < plain, (prec_qkv, plain)

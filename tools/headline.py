@@ -25,6 +25,9 @@ ap.add_argument("--serial", type=int, default=0,
                 help="1: the split's parts one after the other on one stream, eager (bench.py's roofline and "
                      "per-kernel passes: the same launches without the overlap)")
 ap.add_argument("--gemm-cfg", default=None, help="JSON {op: cfg} override (ViViT: model.gemm_cfg)")
+ap.add_argument("--dtype", default="bf16", choices=("bf16", "fp16", "fp16_precise"),
+                help="ViViT operand type: bench.py's fp16 / fp16_precise legs (compute_dtype, precise_layers = 1)")
+ap.add_argument("--precise-ops", default=None, help="fp16_precise: comma list of split-operand GEMMs (model.precise_ops: embed|embed_w,qkv,o_proj,fc1,fc2)")
 a = ap.parse_args()
 if a.streams is None:
     a.streams = 4 if a.mode == "swin" else 2
@@ -47,6 +50,11 @@ else:
     x = torch.from_numpy(make_synthetic_video(a.batch or 4, 32, 224, seed=1)).cuda()
 if a.gemm_cfg:
     m.gemm_cfg = json.loads(a.gemm_cfg)
+if a.dtype != "bf16":
+    m.compute_dtype = torch.float16
+    m.precise_layers = 1 if a.dtype == "fp16_precise" else 0
+    if a.precise_ops:
+        m.precise_ops = tuple(a.precise_ops.split(","))
 m.concurrent_streams = a.streams
 m.graph_replay = bool(a.graph) and not a.serial
 from vclip_amd import streams  # noqa: E402
@@ -59,5 +67,5 @@ with streams.serial_parts(bool(a.serial)):
         m.forward_logits(x)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
-print(json.dumps({"mode": a.mode, "streams": a.streams, "graph": int(m.graph_replay), "serial": a.serial, "batch": x.shape[0],
+print(json.dumps({"mode": a.mode, "dtype": a.dtype, "streams": a.streams, "graph": int(m.graph_replay), "serial": a.serial, "batch": x.shape[0],
                   "ms_per_step": round(dt * 1e3, 3), "clips_s": round(x.shape[0] / dt, 2)}), flush=True)
