@@ -729,6 +729,23 @@ def main():
     dt = timed(a.streams)
     streams = model.last_streams
     graphed = model.graph_replay
+    # the fp16-operand build of the same forward (VC_ELEM_F16: same kernels, same MFMA rate, logits
+    # within 1e-3) and its split-operand variant (precise_layers = 1 with PRECISE_OPS: the weights of
+    # the first layers set the fp16 build's logit error, DESIGN.md §5.5), each timed like the headline
+    # beside a bf16 re-run, alternating bf16 / fp16 / fp16_precise twice: the chip's clock drifts over a
+    # run, so legs timed once after the instrumented passes read low against the opening headline
+    legs = {"bf16": [], "fp16": [], "fp16_precise": []}
+    for _ in range(2):
+        for leg in legs:
+            model.compute_dtype = torch.bfloat16 if leg == "bf16" else torch.float16
+            model.precise_layers = 1 if leg == "fp16_precise" else 0
+            model.precise_ops = PRECISE_OPS
+            model.graph_replay = graphed
+            legs[leg].append(timed(a.streams))
+    model.graph_replay = graphed
+    model.precise_layers = 0
+    model.compute_dtype = torch.bfloat16
+    dt16, dt16p, dtb = float(np.median(legs["fp16"])), float(np.median(legs["fp16_precise"])), float(np.median(legs["bf16"]))
     model.graph_replay = False  # the event-instrumented passes and one-off calls below run eagerly
     # the kernel roofline on the headline's OWN launches: the same split (batch / streams clips per launch,
     # the same kernels and workspaces) with the parts one after the other on one stream and HIP events
@@ -743,30 +760,13 @@ def main():
     evs1 = []
     dt1 = timed(1, evs1)
     attn_ms1 = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs1]))
-
-    # the fp16-operand build of the same forward (VC_ELEM_F16: same kernels, same MFMA rate, logits
-    # within 1e-3) and its split-operand variant (precise_layers = 1 with PRECISE_OPS: the weights of
-    # the first layers set the fp16 build's logit error, DESIGN.md §5.5), each timed like the headline
-    # beside a bf16 re-run, alternating bf16 / fp16 / fp16_precise twice: the chip's clock drifts over a
-    # run, so legs timed once after the instrumented passes read low against the opening headline
-    legs = {"bf16": [], "fp16": [], "fp16_precise": []}
-    for _ in range(2):
-        for leg in legs:
-            model.compute_dtype = torch.bfloat16 if leg == "bf16" else torch.float16
-            model.precise_layers = 1 if leg == "fp16_precise" else 0
-            model.precise_ops = PRECISE_OPS
-            model.graph_replay = graphed
-            legs[leg].append(timed(a.streams))
-    model.graph_replay = False
-    model.precise_layers = 0
-    dt16, dt16p, dtb = float(np.median(legs["fp16"])), float(np.median(legs["fp16_precise"])), float(np.median(legs["bf16"]))
+    # the fp16 build's attention launches, timed like the bf16 roofline pass
     model.compute_dtype = torch.float16
     evs16 = []
     with vstreams.serial_parts():
         timed(a.streams, evs16)
     attn_ms16 = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs16]))
     model.compute_dtype = torch.bfloat16
-
     # per-op and per-kernel tables of the headline's own launches (its split, serialised on one stream)
     model.concurrent_streams = streams
     part_clips = a.batch // streams if a.batch % streams == 0 else a.batch / streams
