@@ -222,9 +222,9 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: str, ou
     """out (+)= epilogue(a[:m] @ w.T + bias).  a bf16 [M,K], w bf16 [N,K], bias f32 [N]; or a, w (and the
     16-bit out) fp16 for the inference epilogues (bias / gelu / resid_f32 / embed_f32).  `flop` / `op`:
     the algorithmic work and op name an installed OpRecorder files this launch under (default
-    2 M N K of the operand shapes); `nbytes` (default: gemm_bytes of the operand shapes when `flop` is
-    not given either) its algorithmic bytes: the launch is filed under whichever bounds it -- bytes
-    when flop / bytes is below RIDGE_FLOP_PER_BYTE (or when only `nbytes` is given), FLOP otherwise."""
+    2 M N K of the operand shapes); `nbytes` (default: gemm_bytes of the operand shapes, scaled by
+    flop / 2 M N K) its algorithmic bytes: the launch is filed under whichever bounds it -- bytes when
+    flop / bytes is below RIDGE_FLOP_PER_BYTE (or when only `nbytes` is given), FLOP otherwise."""
     rec = _REC[0]
     if rec is not None:
         M_ = a.shape[0] if m is None else m
@@ -234,9 +234,12 @@ def gemm(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: str, ou
         if nbytes is not None and flop is None:
             rec.end(e0, label, op, nbytes, "byte")
         else:
-            fl = 2.0 * M_ * w.shape[0] * a.shape[1] if flop is None else flop
+            fl0 = 2.0 * M_ * w.shape[0] * a.shape[1]
+            fl = fl0 if flop is None else flop
+            # default bytes: the operand shapes' (scaled like the FLOP when the caller states real rows /
+            # channels instead of the padded ones)
             nb = nbytes if nbytes is not None else (
-                gemm_bytes(M_, w.shape[0], a.shape[1], epilogue, a.element_size()) if flop is None else None)
+                gemm_bytes(M_, w.shape[0], a.shape[1], epilogue, a.element_size()) * (fl / fl0))
             if nb is not None and fl / nb < RIDGE_FLOP_PER_BYTE:
                 rec.end(e0, label, op, nb, "byte")
             else:
