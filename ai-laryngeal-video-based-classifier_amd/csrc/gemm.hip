@@ -1217,15 +1217,21 @@ gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint
 // (operands L2-resident): the kernel's rate with the load side taken out; 2 (cfg 12) no epilogue
 // stores (the accumulators kept live by an empty asm): the cost of the output write; 3 (cfg 13) the
 // same bytes stored as full 128-B row segments per 8 lanes (values scrambled): the store pattern's cost.
-template <int EPI, int ET = VC_ELEM_BF16, int ABL = 0>
+// BN = 192 (cfg 24): the same schedule on 256 x 192 tiles (wave tile 128 x 48, 4 x 3 blocks, 12 MFMAs per
+// phase), for N = 768 outputs at the two-stream split's 12800 rows: 200 tiles fill one round of the
+// 256 CUs where 256 x 256 tiles leave 106 of them idle (150 tiles).  The W ring slot keeps its 256
+// rows so every wave issues the same LDS-DMAs (the counted vmcnt stays uniform): waves 6-7 restage
+// rows 128-191 into the unused rows 192-255 (in bounds, never read).
+template <int EPI, int ET = VC_ELEM_BF16, int ABL = 0, int BN = 256>
 __global__ void __launch_bounds__(512, 1)
 gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw, int nbm,
                int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
                const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride, int64_t goff, int nka) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int BM = 256, BN = 256, BKH = 32, NS = 4;
-    constexpr int SLOT = (BM + BN) * 64;  // 32 KiB
-    constexpr int TM = 128, TN = 64, MI = 8, NI = 4;
+    static_assert(BN == 256 || (BN == 192 && (ABL == 0 || ABL == 4)), "pp tile width");
+    constexpr int BM = 256, BKH = 32, NS = 4;
+    constexpr int SLOT = (BM + 256) * 64;  // 32 KiB
+    constexpr int TM = 128, TN = BN / 4, MI = 8, NI = TN / 16;
 
     const int nwg = nbm * nbn;
     const int bid = blockIdx.x;
@@ -1245,8 +1251,9 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     const int arow = wave * 32 + (lane >> 2);
     const uint16_t* ag0 = A + (m0 + arow) * lda + swz64(arow, lane & 3) * 8;
     const uint16_t* ag1 = A + (m0 + arow + 16) * lda + swz64(arow + 16, lane & 3) * 8;
-    const uint16_t* wg0 = W + (n0 + arow) * ldw + swz64(arow, lane & 3) * 8;
-    const uint16_t* wg1 = W + (n0 + arow + 16) * ldw + swz64(arow + 16, lane & 3) * 8;
+    const int wrow = arow < BN ? arow : arow - (256 - BN);  // source row (rows >= BN of the slot: filler)
+    const uint16_t* wg0 = W + (n0 + wrow) * ldw + swz64(arow, lane & 3) * 8;
+    const uint16_t* wg1 = W + (n0 + wrow + 16) * ldw + swz64(arow + 16, lane & 3) * 8;
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
     // nka: K-halves of A; W may be longer (K <= 2 nka): A's columns wrap, so W = [W_hi | W_lo] against
     // A gives A.W_hi + A.W_lo in one accumulation chain (vc_gemm_h16_wrap, the split-weight fp16 build)
@@ -1267,10 +1274,10 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
 #pragma unroll
         for (int i = 0; i < 4; ++i) fa[i] = lds_frag64(At, wm * TM + i0 + i * 16 + c16, q);
     };
-    auto read_w = [&](int u, v8s (&fw)[4]) __attribute__((always_inline)) {
+    auto read_w = [&](int u, v8s (&fw)[NI]) __attribute__((always_inline)) {
         const char* Wt = smem + (u & (NS - 1)) * SLOT + BM * 64;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) fw[j] = lds_frag64(Wt, wn * TN + j * 16 + c16, q);
+        for (int j = 0; j < NI; ++j) fw[j] = lds_frag64(Wt, wn * TN + j * 16 + c16, q);
     };
 
     v4f acc[MI][NI];
@@ -1279,7 +1286,7 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
 #pragma unroll
         for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-    auto mma = [&](auto I0, const v8s (&fa)[4], const v8s (&fw)[4]) __attribute__((always_inline)) {
+    auto mma = [&](auto I0, const v8s (&fa)[4], const v8s (&fw)[NI]) __attribute__((always_inline)) {
         constexpr int i0 = decltype(I0)::value;
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's fragment reads
@@ -1288,7 +1295,7 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i0 + i][j] = mfma16x32<ET>(fw[j], fa[i], acc[i0 + i][j]);
+            for (int j = 0; j < NI; ++j) acc[i0 + i][j] = mfma16x32<ET>(fw[j], fa[i], acc[i0 + i][j]);
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
     };
@@ -1296,8 +1303,8 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     using C4 = std::integral_constant<int, 4>;
 
     const int nk = K / BKH;  // even, >= 4
-    v8s alo[4], ahi[4], wA[4], wB[4];
-    auto phase_a = [&](int u, v8s (&fw)[4]) __attribute__((always_inline)) {
+    v8s alo[4], ahi[4], wA[NI], wB[NI];
+    auto phase_a = [&](int u, v8s (&fw)[NI]) __attribute__((always_inline)) {
         read_a(u, 0, alo);
         read_w(u, fw);
         if (u + 2 < nk) stage_w(u + 2);
@@ -1307,7 +1314,7 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
     };
-    auto phase_b = [&](int u, const v8s (&fw)[4]) __attribute__((always_inline)) {
+    auto phase_b = [&](int u, const v8s (&fw)[NI]) __attribute__((always_inline)) {
         read_a(u, 64, ahi);
         if (u + 3 < nk) {
             stage_a(u + 3);
@@ -1378,7 +1385,7 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
             for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(acc[i][j]));
         return;
     }
-    if constexpr (ABL == 3) {  // the same bytes as full 128-B row segments per 8 lanes (values scrambled)
+    if constexpr (ABL == 3 && BN == 256) {  // the same bytes as full 128-B row segments per 8 lanes (values scrambled)
         uint16_t* o16 = reinterpret_cast<uint16_t*>(out);
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
@@ -2263,8 +2270,8 @@ struct GemmCfg {
 static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}, {128, 128}, {0, 0},
                                  {64, 128}, {256, 256}, {256, 128}, {256, 256}, {256, 256}, {256, 256}, {256, 256},
                                  {128, 128}, {256, 256}, {256, 256}, {160, 256}, {256, 256}, {256, 256}, {128, 128},
-                                 {64, 128}, {64, 128}, {128, 128}};
-constexpr int kNumCfgs = 24;
+                                 {64, 128}, {64, 128}, {128, 128}, {256, 192}};
+constexpr int kNumCfgs = 25;
 
 template <int BM, int BN, int WM, int WN, int E, int ST = 3, int ET = VC_ELEM_BF16>
 static int launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
@@ -2300,19 +2307,19 @@ static int launch_big(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t
     return check_launch("vc_gemm_bf16");
 }
 
-template <int E, int ET, int ABL = 0>
+template <int E, int ET, int ABL = 0, int BN = 256>
 static int launch_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
                      const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
                      int64_t gs, int64_t go, hipStream_t stream, int ka = 0) {
     constexpr int lds = 4 * 512 * 64;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_pp_kernel<E, ET, ABL>,
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_pp_kernel<E, ET, ABL, BN>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
         attr_set = true;
     }
-    gemm_pp_kernel<E, ET, ABL><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out,
+    gemm_pp_kernel<E, ET, ABL, BN><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out,
                                                                            ldo, aux, ldaux, G, gs, go,
                                                                            (ka > 0 ? ka : K) / 32);
     return check_launch("vc_gemm_bf16");
@@ -2464,6 +2471,7 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
         case 22: return launch_cfg<64, 128, 2, 4, E, 6, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 23: return launch_cfg<128, 128, 2, 4, E, 4, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 8: return launch_pp<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
+        case 24: return launch_pp<E, ET, 0, 192>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 11:
         case 12:
         case 13:
@@ -2622,7 +2630,7 @@ extern "C" int vc_gemm_h16(const uint16_t* A, int64_t lda, const uint16_t* W, in
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: no tile config divides M x N");
     if ((M / kCfgs[cfg].bm) * (N / kCfgs[cfg].bn) > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: grid too large");
     const int k = (int)K;
-    if ((cfg == 8 || cfg == 9 || cfg == 17 || cfg == 18 || (cfg >= 11 && cfg <= 13)) && K < 128)
+    if ((cfg == 8 || cfg == 9 || cfg == 17 || cfg == 18 || cfg == 24 || (cfg >= 11 && cfg <= 13)) && K < 128)
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfgs 8 / 9 / 17 need K >= 128");
     if ((cfg == 15 || cfg == 16 || cfg == 19) && (K < 640 || K % 64 || N > 8192 || ldo % 8 || ((uintptr_t)out & 15)))
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfgs 15 / 16 need K >= 640, K % 64 == 0, N <= 8192, 16-B output rows");

@@ -183,12 +183,12 @@ def timed(kernel: str, op: str, work: float, unit: str, fn, *args, **kw):
 GEMM_KERNEL = {0: "gemm_bf16_kernel<256, 128, 4, 2, {E}, 3, {ET}>", 1: "gemm_bf16_kernel<128, 128, 2, 4, {E}, 3, {ET}>",
                2: "gemm_bf16_kernel<128, 256, 2, 4, {E}, 3, {ET}>", 3: "gemm_bf16_big_kernel<{E}, {ET}>",
                4: "gemm_bf16_persist_kernel<{E}, {ET}>", 5: "gemm_bf16_kernel<128, 128, 2, 4, {E}, 2, {ET}>",
-               7: "gemm_bf16_kernel<64, 128, 2, 4, {E}, 2, {ET}>", 8: "gemm_pp_kernel<{E}, {ET}, 0>",
+               7: "gemm_bf16_kernel<64, 128, 2, 4, {E}, 2, {ET}>", 8: "gemm_pp_kernel<{E}, {ET}, 0, 256>",
                9: "gemm_pp128_kernel<{E}, {ET}>", 10: "gemm_ppp_kernel<{E}, {ET}>",
                15: "gemm_ppd_kernel<{E}, {ET}, 16>", 16: "gemm_ppd_kernel<{E}, {ET}, 8>",
                17: "gemm_pp160_kernel<{E}, {ET}>", 20: "conv_c_stream_kernel<{K}, {BN}>",
                21: "gemm_bf16_kernel<64, 128, 2, 4, {E}, 4, {ET}>", 22: "gemm_bf16_kernel<64, 128, 2, 4, {E}, 6, {ET}>",
-               23: "gemm_bf16_kernel<128, 128, 2, 4, {E}, 4, {ET}>"}
+               23: "gemm_bf16_kernel<128, 128, 2, 4, {E}, 4, {ET}>", 24: "gemm_pp_kernel<{E}, {ET}, 0, 192>"}
 
 
 # roofline ridge of the bf16 matrix pipe against HBM (MI355X_MICROARCH.md: 2.5 PFLOP/s dense, 8 TB/s):
@@ -308,7 +308,7 @@ def gemm_wrap(a: torch.Tensor, ka: int, w: torch.Tensor, bias: torch.Tensor, epi
               out.stride(0), _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0, group,
               group_stride, group_offset, ELEM_F16 if a.dtype == torch.float16 else 0, _stream(a))
     if rec is not None:
-        rec.end(e0, f"gemm_pp_kernel<{e}, {1 if a.dtype == torch.float16 else 0}, 0>", op,
+        rec.end(e0, f"gemm_pp_kernel<{e}, {1 if a.dtype == torch.float16 else 0}, 0, 256>", op,
                 2.0 * M * N * K if flop is None else flop, "flop")
     return out
 

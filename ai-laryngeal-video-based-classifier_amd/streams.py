@@ -52,6 +52,11 @@ def run_split(owner, x: torch.Tensor, ns: int, part_fn, num_labels: int, prepare
     logits = owner._split_out[key]
     cur = torch.cuda.current_stream(dev)
     bounds = [B * i // ns for i in range(ns + 1)]
+    sizes = getattr(owner, "split_sizes", None)  # clips per part (A/B hook); None = as even as possible
+    if sizes is not None:
+        if len(sizes) != ns or sum(sizes) != B or min(sizes) < 1:
+            raise ValueError(f"split_sizes {sizes} must be {ns} positive part sizes summing to B={B}")
+        bounds = [sum(sizes[:i]) for i in range(ns + 1)]
     if _SERIAL[0]:
         for i in range(ns):
             part_fn(x[bounds[i]:bounds[i + 1]], i, out=logits[bounds[i]:bounds[i + 1]])

@@ -182,6 +182,7 @@ class Swin3d(torch.nn.Module):
         self._ws_used = []
         self.kernel_events = None  # list: HIP events around each window-attention launch (bench.py)
         self.concurrent_streams = None  # n > 1: the inference batch split over n HIP streams
+        self.split_sizes = None  # clips per stream part (streams.run_split); None = as even as possible
         self._streams = None
         self._split_out = {}
         # True: the inference forward is captured once per input / configuration into a hipGraph and
@@ -425,7 +426,7 @@ class Swin3d(torch.nn.Module):
             from .streams import GraphReplay
             if self._graphs is None:
                 self._graphs = GraphReplay()
-            key = (video.data_ptr(), tuple(video.shape), tuple(video.stride()), video.dtype, self.concurrent_streams,
+            key = (video.data_ptr(), tuple(video.shape), tuple(video.stride()), video.dtype, self.concurrent_streams, None if self.split_sizes is None else tuple(self.split_sizes),
                    str(video.device), self._weights_version())
             return self._graphs.run(key, video, self._forward_eager,
                                     keep=lambda: (self._packed, tuple(self._ws_used), self._bias_cache))

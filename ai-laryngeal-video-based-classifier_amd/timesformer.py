@@ -99,11 +99,14 @@ class TimesformerForVideoClassification(torch.nn.Module):
         self._names = list(shapes.keys())
         self.kernel_events = None  # list: HIP events around each spatial-attention launch (bench.py)
         self.concurrent_streams = None  # n > 1: the inference batch split over n HIP streams
+        self.split_sizes = None  # clips per stream part (streams.run_split); None = as even as possible
         # tile config of the two 768 x 768 bf16-output projections per layer (temporal dense, spatial
         # output): the 128x128 kernel (cfg 5), not vc_gemm's pick (the persistent 256x256 kernel,
         # 297 tiles = 1.16 rounds of 256 CUs at B=16): 37.9 vs 46.9 us at M = 25344 and 24.7 vs 25.4
         # at the two-stream M = 12800 (tools/ab_gemm_cfg.py, round 3); None: vc_gemm's pick
         self.proj_cfg = 5
+        # per-GEMM tile config overrides {"qkv_temporal" | "qkv_spatial" | "fc1" | "fc2": cfg} (A/B hook)
+        self.gemm_cfg = {}
         self._streams = None
         self._split_out = {}
         # True: the inference forward is captured once per input / configuration into a hipGraph and
@@ -258,7 +261,8 @@ class TimesformerForVideoClassification(torch.nn.Module):
             from .streams import GraphReplay
             if self._graphs is None:
                 self._graphs = GraphReplay()
-            key = (pix.data_ptr(), tuple(pix.shape), tuple(pix.stride()), pix.dtype, self.concurrent_streams, self.proj_cfg,
+            key = (pix.data_ptr(), tuple(pix.shape), tuple(pix.stride()), pix.dtype, self.concurrent_streams, None if self.split_sizes is None else tuple(self.split_sizes), self.proj_cfg,
+                   tuple(sorted(self.gemm_cfg.items())),
                    str(pix.device), self._weights_version())
             return self._graphs.run(key, pix, self._forward_eager,
                                     keep=lambda: (self._packed, tuple(self._ws_used)))
@@ -298,18 +302,19 @@ class TimesformerForVideoClassification(torch.nn.Module):
         act = "bias_gelu_erf" if c.hidden_act == "gelu" else "bias_gelu_tanh"
         scale = 1.0 / math.sqrt(c.hidden_size // Hn)
         pcfg = -1 if self.proj_cfg is None else self.proj_cfg
+        gc = self.gemm_cfg
         for L in pk["layers"]:
             # temporal branch (clip layout)
             tm("layernorm_kernel", "layernorm", Mc * D * 6, "byte", ops.layernorm, X, L["lnt_g"], L["lnt_b"], eps, Hc,
                m=B * S)
-            ops.gemm(Hc, L["w_qkv_t"], L["b_qkv_t"], "bias", QKV, flop=2.0 * Mc * 3 * D * D, op="qkv_temporal")
+            ops.gemm(Hc, L["w_qkv_t"], L["b_qkv_t"], "bias", QKV, cfg=gc.get("qkv_temporal", -1), flop=2.0 * Mc * 3 * D * D, op="qkv_temporal")
             tm("temporal_attn_lds_kernel", "temporal_attention", 4.0 * T * T * 64 * Hn * B * P, "flop",
                ops.temporal_attention, QKV, B, P, T, Hn, scale, O, q_prescaled=True)
             ops.gemm(O, L["w_t"], L["b_t"], "bias", Yb, cfg=pcfg, flop=2.0 * Mc * D * D, op="proj_temporal")
             # spatial branch (frame layout): X += temporal output, LayerNorm in the frame layout
             tm("tsf_add_ln_kernel", "add_layernorm", Mc * D * (4 + 2 + 4) + Mf * D * 2, "byte",
                ops.divided_add_layernorm, X, Yb, B, P, T, L["ln1_g"], L["ln1_b"], eps, "temporal_to_spatial", Hf)
-            ops.gemm(Hf, L["w_qkv_s"], L["b_qkv_s"], "bias", QKV, flop=2.0 * Mf * 3 * D * D, op="qkv_spatial")
+            ops.gemm(Hf, L["w_qkv_s"], L["b_qkv_s"], "bias", QKV, cfg=gc.get("qkv_spatial", -1), flop=2.0 * Mf * 3 * D * D, op="qkv_spatial")
             ev = self.kernel_events
             if ev is not None:  # recorded on the current stream, the one the kernel runs on
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -325,8 +330,8 @@ class TimesformerForVideoClassification(torch.nn.Module):
             # MLP (clip layout)
             tm("tsf_add_ln_kernel", "add_layernorm", Mf * D * 2 + Mc * D * (4 + 4 + 2), "byte",
                ops.divided_add_layernorm, X, Yb, B, P, T, L["ln2_g"], L["ln2_b"], eps, "spatial_to_mlp", Hc)
-            ops.gemm(Hc, L["w_1"], L["b_1"], act, Hd, flop=2.0 * Mc * I * D, op="fc1")
-            ops.gemm(Hd, L["w_2"], L["b_2"], "bias_resid_f32", X, flop=2.0 * Mc * D * I, op="fc2")
+            ops.gemm(Hc, L["w_1"], L["b_1"], act, Hd, cfg=gc.get("fc1", -1), flop=2.0 * Mc * I * D, op="fc1")
+            ops.gemm(Hd, L["w_2"], L["b_2"], "bias_resid_f32", X, cfg=gc.get("fc2", -1), flop=2.0 * Mc * D * I, op="fc2")
         return ops.cls_head(X, B, S, pk["lnf_g"], pk["lnf_b"], eps, pk["w_cls"], pk["b_cls"],
                             out=ws["logits"] if out is None else out)
 

@@ -86,6 +86,16 @@ class ClassifierOutput:
         return (self.loss, self.logits)[i] if self.loss is not None else (self.logits,)[i]
 
 
+# Clips per stream part where an uneven split measured faster than the even one (model.split_sizes
+# overrides).  ViViT-B B = 8 on two streams: 5 + 3 vs 4 + 4, +2.2 / +1.8 % in two interleaved
+# A/Bs on different boxes (tools/ab_split_sizes.py, profiles/r05_split_sizes.txt; 3 + 5 -0.8 %,
+# 6 + 2 -0.9 %): the 5-clip part's 1500 attention workgroups fill 2.93 rounds of the 512
+# two-per-CU slots where 4 clips' 1200 fill 2.34, and the parts pad 25344 token rows to the
+# 256-row GEMM tiles instead of 25600.  The larger part goes first (its stream starts first).
+# TimeSformer-B (10 + 6, 9 + 7) and ResNet3D (3 + 1) measured slower than even.
+SPLIT_DEFAULT = {(8, 2): (5, 3)}
+
+
 def _round_up(x, m):
     return (x + m - 1) // m * m
 
@@ -116,6 +126,8 @@ class VivitForVideoClassification(torch.nn.Module):
         self._ws_used = []
         self._streams = None
         self.concurrent_streams = None  # None / 1: one stream; n > 1: batch split over n HIP streams
+        # clips per stream part (A/B hook; must sum to the batch): None = as even as possible
+        self.split_sizes = None
         self.last_streams = 1
         self.kernel_events = None
         # True: the inference forward is captured once per input / configuration into a hipGraph
@@ -408,7 +420,8 @@ class VivitForVideoClassification(torch.nn.Module):
                 and not torch.cuda.is_current_stream_capturing()):
             key = (pix.data_ptr(), tuple(pix.shape), tuple(pix.stride()), pix.dtype, self.concurrent_streams,
                    self.compute_dtype, self._weights_version(), tuple(sorted(self.gemm_cfg.items())), self.rows,
-                   self.round_split, self.precise_layers, tuple(sorted(self.precise_ops)))
+                   self.round_split, self.precise_layers, tuple(sorted(self.precise_ops)),
+                   None if self.split_sizes is None else tuple(self.split_sizes))
             return self._graphs.run(key, pix, self._forward_eager, keep=lambda: (self._packed, tuple(self._ws_used)))
         return self._forward_eager(pix)
 
@@ -420,6 +433,7 @@ class VivitForVideoClassification(torch.nn.Module):
         ns = max(1, min(int(ns), B))
         self.last_streams = ns
         if ns == 1:
+            self.last_split = [B]
             return self._forward_part(pix, 0)
         dev = pix.device
         if self._streams is None or len(self._streams) < ns or self._streams[0].device != dev:
@@ -433,6 +447,12 @@ class VivitForVideoClassification(torch.nn.Module):
         # (streams.run_split's rule): packed inside part 0 they would race parts 1..n-1
         self._pack(dev)
         bounds = [B * i // ns for i in range(ns + 1)]
+        sizes = self.split_sizes if self.split_sizes is not None else SPLIT_DEFAULT.get((B, ns))
+        if sizes is not None:
+            if len(sizes) != ns or sum(sizes) != B or min(sizes) < 1:
+                raise ValueError(f"split_sizes {sizes} must be {ns} positive part sizes summing to B={B}")
+            bounds = [sum(sizes[:i]) for i in range(ns + 1)]
+        self.last_split = [bounds[i + 1] - bounds[i] for i in range(ns)]
         if streams.serial():  # instrumentation: the parts one after the other on the caller's stream
             for i in range(ns):
                 self._forward_part(pix[bounds[i]:bounds[i + 1]], i, out=logits[bounds[i]:bounds[i + 1]])

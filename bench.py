@@ -181,12 +181,13 @@ def timed_loop(step, steps: int, warmup: int, dist=None, sync=None):
 PEAK_HBM_GBS = 8000.0            # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def kernel_breakdown(model, step, clips, streams, n_steps):
+def kernel_breakdown(model, step, clips, streams, n_steps, split_desc=None):
     """Per-op table of the ViViT-B forward: `n_steps` extra (untimed) steps with HIP events
     around EVERY launch, on the stream each launch runs on; per op the mean launch duration,
     its share of the step and the achieved rate against the op's own roofline (MFMA for the
     GEMMs / attention in algorithmic FLOPs, HBM for LayerNorm / im2col in algorithmic bytes).
-    `clips` = clips per launch."""
+    `clips` = clips per launch (the mean over the parts when `split_desc` names uneven parts: the
+    rates are then total work over total time)."""
     S, D, F, P = 3137, 768, 3072, 3136
     M = clips * S
     work = {  # (amount per launch, unit, bound)
@@ -219,7 +220,8 @@ def kernel_breakdown(model, step, clips, streams, n_steps):
         out[name] = {"launches_per_step": len(ms) // n_steps, "avg_launch_ms": round(avg, 4),
                      "share_of_step": round(sum(ms) / n_steps / step_ms, 4), "bound": bound,
                      "achieved": round(rate, 1), "unit": unit, "peak": peak, "frac": round(rate / peak, 4)}
-    out["note"] = (f"{n_steps} extra untimed steps with HIP events around every launch ({clips:g} clips per launch: "
+    per = f"{split_desc} clips per launch, mean {clips:g}" if split_desc else f"{clips:g} clips per launch"
+    out["note"] = (f"{n_steps} extra untimed steps with HIP events around every launch ({per}: "
                    f"the headline's {streams}-part split serialised on one stream); step {step_ms:.3f} ms under that "
                    "instrumentation; algorithmic work (M = clips x 3137 rows, no padding)")
     return out
@@ -509,7 +511,7 @@ def run_family(a, dist, rank, world, dev):
             "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (uint8 frames RandomState(1+rank) -> the family's processor affine; weights RandomState(0))",
             "config": {"workload": workload, "global_batch": a.batch * world, "parallelism": f"dp{world}",
-                       "streams": a.streams, "hip_graph": _graph_used(model, a)},
+                       "streams": a.streams, "split": split, "hip_graph": _graph_used(model, a)},
             "logit_max_abs_err": err,
             "logit_err_note": "max |logit - oracle| relative to max(1, max |oracle logit|)" if a.mode == "resnet3d" else None,
             "roofline": roof,
@@ -728,6 +730,8 @@ def main():
     # every kernel is batch-invariant: logits bit-identical to one stream), nothing instrumented
     dt = timed(a.streams)
     streams = model.last_streams
+    split = list(model.last_split)  # clips per part (vivit.SPLIT_DEFAULT: 5 + 3 at B = 8 on two streams)
+    split_desc = " + ".join(str(v) for v in split)
     graphed = model.graph_replay
     # the fp16-operand build of the same forward (VC_ELEM_F16: same kernels, same MFMA rate, logits
     # within 1e-3) and its split-operand variant (precise_layers = 1 with PRECISE_OPS: the weights of
@@ -771,14 +775,16 @@ def main():
     model.concurrent_streams = streams
     part_clips = a.batch // streams if a.batch % streams == 0 else a.batch / streams
     with vstreams.serial_parts():
-        breakdown = kernel_breakdown(model, step, part_clips, streams, 3)
+        breakdown = kernel_breakdown(model, step, part_clips, streams, 3, split_desc)
         ktable, instr_ms = op_breakdown(model, step, 3)
     model.concurrent_streams = 1
 
     clips = a.batch * a.steps * world
     value = clips / dt
     ms_per_step = dt / a.steps * 1e3
-    launch_clips = part_clips  # the roofline pass times the headline's launches: batch / streams clips each
+    # the roofline pass times the headline's launches: `split` clips each, mean batch / streams (mean rate =
+    # total attention work over total launch time)
+    launch_clips = part_clips
     attn_tflops = ATTN_GFLOP_PER_CLIP_LAYER * launch_clips / (attn_ms * 1e-3) / 1e3
     attn_tflops1 = ATTN_GFLOP_PER_CLIP_LAYER * a.batch / (attn_ms1 * 1e-3) / 1e3
     model_tflops = VIVIT_GFLOP_PER_CLIP * a.batch / (ms_per_step * 1e-3) / 1e3
@@ -832,8 +838,9 @@ def main():
                          "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
                          "algorithmic_bytes": ATTN_IO_BYTES_PER_CLIP * launch_clips, "avg_launch_ms": round(attn_ms, 4),
-                         "flop_per_launch": f"{ATTN_GFLOP_PER_CLIP_LAYER:.2f} GF/clip x {launch_clips:g} clips",
-                         "timed_on": f"the headline's own launches ({launch_clips:g} clips each: its {streams}-stream "
+                         "flop_per_launch": f"{ATTN_GFLOP_PER_CLIP_LAYER:.2f} GF/clip x {launch_clips:g} clips (mean of "
+                                            f"the {split_desc}-clip launches)",
+                         "timed_on": f"the headline's own launches ({split_desc} clips: its {streams}-stream "
                                      "split) run one after the other on one HIP stream, HIP events around every "
                                      f"attention launch: clips/s {a.batch * a.steps * world / dts:.2f} there",
                          "whole_batch_launch": {"clips": a.batch, "avg_launch_ms": round(attn_ms1, 4),

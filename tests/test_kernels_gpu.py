@@ -123,6 +123,37 @@ def test_gemm_every_tile_config(cfg, epi):
     assert err < 8e-3, err
 
 
+# the 16x16x32-MFMA tile configurations (csrc/gemm.hip kCfgs): ping-pong 256x256 (8), 256x128 (9), persistent
+# deferred-store (15, 16), 160x256 (17), 256x192 (24), deeper-ring 64x128 / 128x128 (21, 22, 23); each runs the
+# same MFMA chain per output element as the 128x128 kernel (cfg 5), so its output is bit-identical to it
+PP_CFGS = {8: ("bias", "bias_gelu_tanh", "bias_resid_f32"), 9: ("bias", "bias_resid_f32"),
+           15: ("bias",), 16: ("bias",), 17: ("bias", "bias_resid_f32"), 24: ("bias", "bias_resid_f32"),
+           21: ("bias", "bias_resid_f32"), 22: ("bias_resid_f32",), 23: ("bias",)}
+
+
+@pytest.mark.parametrize("cfg,epi", [(c, e) for c, es in PP_CFGS.items() for e in es])
+def test_gemm_tile_configs_bit_identical(cfg, epi):
+    M, N, K = 1280 * 2, 768, 768  # 2560 rows: a multiple of 256, 160 and 128; N: 3 x 256, 4 x 192, 6 x 128
+    if cfg == 22:
+        K = 3072
+    a, w, bias, ref = _gemm_case(M, N, K, 31 * cfg + len(epi))
+    f32 = epi == "bias_resid_f32"
+    init = (torch.randn(M, N, generator=torch.Generator().manual_seed(cfg)) if f32 else
+            torch.zeros(M, N)).to(torch.float32 if f32 else torch.bfloat16)
+    outs = []
+    for c in (5, cfg):
+        out = init.clone().to(DEV)
+        ops().gemm(a.to(DEV), w.to(DEV), bias.to(DEV), epi, out, cfg=c)
+        outs.append(out.cpu())
+    assert torch.equal(outs[0], outs[1]), f"cfg {cfg} differs from cfg 5"
+    if epi == "bias_gelu_tanh":
+        ref = gelu_fast(ref)
+    elif f32:
+        ref = ref + init
+    err = ((outs[1].float() - ref).abs() / (ref.abs() + 1.0)).max().item()
+    assert err < 8e-3, err
+
+
 @pytest.mark.parametrize("M,N,K", [(768, 768, 192), (256, 256, 768), (2304, 768, 3072), (25344, 3072, 768),
                                    (4096, 2304, 256), (12800, 768, 768), (512, 512, 448), (1024, 768, 320)])
 @pytest.mark.parametrize("epi", ["bias", "bias_gelu_erf", "bias_relu"])

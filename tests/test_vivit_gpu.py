@@ -94,8 +94,17 @@ def test_vivit_two_stream_split_bit_exact():
     m.concurrent_streams = 2
     two = m.forward_logits(pix).clone()
     assert m.last_streams == 2
+    assert m.last_split == [5, 3]  # vivit.SPLIT_DEFAULT at B = 8
     assert torch.equal(one, two)
     torch.testing.assert_close(m(pixel_values=pix).logits, one, rtol=0, atol=0)
+    # any part sizes: the even split, the reversed one, three uneven parts
+    for sizes in ([4, 4], [3, 5], [1, 6, 1]):
+        m.concurrent_streams, m.split_sizes = len(sizes), sizes
+        assert torch.equal(m.forward_logits(pix), one), sizes
+        assert m.last_split == sizes
+    m.concurrent_streams, m.split_sizes = 2, [4, 3]
+    with pytest.raises(ValueError):
+        m.forward_logits(pix)
 
 
 def test_vivit_tiny_per_layer_drift():
@@ -242,7 +251,7 @@ def test_vivit_b_batch8_headline_path_graphed():
     m.graph_replay = True
     for _ in range(2):
         got = m.forward_logits(pix).clone()
-        assert m.last_streams == 2
+        assert m.last_streams == 2 and m.last_split == [5, 3]
         assert torch.equal(got, eager)
     assert torch.equal(m.forward_logits(pix2.clone()), eager2)
     err = float(np.abs(got.cpu().numpy() - np.array(g["logits"])).max())

@@ -31,7 +31,7 @@ for M, tag in ((25344, "B8"), (12800, "B4")):
     CASES += [(f"qkv_{tag}", M, 2304, 768, "bias"), (f"fc1_{tag}", M, 3072, 768, "bias_gelu_tanh"),
               (f"fc2_{tag}", M, 768, 3072, "bias_resid_f32"), (f"oproj_{tag}", M, 768, 768, "bias_resid_f32")]
 CASES += [("sq4096", 4096, 4096, 4096, "bias"), ("sq8192", 8192, 8192, 8192, "bias"),
-          ("tsf_fc1_B16", 25344, 3072, 768, "bias_gelu_erf")]
+          ("tsf_fc1_B16", 25344, 3072, 768, "bias_gelu_erf"), ("tsf_fc1_B8", 12800, 3072, 768, "bias_gelu_erf")]
 if a.swin or a.swinpart:
     CASES = []
     geo = ((200704, 96, 128), (50176, 192, 256), (12544, 384, 384), (3136, 768, 768))
@@ -75,9 +75,9 @@ for name, M, N, K, epi in CASES:
     base = lib.vc_gemm_pick(M, N, K, E[epi], out.stride(0), 0, None)
     bf16_out = out.dtype != torch.float32
     TILE = {1: (128, 128), 3: (256, 256), 4: (256, 256), 5: (128, 128), 7: (64, 128), 8: (256, 256), 9: (256, 128),
-            10: (256, 256), 11: (256, 256), 12: (256, 256), 13: (256, 256), 14: (128, 128), 15: (256, 256), 16: (256, 256), 17: (160, 256), 20: (128, 128), 21: (64, 128), 22: (64, 128), 23: (128, 128)}
+            10: (256, 256), 11: (256, 256), 12: (256, 256), 13: (256, 256), 14: (128, 128), 15: (256, 256), 16: (256, 256), 17: (160, 256), 20: (128, 128), 21: (64, 128), 22: (64, 128), 23: (128, 128), 24: (256, 192)}
     ok_shape = lambda c: (c in TILE and M % TILE[c][0] == 0 and N % TILE[c][1] == 0 and K % 64 == 0 and  # noqa: E731
-                          (K >= 192 if c in (4, 10) else K >= 640 if c in (15, 16) else K >= 128 if c in (8, 9, 11, 12, 13, 17) else True))  # cfg 1: 128x128, 3-slot ring
+                          (K >= 192 if c in (4, 10) else K >= 640 if c in (15, 16) else K >= 128 if c in (8, 9, 11, 12, 13, 17, 24) else True))  # cfg 1: 128x128, 3-slot ring
     cfgs = [base] + [c for c in new_cfgs if c != base and ok_shape(c) and (c not in (11, 12, 13) or epi == "bias") and
                      (c != 14 or epi == "bias_resid_relu") and (c != 20 or (epi == "bias_resid_relu" and K in (64, 128, 256))) and
                      (c not in (4, 10, 15, 16) or bf16_out) and (c not in (15, 16) or epi in ("bias", "bias_gelu_tanh", "bias_gelu_erf"))]
