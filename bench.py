@@ -511,7 +511,7 @@ def run_family(a, dist, rank, world, dev):
             "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (uint8 frames RandomState(1+rank) -> the family's processor affine; weights RandomState(0))",
             "config": {"workload": workload, "global_batch": a.batch * world, "parallelism": f"dp{world}",
-                       "streams": a.streams, "split": split, "hip_graph": _graph_used(model, a)},
+                       "streams": a.streams, "hip_graph": _graph_used(model, a)},
             "logit_max_abs_err": err,
             "logit_err_note": "max |logit - oracle| relative to max(1, max |oracle logit|)" if a.mode == "resnet3d" else None,
             "roofline": roof,
@@ -832,7 +832,7 @@ def main():
             "config": {"workload": "ViViT-B/16x2 forward, 32x224x224 clips, batch 8 per GPU (BASELINE configs[1])",
                        "model": "ViViT-B/16x2 (joint space-time, 12L, d768, 12H, 3137 tokens)",
                        "global_batch": a.batch * world, "seq_len": 3137, "parallelism": f"dp{world}",
-                       "streams": a.streams, "hip_graph": _graph_used(model, a)},
+                       "streams": a.streams, "split": split, "hip_graph": _graph_used(model, a)},
             "logit_max_abs_err": logit_err,
             "roofline": {"bound": "mfma", "kernel": ATTN_KERNEL, "achieved": round(attn_tflops, 1),
                          "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4),
