@@ -70,6 +70,8 @@ SIGNATURES = {
                              c_p, c_int, c_p, c_i64, c_p, c_i64, c_p], c_int),
     "vc_conv3d_gemm_bf16_ring": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64,
                                   c_p, c_int, c_p, c_i64, c_p, c_i64, c_int, c_p], c_int),
+    "vc_conv3d_gemm_bf16_cfg": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64,
+                                 c_p, c_int, c_p, c_i64, c_p, c_i64, c_int, c_int, c_p], c_int),
     "vc_conv3d_stem_pack": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p], c_int),
     "vc_conv3d_stem_gemm_bf16": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_int,
                                   c_p, c_i64, c_p], c_int),

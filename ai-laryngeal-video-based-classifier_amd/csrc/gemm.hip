@@ -2146,6 +2146,12 @@ conv_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx, ConvGeomG g, const
         rw[i] = wo * g.sw - g.pw;
         rch[i] = swz(row, lane & 7) * 8;
     }
+    // MODE 0: element offset of each row's tap-(0, 0, 0) input position (outside the clip for rows whose
+    // window starts in the padding: only combined with a tap offset that lands inside, checked per tap)
+    int64_t roff[AL];
+#pragma unroll
+    for (int i = 0; i < AL; ++i)
+        roff[i] = (rbase[i] + ((int64_t)rt[i] * g.Hin + rh[i]) * g.Win + rw[i]) * ldx + rch[i];
 
     const uint16_t* bsrc[BL];
 #pragma unroll
@@ -2154,31 +2160,54 @@ conv_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx, ConvGeomG g, const
         bsrc[i] = W + (n0 + row) * ldw + swz(row, lane & 7) * 8;
     }
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
+    // the tap of the next k-tile to stage, walked incrementally (stage() runs for t = 0, 1, 2, ... in
+    // order): wave-uniform scalar counters instead of five integer divisions per k-tile (round 5: the
+    // divisions and per-row 64-bit address products made the res4 / res5 convolutions 1.3-1.7x slower
+    // than a plain GEMM of the same shape, tools/conv_vs_gemm.py).  MODE 0: channel block c0 of tap
+    // (it, ih, iw); MODE 1: (kt, kh) segment 2t as (sa_t, sa_h), 2t + 1 derived from it
+    int s_c0 = 0, s_iw = 0, s_ih = 0, s_it = 0;
     auto stage = [&](int t, int slot) {
         const uint32_t s = lds0 + slot * SLOT;
         const int k0 = t * 64;
         if constexpr (MODE == 1) {
+            // segment 2t = (s_it, s_ih), 2t + 1 = the next (it, ih) in row-major order
+            int it1 = s_it, ih1 = s_ih + 1;
+            if (ih1 == g.kh) { ih1 = 0; ++it1; }
+            const int nseg = g.kt * g.kh;
 #pragma unroll
             for (int i = 0; i < AL; ++i) {
                 const int lc = rch[i] >> 3;  // this row's logical 16-B chunk (the source side of the swizzle)
-                const int seg = 2 * t + (lc >> 2), sub = lc & 3;
-                const bool sok = seg < g.kt * g.kh;
-                const int it = sok ? seg / g.kh : 0, ih = sok ? seg - it * g.kh : 0;
+                const int hi = lc >> 2, sub = lc & 3;
+                const int seg = 2 * t + hi;
+                const bool sok = seg < nseg;
+                const int it = hi ? it1 : s_it, ih = hi ? ih1 : s_ih;
                 const int64_t soff = ((int64_t)it * g.Hin + ih) * g.Win * 4 + sub * 8;
                 const uint16_t* src = (rok[i] && sok) ? X + rbase[i] * 4 + soff : zrow + rch[i];
                 glds16(src, __builtin_amdgcn_readfirstlane(s + (wave * (BM / 8) + i * 8) * 128));
             }
+            s_it = it1;
+            s_ih = ih1 + 1;
+            if (s_ih == g.kh) { s_ih = 0; ++s_it; }
         } else {
-            const int tap = k0 / g.C, c0 = k0 - tap * g.C;  // wave-uniform
-            const int iw = tap % g.kw, ih = (tap / g.kw) % g.kh, it = tap / (g.kw * g.kh);
+            const int64_t toff = (((int64_t)s_it * g.Hin + s_ih) * g.Win + s_iw) * ldx + s_c0;  // wave-uniform
 #pragma unroll
             for (int i = 0; i < AL; ++i) {
-                const int ti = rt[i] + it, hi = rh[i] + ih, wi = rw[i] + iw;
+                const int ti = rt[i] + s_it, hi = rh[i] + s_ih, wi = rw[i] + s_iw;
                 const bool ok = rok[i] && (unsigned)ti < (unsigned)g.Tin && (unsigned)hi < (unsigned)g.Hin &&
                                 (unsigned)wi < (unsigned)g.Win;
-                const uint16_t* src = ok ? X + (rbase[i] + ((int64_t)ti * g.Hin + hi) * g.Win + wi) * ldx + c0 + rch[i]
-                                         : zrow + rch[i];
+                const uint16_t* src = ok ? X + (roff[i] + toff) : zrow + rch[i];
                 glds16(src, __builtin_amdgcn_readfirstlane(s + (wave * (BM / 8) + i * 8) * 128));
+            }
+            s_c0 += 64;
+            if (s_c0 == g.C) {
+                s_c0 = 0;
+                if (++s_iw == g.kw) {
+                    s_iw = 0;
+                    if (++s_ih == g.kh) {
+                        s_ih = 0;
+                        ++s_it;
+                    }
+                }
             }
         }
 #pragma unroll
@@ -2221,8 +2250,8 @@ conv_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx, ConvGeomG g, const
             for (int i = 0; i < MI; ++i)
 #pragma unroll
                 for (int j = 0; j < NI; ++j) acc[i][j] = mfma16x32<VC_ELEM_BF16>(wf[kk][j], af[kk][i], acc[i][j]);
-        if (ST == 3 && t + 2 < nk) wait_vm<LPT>();
-        else wait_vm<0>();
+        // retire tile t + 1; the tiles staged after it (up to ST - 2) may stay in flight
+        wait_tiles<LPT, ST - 2>(nk - 2 - t);
         block_sync_lds();
     }
     store_tile16<EPI, MI, NI, VC_ELEM_BF16>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bq, out, ldo, aux, ldaux, 1, 0,
@@ -2252,7 +2281,11 @@ template <int BM, int BN, int WM, int WN, int E, int MODE = 0>
 static int launch_conv(const uint16_t* X, int64_t ldx, const ConvGeomG& g, const uint16_t* zrow, const uint16_t* W,
                        int64_t ldw, int nbm, int nbn, int K, const float* bias, void* out, int64_t ldo, const float* aux,
                        int64_t ldaux, hipStream_t stream, int ring = 2) {
-    if (ring == 3)
+    if constexpr (MODE == 0 && BN == 128)
+        if (ring == 4)
+            return launch_conv_st<BM, BN, WM, WN, E, MODE, 4>(X, ldx, g, zrow, W, ldw, nbm, nbn, K, bias, out, ldo, aux,
+                                                              ldaux, stream);
+    if (ring >= 3)  // ring 4 on 256 x 64 tiles and the stem: 3
         return launch_conv_st<BM, BN, WM, WN, E, MODE, 3>(X, ldx, g, zrow, W, ldw, nbm, nbn, K, bias, out, ldo, aux,
                                                           ldaux, stream);
     return launch_conv_st<BM, BN, WM, WN, E, MODE, 2>(X, ldx, g, zrow, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux,
@@ -2665,13 +2698,14 @@ extern "C" int vc_gemm_h16(const uint16_t* A, int64_t lda, const uint16_t* W, in
 // Implicit-GEMM Conv3d (conv_gemm_kernel): out[m][n] = epilogue(sum_(tap, c) x[in(m, tap)][c] *
 // Wt[n][tap * C + c] + bias[n]); output rows m < B*To*Ho*Wo (rows up to the next multiple of 128
 // are written too: the caller's buffer has them), zero_row: >= 64 zero bf16 (16-B aligned).
-extern "C" int vc_conv3d_gemm_bf16_ring(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_t H, int64_t W,
-                                        int64_t C, const int* kernel, const int* stride, const int* pad,
-                                        const uint16_t* zero_row, const uint16_t* Wt, int64_t ldw, int64_t N,
-                                        const float* bias, int epilogue, void* out, int64_t ldo, const void* aux,
-                                        int64_t ldaux, int ring, hipStream_t stream) {
-    if (ring != 0 && ring != 2 && ring != 3)
-        return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16_ring: ring must be 0, 2 or 3");
+extern "C" int vc_conv3d_gemm_bf16_cfg(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_t H, int64_t W,
+                                       int64_t C, const int* kernel, const int* stride, const int* pad,
+                                       const uint16_t* zero_row, const uint16_t* Wt, int64_t ldw, int64_t N,
+                                       const float* bias, int epilogue, void* out, int64_t ldo, const void* aux,
+                                       int64_t ldaux, int ring, int tile, hipStream_t stream) {
+    if (ring != 0 && ring != 2 && ring != 3 && ring != 4)
+        return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16_cfg: ring must be 0, 2, 3 or 4");
+    if (tile < 0 || tile > 2) return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16_cfg: tile must be 0, 1 or 2");
     // ring 0 (automatic): a 3-deep ring when the grid has fewer tiles than two per CU (the workgroups
     // are few, so each one's DMA latency is exposed; ResNet3D res4 / res5 at B = 4: +1.1 / +1.5 % of
     // the forward each), else 2 (res2 / res3: -3.7 / -2.5 %), tools/ab_resnet3d_ring.py, round 4
@@ -2715,9 +2749,11 @@ extern "C" int vc_conv3d_gemm_bf16_ring(const uint16_t* x, int64_t ldx, int64_t 
     }
     const int nbm = (int)((g.M + 127) / 128), nbn = (int)(N / 128);
     if ((int64_t)nbm * nbn > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: grid too large");
+    if (tile == 1 && !(ldo % 8 == 0 && (epilogue == VC_EPI_BIAS_RELU_BF16 || epilogue == VC_EPI_BIAS_BF16)))
+        return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16_cfg: 64 x 128 tiles need bias / bias_relu, ldo % 8 == 0");
     // fewer 128 x 128 tiles than CUs (ResNet3D stage 4: 49 x 4 at B = 4): 64 x 128 tiles, twice the workgroups
-    if (nbm * nbn < num_cus() && ldo % 8 == 0 &&
-        (epilogue == VC_EPI_BIAS_RELU_BF16 || epilogue == VC_EPI_BIAS_BF16)) {
+    if (tile == 1 || (tile == 0 && nbm * nbn < num_cus() && ldo % 8 == 0 &&
+                      (epilogue == VC_EPI_BIAS_RELU_BF16 || epilogue == VC_EPI_BIAS_BF16))) {
         const int nbm64 = (int)((g.M + 63) / 64);
         ring = pick_ring((int64_t)nbm64 * nbn);
         if (epilogue == VC_EPI_BIAS_RELU_BF16)
@@ -2747,13 +2783,24 @@ extern "C" int vc_conv3d_gemm_bf16_ring(const uint16_t* x, int64_t ldx, int64_t 
                                     "(16-B output rows; resid_relu: a bf16 aux with ldaux >= N)");
 }
 
+extern "C" int vc_conv3d_gemm_bf16_ring(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_t H, int64_t W,
+                                        int64_t C, const int* kernel, const int* stride, const int* pad,
+                                        const uint16_t* zero_row, const uint16_t* Wt, int64_t ldw, int64_t N,
+                                        const float* bias, int epilogue, void* out, int64_t ldo, const void* aux,
+                                        int64_t ldaux, int ring, hipStream_t stream) {
+    if (ring != 0 && ring != 2 && ring != 3)
+        return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16_ring: ring must be 0, 2 or 3");
+    return vc_conv3d_gemm_bf16_cfg(x, ldx, B, T, H, W, C, kernel, stride, pad, zero_row, Wt, ldw, N, bias, epilogue, out,
+                                   ldo, aux, ldaux, ring, 0, stream);
+}
+
 extern "C" int vc_conv3d_gemm_bf16(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_t H, int64_t W,
                                    int64_t C, const int* kernel, const int* stride, const int* pad,
                                    const uint16_t* zero_row, const uint16_t* Wt, int64_t ldw, int64_t N,
                                    const float* bias, int epilogue, void* out, int64_t ldo, const void* aux,
                                    int64_t ldaux, hipStream_t stream) {
-    return vc_conv3d_gemm_bf16_ring(x, ldx, B, T, H, W, C, kernel, stride, pad, zero_row, Wt, ldw, N, bias, epilogue, out,
-                                    ldo, aux, ldaux, 0, stream);
+    return vc_conv3d_gemm_bf16_cfg(x, ldx, B, T, H, W, C, kernel, stride, pad, zero_row, Wt, ldw, N, bias, epilogue, out,
+                                   ldo, aux, ldaux, 0, 0, stream);
 }
 
 // Stem input packing for vc_conv3d_stem_gemm_bf16: f32 [B][C][T][H][W] (C <= 4) -> bf16

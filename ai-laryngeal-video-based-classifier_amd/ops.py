@@ -626,7 +626,7 @@ def zero_row(device) -> torch.Tensor:
 
 def conv3d_gemm(x: torch.Tensor, B: int, grid, C: int, kernel, stride, pad, w: torch.Tensor, bias: torch.Tensor,
                 epilogue: str, out: torch.Tensor, aux: torch.Tensor | None = None, flop: float | None = None,
-                op: str = "conv", n: int | None = None, ring: int = 0) -> torch.Tensor:
+                op: str = "conv", n: int | None = None, ring: int = 0, tile: int = 0) -> torch.Tensor:
     """Implicit-GEMM Conv3d (vc_conv3d_gemm_bf16): x channels-last bf16 rows [>= B*T*H*W, >= C],
     w bf16 [>= N, >= kvol*C] (columns (kt, kh, kw, c)), out bf16 [>= roundup(B*To*Ho*Wo, 128), >= N]
     (256-row multiples when N % 128 != 0: 256 x 64 tiles); N = n (a multiple of 64) or w's rows."""
@@ -656,18 +656,20 @@ def conv3d_gemm(x: torch.Tensor, B: int, grid, C: int, kernel, stride, pad, w: t
     if rec is not None:
         # the label first: nothing but the launch may sit between the two events (a first
         # get_device_properties inside them once timed as an 8-ms launch)
-        tile = "256, 64, 8, 1"
+        tl = "256, 64, 8, 1"
         if rt == 128:  # 64 x 128 tiles when the 128 x 128 grid has fewer tiles than CUs (csrc/gemm.hip)
-            small = ((M + 127) // 128) * (N // 128) < _num_cus(x.device) and e in (0, 6)
-            tile = "64, 128, 2, 4" if small else "128, 128, 2, 4"
-        nt = (((M + 127) // 128) * (N // 128) if tile == "128, 128, 2, 4" else ((M + 63) // 64) * (N // 128)
-              if tile == "64, 128, 2, 4" else ((M + 255) // 256) * (N // 64))
+            small = tile == 1 or (tile == 0 and ((M + 127) // 128) * (N // 128) < _num_cus(x.device) and e in (0, 6))
+            tl = "64, 128, 2, 4" if small else "128, 128, 2, 4"
+        nt = (((M + 127) // 128) * (N // 128) if tl == "128, 128, 2, 4" else ((M + 63) // 64) * (N // 128)
+              if tl == "64, 128, 2, 4" else ((M + 255) // 256) * (N // 64))
         st = ring if ring else (3 if nt < 2 * _num_cus(x.device) else 2)  # csrc/gemm.hip pick_ring
-        label = f"conv_gemm_kernel<{tile}, {e}, {st}, 0>"
+        if st == 4 and rt != 128:
+            st = 3
+        label = f"conv_gemm_kernel<{tl}, {e}, {st}, 0>"
     e0 = rec.begin() if rec is not None else None
-    _lib.call("vc_conv3d_gemm_bf16_ring", _p(x), x.stride(0), B, T, H, W, C, ctypes.addressof(k), ctypes.addressof(s),
+    _lib.call("vc_conv3d_gemm_bf16_cfg", _p(x), x.stride(0), B, T, H, W, C, ctypes.addressof(k), ctypes.addressof(s),
               ctypes.addressof(p), _p(zrow), _p(w), w.stride(0), N, _p(bias), e, _p(out), out.stride(0),
-              _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0, ring, _stream(x))
+              _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0, ring, tile, _stream(x))
     if rec is not None:
         rec.end(e0, label, op, 2.0 * M * N * kvol * C if flop is None else flop, "flop")
     return out

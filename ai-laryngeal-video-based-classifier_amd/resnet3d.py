@@ -67,6 +67,13 @@ class ResNet3d(torch.nn.Module):
         # LDS ring depth of the implicit convolutions per res stage ("s2" .. "s5" -> 2 or 3;
         # vc_conv3d_gemm_bf16_ring), absent = automatic by grid size (bit-identical for any setting)
         self.conv_ring = {}
+        # per-convolution overrides {"conv_a.s4": (ring, tile), ...} of vc_conv3d_gemm_bf16_cfg (tile 0 auto,
+        # 1 = 64 x 128, 2 = 128 x 128; ring 0 auto, 2, 3, 4); bit-identical for any setting
+        self.conv_cfg = {}
+
+    def _conv_kw(self, op: str, s: int) -> dict:
+        ring, tile = self.conv_cfg.get(op, (self.conv_ring.get(f"s{s + 2}", 0), 0))
+        return dict(ring=ring, tile=tile)
 
     def state_dict(self, *a, **k):
         return OrderedDict((n, self.params[n.replace(".", "__")].detach()) for n in self._names)
@@ -312,7 +319,7 @@ class ResNet3d(torch.nn.Module):
             if self._graphs is None:
                 self._graphs = GraphReplay()
             key = (video.data_ptr(), tuple(video.shape), tuple(video.stride()), video.dtype, self.concurrent_streams, None if self.split_sizes is None else tuple(self.split_sizes),
-                   self.implicit_conv, tuple(sorted(self.conv_ring.items())),
+                   self.implicit_conv, tuple(sorted(self.conv_ring.items())), tuple(sorted(self.conv_cfg.items())),
                    str(video.device), self._weights_version())
             return self._graphs.run(key, video, self._forward_eager, keep=lambda: (self._packed, tuple(self._ws_used)))
         return self._forward_eager(video)
@@ -397,7 +404,7 @@ class ResNet3d(torch.nn.Module):
                         ops.gemm(xin, blk["b1"][0], blk["b1"][1], "bias", act["sc"], m=rows(g), flop=fl, op=f"branch1.s{s + 2}")
                     elif self.implicit_conv and cin % 64 == 0:
                         ops.conv3d_gemm(xin, B, gi, cin, (1, 1, 1), stride, (0, 0, 0), blk["b1"][0], blk["b1"][1], "bias",
-                                        act["sc"], flop=fl, op=f"branch1.s{s + 2}", ring=self.conv_ring.get(f"s{s + 2}", 0))
+                                        act["sc"], flop=fl, op=f"branch1.s{s + 2}", **self._conv_kw(f"branch1.s{s + 2}", s))
                     else:
                         A = col(rows(g), cin)
                         tm("conv3d_im2col_kernel", "im2col", (vol(gi) + vol(g)) * cin * 2, "byte", ops.conv3d_im2col,
@@ -411,12 +418,13 @@ class ResNet3d(torch.nn.Module):
                 if tuple(ka) == (1, 1, 1) and self.implicit_conv and inner % 128 and inner % 64 == 0 and cin % 64 == 0:
                     # 64 output channels: the 256 x 64 implicit-GEMM tile (no MFMAs on the zero-padded channels)
                     ops.conv3d_gemm(xin, B, gi, cin, ka, (1, 1, 1), (0, 0, 0), blk["a"][0], blk["a"][1], "bias_relu",
-                                    act["a"], flop=fl, op=f"conv_a.s{s + 2}", n=inner, ring=self.conv_ring.get(f"s{s + 2}", 0))
+                                    act["a"], flop=fl, op=f"conv_a.s{s + 2}", n=inner, **self._conv_kw(f"conv_a.s{s + 2}", s))
                 elif tuple(ka) == (1, 1, 1):
                     ops.gemm(xin, blk["a"][0], blk["a"][1], "bias_relu", act["a"], m=rows(gi), flop=fl, op=f"conv_a.s{s + 2}")
                 elif self.implicit_conv and cin % 64 == 0:
                     ops.conv3d_gemm(xin, B, gi, cin, ka, (1, 1, 1), tuple(k // 2 for k in ka), blk["a"][0], blk["a"][1],
-                                    "bias_relu", act["a"], flop=fl, op=f"conv_a.s{s + 2}", n=_ru(inner, 64), ring=self.conv_ring.get(f"s{s + 2}", 0))
+                                    "bias_relu", act["a"], flop=fl, op=f"conv_a.s{s + 2}", n=_ru(inner, 64),
+                                    **self._conv_kw(f"conv_a.s{s + 2}", s))
                 else:
                     A = col(rows(gi), ka[0] * cin)
                     tm("conv3d_im2col_kernel", "im2col", vol(gi) * cin * 2 * (1 + ka[0]), "byte", ops.conv3d_im2col,
@@ -426,7 +434,7 @@ class ResNet3d(torch.nn.Module):
                 if self.implicit_conv and inner % 64 == 0:
                     ops.conv3d_gemm(act["a"], B, gi, inner, (1, 3, 3), stride, (0, 1, 1), blk["b"][0], blk["b"][1],
                                     "bias_relu", act["b"], flop=2.0 * vol(g) * inner * inner * 9, op=f"conv_b.s{s + 2}",
-                                    n=_ru(inner, 64), ring=self.conv_ring.get(f"s{s + 2}", 0))
+                                    n=_ru(inner, 64), **self._conv_kw(f"conv_b.s{s + 2}", s))
                 else:
                     A = col(rows(g), 9 * inner)
                     tm("conv3d_im2col_kernel", "im2col", (vol(gi) + 9 * vol(g)) * inner * 2, "byte", ops.conv3d_im2col,

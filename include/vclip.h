@@ -342,6 +342,15 @@ int vc_conv3d_gemm_bf16_ring(const uint16_t* x, int64_t ldx, int64_t B, int64_t 
                              const int* kernel, const int* stride, const int* pad, const uint16_t* zero_row,
                              const uint16_t* Wt, int64_t ldw, int64_t N, const float* bias, int epilogue, void* out,
                              int64_t ldo, const void* aux, int64_t ldaux, int ring, hipStream_t stream);
+/* The same with the tile chosen by the caller too (a tuning entry): tile 0 = automatic (what
+ * vc_conv3d_gemm_bf16 runs: 256 x 64 for N % 128 != 0, 64 x 128 when 128 x 128 tiles would be fewer
+ * than the CUs, else 128 x 128), 1 = 64 x 128, 2 = 128 x 128 (N % 128 == 0, bias / bias_relu for
+ * tile 1); ring 0, 2, 3 or 4 (4: one workgroup per CU; 3 on 256 x 64 tiles).  Bit-identical for every
+ * tile and ring. */
+int vc_conv3d_gemm_bf16_cfg(const uint16_t* x, int64_t ldx, int64_t B, int64_t T, int64_t H, int64_t W, int64_t C,
+                            const int* kernel, const int* stride, const int* pad, const uint16_t* zero_row,
+                            const uint16_t* Wt, int64_t ldw, int64_t N, const float* bias, int epilogue, void* out,
+                            int64_t ldo, const void* aux, int64_t ldaux, int ring, int tile, hipStream_t stream);
 
 /* The stem Conv3d (3 input channels, kernel (kt, kh, kw <= 8), even w stride) as an implicit GEMM:
  * vc_conv3d_stem_pack writes the f32 [B][C][T][H][W] clip (C <= 4) as zero-padded channels-last
