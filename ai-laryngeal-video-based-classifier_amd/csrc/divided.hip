@@ -128,25 +128,25 @@ __global__ void __launch_bounds__(256) temporal_attn_lds_kernel(const uint16_t* 
     const int64_t row0 = b * (1 + (int64_t)P * T) + 1 + p * T;
     const int rw = 3 * H * 8;  // 16-byte pieces per staged row
     uint4* lds = reinterpret_cast<uint4*>(smem);
-    for (int i = threadIdx.x; i < T * rw; i += 256) {
+    for (int i = threadIdx.x; i < T * rw; i += blockDim.x) {
         const int t = i / rw, j = i - t * rw;
         lds[i] = reinterpret_cast<const uint4*>(qkv + (row0 + t) * ld)[j];
     }
     __syncthreads();
     const int hf = threadIdx.x & 1;
-    for (int pair = threadIdx.x >> 1; pair < T * H; pair += 128) {  // uniform trip count per lane pair
+    // the block is sized to one lane pair per (frame, head) where it can be (vc_temporal_attention):
+    // TimeSformer-B T x H = 96 pairs on 192 threads instead of 96 of 256 lanes busy
+    for (int pair = threadIdx.x >> 1; pair < T * H; pair += blockDim.x >> 1) {  // uniform trip count per lane pair
         const int t = pair / H, hh = pair - t * H;
         const uint4* qp = lds + t * rw + hh * 8 + hf * 4;
-        float q[32];
+        // QK^T on the packed bf16 pairs (v_dot2c_f32_bf16: two exact bf16 products into the f32 sum per
+        // instruction, no bf16 -> f32 unpacking of q and k: round 5, 2 instead of ~5 VALU per product
+        // pair); the scale c applies to the finished dot
+        unsigned qw[16];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint4 u = qp[j];
-            const unsigned w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                q[8 * j + 2 * e] = bf2f((unsigned short)(w[e] & 0xffff)) * c;
-                q[8 * j + 2 * e + 1] = bf2f((unsigned short)(w[e] >> 16)) * c;
-            }
+            qw[4 * j] = u.x; qw[4 * j + 1] = u.y; qw[4 * j + 2] = u.z; qw[4 * j + 3] = u.w;
         }
         float s[TMAX];
         float m = -INFINITY;
@@ -158,14 +158,13 @@ __global__ void __launch_bounds__(256) temporal_attn_lds_kernel(const uint16_t* 
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const uint4 u = kp[j];
-                    const unsigned w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        a += q[8 * j + 2 * e] * bf2f((unsigned short)(w[e] & 0xffff));
-                        a += q[8 * j + 2 * e + 1] * bf2f((unsigned short)(w[e] >> 16));
-                    }
+                    a = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(v2bf, qw[4 * j]), __builtin_bit_cast(v2bf, u.x), a, false);
+                    a = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(v2bf, qw[4 * j + 1]), __builtin_bit_cast(v2bf, u.y), a, false);
+                    a = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(v2bf, qw[4 * j + 2]), __builtin_bit_cast(v2bf, u.z), a, false);
+                    a = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(v2bf, qw[4 * j + 3]), __builtin_bit_cast(v2bf, u.w), a, false);
                 }
                 a += __shfl_xor(a, 1, 64);
+                a *= c;
                 s[k] = a;
                 m = fmaxf(m, a);
             }
@@ -335,10 +334,13 @@ int vc_temporal_attention(const uint16_t* qkv, int64_t ld, int64_t B, int64_t P,
     const int64_t lds = T * 3 * H * 64 * 2;  // one patch's q|k|v rows
     if (T <= 16 && lds <= 64 * 1024 && B * P < (1LL << 31)) {
         const unsigned nwg = (unsigned)(B * P);
+        // one lane pair per (frame, head), whole waves, at most 256 threads (TimeSformer-B: 192)
+        const int64_t want = (2 * T * H + 63) / 64 * 64;
+        const unsigned nt = (unsigned)(want < 256 ? want : 256);
         if (T <= 8)
-            temporal_attn_lds_kernel<8><<<nwg, 256, lds, stream>>>(qkv, ld, (int)P, (int)T, (int)H, c, q_prescaled, out, ldo);
+            temporal_attn_lds_kernel<8><<<nwg, nt, lds, stream>>>(qkv, ld, (int)P, (int)T, (int)H, c, q_prescaled, out, ldo);
         else
-            temporal_attn_lds_kernel<16><<<nwg, 256, lds, stream>>>(qkv, ld, (int)P, (int)T, (int)H, c, q_prescaled, out, ldo);
+            temporal_attn_lds_kernel<16><<<nwg, nt, lds, stream>>>(qkv, ld, (int)P, (int)T, (int)H, c, q_prescaled, out, ldo);
     } else if (T <= 8)
         temporal_attn_kernel<8><<<nb, 256, 0, stream>>>(qkv, ld, nq, (int)P, (int)T, (int)H, c, q_prescaled, out, ldo);
     else if (T <= 16)
