@@ -2166,6 +2166,7 @@ conv_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx, ConvGeomG g, const
     // than a plain GEMM of the same shape, tools/conv_vs_gemm.py).  MODE 0: channel block c0 of tap
     // (it, ih, iw); MODE 1: (kt, kh) segment 2t as (sa_t, sa_h), 2t + 1 derived from it
     int s_c0 = 0, s_iw = 0, s_ih = 0, s_it = 0;
+    int64_t s_toff = 0;  // MODE 0: element offset of (s_it, s_ih, s_iw, s_c0) from a row's tap-(0, 0, 0) position
     auto stage = [&](int t, int slot) {
         const uint32_t s = lds0 + slot * SLOT;
         const int k0 = t * 64;
@@ -2189,17 +2190,17 @@ conv_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx, ConvGeomG g, const
             s_ih = ih1 + 1;
             if (s_ih == g.kh) { s_ih = 0; ++s_it; }
         } else {
-            const int64_t toff = (((int64_t)s_it * g.Hin + s_ih) * g.Win + s_iw) * ldx + s_c0;  // wave-uniform
 #pragma unroll
             for (int i = 0; i < AL; ++i) {
                 const int ti = rt[i] + s_it, hi = rh[i] + s_ih, wi = rw[i] + s_iw;
                 const bool ok = rok[i] && (unsigned)ti < (unsigned)g.Tin && (unsigned)hi < (unsigned)g.Hin &&
                                 (unsigned)wi < (unsigned)g.Win;
-                const uint16_t* src = ok ? X + (roff[i] + toff) : zrow + rch[i];
+                const uint16_t* src = ok ? X + (roff[i] + s_toff) : zrow + rch[i];
                 glds16(src, __builtin_amdgcn_readfirstlane(s + (wave * (BM / 8) + i * 8) * 128));
             }
             s_c0 += 64;
-            if (s_c0 == g.C) {
+            s_toff += 64;
+            if (s_c0 == g.C) {  // next tap: its offset recomputed once per C / 64 k-tiles
                 s_c0 = 0;
                 if (++s_iw == g.kw) {
                     s_iw = 0;
@@ -2208,6 +2209,7 @@ conv_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx, ConvGeomG g, const
                         ++s_it;
                     }
                 }
+                s_toff = (((int64_t)s_it * g.Hin + s_ih) * g.Win + s_iw) * ldx;
             }
         }
 #pragma unroll
