@@ -2711,7 +2711,14 @@ extern "C" int vc_conv3d_gemm_bf16_cfg(const uint16_t* x, int64_t ldx, int64_t B
     // ring 0 (automatic): a 3-deep ring when the grid has fewer tiles than two per CU (the workgroups
     // are few, so each one's DMA latency is exposed; ResNet3D res4 / res5 at B = 4: +1.1 / +1.5 % of
     // the forward each), else 2 (res2 / res3: -3.7 / -2.5 %), tools/ab_resnet3d_ring.py, round 4
-    auto pick_ring = [&](int64_t tiles) { return ring ? ring : (tiles < 2 * (int64_t)num_cus() ? 3 : 2); };
+    // (round 5: a 3-deep ring puts 128 x 128 tiles at ONE workgroup per CU (96 KiB of LDS), so there it pays
+    // only when the tiles fit one round of CUs: res3 conv_b, 392 tiles, ring 2 +1.6 % of the forward,
+    // tools/ab_resnet3d_conv.py; 64 x 128 and 256 x 64 tiles keep two workgroups per CU at ring 3)
+    auto pick_ring = [&](int64_t tiles, bool big = false) {
+        if (ring) return ring;
+        const int64_t cus = num_cus();
+        return (big ? tiles <= cus : tiles < 2 * cus) ? 3 : 2;
+    };
     if (!x || !kernel || !stride || !pad || !zero_row || !Wt || !bias || !out)
         return fail(VC_ERR_INVALID_ARG, "vc_conv3d_gemm_bf16: null pointer");
     for (int d = 0; d < 3; ++d)
@@ -2764,7 +2771,7 @@ extern "C" int vc_conv3d_gemm_bf16_cfg(const uint16_t* x, int64_t ldx, int64_t B
         return launch_conv<64, 128, 2, 4, VC_EPI_BIAS_BF16>(x, ldx, g, zero_row, Wt, ldw, nbm64, nbn, (int)K, bias, out,
                                                              ldo, auxf, ldaux, stream, ring);
     }
-    ring = pick_ring((int64_t)nbm * nbn);
+    ring = pick_ring((int64_t)nbm * nbn, true);
     switch (epilogue) {
         case VC_EPI_BIAS_BF16:
             if (ldo % 8) break;

@@ -662,7 +662,8 @@ def conv3d_gemm(x: torch.Tensor, B: int, grid, C: int, kernel, stride, pad, w: t
             tl = "64, 128, 2, 4" if small else "128, 128, 2, 4"
         nt = (((M + 127) // 128) * (N // 128) if tl == "128, 128, 2, 4" else ((M + 63) // 64) * (N // 128)
               if tl == "64, 128, 2, 4" else ((M + 255) // 256) * (N // 64))
-        st = ring if ring else (3 if nt < 2 * _num_cus(x.device) else 2)  # csrc/gemm.hip pick_ring
+        cus = _num_cus(x.device)  # csrc/gemm.hip pick_ring (128 x 128: 3-deep only within one round of CUs)
+        st = ring if ring else (3 if (nt <= cus if tl == "128, 128, 2, 4" else nt < 2 * cus) else 2)
         if st == 4 and rt != 128:
             st = 3
         label = f"conv_gemm_kernel<{tl}, {e}, {st}, 0>"

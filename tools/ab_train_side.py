@@ -2,6 +2,8 @@
 over TrainEngine settings, in one process; default arms: weight / bias gradients on a side stream
 (side_wgrad) vs one stream.
   python tools/ab_train_side.py ['{"side_wgrad": false}' '{"side_wgrad": true, "wgrad_max_splits": 4}' ...]
+  (arm key "_chain_priority": -1 runs the step, i.e. the data-gradient chain, on a high-priority HIP stream, so the
+  side streams' weight gradients yield to it)
                                     [--B 4] [--rounds 6] [--steps 5]"""
 import argparse
 import json
@@ -41,16 +43,30 @@ def step():
 step()
 eng = model._engine
 arms = [json.loads(x) for x in a.arms]
+hp = torch.cuda.Stream(device=dev, priority=-1)
+print("stream priority range", torch.cuda.Stream.priority_range(), "hp", hp.priority, flush=True)
+
+
+def run(arm):
+    if arm.get("_chain_priority", 0) < 0:
+        hp.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(hp):
+            step()
+        torch.cuda.current_stream(dev).wait_stream(hp)
+    else:
+        step()
+
 res = [[] for _ in arms]
 for r in range(a.rounds):
     for i in (range(len(arms)) if r % 2 == 0 else reversed(range(len(arms)))):
         for k, v in arms[i].items():
-            setattr(eng, k, v)
-        step()
+            if not k.startswith("_"):
+                setattr(eng, k, v)
+        run(arms[i])
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(a.steps):
-            step()
+            run(arms[i])
         torch.cuda.synchronize()
         res[i].append((time.perf_counter() - t0) / a.steps * 1e3)
 for arm, t in zip(a.arms, res):
