@@ -157,6 +157,25 @@ def test_colsum(dtype, R, N):
     np.testing.assert_allclose(out.cpu().double().numpy(), ref.numpy(), rtol=1e-5, atol=1e-4 * math.sqrt(R))
 
 
+@pytest.mark.parametrize("R,N", [(12800, 3072), (12800, 2304), (1000, 520)])
+def test_colsum_bf16_vector_pass_bit_identical(R, N):
+    """The 16-B-per-lane bf16 first pass (aligned rows, N % 8 == 0) keeps the 2-B pass's summation
+    order per column: the same input through a row stride that is not a multiple of 8 (the 2-B pass)
+    gives the same bits."""
+    O = ops()
+    g = torch.Generator().manual_seed(R * 7 + N)
+    x = torch.randn(R, N, generator=g).to(torch.bfloat16)
+    xa = x.to(DEV)
+    xs = torch.zeros(R, N + 1, dtype=torch.bfloat16, device=DEV)
+    xs[:, :N] = xa
+    outs = []
+    for src in (xa, xs[:, :N]):
+        out = torch.zeros(N, device=DEV)
+        O.colsum(src, out, torch.empty(256 * N, device=DEV), nscaled=N // 3, scale=0.5)
+        outs.append(out.cpu())
+    assert torch.equal(outs[0], outs[1])
+
+
 # ------------------------------------------------------------------------- weight gradient GEMM
 @pytest.mark.parametrize("M,N1,N2,split", [(256, 128, 128, False), (12800, 768, 768, True), (4096, 2304, 768, True),
                                            (12800, 768, 3072, True), (3200, 3072, 768, False), (6272, 768, 1536, True),
