@@ -182,6 +182,28 @@ def test_conv3d_implicit_gemm_bit_exact(kernel, stride, pad, C, epi):
     got3 = torch.full((Mp, N), 7.0, dtype=torch.bfloat16, device=DEV)
     O.conv3d_gemm(xd, B, (T, H, W), C, kernel, stride, pad, w, b, epi, got3, aux=aux, n=64 if n64 else None, ring=3)
     assert torch.equal(got3[:M, :nc], want[:M, :nc])
+    # every tile / ring vc_conv3d_gemm_bf16_cfg accepts here (64 x 128 takes bias / bias_relu only; ring 4
+    # is one workgroup per CU, 3 on the 256 x 64 tile): bit-identical too
+    tiles = (0,) if n64 else ((0, 1, 2) if epi != "bias_resid_relu" else (0, 2))
+    for tile in tiles:
+        for ring in (0, 2, 3, 4):
+            gt = torch.full((Mp, N), 7.0, dtype=torch.bfloat16, device=DEV)
+            O.conv3d_gemm(xd, B, (T, H, W), C, kernel, stride, pad, w, b, epi, gt, aux=aux, n=64 if n64 else None,
+                          ring=ring, tile=tile)
+            assert torch.equal(gt[:M, :nc], want[:M, :nc]), (tile, ring)
+
+
+def test_resnet3d_split_sizes_and_conv_cfg_bit_identical():
+    """Uneven stream parts (model.split_sizes) and per-convolution tile / ring overrides (model.conv_cfg)
+    change only the schedule: logits bit-identical to the one-stream default."""
+    video = torch.from_numpy(make_synthetic_video(3, 8, 224, seed=9)).to(DEV)
+    m = _model()
+    ref = m(video).clone()
+    m.concurrent_streams, m.split_sizes = 2, [2, 1]
+    assert torch.equal(m(video), ref)
+    m.concurrent_streams, m.split_sizes = 1, None
+    m.conv_cfg = {"conv_a.s4": (4, 1), "conv_b.s4": (2, 2), "conv_b.s3": (3, 2), "conv_a.s5": (3, 1)}
+    assert torch.equal(m(video), ref)
 
 
 def test_resnet3d_implicit_conv_matches_im2col_path():

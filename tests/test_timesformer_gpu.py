@@ -178,6 +178,12 @@ def test_timesformer_two_stream_split_bit_exact():
     m.concurrent_streams = 2
     two = m.forward_logits(pix).clone()
     assert torch.equal(one, two)
+    # uneven parts (model.split_sizes) and a per-GEMM tile override (model.gemm_cfg): the same bits
+    m.split_sizes = [4, 1]
+    assert torch.equal(m.forward_logits(pix), one)
+    m.concurrent_streams, m.split_sizes = 1, None
+    m.gemm_cfg = {"fc1": 8, "fc2": 24}
+    assert torch.equal(m.forward_logits(pix), one)
 
 
 @pytest.mark.parametrize("streams", [1, 2])
