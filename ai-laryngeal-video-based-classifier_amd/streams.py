@@ -31,6 +31,17 @@ def serial() -> bool:
     return _SERIAL[0]
 
 
+def split_bounds(B: int, ns: int, sizes=None) -> list:
+    """Row bounds [0, b1, ..., B] of `ns` contiguous batch parts: `sizes` (clips per part, summing to B)
+    or, when None, as even as possible (B * i // ns).  Raises ValueError on sizes that do not fit."""
+    if sizes is None:
+        return [B * i // ns for i in range(ns + 1)]
+    sizes = [int(v) for v in sizes]
+    if len(sizes) != ns or sum(sizes) != B or min(sizes) < 1:
+        raise ValueError(f"split_sizes {sizes} must be {ns} positive part sizes summing to B={B}")
+    return [sum(sizes[:i]) for i in range(ns + 1)]
+
+
 def run_split(owner, x: torch.Tensor, ns: int, part_fn, num_labels: int, prepare=None) -> torch.Tensor:
     """part_fn(x_part, part_index, out=logits_rows) for each of `ns` contiguous batch parts, part i on
     owner._streams[i]; returns the [B, num_labels] logits (a buffer of `owner`, reused per call).
@@ -51,12 +62,7 @@ def run_split(owner, x: torch.Tensor, ns: int, part_fn, num_labels: int, prepare
         owner._split_out[key] = torch.zeros(B, num_labels, dtype=torch.float32, device=dev)
     logits = owner._split_out[key]
     cur = torch.cuda.current_stream(dev)
-    bounds = [B * i // ns for i in range(ns + 1)]
-    sizes = getattr(owner, "split_sizes", None)  # clips per part (A/B hook); None = as even as possible
-    if sizes is not None:
-        if len(sizes) != ns or sum(sizes) != B or min(sizes) < 1:
-            raise ValueError(f"split_sizes {sizes} must be {ns} positive part sizes summing to B={B}")
-        bounds = [sum(sizes[:i]) for i in range(ns + 1)]
+    bounds = split_bounds(B, ns, getattr(owner, "split_sizes", None))  # clips per part; None = as even as possible
     if _SERIAL[0]:
         for i in range(ns):
             part_fn(x[bounds[i]:bounds[i + 1]], i, out=logits[bounds[i]:bounds[i + 1]])

@@ -446,12 +446,8 @@ class VivitForVideoClassification(torch.nn.Module):
         # the packed weights every part reads are built on the caller's stream before the fork
         # (streams.run_split's rule): packed inside part 0 they would race parts 1..n-1
         self._pack(dev)
-        bounds = [B * i // ns for i in range(ns + 1)]
-        sizes = self.split_sizes if self.split_sizes is not None else SPLIT_DEFAULT.get((B, ns))
-        if sizes is not None:
-            if len(sizes) != ns or sum(sizes) != B or min(sizes) < 1:
-                raise ValueError(f"split_sizes {sizes} must be {ns} positive part sizes summing to B={B}")
-            bounds = [sum(sizes[:i]) for i in range(ns + 1)]
+        bounds = streams.split_bounds(B, ns, self.split_sizes if self.split_sizes is not None
+                                      else SPLIT_DEFAULT.get((B, ns)))
         self.last_split = [bounds[i + 1] - bounds[i] for i in range(ns)]
         if streams.serial():  # instrumentation: the parts one after the other on the caller's stream
             for i in range(ns):
