@@ -105,6 +105,7 @@ SIGNATURES = {
                           c_p, c_i64, c_p], c_int),
     "vc_colsum": ([c_p, c_int, c_i64, c_i64, c_i64, c_i64, c_f, c_p, c_p, c_i64, c_p], c_int),
     "vc_wgrad_bf16": ([c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_p, c_i64, c_p, c_i64, c_p], c_int),
+    "vc_wgrad_pick": ([c_i64, c_i64, c_i64, c_i64], c_int),
     "vc_cls_head_bwd": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_p, c_i64, c_p, c_p, c_i64, c_p, c_i64, c_p,
                          c_p, c_p, c_p, c_p], c_int),
     "vc_embed_bwd": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_i64, c_p], c_int),

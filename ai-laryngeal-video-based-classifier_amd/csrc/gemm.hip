@@ -594,166 +594,6 @@ gemm_bf16_big_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t
 }
 
 // ---------------------------------------------------------------------------------
-// 160x256 ping-pong kernel (cfg 17) -- the cfg 8 schedule on 160-row tiles, for the grids that 256-row
-// tiles quantise badly at the ViViT-B two-stream split (4 clips = 12800 padded rows = 80 x 160): fc2 /
-// o_proj 150 tiles of 256 x 256 fill 150 of 256 CUs for one tile-time, 240 tiles of 160 x 256 fill 240
-// for 0.625 of it; fc1 600 -> 960 tiles (3 rounds of 1.0 -> 4 of 0.625), q|k|v 450 -> 720 (2 -> 3 x 0.625).
-//   * 8 waves as 2 (rows) x 4 (cols), wave tile 80 x 64 = 5 x 4 blocks of v_mfma_f32_16x16x32;
-//     group 0 = waves 0-3 (tile rows 0-79), group 1 = waves 4-7 (rows 80-159), one barrier behind;
-//   * phases split by COLUMNS (10 MFMAs each, balanced): a(u) reads the wave's 5 A fragments and W
-//     blocks 0-1, stages W(u+2), MFMAs on column blocks 0-1; b(u) reads W blocks 2-3 (the A fragments
-//     stay in registers), stages A(u+3), retires K-half u+1, MFMAs on column blocks 2-3;
-//   * ring of 4 K-half slots (A 160 x 32 then W 256 x 32, 64-B rows, swz64): 104 KiB.  A is 10 LDS-DMA
-//     pieces per K-half: waves 0-4 stage two each, waves 5-7 none, so their counted waits differ
-//     (vmcnt(6) / vmcnt(2): the DMAs younger than W(u+1) are A(u+2), W(u+2), A(u+3) vs W(u+2) alone);
-//   * WAR: W(u+2) overwrites W(u-2), last read in b(u-2), A(u+3) overwrites A(u-1), last read in
-//     a(u-1): both >= 3 barriers after the lagging group's reads completed.
-// Same K order and MFMA chain per output as every other config: bit-identical.  Epilogue: store_tile16
-// (every epilogue, incl. the f32 residual).
-// ---------------------------------------------------------------------------------
-template <int EPI, int ET = VC_ELEM_BF16>
-__global__ void __launch_bounds__(512, 1)
-gemm_pp160_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw, int nbm,
-                  int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
-                  const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride, int64_t goff) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int BM = 160, BN = 256, BKH = 32, NS = 4;
-    constexpr int SLOT = (BM + BN) * 64;  // 26 KiB
-    constexpr int TM = 80, TN = 64, MI = 5, NI = 4;
-
-    const int nwg = nbm * nbn;
-    const int bid = blockIdx.x;
-    const int xcd = bid & 7, xq = nwg >> 3, rr = nwg & 7;
-    const int wgid = (xcd < rr ? xcd * (xq + 1) : rr * (xq + 1) + (xcd - rr) * xq) + (bid >> 3);
-    const int tm = wgid / nbn, tn = wgid % nbn;
-    const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 2, wn = wave & 3;
-    const int c16 = lane & 15, q = lane >> 4;
-    float4 bq[NI];  // this lane's bias columns, loaded now (their latency hides under the main loop)
-    load_bias16<NI>(bias, n0 + wn * TN, q, bq);
-    const bool astager = wave < 5;  // waves 0-4 stage A rows [32w, 32w + 32)
-
-    // staging sources (byte offsets from the wave-uniform panel bases)
-    const int srow = wave * 32 + (lane >> 2);
-    const int arow = astager ? srow : 0;
-    const uint32_t aoff0 = (uint32_t)(arow * lda + swz64(arow, lane & 3) * 8) * 2;
-    const uint32_t aoff1 = (uint32_t)((arow + 16) * lda + swz64(arow + 16, lane & 3) * 8) * 2;
-    const uint32_t woff0 = (uint32_t)(srow * ldw + swz64(srow, lane & 3) * 8) * 2;
-    const uint32_t woff1 = (uint32_t)((srow + 16) * ldw + swz64(srow + 16, lane & 3) * 8) * 2;
-    const uint16_t* Ap = A + m0 * lda;
-    const uint16_t* Wp = W + n0 * ldw;
-    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
-    auto stage_a = [&](int u) __attribute__((always_inline)) {
-        const uint32_t s = lds0 + (u & (NS - 1)) * SLOT + wave * 32 * 64;
-        glds16s(Ap + u * BKH, aoff0, __builtin_amdgcn_readfirstlane(s));
-        glds16s(Ap + u * BKH, aoff1, __builtin_amdgcn_readfirstlane(s + 16 * 64));
-    };
-    auto stage_w = [&](int u) __attribute__((always_inline)) {
-        const uint32_t s = lds0 + (u & (NS - 1)) * SLOT + BM * 64 + wave * 32 * 64;
-        glds16s(Wp + u * BKH, woff0, __builtin_amdgcn_readfirstlane(s));
-        glds16s(Wp + u * BKH, woff1, __builtin_amdgcn_readfirstlane(s + 16 * 64));
-    };
-    auto read_a = [&](int u, v8s (&fa)[MI]) __attribute__((always_inline)) {
-        const char* At = smem + (u & (NS - 1)) * SLOT;
-#pragma unroll
-        for (int i = 0; i < MI; ++i) fa[i] = lds_frag64(At, wm * TM + i * 16 + c16, q);
-    };
-    auto read_w = [&](int u, int j0, v8s (&fw)[2]) __attribute__((always_inline)) {
-        const char* Wt = smem + (u & (NS - 1)) * SLOT + BM * 64;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) fw[j] = lds_frag64(Wt, wn * TN + (j0 + j) * 16 + c16, q);
-    };
-
-    v4f acc[MI][NI];
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-
-    auto mma = [&](auto J0, const v8s (&fa)[MI], const v8s (&fw)[2]) __attribute__((always_inline)) {
-        constexpr int j0 = decltype(J0)::value;
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's fragment reads
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j0 + j] = mfma16x32<ET>(fw[j], fa[i], acc[i][j0 + j]);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    using C0 = std::integral_constant<int, 0>;
-    using C2 = std::integral_constant<int, 2>;
-
-    const int nk = K / BKH;  // even, >= 4
-    v8s fa[MI], fw[2];
-    auto phase_a = [&](int u) __attribute__((always_inline)) {
-        read_a(u, fa);
-        read_w(u, 0, fw);
-        if (u + 2 < nk) stage_w(u + 2);
-        __builtin_amdgcn_sched_barrier(0);
-        mma(C0{}, fa, fw);
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto phase_b = [&](int u) __attribute__((always_inline)) {
-        read_w(u, 2, fw);
-        if (astager) {
-            if (u + 3 < nk) {
-                stage_a(u + 3);
-                wait_vm<6>();
-            } else if (u + 2 < nk) {
-                wait_vm<4>();
-            } else {
-                wait_vm<0>();
-            }
-        } else {
-            if (u + 2 < nk) wait_vm<2>();
-            else wait_vm<0>();
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        mma(C2{}, fa, fw);
-        // the lagging group skips its last barrier: both groups then pass the same number
-        if (u + 1 < nk || wm == 0) __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-    };
-
-    // prologue: A0 W0 A1 W1 A2 in flight (waves 5-7: W0 W1), retire K-half 0, publish; group 1 one
-    // barrier behind
-    if (astager) {
-        stage_a(0);
-        stage_w(0);
-        stage_a(1);
-        stage_w(1);
-        stage_a(2);
-        wait_vm<6>();
-    } else {
-        stage_w(0);
-        stage_w(1);
-        wait_vm<2>();
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    if (wm == 1) __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-
-    for (int u = 0; u < nk; ++u) {
-        phase_a(u);
-        phase_b(u);
-    }
-    store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bq, out, ldo, aux, ldaux, G, gstride,
-                                  goff);
-}
-
-// ---------------------------------------------------------------------------------
 // Streaming 1x1x1-conv kernel for the ResNet3D conv_c (cfg 20; round 5): out = relu(A.W^T + b + res),
 // bf16 residual, K in {64, 128}.  At K = 64 / 128 the launch is HBM-bound (res2: 461 MB per launch for
 // 26 GFLOP): the 128 x 128 two-workgroups-per-CU kernel loaded, computed and stored each tile in turn
@@ -1213,24 +1053,14 @@ gemm_bf16_persist_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint
 // Epilogue: the shared store_tile16 (all epilogues); a workgroup per output tile with the
 // bijective XCD remap, consecutive tiles of one XCD walking the N tiles of one A row panel.
 // ---------------------------------------------------------------------------------
-// ABL (timing-only ablations, wrong results): 1 (cfg 11) every K-half is staged from k = 0..3
-// (operands L2-resident): the kernel's rate with the load side taken out; 2 (cfg 12) no epilogue
-// stores (the accumulators kept live by an empty asm): the cost of the output write; 3 (cfg 13) the
-// same bytes stored as full 128-B row segments per 8 lanes (values scrambled): the store pattern's cost.
-// BN = 192 (cfg 24): the same schedule on 256 x 192 tiles (wave tile 128 x 48, 4 x 3 blocks, 12 MFMAs per
-// phase), for N = 768 outputs at the two-stream split's 12800 rows: 200 tiles fill one round of the
-// 256 CUs where 256 x 256 tiles leave 106 of them idle (150 tiles).  The W ring slot keeps its 256
-// rows so every wave issues the same LDS-DMAs (the counted vmcnt stays uniform): waves 6-7 restage
-// rows 128-191 into the unused rows 192-255 (in bounds, never read).
-template <int EPI, int ET = VC_ELEM_BF16, int ABL = 0, int BN = 256>
+template <int EPI, int ET = VC_ELEM_BF16>
 __global__ void __launch_bounds__(512, 1)
 gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw, int nbm,
                int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
                const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride, int64_t goff, int nka) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    static_assert(BN == 256 || (BN == 192 && (ABL == 0 || ABL == 4)), "pp tile width");
-    constexpr int BM = 256, BKH = 32, NS = 4;
-    constexpr int SLOT = (BM + 256) * 64;  // 32 KiB
+    constexpr int BM = 256, BN = 256, BKH = 32, NS = 4;
+    constexpr int SLOT = (BM + BN) * 64;  // 32 KiB
     constexpr int TM = 128, TN = BN / 4, MI = 8, NI = TN / 16;
 
     const int nwg = nbm * nbn;
@@ -1251,23 +1081,21 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     const int arow = wave * 32 + (lane >> 2);
     const uint16_t* ag0 = A + (m0 + arow) * lda + swz64(arow, lane & 3) * 8;
     const uint16_t* ag1 = A + (m0 + arow + 16) * lda + swz64(arow + 16, lane & 3) * 8;
-    const int wrow = arow < BN ? arow : arow - (256 - BN);  // source row (rows >= BN of the slot: filler)
-    const uint16_t* wg0 = W + (n0 + wrow) * ldw + swz64(arow, lane & 3) * 8;
-    const uint16_t* wg1 = W + (n0 + wrow + 16) * ldw + swz64(arow + 16, lane & 3) * 8;
+    const uint16_t* wg0 = W + (n0 + arow) * ldw + swz64(arow, lane & 3) * 8;
+    const uint16_t* wg1 = W + (n0 + arow + 16) * ldw + swz64(arow + 16, lane & 3) * 8;
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
     // nka: K-halves of A; W may be longer (K <= 2 nka): A's columns wrap, so W = [W_hi | W_lo] against
     // A gives A.W_hi + A.W_lo in one accumulation chain (vc_gemm_h16_wrap, the split-weight fp16 build)
     auto stage_a = [&](int u) __attribute__((always_inline)) {
         const uint32_t s = lds0 + (u & (NS - 1)) * SLOT + wave * 32 * 64;
-        const int ku = ABL == 1 ? (u & 3) : (u < nka ? u : u - nka);
+        const int ku = u < nka ? u : u - nka;
         glds16(ag0 + ku * BKH, __builtin_amdgcn_readfirstlane(s));
         glds16(ag1 + ku * BKH, __builtin_amdgcn_readfirstlane(s + 16 * 64));
     };
     auto stage_w = [&](int u) __attribute__((always_inline)) {
         const uint32_t s = lds0 + (u & (NS - 1)) * SLOT + BM * 64 + wave * 32 * 64;
-        const int ku = ABL == 1 ? (u & 3) : u;
-        glds16(wg0 + ku * BKH, __builtin_amdgcn_readfirstlane(s));
-        glds16(wg1 + ku * BKH, __builtin_amdgcn_readfirstlane(s + 16 * 64));
+        glds16(wg0 + u * BKH, __builtin_amdgcn_readfirstlane(s));
+        glds16(wg1 + u * BKH, __builtin_amdgcn_readfirstlane(s + 16 * 64));
     };
     auto read_a = [&](int u, int i0, v8s (&fa)[4]) __attribute__((always_inline)) {
         const char* At = smem + (u & (NS - 1)) * SLOT;
@@ -1332,14 +1160,6 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
         __builtin_amdgcn_sched_barrier(0);
     };
 
-    // ABL 4 (cfg 18, diagnostics): wave 0 and wave 4 stamp s_memrealtime (100 MHz, chip-wide) and
-    // s_memtime (shader clock) at entry, after the prologue wait, after the main loop, after issuing the
-    // epilogue stores and after they drained; aux = u64 [nwg][2 waves][8], results as with cfg 8
-    unsigned long long st_r[5], st_c[2];
-    if constexpr (ABL == 4) {
-        st_r[0] = __builtin_amdgcn_s_memrealtime();
-        st_c[0] = __builtin_amdgcn_s_memtime();
-    }
     // prologue: A0 W0 A1 W1 A2 in flight, retire A0 W0, publish; group 1 falls one barrier behind
     stage_a(0);
     stage_w(0);
@@ -1348,7 +1168,6 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     stage_a(2);
     wait_vm<6>();
     __builtin_amdgcn_s_waitcnt(0xC07F);
-    if constexpr (ABL == 4) st_r[1] = __builtin_amdgcn_s_memrealtime();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -1361,389 +1180,8 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
         phase_a(u + 1, wB);
         phase_b(u + 1, wB);
     }
-    if constexpr (ABL == 4) {
-        st_r[2] = __builtin_amdgcn_s_memrealtime();
-        store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bq, out, ldo, nullptr, 0, 0, 0, 0);
-        st_r[3] = __builtin_amdgcn_s_memrealtime();
-        __builtin_amdgcn_s_waitcnt(0);
-        st_r[4] = __builtin_amdgcn_s_memrealtime();
-        st_c[1] = __builtin_amdgcn_s_memtime();
-        if ((wave & 3) == 0 && lane == 0) {
-            unsigned long long* o = reinterpret_cast<unsigned long long*>(const_cast<float*>(aux)) +
-                                    ((int64_t)wgid * 2 + (wave >> 2)) * 8;
-            o[0] = st_r[0]; o[1] = st_r[1]; o[2] = st_r[2]; o[3] = st_r[3]; o[4] = st_r[4];
-            o[5] = st_c[1] - st_c[0];
-            o[6] = (unsigned long long)xcd;
-            o[7] = (unsigned long long)bid;
-        }
-        return;
-    }
-    if constexpr (ABL == 2) {
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(acc[i][j]));
-        return;
-    }
-    if constexpr (ABL == 3 && BN == 256) {  // the same bytes as full 128-B row segments per 8 lanes (values scrambled)
-        uint16_t* o16 = reinterpret_cast<uint16_t*>(out);
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-            const v4f a0 = acc[s >> 1][(s & 1) * 2], a1 = acc[s >> 1][(s & 1) * 2 + 1];
-            uint4 v;
-            v.x = pack2bf(a0[0], a0[1]); v.y = pack2bf(a0[2], a0[3]);
-            v.z = pack2bf(a1[0], a1[1]); v.w = pack2bf(a1[2], a1[3]);
-            *reinterpret_cast<uint4*>(o16 + (m0 + wm * TM + s * 8 + (lane >> 3)) * ldo + n0 + wn * TN + (lane & 7) * 8) = v;
-        }
-        return;
-    }
     store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bq, out, ldo, aux, ldaux, G, gstride,
                                   goff);
-}
-
-// ---------------------------------------------------------------------------------
-// 256x128 ping-pong kernel (cfg 9): the cfg 8 schedule on a narrower tile, for N = 768 outputs
-// (o_proj / fc2: 300 tiles per 12800 rows instead of 150).  Waves as 4 (rows) x 2 (cols), wave
-// tile 64 x 64 (4 x 4 blocks), so one K-half is one phase of 16 MFMAs reading 4 A + 4 W
-// fragments; group 0 = waves 0-3 (tile rows 0-127), group 1 = waves 4-7, one barrier behind.
-// Ring of 6 K-half slots (A 256 x 32 + W 128 x 32 = 24 KiB each, 144 KiB): phase u stages
-// K-half u + 4 into the slot read at phase u - 2 (WAR: two phases after its last read) and
-// retires K-half u + 1 with vmcnt(9) before its first barrier (three phases' DMAs in flight).
-// ---------------------------------------------------------------------------------
-template <int EPI, int ET = VC_ELEM_BF16>
-__global__ void __launch_bounds__(512, 1)
-gemm_pp128_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw, int nbm,
-                  int nbn, int K, const float* __restrict__ bias, void* __restrict__ out, int64_t ldo,
-                  const float* __restrict__ aux, int64_t ldaux, int64_t G, int64_t gstride, int64_t goff) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int BM = 256, BN = 128, BKH = 32, NS = 6;
-    constexpr int SLOT = (BM + BN) * 64;  // 24 KiB
-    constexpr int TM = 64, TN = 64, MI = 4, NI = 4;
-
-    const int nwg = nbm * nbn;
-    const int bid = blockIdx.x;
-    const int xcd = bid & 7, xq = nwg >> 3, rr = nwg & 7;
-    const int wgid = (xcd < rr ? xcd * (xq + 1) : rr * (xq + 1) + (xcd - rr) * xq) + (bid >> 3);
-    const int tm = wgid / nbn, tn = wgid % nbn;
-    const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 1, wn = wave & 1, grp = wave >> 2;
-    const int c16 = lane & 15, q = lane >> 4;
-    float4 bq[NI];  // this lane's bias columns, loaded now (their latency hides under the main loop)
-    load_bias16<NI>(bias, n0 + wn * TN, q, bq);
-
-    // staging: wave w fills A rows [32w, 32w + 32) (two DMAs) and W rows [16w, 16w + 16) (one)
-    const int arow = wave * 32 + (lane >> 2), wrow = wave * 16 + (lane >> 2);
-    const uint16_t* ag0 = A + (m0 + arow) * lda + swz64(arow, lane & 3) * 8;
-    const uint16_t* ag1 = A + (m0 + arow + 16) * lda + swz64(arow + 16, lane & 3) * 8;
-    const uint16_t* wg0 = W + (n0 + wrow) * ldw + swz64(wrow, lane & 3) * 8;
-    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
-    auto stage = [&](int u) __attribute__((always_inline)) {
-        const uint32_t s = lds0 + (u % NS) * SLOT;
-        glds16(ag0 + u * BKH, __builtin_amdgcn_readfirstlane(s + wave * 32 * 64));
-        glds16(ag1 + u * BKH, __builtin_amdgcn_readfirstlane(s + (wave * 32 + 16) * 64));
-        glds16(wg0 + u * BKH, __builtin_amdgcn_readfirstlane(s + BM * 64 + wave * 16 * 64));
-    };
-
-    v4f acc[MI][NI];
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
-
-    const int nk = K / BKH;  // even, >= 4
-    v8s faA[4], fwA[4], faB[4], fwB[4];
-    auto phase = [&](int u, v8s (&fa)[4], v8s (&fw)[4]) __attribute__((always_inline)) {
-        const char* At = smem + (u % NS) * SLOT;
-        const char* Wt = At + BM * 64;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = lds_frag64(At, wm * TM + i * 16 + c16, q);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) fw[j] = lds_frag64(Wt, wn * TN + j * 16 + c16, q);
-        // retire K-half u + 1 (its younger DMAs: u + 2, u + 3 and, if staged now, u + 4)
-        if (u + 4 < nk) {
-            stage(u + 4);
-            wait_vm<9>();
-        } else if (u + 3 < nk) {
-            wait_vm<6>();
-        } else if (u + 2 < nk) {
-            wait_vm<3>();
-        } else {
-            wait_vm<0>();
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's fragment reads
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x32<ET>(fw[j], fa[i], acc[i][j]);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (u + 1 < nk || grp == 0) __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-    };
-
-    stage(0);
-    stage(1);
-    stage(2);
-    stage(3);
-    wait_vm<9>();
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    if (grp == 1) __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-
-    for (int u = 0; u < nk; u += 2) {
-        phase(u, faA, fwA);
-        phase(u + 1, faB, fwB);
-    }
-    store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bq, out, ldo, aux, ldaux, G, gstride,
-                                  goff);
-}
-
-// ---------------------------------------------------------------------------------
-// Persistent 256x256 ping-pong kernel (cfg 10) for the 16-bit-output epilogues (q|k|v, fc1):
-// the cfg 8 phase schedule over one continuous sequence of K-halves that runs through all the
-// tiles of a workgroup (one per CU), so the ring never drains between tiles: the next tile's first
-// K-halves are staged during the current tile's last phases, and each group's epilogue (bias from
-// LDS, activation, 16-B stores) runs while the other group's MFMAs of the tile's last (or the
-// next tile's first) phase keep its SIMDs busy.  The epilogue's NST stores per wave are younger
-// than the DMAs of the K-half retired next, so that one wait counts them (vmcnt(6 + NST)).  The
-// first K-half of a tile starts its accumulators from a zero C operand (no 128-register clear).
-// Tile order as cfg 4: in round `it` the 32 workgroups of one XCD take 32 consecutive tiles
-// (row-major, N fastest), so the XCD's L2 holds ~3.5 A row panels and the whole W of q|k|v.
-// ---------------------------------------------------------------------------------
-template <int EPI, int ET = VC_ELEM_BF16>
-__global__ void __launch_bounds__(512, 1)
-gemm_ppp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw, int nbm,
-                int nbn, int K, int N, const float* __restrict__ bias, uint16_t* __restrict__ out, int64_t ldo,
-                uint16_t* __restrict__ pre_out, int64_t ldpre) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    constexpr int BM = 256, BN = 256, BKH = 32, NS = 4;
-    constexpr int SLOT = (BM + BN) * 64;  // 32 KiB
-    constexpr int TM = 128, TN = 64, MI = 8, NI = 4;
-    constexpr bool SAVE = EPI == VC_EPI_BIAS_GELU_TANH_SAVE;
-    constexpr int NST = MI * (NI / 2) * (SAVE ? 2 : 1);  // 16-B stores per wave per tile epilogue
-    float* bias_lds = reinterpret_cast<float*>(smem + NS * SLOT);
-
-    const int ntiles = nbm * nbn;
-    const int G = gridDim.x;
-    const int b = blockIdx.x;
-    const int lane_slot = (b & 7) * (G >> 3) + (b >> 3);
-    const int mine = lane_slot < ntiles ? (ntiles - 1 - lane_slot) / G + 1 : 0;  // tiles of this workgroup
-    if (mine == 0) return;
-
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 2, wn = wave & 3;
-    const int c16 = lane & 15, q = lane >> 4;
-
-    for (int n = tid * 4; n < N; n += 512 * 4)
-        *reinterpret_cast<float4*>(bias_lds + n) = *reinterpret_cast<const float4*>(bias + n);
-    __syncthreads();
-
-    const int nk = K / BKH;  // even, >= 4
-    const int total = mine * nk;  // K-halves of this workgroup, all tiles
-    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr_of(smem));
-    const int arow = wave * 32 + (lane >> 2);
-    const int64_t aoff0 = (int64_t)arow * lda + swz64(arow, lane & 3) * 8;
-    const int64_t aoff1 = (int64_t)(arow + 16) * lda + swz64(arow + 16, lane & 3) * 8;
-    const int64_t woff0 = (int64_t)arow * ldw + swz64(arow, lane & 3) * 8;
-    const int64_t woff1 = (int64_t)(arow + 16) * ldw + swz64(arow + 16, lane & 3) * 8;
-    auto tile_origin = [&](int it, int64_t& m0, int64_t& n0) __attribute__((always_inline)) {
-        const int tile = it * G + lane_slot;
-        const int tm = tile / nbn;
-        m0 = (int64_t)tm * BM;
-        n0 = (int64_t)(tile - tm * nbn) * BN;
-    };
-    // staging cursors: the A stream runs 3 K-halves ahead of the phase being computed, the W
-    // stream 2; each walks (tile, k) in order and moves its base pointer at a tile change
-    struct Cursor {
-        int it, u;
-        const uint16_t* p;
-    };
-    auto cursor_at = [&](int U, bool is_a) __attribute__((always_inline)) {
-        Cursor c;
-        c.it = U / nk;
-        c.u = U - c.it * nk;
-        int64_t m0, n0;
-        tile_origin(c.it < mine ? c.it : mine - 1, m0, n0);
-        c.p = is_a ? A + m0 * lda : W + n0 * ldw;
-        return c;
-    };
-    Cursor ca = cursor_at(0, true), cw = cursor_at(0, false);
-    auto advance = [&](Cursor& c, bool is_a) __attribute__((always_inline)) {
-        if (++c.u == nk) {
-            c.u = 0;
-            ++c.it;
-            if (c.it < mine) {
-                int64_t m0, n0;
-                tile_origin(c.it, m0, n0);
-                c.p = is_a ? A + m0 * lda : W + n0 * ldw;
-            }
-        }
-    };
-    auto stage_a = [&](int U) __attribute__((always_inline)) {  // K-half U = (ca.it, ca.u)
-        const uint32_t s = lds0 + (U & (NS - 1)) * SLOT + wave * 32 * 64;
-        glds16(ca.p + aoff0 + ca.u * BKH, __builtin_amdgcn_readfirstlane(s));
-        glds16(ca.p + aoff1 + ca.u * BKH, __builtin_amdgcn_readfirstlane(s + 16 * 64));
-        advance(ca, true);
-    };
-    auto stage_w = [&](int U) __attribute__((always_inline)) {
-        const uint32_t s = lds0 + (U & (NS - 1)) * SLOT + BM * 64 + wave * 32 * 64;
-        glds16(cw.p + woff0 + cw.u * BKH, __builtin_amdgcn_readfirstlane(s));
-        glds16(cw.p + woff1 + cw.u * BKH, __builtin_amdgcn_readfirstlane(s + 16 * 64));
-        advance(cw, false);
-    };
-    auto read_a = [&](int U, int i0, v8s (&fa)[4]) __attribute__((always_inline)) {
-        const char* At = smem + (U & (NS - 1)) * SLOT;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fa[i] = lds_frag64(At, wm * TM + i0 + i * 16 + c16, q);
-    };
-    auto read_w = [&](int U, v8s (&fw)[4]) __attribute__((always_inline)) {
-        const char* Wt = smem + (U & (NS - 1)) * SLOT + BM * 64;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) fw[j] = lds_frag64(Wt, wn * TN + j * 16 + c16, q);
-    };
-
-    v4f acc[MI][NI];
-    auto mma = [&](auto I0, auto FIRST, const v8s (&fa)[4], const v8s (&fw)[4]) __attribute__((always_inline)) {
-        constexpr int i0 = decltype(I0)::value;
-        constexpr bool first = decltype(FIRST)::value;
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                acc[i0 + i][j] = mfma16x32<ET>(fw[j], fa[i], first ? v4f{0.f, 0.f, 0.f, 0.f} : acc[i0 + i][j]);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    using C0 = std::integral_constant<int, 0>;
-    using C4 = std::integral_constant<int, 4>;
-    using T_ = std::true_type;
-    using F_ = std::false_type;
-
-    v8s alo[4], ahi[4], wA[4], wB[4];
-    auto phase_a = [&](auto FIRST, int U, v8s (&fw)[4]) __attribute__((always_inline)) {
-        read_a(U, 0, alo);
-        read_w(U, fw);
-        if (U + 2 < total) stage_w(U + 2);
-        __builtin_amdgcn_sched_barrier(0);
-        mma(C0{}, FIRST, alo, fw);
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    // POST: the first b phase after an epilogue (its NST stores are younger than K-half U + 1)
-    auto phase_b = [&](auto FIRST, auto POST, int U, const v8s (&fw)[4]) __attribute__((always_inline)) {
-        constexpr int X = decltype(POST)::value ? NST : 0;
-        read_a(U, 64, ahi);
-        if (U + 3 < total) {
-            stage_a(U + 3);
-            wait_vm<6 + X>();
-        } else if (U + 2 < total) {
-            wait_vm<4 + X>();
-        } else {
-            wait_vm<0>();
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        mma(C4{}, FIRST, ahi, fw);
-        if (U + 1 < total || wm == 0) __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-    };
-
-    // prologue: A0 W0 A1 W1 A2 of the first tile in flight, retire A0 W0, publish; group 1 one barrier behind
-    stage_a(0);
-    stage_w(0);
-    stage_a(1);
-    stage_w(1);
-    stage_a(2);
-    wait_vm<6>();
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    if (wm == 1) __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-
-    using Zero = std::integral_constant<int, 0>;
-    using One = std::integral_constant<int, 1>;
-    int U = 0;
-    for (int it = 0; it < mine; ++it) {
-        int64_t m0, n0;
-        tile_origin(it, m0, n0);
-        phase_a(T_{}, U, wA);
-        if (it == 0) phase_b(T_{}, Zero{}, U, wA);
-        else phase_b(T_{}, One{}, U, wA);
-        phase_a(F_{}, U + 1, wB);
-        phase_b(F_{}, Zero{}, U + 1, wB);
-        for (int u = 2; u < nk; u += 2) {
-            phase_a(F_{}, U + u, wA);
-            phase_b(F_{}, Zero{}, U + u, wA);
-            phase_a(F_{}, U + u + 1, wB);
-            phase_b(F_{}, Zero{}, U + u + 1, wB);
-        }
-        U += nk;
-
-        // epilogue: + bias (LDS), activation, 16-bit, permlane16 pairs -> 16-B row stores
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-            const int64_t m = m0 + wm * TM + i * 16 + c16;
-            uint16_t* orow = out + m * ldo;
-            uint16_t* prow = SAVE ? pre_out + m * ldpre : nullptr;
-#pragma unroll
-            for (int jp = 0; jp < NI / 2; ++jp) {
-                unsigned pk[2][2], pp[2][2];
-#pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    const int nl = (int)n0 + wn * TN + (2 * jp + s) * 16 + 4 * q;
-                    const float4 bb = *reinterpret_cast<const float4*>(bias_lds + nl);
-                    float v0 = acc[i][2 * jp + s][0] + bb.x, v1 = acc[i][2 * jp + s][1] + bb.y;
-                    float v2 = acc[i][2 * jp + s][2] + bb.z, v3 = acc[i][2 * jp + s][3] + bb.w;
-                    if constexpr (SAVE) {
-                        pp[s][0] = pack2bf(v0, v1);
-                        pp[s][1] = pack2bf(v2, v3);
-                    }
-                    if (EPI == VC_EPI_BIAS_GELU_TANH || SAVE) {
-                        v0 = gelu_tanh(v0); v1 = gelu_tanh(v1); v2 = gelu_tanh(v2); v3 = gelu_tanh(v3);
-                    } else if (EPI == VC_EPI_BIAS_GELU_ERF) {
-                        v0 = gelu_erf(v0); v1 = gelu_erf(v1); v2 = gelu_erf(v2); v3 = gelu_erf(v3);
-                    } else if (EPI == VC_EPI_BIAS_RELU_BF16) {
-                        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
-                    }
-                    pk[s][0] = pack2<ET>(v0, v1);
-                    pk[s][1] = pack2<ET>(v2, v3);
-                }
-                const int64_t col = n0 + wn * TN + (2 * jp + (q & 1)) * 16 + 4 * (q & 2);
-                auto s0 = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
-                auto s1 = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
-                uint4 v;
-                v.x = s0[0]; v.y = s1[0]; v.z = s0[1]; v.w = s1[1];
-                *reinterpret_cast<uint4*>(orow + col) = v;
-                if constexpr (SAVE) {
-                    auto u0 = __builtin_amdgcn_permlane16_swap(pp[0][0], pp[1][0], false, false);
-                    auto u1 = __builtin_amdgcn_permlane16_swap(pp[0][1], pp[1][1], false, false);
-                    uint4 w;
-                    w.x = u0[0]; w.y = u1[0]; w.z = u0[1]; w.w = u1[1];
-                    *reinterpret_cast<uint4*>(prow + col) = w;
-                }
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1762,18 +1200,16 @@ gemm_ppp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
 // ping-pong's reads of a phase come after the previous phase's MFMAs issued -- which leaves room for
 // the 64 pending registers next to the 128 accumulators.
 // ---------------------------------------------------------------------------------
-template <int EPI, int ET = VC_ELEM_BF16, int NDEF = 16>
+template <int EPI, int ET = VC_ELEM_BF16>
 __global__ void __launch_bounds__(512, 1)
 gemm_ppd_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __restrict__ W, int64_t ldw, int nbm,
-                int nbn, int K, int N, const float* __restrict__ bias, uint16_t* __restrict__ out, int64_t ldo,
-                unsigned long long* __restrict__ stamps) {
+                int nbn, int K, int N, const float* __restrict__ bias, uint16_t* __restrict__ out, int64_t ldo) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     constexpr int BM = 256, BN = 256, BKH = 32, NS = 4;
     constexpr int SLOT = (BM + BN) * 64;  // 32 KiB
     constexpr int TM = 128, TN = 64, MI = 8, NI = 4;
-    constexpr int NST = MI * (NI / 2);  // 16-B row pieces per wave per tile
-    constexpr int P0 = NST - NDEF;      // pieces stored at once at the end of a tile (the rest deferred)
-    static_assert(NDEF >= 1 && NDEF <= 16, "deferred pieces");
+    constexpr int NST = MI * (NI / 2);  // 16-B row pieces per wave per tile, all deferred
+    constexpr int NDEF = NST, P0 = 0;
     static_assert(EPI == VC_EPI_BIAS_BF16 || EPI == VC_EPI_BIAS_GELU_TANH || EPI == VC_EPI_BIAS_GELU_ERF ||
                       EPI == VC_EPI_BIAS_RELU_BF16,
                   "16-bit-output epilogues without a second output");
@@ -2041,19 +1477,13 @@ gemm_ppd_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
     if (wm == 1) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
 
-    // diagnostics (tools/gemm_stamps.py --ppd): s_memrealtime at entry and after each tile's main loop,
-    // wave 0 of each workgroup, into stamps[b][16] (entry, tiles 0 .. 13, end)
-    const bool stamp = stamps != nullptr && tid == 0;
-    if (stamp) stamps[b * 16] = __builtin_amdgcn_s_memrealtime();
     int64_t m0, n0;
     tile_origin(0, m0, n0);
     run_tile(F_{}, 0);
-    if (stamp) stamps[b * 16 + 1] = __builtin_amdgcn_s_memrealtime();
     finish(m0, n0);
     for (int it = 1; it < mine; ++it) {
         tile_origin(it, m0, n0);
         run_tile(T_{}, it * nk);
-        if (stamp && it < 14) stamps[b * 16 + 1 + it] = __builtin_amdgcn_s_memrealtime();
         finish(m0, n0);
     }
     auto store_rest = [&](auto self, auto T) __attribute__((always_inline)) {
@@ -2064,10 +1494,6 @@ gemm_ppd_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __r
         }
     };
     store_rest(store_rest, std::integral_constant<int, P0>{});
-    if (stamp) {
-        __builtin_amdgcn_s_waitcnt(0);
-        stamps[b * 16 + 15] = __builtin_amdgcn_s_memrealtime();
-    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -2294,19 +1720,21 @@ static int launch_conv(const uint16_t* X, int64_t ldx, const ConvGeomG& g, const
                                                       stream);
 }
 
-// Tile configurations (BM, BN); cfg 6 (a ping-pong schedule of the persistent kernel, 23 %
-// slower in round 1) is retired.  Round 4: a 128x256 4-wave kernel at two workgroups per CU (one
-// workgroup's epilogue store burst overlapping the other's main loop) measured slower on every
-// shape (q|k|v 12800 rows 59.9 vs 50.7 us, K = 6144 383 vs 277 us: without the ping-pong the main
-// loop loses more than the overlap gains) and was removed.
+// Tile configurations (BM, BN), indexed by the cfg number of vc_gemm_bf16_cfg / model.gemm_cfg; the
+// numbers are stable, a retired configuration keeps its slot as {0, 0} (rejected).  Round 6 pruned the
+// product library to the configurations pick_cfg chooses (3, 4, 5, 7, 8, 15, 20, 21); the round-4/5
+// timing ablations and diagnostics (11-14, 16, 18, 19), the 3-slot 128-wide / 256x128 / 128x256 tiles
+// (0-2), the 160x256 / 256x128 / persistent ping-pong kernels (17, 9, 10), the deeper Swin rings (22, 23)
+// and the 256x192 ping-pong tile (24) were measured and not picked (their source:
+// tools/experiments/gemm_retired_r06.hip.txt and the git history).
 struct GemmCfg {
     int bm, bn;
 };
-static const GemmCfg kCfgs[] = {{256, 128}, {128, 128}, {128, 256}, {256, 256}, {256, 256}, {128, 128}, {0, 0},
-                                 {64, 128}, {256, 256}, {256, 128}, {256, 256}, {256, 256}, {256, 256}, {256, 256},
-                                 {128, 128}, {256, 256}, {256, 256}, {160, 256}, {256, 256}, {256, 256}, {128, 128},
-                                 {64, 128}, {64, 128}, {128, 128}, {256, 192}};
-constexpr int kNumCfgs = 25;
+static const GemmCfg kCfgs[] = {{0, 0},     {0, 0},     {0, 0},    {256, 256}, {256, 256}, {128, 128}, {0, 0},
+                                 {64, 128},  {256, 256}, {0, 0},    {0, 0},     {0, 0},     {0, 0},     {0, 0},
+                                 {0, 0},     {256, 256}, {0, 0},    {0, 0},     {0, 0},     {0, 0},     {128, 128},
+                                 {64, 128}};
+constexpr int kNumCfgs = 22;
 
 template <int BM, int BN, int WM, int WN, int E, int ST = 3, int ET = VC_ELEM_BF16>
 static int launch_cfg(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
@@ -2342,55 +1770,21 @@ static int launch_big(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t
     return check_launch("vc_gemm_bf16");
 }
 
-template <int E, int ET, int ABL = 0, int BN = 256>
+template <int E, int ET>
 static int launch_pp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
                      const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
                      int64_t gs, int64_t go, hipStream_t stream, int ka = 0) {
     constexpr int lds = 4 * 512 * 64;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_pp_kernel<E, ET, ABL, BN>,
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_pp_kernel<E, ET>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
         attr_set = true;
     }
-    gemm_pp_kernel<E, ET, ABL, BN><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out,
+    gemm_pp_kernel<E, ET><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out,
                                                                            ldo, aux, ldaux, G, gs, go,
                                                                            (ka > 0 ? ka : K) / 32);
-    return check_launch("vc_gemm_bf16");
-}
-
-template <int E, int ET>
-static int launch_pp160(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
-                        const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
-                        int64_t gs, int64_t go, hipStream_t stream) {
-    constexpr int lds = 4 * (160 + 256) * 64;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_pp160_kernel<E, ET>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
-        attr_set = true;
-    }
-    gemm_pp160_kernel<E, ET><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo,
-                                                                          aux, ldaux, G, gs, go);
-    return check_launch("vc_gemm_bf16");
-}
-
-template <int E, int ET>
-static int launch_pp128(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K,
-                        const float* bias, void* out, int64_t ldo, const float* aux, int64_t ldaux, int64_t G,
-                        int64_t gs, int64_t go, hipStream_t stream) {
-    constexpr int lds = 6 * 384 * 64;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_pp128_kernel<E, ET>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
-        attr_set = true;
-    }
-    gemm_pp128_kernel<E, ET><<<(unsigned)(nbm * nbn), 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo,
-                                                                         aux, ldaux, G, gs, go);
     return check_launch("vc_gemm_bf16");
 }
 
@@ -2428,33 +1822,12 @@ static int launch_persist(const uint16_t* A, int64_t lda, const uint16_t* W, int
 }
 
 template <int E, int ET>
-static int launch_ppp(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K, int N,
-                      const float* bias, void* out, int64_t ldo, hipStream_t stream, const float* aux = nullptr,
-                      int64_t ldaux = 0) {
-    const int lds = 4 * 512 * 64 + N * 4;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_ppp_kernel<E, ET>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
-        attr_set = true;
-    }
-    const int ntiles = nbm * nbn;
-    int grid = num_cus() / 8 * 8;
-    if (grid > (ntiles + 7) / 8 * 8) grid = (ntiles + 7) / 8 * 8;
-    gemm_ppp_kernel<E, ET><<<(unsigned)grid, 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, N, bias, (uint16_t*)out,
-                                                                 ldo, (uint16_t*)const_cast<float*>(aux), ldaux);
-    return check_launch("vc_gemm_bf16");
-}
-
-template <int E, int ET, int NDEF>
 static int launch_ppd(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t ldw, int nbm, int nbn, int K, int N,
-                      const float* bias, void* out, int64_t ldo, hipStream_t stream,
-                      unsigned long long* stamps = nullptr) {
+                      const float* bias, void* out, int64_t ldo, hipStream_t stream) {
     const int lds = 4 * 512 * 64 + N * 4;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_ppd_kernel<E, ET, NDEF>,
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_ppd_kernel<E, ET>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return fail((int)e, std::string("vc_gemm_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
         attr_set = true;
@@ -2462,8 +1835,8 @@ static int launch_ppd(const uint16_t* A, int64_t lda, const uint16_t* W, int64_t
     const int ntiles = nbm * nbn;
     int grid = num_cus() / 8 * 8;
     if (grid > (ntiles + 7) / 8 * 8) grid = (ntiles + 7) / 8 * 8;
-    gemm_ppd_kernel<E, ET, NDEF><<<(unsigned)grid, 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, N, bias,
-                                                                       (uint16_t*)out, ldo, stamps);
+    gemm_ppd_kernel<E, ET><<<(unsigned)grid, 512, lds, stream>>>(A, lda, W, ldw, nbm, nbn, K, N, bias,
+                                                                       (uint16_t*)out, ldo);
     return check_launch("vc_gemm_bf16");
 }
 
@@ -2495,42 +1868,12 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
                       int64_t gs, int64_t go, hipStream_t s) {
     const int nbm = (int)(M / kCfgs[cfg].bm), nbn = (int)(N / kCfgs[cfg].bn);
     switch (cfg) {
-        case 0: return launch_cfg<256, 128, 4, 2, E, 3, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-        case 1: return launch_cfg<128, 128, 2, 4, E, 3, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-        case 2: return launch_cfg<128, 256, 2, 4, E, 3, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 3: return launch_big<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 5: return launch_cfg<128, 128, 2, 4, E, 2, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 7: return launch_cfg<64, 128, 2, 4, E, 2, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-        // round 5: deeper rings for the latency-bound small launches (Swin-T's per-stream parts)
+        // round 5: a deeper ring for the latency-bound small launches (Swin-T's per-stream parts)
         case 21: return launch_cfg<64, 128, 2, 4, E, 4, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-        case 22: return launch_cfg<64, 128, 2, 4, E, 6, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-        case 23: return launch_cfg<128, 128, 2, 4, E, 4, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 8: return launch_pp<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-        case 24: return launch_pp<E, ET, 0, 192>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-        case 11:
-        case 12:
-        case 13:
-        case 18:
-            if constexpr ((E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_RESID_F32) &&
-                          ET == VC_ELEM_BF16) {
-                if (cfg == 18)  // diagnostics: cfg 8 with per-workgroup time stamps into aux (ABL 4)
-                    return launch_pp<E, ET, 4>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-            }
-            if constexpr (E == VC_EPI_BIAS_BF16 && ET == VC_ELEM_BF16) {
-                if (cfg == 11)
-                    return launch_pp<E, ET, 1>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-                if (cfg == 12)
-                    return launch_pp<E, ET, 2>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-                return launch_pp<E, ET, 3>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-            }
-            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfgs 11 / 12 / 13 / 18 (timing ablations) are bias / bf16 only");
-        case 14:  // timing ablation: cfg 5 with the bf16 residual read in the epilogue (G < 0), not prefetched
-            if constexpr (E == VC_EPI_BIAS_RESID_RELU_BF16)
-                return launch_cfg<128, 128, 2, 4, E, 2, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, -1, gs,
-                                                            go, s);
-            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 14 (timing ablation) is bias_resid_relu only");
-        case 9: return launch_pp128<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
-        case 17: return launch_pp160<E, ET>(A, lda, W, ldw, nbm, nbn, K, bias, out, ldo, aux, ldaux, G, gs, go, s);
         case 20:  // streaming 1x1x1 conv with the bf16 residual (ResNet3D conv_c), K 64 / 128 (N % 256), 256
             if constexpr (E == VC_EPI_BIAS_RESID_RELU_BF16 && ET == VC_ELEM_BF16) {
                 if (K == 64 && N % 256 == 0)
@@ -2545,21 +1888,11 @@ static int launch_epi(int cfg, const uint16_t* A, int64_t lda, const uint16_t* W
                           E == VC_EPI_BIAS_RELU_BF16 || E == VC_EPI_BIAS_GELU_TANH_SAVE)
                 return launch_persist<E, ET>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s, aux, ldaux);
             return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 4 supports bf16-output epilogues only");
-        case 10:
-            if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
-                          E == VC_EPI_BIAS_RELU_BF16 || E == VC_EPI_BIAS_GELU_TANH_SAVE)
-                return launch_ppp<E, ET>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s, aux, ldaux);
-            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 10 supports 16-bit-output epilogues only");
         case 15:
-        case 16:  // cfg 16: half the pieces deferred, half stored at the end of the tile (A/B)
-        case 19:  // diagnostics: cfg 15 writing per-tile time stamps into aux (u64 [grid][16])
             if constexpr (E == VC_EPI_BIAS_BF16 || E == VC_EPI_BIAS_GELU_TANH || E == VC_EPI_BIAS_GELU_ERF ||
-                          E == VC_EPI_BIAS_RELU_BF16) {
-                if (cfg == 16) return launch_ppd<E, ET, 8>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
-                auto* st = cfg == 19 ? reinterpret_cast<unsigned long long*>(const_cast<float*>(aux)) : nullptr;
-                return launch_ppd<E, ET, 16>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s, st);
-            }
-            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfgs 15 / 16 / 19 support the plain 16-bit-output epilogues only");
+                          E == VC_EPI_BIAS_RELU_BF16)
+                return launch_ppd<E, ET>(A, lda, W, ldw, nbm, nbn, K, (int)N, bias, out, ldo, s);
+            return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 15 supports the plain 16-bit-output epilogues only");
     }
     return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad config");
 }
@@ -2639,8 +1972,8 @@ extern "C" int vc_gemm_h16(const uint16_t* A, int64_t lda, const uint16_t* W, in
     if (elem == VC_ELEM_F16 && epilogue > VC_EPI_EMBED_F32)
         return fail(VC_ERR_UNSUPPORTED, "vc_gemm: fp16 operands support epilogues 0-4 (the inference forward) only");
     if (!A || !W || !bias || !out) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: null pointer");
-    if (M <= 0 || N <= 0 || K <= 0 || (M % 128 && M % 160) || N % 128 || K % GBK)
-        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: need M % 128 == 0 (or M % 160 == 0 for cfg 17), N % 128 == 0, K % 64 == 0 (got M=" +
+    if (M <= 0 || N <= 0 || K <= 0 || M % 128 || N % 128 || K % GBK)
+        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: need M % 128 == 0, N % 128 == 0, K % 64 == 0 (got M=" +
                                             std::to_string(M) + " N=" + std::to_string(N) + " K=" + std::to_string(K) + ")");
     if (lda % 8 || ldw % 8 || ldo % 4 || lda < K || ldw < K || ldo < N)
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: bad leading dimension");
@@ -2657,19 +1990,24 @@ extern "C" int vc_gemm_h16(const uint16_t* A, int64_t lda, const uint16_t* W, in
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: BIAS_ADD_F32 epilogue needs an f32 aux with ldaux >= N");
     // the persistent kernel writes 16-byte row chunks of out (and of the saved pre-activation)
     const bool st16_ok = ldo % 8 == 0 && (epilogue != VC_EPI_BIAS_GELU_TANH_SAVE || (ldaux % 8 == 0 && !((uintptr_t)aux & 15)));
+    // the streaming conv_c kernel (cfg 20) moves 16-B pieces of out and of the bf16 residual and has no
+    // grouped-row addressing
+    const bool c20_ok = ldo % 8 == 0 && ldaux % 8 == 0 && !(((uintptr_t)out | (uintptr_t)aux) & 15) && G <= 1;
     if (cfg < 0) {
         cfg = pick_cfg(M, N, K, epilogue);
         if ((cfg == 4 || cfg == 15) && (!st16_ok || ((uintptr_t)out & 15))) cfg = 5;
+        if (cfg == 20 && !c20_ok) cfg = 5;
     }
+    if (cfg == 20 && !c20_ok)
+        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 20 needs ldo, ldaux % 8 == 0, 16-B aligned out / aux, G <= 1");
     if (cfg < 0 || cfg >= kNumCfgs || kCfgs[cfg].bm == 0 || M % kCfgs[cfg].bm || N % kCfgs[cfg].bn)
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: no tile config divides M x N");
     if ((M / kCfgs[cfg].bm) * (N / kCfgs[cfg].bn) > (1 << 30)) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: grid too large");
     const int k = (int)K;
-    if ((cfg == 8 || cfg == 9 || cfg == 17 || cfg == 18 || cfg == 24 || (cfg >= 11 && cfg <= 13)) && K < 128)
-        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfgs 8 / 9 / 17 need K >= 128");
-    if ((cfg == 15 || cfg == 16 || cfg == 19) && (K < 640 || K % 64 || N > 8192 || ldo % 8 || ((uintptr_t)out & 15)))
-        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfgs 15 / 16 need K >= 640, K % 64 == 0, N <= 8192, 16-B output rows");
-    if ((cfg == 4 || cfg == 10) && (K / 32 < 6 || N > 8192 || !st16_ok ||
+    if (cfg == 8 && K < 128) return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 8 needs K >= 128");
+    if (cfg == 15 && (K < 640 || K % 64 || N > 8192 || ldo % 8 || ((uintptr_t)out & 15)))
+        return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 15 needs K >= 640, K % 64 == 0, N <= 8192, 16-B output rows");
+    if (cfg == 4 && (K / 32 < 6 || N > 8192 || !st16_ok ||
                      (epilogue > VC_EPI_BIAS_GELU_ERF && epilogue != VC_EPI_BIAS_RELU_BF16 &&
                       epilogue != VC_EPI_BIAS_GELU_TANH_SAVE)))
         return fail(VC_ERR_INVALID_ARG, "vc_gemm_bf16: cfg 4 needs K>=192, N<=8192, ldo%8==0, a 16-bit-output epilogue");
@@ -2943,6 +2281,7 @@ extern "C" int vc_gemm_pick(int64_t M, int64_t N, int64_t K, int epilogue, int64
         ldo % 8 == 0 && (epilogue != VC_EPI_BIAS_GELU_TANH_SAVE || (ldaux % 8 == 0 && !((uintptr_t)aux & 15)));
     int cfg = pick_cfg(M, N, K, epilogue);
     if ((cfg == 4 || cfg == 15) && !st16_ok) cfg = 5;
+    if (cfg == 20 && (ldo % 8 || ldaux % 8 || ((uintptr_t)aux & 15))) cfg = 5;
     return cfg;
 }
 

@@ -1037,6 +1037,50 @@ static bool wgrad_pp_enabled() {
     return v == 1;
 }
 
+// The 256 x 256 weight-gradient schedule for M rows of reduction: split count sp (fewest workgroup rounds x
+// half-tiles per workgroup over 1 .. ceil(CUs / tiles) splits, capped by the scratch), rows per split mch,
+// and whether every split is long enough for the ping-pong kernel.  Shared by vc_wgrad_bf16 and
+// vc_wgrad_pick (the host-side label query), so the two cannot disagree.
+struct WgradPlan {
+    int64_t sp, mch;
+    bool pp;
+};
+static WgradPlan wgrad_plan(int64_t M, int64_t N1, int64_t N2, bool have_work, int64_t work_elems) {
+    const int64_t nt2 = (N1 / 256) * (N2 / 256);
+    const int64_t kt2 = M / 32;
+    // round 5: ceil(256 / tiles) alone gave 270 / 261 / 288 workgroups for the ViViT-B q|k|v / o_proj / fc1
+    // weights -- a second round of 14 / 5 / 32 (floor: 243 / 252 / 252 workgroups in one round)
+    static int ncu_s = 0;
+    if (!ncu_s) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&ncu_s, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu_s <= 0)
+            ncu_s = 256;
+    }
+    const int64_t ncu = ncu_s;
+    int64_t sp = 1, best = -1;
+    for (int64_t c = 1; c <= (ncu + nt2 - 1) / nt2 && c <= (kt2 / 4 > 0 ? kt2 / 4 : 1); ++c) {
+        const int64_t cost = ((nt2 * c + ncu - 1) / ncu) * ((kt2 + c - 1) / c);
+        if (best < 0 || cost <= best) { best = cost; sp = c; }
+    }
+    if (!have_work || work_elems < 2 * N1 * N2) sp = 1;
+    else if (sp * N1 * N2 > work_elems) sp = work_elems / (N1 * N2);
+    if (sp < 1) sp = 1;
+    WgradPlan p;
+    p.mch = (kt2 + sp - 1) / sp * 32;
+    p.sp = (M + p.mch - 1) / p.mch;
+    // the ping-pong schedule when every split has >= 3 half-tiles (the last split is the shortest)
+    p.pp = (M - (p.sp - 1) * p.mch) / 32 >= 3 && wgrad_pp_enabled();
+    return p;
+}
+
+int vc_wgrad_pick(int64_t M, int64_t N1, int64_t N2, int64_t work_elems) {
+    if (M <= 0 || N1 <= 0 || N2 <= 0) return fail(VC_ERR_INVALID_ARG, "vc_wgrad_pick: need M, N1, N2 > 0");
+    if (N1 % 256 || N2 % 256) return 0;
+    const WgradPlan p = wgrad_plan(M, N1, N2, work_elems > 0, work_elems);
+    return (p.pp ? 2 : 1) | (int)(p.sp << 4);
+}
+
 int vc_wgrad_bf16(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx, int64_t M, int64_t N1, int64_t N2,
                   int64_t nscaled, float scale, float* out, int64_t ldo, float* work, int64_t work_elems,
                   hipStream_t stream) {
@@ -1052,29 +1096,8 @@ int vc_wgrad_bf16(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx
         // 256 x 256 LDS-DMA kernel, split-K sized for ~one workgroup per CU
         const int nJ2 = (int)(N2 / 256);
         const int nt2 = (int)(N1 / 256) * nJ2;
-        const int64_t kt2 = M / 32;
-        // split count: fewest (workgroup rounds x half-tiles per workgroup) over 1 .. ceil(256 / tiles)
-        // splits (one workgroup per CU).  round 5: ceil(256 / tiles) alone gave 270 / 261 / 288
-        // workgroups for the ViViT-B q|k|v / o_proj / fc1 weights -- a second round of 14 / 5 / 32
-        // (floor: 243 / 252 / 252 workgroups in one round)
-        static int ncu_s = 0;
-        if (!ncu_s) {
-            int dev = 0;
-            (void)hipGetDevice(&dev);
-            if (hipDeviceGetAttribute(&ncu_s, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu_s <= 0)
-                ncu_s = 256;
-        }
-        const int64_t ncu = ncu_s;
-        int64_t sp = 1, best = -1;
-        for (int64_t c = 1; c <= (ncu + nt2 - 1) / nt2 && c <= (kt2 / 4 > 0 ? kt2 / 4 : 1); ++c) {
-            const int64_t cost = ((nt2 * c + ncu - 1) / ncu) * ((kt2 + c - 1) / c);
-            if (best < 0 || cost <= best) { best = cost; sp = c; }
-        }
-        if (!work || work_elems < 2 * N1 * N2) sp = 1;
-        else if (sp * N1 * N2 > work_elems) sp = work_elems / (N1 * N2);
-        if (sp < 1) sp = 1;
-        const int64_t mch = (kt2 + sp - 1) / sp * 32;
-        sp = (M + mch - 1) / mch;
+        const WgradPlan plan = wgrad_plan(M, N1, N2, work != nullptr, work_elems);
+        const int64_t sp = plan.sp, mch = plan.mch;
         static bool attr = false;
         if (!attr) {
             hipError_t e = hipFuncSetAttribute((const void*)wgrad_big_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1085,9 +1108,7 @@ int vc_wgrad_bf16(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx
             if (e != hipSuccess) return fail((int)e, std::string("vc_wgrad_bf16: hipFuncSetAttribute: ") + hipGetErrorString(e));
             attr = true;
         }
-        // the ping-pong schedule when every split has >= 3 half-tiles (the last split is the shortest)
-        const bool pp = (M - (sp - 1) * mch) / 32 >= 3 && wgrad_pp_enabled();
-        auto kern = pp ? wgrad_pp_kernel : wgrad_big_kernel;
+        auto kern = plan.pp ? wgrad_pp_kernel : wgrad_big_kernel;
         if (sp == 1) {
             kern<<<dim3((unsigned)nt2, 1), 512, WBNS * WBSLOT, stream>>>(G, ldg, X, ldx, M, nJ2, mch, out, ldo, 0, nscaled,
                                                                          scale);

@@ -180,15 +180,10 @@ def timed(kernel: str, op: str, work: float, unit: str, fn, *args, **kw):
 
 
 # rocprofv3 names of the GEMM kernels per tile config (csrc/gemm.hip kCfgs; E = the epilogue, ET = 0 bf16)
-GEMM_KERNEL = {0: "gemm_bf16_kernel<256, 128, 4, 2, {E}, 3, {ET}>", 1: "gemm_bf16_kernel<128, 128, 2, 4, {E}, 3, {ET}>",
-               2: "gemm_bf16_kernel<128, 256, 2, 4, {E}, 3, {ET}>", 3: "gemm_bf16_big_kernel<{E}, {ET}>",
-               4: "gemm_bf16_persist_kernel<{E}, {ET}>", 5: "gemm_bf16_kernel<128, 128, 2, 4, {E}, 2, {ET}>",
-               7: "gemm_bf16_kernel<64, 128, 2, 4, {E}, 2, {ET}>", 8: "gemm_pp_kernel<{E}, {ET}, 0, 256>",
-               9: "gemm_pp128_kernel<{E}, {ET}>", 10: "gemm_ppp_kernel<{E}, {ET}>",
-               15: "gemm_ppd_kernel<{E}, {ET}, 16>", 16: "gemm_ppd_kernel<{E}, {ET}, 8>",
-               17: "gemm_pp160_kernel<{E}, {ET}>", 20: "conv_c_stream_kernel<{K}, {BN}>",
-               21: "gemm_bf16_kernel<64, 128, 2, 4, {E}, 4, {ET}>", 22: "gemm_bf16_kernel<64, 128, 2, 4, {E}, 6, {ET}>",
-               23: "gemm_bf16_kernel<128, 128, 2, 4, {E}, 4, {ET}>", 24: "gemm_pp_kernel<{E}, {ET}, 0, 192>"}
+GEMM_KERNEL = {3: "gemm_bf16_big_kernel<{E}, {ET}>", 4: "gemm_bf16_persist_kernel<{E}, {ET}>",
+               5: "gemm_bf16_kernel<128, 128, 2, 4, {E}, 2, {ET}>", 7: "gemm_bf16_kernel<64, 128, 2, 4, {E}, 2, {ET}>",
+               8: "gemm_pp_kernel<{E}, {ET}>", 15: "gemm_ppd_kernel<{E}, {ET}>", 20: "conv_c_stream_kernel<{K}, {BN}>",
+               21: "gemm_bf16_kernel<64, 128, 2, 4, {E}, 4, {ET}>"}
 
 
 # roofline ridge of the bf16 matrix pipe against HBM (MI355X_MICROARCH.md: 2.5 PFLOP/s dense, 8 TB/s):
@@ -300,6 +295,7 @@ def gemm_wrap(a: torch.Tensor, ka: int, w: torch.Tensor, bias: torch.Tensor, epi
     _need(e <= 4, "gemm_wrap: inference epilogues only")
     if e == 4:
         _need(aux is not None and aux.dtype == torch.float32 and group > 0, "gemm_wrap embed aux")
+        _need((M - 1) // group * group_stride + group_offset + (M - 1) % group < out.shape[0], "gemm_wrap embed out rows")
     else:
         _need(out.shape[0] >= M, "gemm_wrap out rows")
     rec = _REC[0]
@@ -308,7 +304,7 @@ def gemm_wrap(a: torch.Tensor, ka: int, w: torch.Tensor, bias: torch.Tensor, epi
               out.stride(0), _p(aux) if aux is not None else None, aux.stride(0) if aux is not None else 0, group,
               group_stride, group_offset, ELEM_F16 if a.dtype == torch.float16 else 0, _stream(a))
     if rec is not None:
-        rec.end(e0, f"gemm_pp_kernel<{e}, {1 if a.dtype == torch.float16 else 0}, 0, 256>", op,
+        rec.end(e0, f"gemm_pp_kernel<{e}, {1 if a.dtype == torch.float16 else 0}>", op,
                 2.0 * M * N * K if flop is None else flop, "flop")
     return out
 
@@ -329,9 +325,6 @@ def patch_im2col_split(pix: torch.Tensor, tubelet, out: torch.Tensor, order: str
     return out
 
 
-# tile rows, tile cols and workgroups per CU of the GEMM configs gemm_rounds() composes
-# (csrc/gemm.hip kCfgs; cfg 4 is the persistent 256x256 kernel, one workgroup per CU)
-_GEMM_TILES = {1: (128, 128, 1), 4: (256, 256, 1), 5: (128, 128, 2), 7: (64, 128, 2)}
 _NUM_CUS = {}
 
 
@@ -340,35 +333,6 @@ def _num_cus(dev: torch.device) -> int:
     if key not in _NUM_CUS:
         _NUM_CUS[key] = torch.cuda.get_device_properties(key).multi_processor_count
     return _NUM_CUS[key]
-
-
-def gemm_rounds(a: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, epilogue: str, out: torch.Tensor,
-                main_cfg: int, tail_cfg: int, m: int | None = None, flop: float | None = None,
-                op: str = "gemm") -> torch.Tensor:
-    """gemm() as two launches when the tiles of `main_cfg` leave a partial last round on the
-    CUs: the main launch covers whole rounds (rows rounded down to its row tile), the tail
-    launch the remaining rows with the smaller tiles of `tail_cfg` in one round of its own.
-    Each output element runs the same MFMA sequence over K in either launch, so the result is
-    bit-identical to one launch (and stays batch-invariant).  Measured at ViViT-B B = 8
-    (tools/quant_probe.py): q|k|v 111.1 -> 105.5 us (cfg 4 + tail cfg 5), fc2 149.1 -> 139.2 us
-    (cfg 5 + tail cfg 1); o_proj and fc1 are slower split.  Inside the model forward the split
-    q|k|v + fc2 came out 0.6 % slower end to end (tools/ab_model.py round_split), so the ViViT
-    forward keeps one launch by default (VivitForVideoClassification.round_split)."""
-    M = a.shape[0] if m is None else m
-    N = w.shape[0]
-    bm, bn, per_cu = _GEMM_TILES[main_cfg]
-    tbm, tbn, tper_cu = _GEMM_TILES[tail_cfg]
-    cus = _num_cus(a.device)
-    slots, nbn = cus * per_cu, N // bn
-    rounds = (M // bm) * nbn // slots
-    m1 = (rounds * slots // nbn) * bm if rounds else 0
-    tail_tiles = (M - m1) // tbm * (N // tbn)
-    if (rounds == 0 or M % bm or N % bn or N % tbn or (M - m1) % tbm or m1 >= M
-            or tail_tiles > cus * tper_cu):
-        return gemm(a, w, bias, epilogue, out, m=M)
-    gemm(a, w, bias, epilogue, out, m=m1, cfg=main_cfg)
-    gemm(a[m1:], w, bias, epilogue, out[m1:], m=M - m1, cfg=tail_cfg)
-    return out
 
 
 def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, out: torch.Tensor,
@@ -708,6 +672,14 @@ def conv3d_stem_gemm(xp: torch.Tensor, B: int, grid, kernel, stride, pad, w: tor
           bias.numel() >= N and bias.dtype == torch.float32, "conv3d_stem_gemm weights")
     _need(out.dtype == torch.bfloat16 and out.stride(1) == 1 and out.shape[0] >= (M + rt - 1) // rt * rt and
           out.shape[1] >= N, "conv3d_stem_gemm out")
+    # each (kt, kh) tap row is read as 8 pixels x 4 channels from a 16-B aligned start: an even padded width,
+    # and the last output's window (8 pixels from 2 wo) inside the packed clip
+    Tp, Hp, Wp = T + 2 * pad[0], H + 2 * pad[1], W + 2 * pad[2]
+    _need(Wp % 2 == 0 and stride[2] % 2 == 0, "conv3d_stem_gemm: the padded width must be even (16-B aligned "
+          "8-pixel reads; the forward takes the im2col stem otherwise)")
+    last = ((((B - 1) * Tp + (To - 1) * stride[0] + kernel[0] - 1) * Hp + (Ho - 1) * stride[1] + kernel[1] - 1) * Wp
+            + (Wo - 1) * stride[2] + 8) * 4
+    _need(xp.numel() >= last, "conv3d_stem_gemm: the packed clip ends before the last window's 8-pixel read")
     zrow = zero_row(xp.device)
     k, s, p = ((ctypes.c_int * 3)(*v) for v in (kernel, stride, pad))
     rec = _REC[0]
@@ -848,24 +820,11 @@ def wgrad_work(M: int, N1: int, N2: int, device) -> torch.Tensor:
 
 
 def wgrad_kernel_name(M: int, N1: int, N2: int, work_elems: int) -> str:
-    """The rocprofv3 name of the kernel vc_wgrad_bf16 runs for this call (csrc/train.hip's dispatch:
-    the split count it derives from the scratch size, then the ping-pong kernel when every split has
-    >= 3 32-row half-tiles, unless VCLIP_WGRAD_PP=0)"""
-    import os
-    if N1 % 256 or N2 % 256:
-        return "trn::wgrad_kernel"
-    nt2 = (N1 // 256) * (N2 // 256)
-    kt2 = M // 32
-    sp = min(-(-256 // nt2), kt2 // 4)
-    if work_elems < 2 * N1 * N2:
-        sp = 1
-    elif sp * N1 * N2 > work_elems:
-        sp = work_elems // (N1 * N2)
-    sp = max(sp, 1)
-    mch = -(-kt2 // sp) * 32
-    sp = -(-M // mch)
-    pp = (M - (sp - 1) * mch) // 32 >= 3 and os.environ.get("VCLIP_WGRAD_PP", "1")[:1] != "0"
-    return "trn::wgrad_pp_kernel" if pp else "trn::wgrad_big_kernel"
+    """The rocprofv3 name of the kernel vc_wgrad_bf16 runs for this call: csrc/train.hip's own plan
+    (vc_wgrad_pick: split count from the device's CU count and the scratch size, then the ping-pong kernel
+    when every split has >= 3 32-row half-tiles, unless VCLIP_WGRAD_PP=0)"""
+    k = _lib.load().vc_wgrad_pick(M, N1, N2, work_elems) & 15
+    return {0: "trn::wgrad_kernel", 1: "trn::wgrad_big_kernel", 2: "trn::wgrad_pp_kernel"}[k]
 
 
 def wgrad(g: torch.Tensor, x: torch.Tensor, out: torch.Tensor, work: torch.Tensor | None = None,

@@ -21,7 +21,7 @@ from collections import OrderedDict
 import numpy as np
 import torch
 
-from . import ops
+from . import ops, streams
 from .weights import resnet3d_param_shapes
 
 RESNET3D_50 = dict(depths=(3, 4, 6, 3), stem_dim=64, conv_a_kernels=((1, 1, 1), (1, 1, 1), (3, 1, 1), (3, 1, 1)),
@@ -314,7 +314,7 @@ class ResNet3d(torch.nn.Module):
         `graph_replay` the forward is replayed from a captured hipGraph (bit-identical either way)."""
         if video.shape[1] != 3:
             raise ValueError("video must be [B, 3, T, H, W]")
-        if self.graph_replay and not torch.cuda.is_current_stream_capturing():
+        if self.graph_replay and not streams.serial() and not torch.cuda.is_current_stream_capturing():
             from .streams import GraphReplay
             if self._graphs is None:
                 self._graphs = GraphReplay()

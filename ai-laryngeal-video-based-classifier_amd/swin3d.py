@@ -28,7 +28,7 @@ from collections import OrderedDict
 import numpy as np
 import torch
 
-from . import ops
+from . import ops, streams
 from .weights import swin3d_param_shapes
 
 LOG2E = ops.LOG2E
@@ -422,7 +422,8 @@ class Swin3d(torch.nn.Module):
         B, Cin = video.shape[0], video.shape[1]
         if Cin != 3:
             raise ValueError("video must be [B, 3, T, H, W]")
-        if self.graph_replay and self.kernel_events is None and not torch.cuda.is_current_stream_capturing():
+        if (self.graph_replay and self.kernel_events is None and not streams.serial()
+                and not torch.cuda.is_current_stream_capturing()):
             from .streams import GraphReplay
             if self._graphs is None:
                 self._graphs = GraphReplay()

@@ -29,7 +29,7 @@ from collections import OrderedDict
 import numpy as np
 import torch
 
-from . import ops
+from . import ops, streams
 from .vivit import ClassifierOutput, _round_up
 from .weights import timesformer_param_shapes
 
@@ -257,7 +257,8 @@ class TimesformerForVideoClassification(torch.nn.Module):
         if T != c.num_frames or H != c.image_size or W != c.image_size or C != c.num_channels:
             raise ValueError(f"pixel_values {tuple(pix.shape)} do not match config "
                              f"(T={c.num_frames}, C={c.num_channels}, {c.image_size}^2)")
-        if self.graph_replay and self.kernel_events is None and not torch.cuda.is_current_stream_capturing():
+        if (self.graph_replay and self.kernel_events is None and not streams.serial()
+                and not torch.cuda.is_current_stream_capturing()):
             from .streams import GraphReplay
             if self._graphs is None:
                 self._graphs = GraphReplay()

@@ -139,10 +139,6 @@ class VivitForVideoClassification(torch.nn.Module):
         # "tight" = B*S rounded up to the tile height (the padding rows keep their initial zeros)
         self.gemm_cfg = {}
         self.rows = "pad"
-        # q|k|v and fc2 as whole-round + tail launches (ops.gemm_rounds): bit-identical, 5-7 %
-        # faster per GEMM in isolation but 0.6 % SLOWER in the model (tools/ab_model.py
-        # round_split, interleaved, B = 8: 9.340 vs 9.285 ms/step), so off by default
-        self.round_split = False
         # 16-bit operand type of the inference forward: bf16 (the benchmarked configuration) or
         # torch.float16 (same kernels and MFMA rate, logits ~6x closer to the fp32 reference;
         # DESIGN.md §5.5).  The train step (vivit_train.py) is bf16 either way.
@@ -373,10 +369,21 @@ class VivitForVideoClassification(torch.nn.Module):
         npatch, S, Mpad, Memb = self.geometry(B)
         bf = self.compute_dtype
         z = lambda *s, dt=bf: torch.zeros(s, dtype=dt, device=device)  # noqa: E731
-        ws = dict(A_emb=z(Memb, c.num_channels * kt * kh * kw), X=z(Mpad, D, dt=torch.float32), Y=z(Mpad, D),
+        Kemb = c.num_channels * kt * kh * kw
+        precise = self.precise_layers > 0 and bf == torch.float16
+        if precise:
+            # the split-operand embedding runs on the 256-row ping-pong kernel (vc_gemm_h16_wrap): its A rows
+            # rounded up to 256 (zero rows past B*npatch), and X 256 rows deeper so the remapped rows of that
+            # padding (tokens B*S+1 .. B*S+256, values bias + pos: finite) stay inside the buffer; the layers
+            # address X[:Mpad] as always
+            Memb = _round_up(B * npatch, 256)
+            Xe = z(Mpad + 256, D, dt=torch.float32)
+        else:
+            Xe = z(Mpad, D, dt=torch.float32)
+        ws = dict(A_emb=z(Memb, Kemb), X=Xe[:Mpad], X_emb=Xe, Y=z(Mpad, D),
                   QKV=z(Mpad, 3 * D), O=z(Mpad, D), Hd=z(Mpad, I), logits=z(B, c.num_labels, dt=torch.float32))
-        if self.precise_layers > 0 and bf == torch.float16 and (B * npatch) % 256 == 0:
-            ws["A_emb_split"] = z(B * npatch, 2 * c.num_channels * kt * kh * kw)
+        if precise:
+            ws["A_emb_split"] = z(Memb, 2 * Kemb)
         self._ws[key] = ws
         self._ws_used.append(ws)
         return ws
@@ -420,7 +427,7 @@ class VivitForVideoClassification(torch.nn.Module):
                 and not torch.cuda.is_current_stream_capturing()):
             key = (pix.data_ptr(), tuple(pix.shape), tuple(pix.stride()), pix.dtype, self.concurrent_streams,
                    self.compute_dtype, self._weights_version(), tuple(sorted(self.gemm_cfg.items())), self.rows,
-                   self.round_split, self.precise_layers, tuple(sorted(self.precise_ops)),
+                   self.precise_layers, tuple(sorted(self.precise_ops)),
                    None if self.split_sizes is None else tuple(self.split_sizes))
             return self._graphs.run(key, pix, self._forward_eager, keep=lambda: (self._packed, tuple(self._ws_used)))
         return self._forward_eager(pix)
@@ -501,15 +508,16 @@ class VivitForVideoClassification(torch.nn.Module):
             # split weights only: A (plain fp16 im2col) wrapping against [W_hi | W_lo]
             run("im2col", tm, "im2col_kernel", "im2col", B * (T_ * c.num_channels * H_ * H_ * 4 + npatch * Kemb * 2),
                 "byte", ops.tubelet_im2col, pix, c.tubelet_size, ws["A_emb"])
-            run("embed", ops.gemm_wrap, ws["A_emb"], Kemb, pk["w_emb_split"], pk["b_emb"], "embed_f32", X,
-                aux=pk["pos"][1:], group=npatch, group_stride=S, group_offset=1, m=B * npatch,
+            run("embed", ops.gemm_wrap, ws["A_emb"], Kemb, pk["w_emb_split"], pk["b_emb"], "embed_f32", ws["X_emb"],
+                aux=pk["pos"][1:], group=npatch, group_stride=S, group_offset=1, m=ws["A_emb"].shape[0],
                 flop=2.0 * B * npatch * D * Kemb, op="embed")
         elif "A_emb_split" in ws and "w_emb_split" in pk:
             # split operands: [A_hi | A_lo] against [W_hi | W_hi | W_lo] (A_hi W_hi + A_lo W_hi + A_hi W_lo)
             run("im2col", tm, "im2col_kernel", "im2col", B * (T_ * c.num_channels * H_ * H_ * 4 + npatch * Kemb * 4),
                 "byte", ops.patch_im2col_split, pix, c.tubelet_size, ws["A_emb_split"])
-            run("embed", ops.gemm_wrap, ws["A_emb_split"], 2 * Kemb, pk["w_emb_split"], pk["b_emb"], "embed_f32", X,
-                aux=pk["pos"][1:], group=npatch, group_stride=S, group_offset=1, m=B * npatch,
+            run("embed", ops.gemm_wrap, ws["A_emb_split"], 2 * Kemb, pk["w_emb_split"], pk["b_emb"], "embed_f32",
+                ws["X_emb"], aux=pk["pos"][1:], group=npatch, group_stride=S, group_offset=1,
+                m=ws["A_emb_split"].shape[0],
                 flop=2.0 * B * npatch * D * Kemb, op="embed")
         else:
             run("im2col", tm, "im2col_kernel", "im2col", B * (T_ * c.num_channels * H_ * H_ * 4 + npatch * Kemb * 2),
@@ -519,11 +527,7 @@ class VivitForVideoClassification(torch.nn.Module):
         ops.cls_init(pk["cls"], pk["pos"], X, B, S)
         act = "bias_gelu_tanh" if c.hidden_act in ("gelu_fast", "gelu_pytorch_tanh", "gelu_new") else "bias_gelu_erf"
         scale = 1.0 / math.sqrt(D // c.num_attention_heads)
-        if self.round_split:
-            qkv_gemm = lambda *a, cfg=-1, **k: ops.gemm_rounds(*a, main_cfg=4, tail_cfg=5, **k)  # noqa: E731
-            fc2_gemm = lambda *a, cfg=-1, **k: ops.gemm_rounds(*a, main_cfg=5, tail_cfg=1, **k)  # noqa: E731
-        else:
-            qkv_gemm = fc2_gemm = ops.gemm
+        qkv_gemm = fc2_gemm = ops.gemm
         gc = self.gemm_cfg
         tight = self.rows == "tight"
 
@@ -533,7 +537,7 @@ class VivitForVideoClassification(torch.nn.Module):
             cfg = gc.get(name)
             if not tight:
                 return None, -1 if cfg is None else cfg
-            h = 128 if cfg in (1, 2, 5, 7) else 256
+            h = 128 if cfg in (5, 7, 21) else 256
             return _round_up(B * S, h), -1 if cfg is None else cfg
 
         m_ln = B * S if tight else None

@@ -569,6 +569,11 @@ int vc_wgrad_bf16(const uint16_t* G, int64_t ldg, const uint16_t* X, int64_t ldx
                   int64_t nscaled, float scale, float* out, int64_t ldo, float* work, int64_t work_elems,
                   hipStream_t stream);
 
+/* The weight-gradient schedule vc_wgrad_bf16 runs for (M, N1, N2) with `work_elems` floats of split-K
+ * scratch (host-only query, no launch; instrumentation labels launches with it): bits 0-3 = kernel
+ * (0 wgrad_kernel 128 x 128, 1 wgrad_big_kernel, 2 wgrad_pp_kernel), bits 4.. = split count. */
+int vc_wgrad_pick(int64_t M, int64_t N1, int64_t N2, int64_t work_elems);
+
 /*
  * Backward of the final LayerNorm on the CLS rows + classifier (TF5/.../modeling_vivit.py:427,556)
  * given dlogits f32 [B][num_labels]: writes dx / dxb of the B CLS rows (row b*S; other rows are

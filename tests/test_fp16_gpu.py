@@ -65,7 +65,7 @@ def _case(M, N, K, seed):
     return a, w, bias, a.float() @ w.float().T + bias
 
 
-@pytest.mark.parametrize("cfg", [1, 3, 4, 5, 7])
+@pytest.mark.parametrize("cfg", [3, 4, 5, 7, 8, 15])
 @pytest.mark.parametrize("epi", ["bias", "bias_gelu_tanh", "bias_gelu_erf"])
 def test_gemm_fp16_16bit_out(cfg, epi):
     M, N, K = 25344, 2304, 768
@@ -80,7 +80,7 @@ def test_gemm_fp16_16bit_out(cfg, epi):
     assert err < 1.2e-3, err  # fp16 output rounding (4.9e-4 relative) + fp32 accumulation order
 
 
-@pytest.mark.parametrize("cfg", [-1, 1, 5, 7])
+@pytest.mark.parametrize("cfg", [-1, 5, 7, 8])
 def test_gemm_fp16_resid_f32(cfg):
     M, N, K = 512, 768, 3072
     a, w, bias, ref = _case(M, N, K, 12)
@@ -243,3 +243,29 @@ def test_vivit_b_precise_layers_fp16():
     assert prec < plain, (prec, plain)
     assert prec_qkv <= 1e-3, prec_qkv
     assert prec_qkv < plain, (prec_qkv, plain)
+
+
+def test_vivit_b_precise_default_two_streams_batch8():
+    """The fp16_precise build exactly as bench.py times it (B = 8 as 5 + 3 clips on two HIP streams, the
+    default precise_ops: split embedding weights + layer-0 q|k|v): each part's embedding runs the
+    split-weight GEMM although its patch rows (15680, 9408) are not a multiple of 256, so the logits are
+    bit-identical to the one-stream B = 8 forward (25088 rows) and to a one-stream run of each part's clips."""
+    from vclip_amd.weights import make_synthetic_clips
+    cfg = dict(image_size=224, num_frames=32, tubelet_size=[2, 16, 16], num_channels=3, hidden_size=768,
+               num_hidden_layers=12, num_attention_heads=12, intermediate_size=3072, hidden_act="gelu_fast",
+               layer_norm_eps=1e-6, qkv_bias=True)
+    pix = torch.from_numpy(make_synthetic_clips(8, 32, 224, seed=1)).cuda()
+    m = _vivit(cfg, H)
+    m.precise_layers = 1
+    assert "embed_w" in m.precise_ops
+    one = m(pixel_values=pix).logits.clone()
+    part5 = m(pixel_values=pix[:5].contiguous()).logits.clone()
+    m.concurrent_streams = 2
+    two = m(pixel_values=pix).logits.clone()
+    assert m.last_split == [5, 3], m.last_split
+    assert torch.equal(one, two), (one - two).abs().max().item()
+    assert torch.equal(one[:5], part5)
+    m.concurrent_streams = 1
+    m.precise_layers = 0
+    plain = m(pixel_values=pix).logits.clone()
+    assert not torch.equal(plain, one)  # the split changed the arithmetic

@@ -108,7 +108,7 @@ def test_gemm_bias_bf16(M, N, K):
     assert err < 8e-3, err
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 7])
+@pytest.mark.parametrize("cfg", [3, 4, 5, 7, 8, 15])
 @pytest.mark.parametrize("epi", ["bias", "bias_gelu_tanh"])
 def test_gemm_every_tile_config(cfg, epi):
     """Every block-tile configuration on a shape with more tiles than CUs (the persistent
@@ -123,19 +123,16 @@ def test_gemm_every_tile_config(cfg, epi):
     assert err < 8e-3, err
 
 
-# the 16x16x32-MFMA tile configurations (csrc/gemm.hip kCfgs): ping-pong 256x256 (8), 256x128 (9), persistent
-# deferred-store (15, 16), 160x256 (17), 256x192 (24), deeper-ring 64x128 / 128x128 (21, 22, 23); each runs the
-# same MFMA chain per output element as the 128x128 kernel (cfg 5), so its output is bit-identical to it
-PP_CFGS = {8: ("bias", "bias_gelu_tanh", "bias_resid_f32"), 9: ("bias", "bias_resid_f32"),
-           15: ("bias",), 16: ("bias",), 17: ("bias", "bias_resid_f32"), 24: ("bias", "bias_resid_f32"),
-           21: ("bias", "bias_resid_f32"), 22: ("bias_resid_f32",), 23: ("bias",)}
+# the 16x16x32-MFMA tile configurations (csrc/gemm.hip kCfgs): ping-pong 256x256 (8), persistent
+# deferred-store (15), persistent 256x256 (4), deeper-ring 64x128 (21), 64x128 (7); each runs the same MFMA chain
+# per output element as the 128x128 kernel (cfg 5), so its output is bit-identical to it
+PP_CFGS = {8: ("bias", "bias_gelu_tanh", "bias_resid_f32"), 15: ("bias", "bias_gelu_tanh"), 4: ("bias", "bias_gelu_tanh"),
+           21: ("bias", "bias_resid_f32"), 7: ("bias", "bias_resid_f32")}
 
 
 @pytest.mark.parametrize("cfg,epi", [(c, e) for c, es in PP_CFGS.items() for e in es])
 def test_gemm_tile_configs_bit_identical(cfg, epi):
-    M, N, K = 1280 * 2, 768, 768  # 2560 rows: a multiple of 256, 160 and 128; N: 3 x 256, 4 x 192, 6 x 128
-    if cfg == 22:
-        K = 3072
+    M, N, K = 1280 * 2, 768, 768  # 2560 rows: a multiple of 256 and 128; N: 3 x 256, 6 x 128
     a, w, bias, ref = _gemm_case(M, N, K, 31 * cfg + len(epi))
     f32 = epi == "bias_resid_f32"
     init = (torch.randn(M, N, generator=torch.Generator().manual_seed(cfg)) if f32 else
@@ -172,31 +169,6 @@ def test_gemm_persistent_edge_shapes(M, N, K, epi):
     assert err < 8e-3, err
 
 
-@pytest.mark.parametrize("M,N,K,epi,main_cfg,tail_cfg", [
-    (25344, 2304, 768, "bias", 4, 5),              # ViViT-B B=8 q|k|v: 3 rounds of 256 + a 28-row-block tail
-    (25344, 768, 3072, "bias_resid_f32", 5, 1),    # ViViT-B B=8 fc2: 2 rounds of 512 + tail
-    (12800, 768, 3072, "bias_resid_f32", 5, 1),    # B=4: 1 round + tail
-    (12800, 2304, 768, "bias", 4, 7),
-    (3328, 768, 3072, "bias_resid_f32", 5, 1),     # B=1: no whole round, one launch
-])
-def test_gemm_rounds_bit_identical(M, N, K, epi, main_cfg, tail_cfg):
-    """gemm_rounds (main launch over whole rounds of tiles + a small-tile tail launch) equals one
-    launch bit for bit: every output element runs the same MFMA sequence over K."""
-    a, w, bias, ref = _gemm_case(M, N, K, M + 3 * N + K)
-    ad, wd, bd = a.to(DEV), w.to(DEV), bias.to(DEV)
-    dt = torch.float32 if "f32" in epi else torch.bfloat16
-    x0 = (torch.randn(M, N, generator=torch.Generator().manual_seed(1)) if "f32" in epi
-          else torch.zeros(M, N)).to(DEV, dt)
-    one, two = x0.clone(), x0.clone()
-    ops().gemm(ad, wd, bd, epi, one)
-    ops().gemm_rounds(ad, wd, bd, epi, two, main_cfg, tail_cfg)
-    assert torch.equal(one, two)
-    if "f32" in epi:
-        ref = ref + x0.float().cpu()
-    err = ((two.float().cpu() - ref).abs() / (ref.abs() + 1.0)).max().item()
-    assert err < 8e-3, err
-
-
 def test_gemm_orientation_asymmetric():
     """A = I with an asymmetric W catches a transposed C write (cdna_hip_programming.md §3)."""
     M = N = K = 128
@@ -219,7 +191,7 @@ def test_gemm_gelu(act):
     assert err < 8e-3, err
 
 
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 5, 7])
+@pytest.mark.parametrize("cfg", [-1, 5, 7, 21])
 def test_gemm_resid_f32(cfg):
     """f32 residual epilogue on every 128/64-row config (each prefetches the residual into
     registers before the K loop)."""

@@ -220,6 +220,30 @@ def test_resnet3d_implicit_conv_matches_im2col_path():
     assert float((a - b).abs().max()) <= 1e-2 * max(1.0, float(b.abs().max())), (a, b)
 
 
+def test_resnet3d_stem_odd_padded_width_falls_back():
+    """The implicit stem reads 16-B aligned 8-pixel rows of the padded clip, so an odd padded width (image
+    width 225 -> 231) must take the im2col stem.  The bottleneck convolutions are bit-identical between
+    the implicit and the im2col paths, so with the stem on im2col in both the whole forward is too (the
+    implicit stem would differ by bf16 rounding); and the stem GEMM entry rejects such a width itself."""
+    v = torch.from_numpy(make_synthetic_video(1, 8, 224, seed=6))
+    video = torch.cat([v, v[..., -1:]], dim=-1).contiguous().to(DEV)  # W = 225
+    m = _model()
+    m.implicit_conv = True
+    a = m(video).clone()
+    m.implicit_conv = False
+    b = m(video).clone()
+    assert torch.equal(a, b), (a, b)
+    O = ops()
+    x = torch.randn(1, 3, 4, 20, 19, device=DEV)  # padded width 25
+    xp = torch.zeros(1 * 6 * 26 * 25 * 4, dtype=torch.bfloat16, device=DEV)
+    O.conv3d_stem_pack(x, (1, 3, 3), xp)
+    w = torch.zeros(128, 64 * 11, dtype=torch.bfloat16, device=DEV)
+    out = torch.zeros(1024, 128, dtype=torch.bfloat16, device=DEV)
+    with pytest.raises(RuntimeError, match="even"):
+        O.conv3d_stem_gemm(xp, 1, (4, 20, 19), (3, 7, 7), (1, 2, 2), (1, 3, 3), w, torch.zeros(128, device=DEV),
+                           "bias_relu", out)
+
+
 @pytest.mark.parametrize("T,H,W", [(4, 20, 18), (3, 17, 22)])
 def test_conv3d_stem_implicit_gemm_matches_im2col(T, H, W):
     """The implicit stem (vc_conv3d_stem_pack + vc_conv3d_stem_gemm_bf16, one 32-column segment per
@@ -311,3 +335,26 @@ def test_conv_c_stream_bit_identical(M, N, K, lda, ldr):
     if M <= 8192:  # and the fp32 torch reference
         ref = torch.relu(a.float() @ w.float().T + b + r.float())
         assert torch.allclose(got.float(), ref, rtol=2 ** -7, atol=1e-3)
+
+
+def test_conv_c_stream_alignment_gate():
+    """cfg 20 moves 16-B pieces of out and of the bf16 residual: with a residual row stride that is not a
+    multiple of 8 elements the automatic pick falls back to cfg 5 (same result) and an explicit cfg 20
+    is rejected instead of running misaligned 16-B accesses."""
+    O = ops()
+    M, N, K = 1024, 256, 64
+    g = torch.Generator(device=DEV).manual_seed(5)
+    a = (torch.randn(M, K, device=DEV, generator=g) * 0.5).bfloat16()
+    w = (torch.randn(N, K, device=DEV, generator=g) * 0.05).bfloat16()
+    b = torch.randn(N, device=DEV, generator=g) * 0.1
+    rbuf = torch.randn(M, N + 4, device=DEV, generator=g).bfloat16()
+    r = rbuf[:, :N]  # ldaux = N + 4: 8-B aligned rows, not 16-B
+    assert O.gemm_kernel_name(M, N, K, "bias_resid_relu", torch.empty(M, N, device=DEV), r).startswith(
+        "gemm_bf16_kernel<128, 128")
+    want = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    got = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    O.gemm(a, w, b, "bias_resid_relu", want, aux=r, cfg=5)
+    O.gemm(a, w, b, "bias_resid_relu", got, aux=r)
+    assert torch.equal(got, want)
+    with pytest.raises(RuntimeError, match="cfg 20"):
+        O.gemm(a, w, b, "bias_resid_relu", got, aux=r, cfg=20)
