@@ -426,7 +426,8 @@ class VivitForVideoClassification(torch.nn.Module):
         if (self.graph_replay and self.kernel_events is None and not streams.serial()
                 and not torch.cuda.is_current_stream_capturing()):
             key = (pix.data_ptr(), tuple(pix.shape), tuple(pix.stride()), pix.dtype, self.concurrent_streams,
-                   self.compute_dtype, self._weights_version(), tuple(sorted(self.gemm_cfg.items())), self.rows,
+                   self.compute_dtype, self._weights_version(),
+                   tuple(sorted((k, tuple(v) if isinstance(v, list) else v) for k, v in self.gemm_cfg.items())), self.rows,
                    self.precise_layers, tuple(sorted(self.precise_ops)),
                    None if self.split_sizes is None else tuple(self.split_sizes))
             return self._graphs.run(key, pix, self._forward_eager, keep=lambda: (self._packed, tuple(self._ws_used)))
@@ -535,6 +536,8 @@ class VivitForVideoClassification(torch.nn.Module):
             """(m, cfg) of one GEMM: every padded row, or B*S up to its tile height (256 rows for the
             256-row configs 0/3/4 and for vc_gemm's own pick, which prefers them, else 128)"""
             cfg = gc.get(name)
+            if isinstance(cfg, (list, tuple)):  # one config per stream part
+                cfg = cfg[part]
             if not tight:
                 return None, -1 if cfg is None else cfg
             h = 128 if cfg in (5, 7, 21) else 256

@@ -1,6 +1,8 @@
 """Interleaved A/B of ViViT-B forward GEMM tile choices in one process (cdna_hip_programming.md §5.4
 rule 24): python tools/ab_model_cfg.py '{}' '{"o_proj": 7, "fc2": 7}' [--B 8] [--streams 2] —
-times model.forward_logits under each model.gemm_cfg in alternating rounds; logits must match."""
+times model.forward_logits under each model.gemm_cfg in alternating rounds; logits must match.
+A list value gives one config per stream part ({"fc1": [26, 25]}); the key "_rows" sets model.rows for
+that variant ("pad" / "tight")."""
 import argparse
 import json
 import sys
@@ -29,15 +31,23 @@ m.graph_replay = bool(a.graph)
 if a.rows:
     m.rows = a.rows
 cfgs = [json.loads(c) for c in a.cfgs]
+
+
+def apply(c):
+    c = dict(c)
+    m.rows = c.pop("_rows", a.rows or "pad")
+    m.gemm_cfg = c
+
+
 outs = []
 for c in cfgs:
-    m.gemm_cfg = c
+    apply(c)
     outs.append(m.forward_logits(pix).clone())
 print("logits identical:", [bool(torch.equal(o, outs[0])) for o in outs], flush=True)
 res = [[] for _ in cfgs]
 for r in range(a.rounds):
     for i in (range(len(cfgs)) if r % 2 == 0 else reversed(range(len(cfgs)))):
-        m.gemm_cfg = cfgs[i]
+        apply(cfgs[i])
         for _ in range(2):
             m.forward_logits(pix)
         torch.cuda.synchronize()

@@ -45,6 +45,33 @@ __device__ void body(float* x, v16f* acc, v8bf a, v8bf b) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int c = 0; c < 4; ++c) a4[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, a4[c], 0, 0, 0);
+    } else if constexpr (ROLE == 8) {  // 32 v_exp_f16 (low halves)
+#pragma unroll
+        for (int i = 0; i < 32; ++i) asm volatile("v_exp_f16 %0, %0" : "+v"(x[i]));
+    } else if constexpr (ROLE == 9) {  // 32 f16 exps on 16 packed registers: low half + high half (SDWA)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            asm volatile("v_exp_f16 %0, %0" : "+v"(x[i]));
+            asm volatile("v_exp_f16_sdwa %0, %0 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1" : "+v"(x[i]));
+        }
+    } else if constexpr (ROLE == 10) {  // f16 softmax step for 32 scores: 16 cvt_pk_f16 + 32 f16 exps
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            unsigned pk;
+            asm volatile("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(pk) : "v"(x[2 * i]), "v"(x[2 * i + 1]));
+            asm volatile("v_exp_f16 %0, %0" : "+v"(pk));
+            asm volatile("v_exp_f16_sdwa %0, %0 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1" : "+v"(pk));
+            x[2 * i] = __builtin_bit_cast(float, pk);
+        }
+    } else if constexpr (ROLE == 11) {  // bf16 softmax step for 32 scores: 32 exp_f32 + 16 cvt_pk_bf16
+#pragma unroll
+        for (int i = 0; i < 32; ++i) asm volatile("v_exp_f32 %0, %0" : "+v"(x[i]));
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            unsigned pk;
+            asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(pk) : "v"(x[2 * i]), "v"(x[2 * i + 1]));
+            x[2 * i] = __builtin_bit_cast(float, pk);
+        }
     } else if constexpr (ROLE == 4) {
 #pragma unroll
         for (int i = 0; i < 32; ++i) asm volatile("v_exp_f32 %0, %0" : "+v"(x[i]));
@@ -120,19 +147,15 @@ static void run(const char* name, int nthreads) {
 }
 
 int main() {
-    run<5, 0>("A: 16 MFMA 1 chain alone", 256);
-    run<3, 0>("A: 16 MFMA 2 chains alone", 256);
-    run<6, 0>("A: 16 MFMA 4 chains alone", 256);
-    run<7, 0>("A: 16 MFMA16x16x32 4 chains alone", 256);
-    run<1, 0>("A: 32 exp alone (1 wave/SIMD)", 256);
-    run<2, 0>("A: 32 add alone", 256);
+    run<1, 0>("A: 32 exp_f32 alone (1 wave/SIMD)", 256);
+    run<8, 0>("A: 32 exp_f16 alone", 256);
+    run<9, 0>("A: 32 exp_f16 lo+hi(sdwa) alone", 256);
+    run<11, 0>("A: bf16 softmax 32 exp_f32 + 16 cvt alone", 256);
+    run<10, 0>("A: f16 softmax 16 cvt + 32 exp_f16 alone", 256);
+    run<1, 1>("A: 32 exp_f32 | B: 32 exp_f32", 512);
+    run<8, 8>("A: 32 exp_f16 | B: 32 exp_f16", 512);
+    run<3, 11>("A: 16 MFMA | B: bf16 softmax", 512);
+    run<3, 10>("A: 16 MFMA | B: f16 softmax", 512);
     run<3, 0>("A: 16 MFMA alone", 256);
-    run<4, 0>("A: softmax mix alone", 256);
-    run<1, 1>("A: 32 exp | B: 32 exp", 512);
-    run<2, 2>("A: 32 add | B: 32 add", 512);
-    run<3, 3>("A: 16 MFMA | B: 16 MFMA", 512);
-    run<3, 1>("A: 16 MFMA | B: 32 exp", 512);
-    run<3, 2>("A: 16 MFMA | B: 32 add", 512);
-    run<3, 4>("A: 16 MFMA | B: softmax mix", 512);
     return 0;
 }
