@@ -111,6 +111,9 @@ SIGNATURES = {
     "vc_embed_bwd": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_p, c_i64, c_p], c_int),
     "vc_adamw_multi": ([c_p, c_i64, c_i64, c_f, c_f, c_f, c_f, c_f, c_i64, c_f, c_p], c_int),
     "vc_adamw": ([c_p, c_p, c_p, c_p, c_i64, c_f, c_f, c_f, c_f, c_f, c_i64, c_f, c_p], c_int),
+    "vc_adamw_step_table": ([c_f, c_f, c_f, c_i64, c_p], c_int),
+    "vc_adamw_tab": ([c_p, c_p, c_p, c_p, c_i64, c_f, c_f, c_f, c_f, c_f, c_p, c_p, c_i64, c_f, c_p], c_int),
+    "vc_adamw_step_tick": ([c_p, c_p], c_int),
     "vc_pack_weight": ([c_p, c_i64, c_i64, c_i64, c_f, c_p, c_p, c_p], c_int),
     # TimeSformer train step
     "vc_temporal_attention_bwd": ([c_p, c_i64, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_p, c_i64, c_p], c_int),

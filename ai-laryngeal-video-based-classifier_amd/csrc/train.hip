@@ -886,6 +886,27 @@ __global__ void __launch_bounds__(256) adamw_kernel(float* __restrict__ p, const
         adamw_elem(p, g, m, v, i, lr, b1, b2, eps, wd, step_size, bc2_sqrt, gscale);
 }
 
+// The same update with the step taken on the device (a captured train-step graph replays one launch for
+// every step): step = *counter + 1, its bias-correction constants (lr / bc1, sqrt(bc2)) read from a host-built
+// table (the values vc_adamw derives for that step, so both paths give the same bits); vc_adamw_step_tick
+// advances the counter after the update.
+__global__ void __launch_bounds__(256) adamw_tab_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v, int64_t n,
+                                                        float lr, float b1, float b2, float eps, float wd,
+                                                        const float* __restrict__ tab, const int64_t* __restrict__ counter,
+                                                        int64_t tab_len, float gscale) {
+    int64_t t = *counter;  // steps done
+    if (t >= tab_len) t = tab_len - 1;  // beyond the table: the host refuses to replay (vc checks), clamp anyway
+    const float step_size = tab[2 * t], bc2_sqrt = tab[2 * t + 1];
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+        adamw_elem(p, g, m, v, i, lr, b1, b2, eps, wd, step_size, bc2_sqrt, gscale);
+}
+
+__global__ void adamw_step_tick_kernel(int64_t* __restrict__ counter) {
+    if (threadIdx.x == 0) *counter += 1;
+}
+
 // Multi-tensor AdamW: tab[i] = {p, g, m, v (addresses), n, chunk0}, chunk0 = the entry's first
 // 1024-element chunk (prefix sum over the entries); one workgroup per chunk finds its entry by
 // binary search over the (uniform, scalar-loaded) table; the element arithmetic is adamw_kernel's.
@@ -1177,6 +1198,36 @@ int vc_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
     adamw_kernel<<<(unsigned)nb, 256, 0, stream>>>(param, grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps,
                                                    weight_decay, step_size, bc2_sqrt, grad_scale);
     return check_launch("vc_adamw");
+}
+
+int vc_adamw_step_table(float beta1, float beta2, float lr, int64_t steps, float* out) {
+    if (!out || steps <= 0) return fail(VC_ERR_INVALID_ARG, "vc_adamw_step_table: null output / steps <= 0");
+    for (int64_t t = 1; t <= steps; ++t) {  // exactly vc_adamw's arithmetic for step t
+        const double bc1 = 1.0 - std::pow((double)beta1, (double)t);
+        const double bc2 = 1.0 - std::pow((double)beta2, (double)t);
+        out[2 * (t - 1)] = (float)(lr / bc1);
+        out[2 * (t - 1) + 1] = (float)std::sqrt(bc2);
+    }
+    return 0;
+}
+
+int vc_adamw_tab(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr, float beta1,
+                 float beta2, float eps, float weight_decay, const float* tab, const int64_t* counter, int64_t tab_len,
+                 float grad_scale, hipStream_t stream) {
+    if (!param || !grad || !exp_avg || !exp_avg_sq || !tab || !counter)
+        return fail(VC_ERR_INVALID_ARG, "vc_adamw_tab: null pointer");
+    if (n <= 0 || tab_len <= 0) return fail(VC_ERR_INVALID_ARG, "vc_adamw_tab: n > 0, tab_len > 0");
+    int64_t nb = (n + 255) / 256;
+    if (nb > 8192) nb = 8192;
+    adamw_tab_kernel<<<(unsigned)nb, 256, 0, stream>>>(param, grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps,
+                                                       weight_decay, tab, counter, tab_len, grad_scale);
+    return check_launch("vc_adamw_tab");
+}
+
+int vc_adamw_step_tick(int64_t* counter, hipStream_t stream) {
+    if (!counter) return fail(VC_ERR_INVALID_ARG, "vc_adamw_step_tick: null counter");
+    adamw_step_tick_kernel<<<1, 64, 0, stream>>>(counter);
+    return check_launch("vc_adamw_step_tick");
 }
 
 int vc_adamw_multi(const int64_t* table, int64_t ntab, int64_t nchunks, float lr, float beta1, float beta2, float eps,

@@ -878,6 +878,34 @@ def adamw(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay,
               int(step), grad_scale, _stream(param))
 
 
+def adamw_step_table(beta1: float, beta2: float, lr: float, steps: int, device) -> torch.Tensor:
+    """Device f32 [steps, 2]: row t-1 = (lr / (1 - beta1^t), sqrt(1 - beta2^t)) exactly as vc_adamw derives them
+    for step t (vc_adamw_step_table computes them in the library with the same double arithmetic)."""
+    import numpy as np
+    host = np.zeros((steps, 2), dtype=np.float32)
+    _lib.call("vc_adamw_step_table", beta1, beta2, lr, steps, host.ctypes.data)
+    return torch.from_numpy(host).to(device)
+
+
+def adamw_tab(param, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps, weight_decay, tab, counter, grad_scale=1.0):
+    """adamw() with the step on the device: step = counter + 1 (int64 [1] device tensor), constants from tab
+    (adamw_step_table); the counter is not advanced here (adamw_step_tick)."""
+    _dev(param, grad, exp_avg, exp_avg_sq, tab, counter)
+    n = param.numel()
+    _need(all(t.dtype == torch.float32 and t.is_contiguous() and t.numel() == n for t in
+              (param, grad, exp_avg, exp_avg_sq)), "adamw_tab: contiguous f32 buffers of one size")
+    _need(tab.dtype == torch.float32 and tab.is_contiguous() and tab.dim() == 2 and tab.shape[1] == 2 and
+          counter.dtype == torch.int64 and counter.numel() >= 1, "adamw_tab: tab f32 [steps, 2], counter int64")
+    _lib.call("vc_adamw_tab", _p(param), _p(grad), _p(exp_avg), _p(exp_avg_sq), n, lr, beta1, beta2, eps,
+              weight_decay, _p(tab), _p(counter), tab.shape[0], grad_scale, _stream(param))
+
+
+def adamw_step_tick(counter: torch.Tensor):
+    _dev(counter)
+    _need(counter.dtype == torch.int64, "adamw_step_tick: int64 counter")
+    _lib.call("vc_adamw_step_tick", _p(counter), _stream(counter))
+
+
 def adamw_multi(params, grads, exp_avgs, exp_avg_sqs, lr, beta1, beta2, eps, weight_decay, step, grad_scale=1.0):
     """vc_adamw on every (param, grad, exp_avg, exp_avg_sq) quadruple in one launch."""
     rows, c0 = [], 0

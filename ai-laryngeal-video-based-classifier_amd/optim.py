@@ -25,6 +25,9 @@ class AdamW(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.grad_scale = grad_scale
         self._flat_state = None  # (param storage ptr, grad storage ptr, exp_avg, exp_avg_sq, step)
+        # device-step mode (vclip_amd.vivit_train.GraphedTrainStep): the flat update reads its step from a
+        # device counter and bias-correction table, so a captured step stays correct on every replay
+        self._dev_step = None  # (tab f32 [steps, 2], counter int64 [1])
 
     @staticmethod
     def _flat_view_set(params):
@@ -78,8 +81,17 @@ class AdamW(torch.optim.Optimizer):
                 if st.get("key") != key:
                     st.update(key=key, exp_avg=torch.zeros_like(fp), exp_avg_sq=torch.zeros_like(fp), step=0)
                 st["step"] += 1
-                ops.adamw(fp, fg, st["exp_avg"], st["exp_avg_sq"], lr, b1, b2, eps, wd, st["step"], self.grad_scale)
+                if self._dev_step is not None:
+                    tab, counter = self._dev_step
+                    ops.adamw_tab(fp, fg, st["exp_avg"], st["exp_avg_sq"], lr, b1, b2, eps, wd, tab, counter,
+                                  self.grad_scale)
+                    ops.adamw_step_tick(counter)
+                else:
+                    ops.adamw(fp, fg, st["exp_avg"], st["exp_avg_sq"], lr, b1, b2, eps, wd, st["step"],
+                              self.grad_scale)
             else:
+                if self._dev_step is not None:
+                    raise RuntimeError("AdamW device-step mode (a captured train step) needs the model's flat buffers")
                 # every tensor of the group in one multi-tensor launch per distinct step count
                 by_step = {}
                 for p in params:

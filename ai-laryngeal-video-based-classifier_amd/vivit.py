@@ -126,6 +126,8 @@ class VivitForVideoClassification(torch.nn.Module):
         self._ws_used = []
         self._streams = None
         self.concurrent_streams = None  # None / 1: one stream; n > 1: batch split over n HIP streams
+        # HIP stream priority per part (torch.cuda.Stream(priority=...): lower is higher; None: all default)
+        self.stream_priorities = None
         # clips per stream part (A/B hook; must sum to the batch): None = as even as possible
         self.split_sizes = None
         self.last_streams = 1
@@ -429,7 +431,8 @@ class VivitForVideoClassification(torch.nn.Module):
                    self.compute_dtype, self._weights_version(),
                    tuple(sorted((k, tuple(v) if isinstance(v, list) else v) for k, v in self.gemm_cfg.items())), self.rows,
                    self.precise_layers, tuple(sorted(self.precise_ops)),
-                   None if self.split_sizes is None else tuple(self.split_sizes))
+                   None if self.split_sizes is None else tuple(self.split_sizes),
+                   None if self.stream_priorities is None else tuple(self.stream_priorities))
             return self._graphs.run(key, pix, self._forward_eager, keep=lambda: (self._packed, tuple(self._ws_used)))
         return self._forward_eager(pix)
 
@@ -444,8 +447,11 @@ class VivitForVideoClassification(torch.nn.Module):
             self.last_split = [B]
             return self._forward_part(pix, 0)
         dev = pix.device
-        if self._streams is None or len(self._streams) < ns or self._streams[0].device != dev:
-            self._streams = [torch.cuda.Stream(device=dev) for _ in range(ns)]
+        prio = tuple(self.stream_priorities) if self.stream_priorities is not None else None
+        if (self._streams is None or len(self._streams) < ns or self._streams[0].device != dev
+                or getattr(self, "_streams_prio", None) != prio):
+            self._streams = [torch.cuda.Stream(device=dev, priority=prio[i] if prio else 0) for i in range(ns)]
+            self._streams_prio = prio
         key = (B, str(dev), "logits")
         if key not in self._ws:
             self._ws[key] = torch.zeros(B, c.num_labels, dtype=torch.float32, device=dev)

@@ -335,3 +335,91 @@ class VivitTrainFn(torch.autograd.Function):
         model, eng = ctx.model, ctx.engine
         model._run_backward(eng, dlogits.float().contiguous())
         return (None, None) + (None,) * len(model._param_list())
+
+
+class GraphedTrainStep:
+    """The reference's train step (vivit_transformer/vivit_classifier/trainers/trainer.py:140-146:
+    zero_grad, model(**inputs), CrossEntropyLoss, backward, optimizer.step) captured once into a hipGraph and
+    replayed: ~450 HIP launches per ViViT-B step over three streams (the data-gradient chain, the weight
+    gradients beside it, the attention backward's dQ) go to the GPU as one graph, with no host launch work
+    per step.  The same kernels in the same order as the eager step, so parameters, moments and losses are
+    bit-identical to it (tests/test_vivit_train_gpu.py).  At ViViT-B B = 4 the eager step is not
+    launch-bound and the replay measured 2 % slower (212.3 vs 216.6 clips/s, round 6), so bench.py runs it
+    only with --train-graph 1; it is for steps whose launches the host cannot keep ahead of.
+
+        step = GraphedTrainStep(model, optimizer, criterion, pixel_values, labels)
+        loss = step(pixel_values, labels)   # new inputs are copied into the captured buffers
+
+    Needs the flat-buffer AdamW of vclip_amd.optim (its step count moves to a device counter, so the
+    captured update stays correct on every replay) and no grad_ready_hooks (the data-parallel all-reduce
+    runs eagerly; bench.py captures at world size 1 only).  Capture happens after `warmup` eager steps
+    (workspaces, packs, kernel attributes are created outside the capture).  Host-side state that the eager
+    step advances (the optimizer's step count, MASTER_EPOCH for the inference packs) is advanced per replay."""
+
+    MAX_STEPS = 1 << 20  # rows of the device bias-correction table (8 MiB)
+
+    def __init__(self, model, optimizer, criterion, pixel_values, labels, warmup: int = 2):
+        from .optim import AdamW
+        if not isinstance(optimizer, AdamW):
+            raise TypeError("GraphedTrainStep needs vclip_amd.optim.AdamW")
+        if model.grad_ready_hooks:
+            raise RuntimeError("GraphedTrainStep: grad_ready_hooks (data-parallel all-reduce) run eagerly")
+        if len(optimizer.param_groups) != 1:
+            raise RuntimeError("GraphedTrainStep: one parameter group (the flat-buffer update)")
+        self.model, self.opt, self.crit = model, optimizer, criterion
+        dev = pixel_values.device
+        self.pix = pixel_values.detach().clone()
+        self.labels = labels.detach().clone()
+
+        def eager():
+            self.opt.zero_grad()
+            out = self.model(pixel_values=self.pix)
+            loss = self.crit(out.logits, self.labels)
+            loss.backward()
+            self.opt.step()
+            return loss
+
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):
+                eager()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        st = self.opt.state.get("flat")
+        if st is None:
+            raise RuntimeError("GraphedTrainStep: the optimizer did not take the flat-buffer path")
+        g = self.opt.param_groups[0]
+        b1, b2 = g["betas"]
+        self.tab = ops.adamw_step_table(b1, b2, g["lr"], self.MAX_STEPS, dev)
+        self.counter = torch.tensor([st["step"]], dtype=torch.int64, device=dev)
+        self._hyper = (g["lr"], b1, b2, g["eps"], g["weight_decay"], self.opt.grad_scale)
+        self.opt.zero_grad()
+        torch.cuda.synchronize(dev)
+        self.graph = torch.cuda.CUDAGraph()
+        self.opt._dev_step = (self.tab, self.counter)
+        try:
+            with torch.cuda.graph(self.graph):
+                out = self.model(pixel_values=self.pix)
+                self.loss = self.crit(out.logits, self.labels)
+                self.loss.backward()
+                self.opt.step()
+        finally:
+            self.opt._dev_step = None
+        st["step"] -= 1  # the capture ran the step's host code once without running the step
+        MASTER_EPOCH[0] -= 1
+
+    def __call__(self, pixel_values=None, labels=None) -> torch.Tensor:
+        g = self.opt.param_groups[0]
+        if (g["lr"], *g["betas"], g["eps"], g["weight_decay"], self.opt.grad_scale) != self._hyper:
+            raise RuntimeError("GraphedTrainStep: optimizer hyper-parameters changed since the capture; build a new step")
+        st = self.opt.state["flat"]
+        if st["step"] >= self.MAX_STEPS:
+            raise RuntimeError("GraphedTrainStep: past the bias-correction table; build a new step")
+        if pixel_values is not None and pixel_values.data_ptr() != self.pix.data_ptr():
+            self.pix.copy_(pixel_values)
+        if labels is not None and labels.data_ptr() != self.labels.data_ptr():
+            self.labels.copy_(labels)
+        self.graph.replay()
+        st["step"] += 1
+        MASTER_EPOCH[0] += 1
+        return self.loss

@@ -578,12 +578,30 @@ def run_train(a, dist, rank, world, dev):
         opt.step()
         losses.append(loss.detach())
 
-    for _ in range(a.warmup):
-        step()
+    # --train-graph 1 at world size 1: the whole step (forward, loss, backward, AdamW) captured once into a
+    # hipGraph and replayed (vivit_train.GraphedTrainStep: the same kernels in the same order, bit-identical to
+    # the eager step).  Off by default: at B = 4 the eager step is not launch-bound and the replay measured
+    # 2 % slower (212.3 vs 216.6 clips/s, round 6)
+    graphed = bool(a.train_graph) and not dist
+    if graphed:
+        from vclip_amd.vivit_train import GraphedTrainStep
+        gstep = GraphedTrainStep(model, opt, crit, pix, labels, warmup=max(2, a.warmup))
+
+        def timed_step():
+            losses.append(gstep().detach().clone())
+    else:
+        timed_step = step
+        for _ in range(a.warmup):
+            step()
     torch.cuda.synchronize()
+    dt = timed_loop(timed_step, a.steps, 1 if graphed else 0, dist, torch.cuda.synchronize)
+    # the attention backward's roofline: HIP events around each of its launches in 2 extra eager steps (an
+    # event inside a replayed graph would be frozen at capture)
     evs = []
     model._engine.kernel_events = evs
-    dt = timed_loop(step, a.steps, 0, dist, torch.cuda.synchronize)
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
     model._engine.kernel_events = None
     attn_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
     # the step's largest kernel by GPU time, the weight gradients (vc_wgrad_bf16: trn::wgrad_big_kernel +
@@ -626,7 +644,8 @@ def run_train(a, dist, rank, world, dev):
             "config": {"workload": f"ViViT-B/16x2 train step, 32x224x224 clips, batch {a.batch} per GPU, AdamW(lr 1e-3, "
                                    "wd 0.01), RCCL gradient all-reduce for N > 1 (BASELINE configs[4])",
                        "model": "ViViT-B/16x2 (joint space-time, 12L, d768, 12H, 3137 tokens)",
-                       "global_batch": a.batch * world, "seq_len": 3137, "parallelism": f"dp{world}"},
+                       "global_batch": a.batch * world, "seq_len": 3137, "parallelism": f"dp{world}",
+                       "hip_graph": graphed},
             "loss_first_last": [round(float(losses[0]), 5), round(float(losses[-1]), 5)],
             "roofline": {"bound": "mfma", "kernel": "attention backward (attn_bwd_dkdv + attn_bwd_dq + prep)",
                          "achieved": round(attn_tflops, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
@@ -661,7 +680,11 @@ def main():
                          "(default 2; swin 4: its late stages' short launches, measured under graph replay)")
     ap.add_argument("--graph", type=int, default=1,
                     help="inference modes: 1 = the headline forward replayed from its captured hipGraph "
-                         "(model.graph_replay; the event-instrumented roofline passes stay eager), 0 = eager")
+                         "(model.graph_replay; the event-instrumented roofline passes stay eager), 0 = eager; "
+                         "train: see --train-graph")
+    ap.add_argument("--train-graph", type=int, default=0,
+                    help="train at world size 1: 1 = the whole step captured once into a hipGraph and replayed "
+                         "(vivit_train.GraphedTrainStep), 0 = the eager step (default)")
     ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)  # CPU test of the spawn path
     a = ap.parse_args()
     if a.streams is None:

@@ -619,6 +619,17 @@ int vc_gelu_erf_bwd(const void* dy, int dy_bf16, int64_t lddy, const uint16_t* x
 int vc_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr, float beta1,
              float beta2, float eps, float weight_decay, int64_t step, float grad_scale, hipStream_t stream);
 
+/* vc_adamw with the step on the device, for a train step captured into a hipGraph and replayed: the step is
+ * *counter + 1 (counter = device int64, steps done), its constants (lr / (1 - beta1^t), sqrt(1 - beta2^t))
+ * are row t - 1 of `tab` (device f32 [tab_len][2], filled by vc_adamw_step_table with vc_adamw's own
+ * double-precision arithmetic, so both paths give the same bits); vc_adamw_step_tick adds 1 to the counter
+ * (launched after the update).  vc_adamw_step_table writes the host table for steps 1 .. steps. */
+int vc_adamw_step_table(float beta1, float beta2, float lr, int64_t steps, float* out);
+int vc_adamw_tab(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, float lr, float beta1,
+                 float beta2, float eps, float weight_decay, const float* tab, const int64_t* counter, int64_t tab_len,
+                 float grad_scale, hipStream_t stream);
+int vc_adamw_step_tick(int64_t* counter, hipStream_t stream);
+
 /* Multi-tensor vc_adamw in one launch (the per-tensor optimizer path of the autograd families):
  * table = device int64 [ntab][6] = {param, grad, exp_avg, exp_avg_sq (f32 device addresses),
  * numel, chunk0}, chunk0 = prefix sum of ceil(numel / 1024) over the preceding entries, nchunks =

@@ -255,3 +255,42 @@ def test_train_step_configs4_geometry():
         rlosses.append(float(rl))
     print("configs[4] AdamW loss trajectory (HIP, oracle):", losses, rlosses)
     np.testing.assert_allclose(losses, rlosses, rtol=0, atol=2e-2)
+
+
+@pytest.mark.parametrize("cfg,B", [(SMALL, 2), (WIDE, 2)], ids=["small-B2", "wide-B2"])
+def test_graphed_train_step_bit_identical(cfg, B):
+    """vivit_train.GraphedTrainStep (the reference's step captured into a hipGraph and replayed, AdamW's step
+    count on the device) == the same loop run eagerly: losses, parameters and AdamW moments bit for bit over
+    4 steps (2 eager warm-up steps inside the capture helper + 2 replays, one with new inputs copied in), and
+    the host-side step count / inference-pack epoch advance as in the eager loop."""
+    from vclip_amd import vivit_train
+    from vclip_amd.optim import AdamW
+    runs = {}
+    for graphed in (False, True):
+        model, sd, pix, labels = _setup(cfg, B)
+        x, y = pix.to(DEV), labels.to(DEV)
+        x2 = torch.flip(x, dims=[0]).contiguous()
+        opt = AdamW(model.parameters(), lr=1e-3, weight_decay=0.01)
+        crit = torch.nn.CrossEntropyLoss()
+        losses = []
+        ep0 = vivit_train.MASTER_EPOCH[0]
+        if graphed:
+            step = vivit_train.GraphedTrainStep(model, opt, crit, x, y, warmup=2)
+            losses.append(float(step(x, y)))
+            losses.append(float(step(x2, y)))
+        else:
+            for xi in (x, x, x, x2):
+                opt.zero_grad()
+                loss = crit(model(pixel_values=xi).logits, y)
+                loss.backward()
+                opt.step()
+                losses.append(float(loss))
+            losses = losses[2:]
+        torch.cuda.synchronize()
+        st = opt.state["flat"]
+        runs[graphed] = (losses, model._flat.clone(), st["exp_avg"].clone(), st["exp_avg_sq"].clone(), st["step"],
+                         vivit_train.MASTER_EPOCH[0] - ep0)
+    e, g = runs[False], runs[True]
+    assert e[0] == g[0], (e[0], g[0])
+    assert torch.equal(e[1], g[1]) and torch.equal(e[2], g[2]) and torch.equal(e[3], g[3])
+    assert e[4] == g[4] == 4 and e[5] == g[5] == 4

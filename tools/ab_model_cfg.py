@@ -2,7 +2,8 @@
 rule 24): python tools/ab_model_cfg.py '{}' '{"o_proj": 7, "fc2": 7}' [--B 8] [--streams 2] —
 times model.forward_logits under each model.gemm_cfg in alternating rounds; logits must match.
 A list value gives one config per stream part ({"fc1": [26, 25]}); the key "_rows" sets model.rows for
-that variant ("pad" / "tight")."""
+that variant ("pad" / "tight"), "_prio" the per-part HIP stream priorities ([-1, 0]: part 0 high), "_split"
+the clips per part."""
 import argparse
 import json
 import sys
@@ -36,6 +37,8 @@ cfgs = [json.loads(c) for c in a.cfgs]
 def apply(c):
     c = dict(c)
     m.rows = c.pop("_rows", a.rows or "pad")
+    m.stream_priorities = c.pop("_prio", None)
+    m.split_sizes = c.pop("_split", None)
     m.gemm_cfg = c
 
 
