@@ -126,7 +126,10 @@ class VivitForVideoClassification(torch.nn.Module):
         self._ws_used = []
         self._streams = None
         self.concurrent_streams = None  # None / 1: one stream; n > 1: batch split over n HIP streams
-        # HIP stream priority per part (torch.cuda.Stream(priority=...): lower is higher; None: all default)
+        # HIP stream priority per part (torch.cuda.Stream(priority=...): lower is higher).  None: part 0 (the
+        # largest) high, the others normal -- the eager two-stream B = 8 forward 843.6 -> 968.6 clips/s (and far
+        # steadier: min 8.49 vs median 9.48 ms without); under graph replay it makes no difference (976.1 vs
+        # 975.0).  profiles/r06_stream_prio.txt
         self.stream_priorities = None
         # clips per stream part (A/B hook; must sum to the batch): None = as even as possible
         self.split_sizes = None
@@ -447,7 +450,8 @@ class VivitForVideoClassification(torch.nn.Module):
             self.last_split = [B]
             return self._forward_part(pix, 0)
         dev = pix.device
-        prio = tuple(self.stream_priorities) if self.stream_priorities is not None else None
+        prio = (tuple(self.stream_priorities) if self.stream_priorities is not None
+                else (-1,) + (0,) * (ns - 1))
         if (self._streams is None or len(self._streams) < ns or self._streams[0].device != dev
                 or getattr(self, "_streams_prio", None) != prio):
             self._streams = [torch.cuda.Stream(device=dev, priority=prio[i] if prio else 0) for i in range(ns)]
