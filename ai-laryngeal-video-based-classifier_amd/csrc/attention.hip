@@ -393,8 +393,12 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
             // the next step's 4 P packs.  Bit-identical; ViViT-B B = 8 247.8 -> 244.2 us, B = 4
             // 133.9 -> 129.7 us per launch (tools/ab_attn.py, interleaved in one process, round 3;
             // fences around every MFMA as well: 245.1 / 129.0, not kept).
-            constexpr bool PIPE = !RB && NEXT == 0 && QB == 1;
-            if (t + NS - 1 < ntiles) stage(t + NS - 1);
+            // NEXT = 3: a main-loop iteration whose staging (tile t+3), retire count and barrier are known to
+            // be needed: no runtime tests (their scalar compares and branches, ~5 per tile, leave the loop)
+            constexpr bool FULLNEXT = NEXT == 0 || NEXT == 3;
+            constexpr bool PIPE = !RB && FULLNEXT && QB == 1;
+            if constexpr (NEXT == 3) stage(t + NS - 1);
+            else if (t + NS - 1 < ntiles) stage(t + NS - 1);
             v16f snext[QB][2];
             v8s vcur[2], vnxt[2];  // PIPE: V^T fragments (d-blocks 0 / 1) of the current / next 16-key step
             if constexpr (PIPE) {
@@ -426,7 +430,7 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
                     __builtin_amdgcn_sched_barrier(0);
                 }
                 ex(28); ex(29); ex(30); ex(31);
-            } else if constexpr (NEXT == 0) {
+            } else if constexpr (FULLNEXT) {
                 qk_mfma(nslot, snext);
             } else if constexpr (NEXT == 1) {
                 qk(nslot, t + 1, snext);
@@ -533,7 +537,10 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
             // ---- tile t+2 must be resident for the next iteration's K read (t+3 may stay in
             //      flight); the barrier also retires every wave's reads of slot t before the
             //      next iteration stages t+4 into it
-            if (t + 2 < ntiles) {
+            if constexpr (NEXT == 3) {
+                attn_wait_vm<4>();
+                attn_sync();
+            } else if (t + 2 < ntiles) {
                 if (t + 3 < ntiles) attn_wait_vm<4>();
                 else attn_wait_vm<0>();
                 attn_sync();
@@ -545,8 +552,17 @@ attn_fwd_d64_kernel(const uint16_t* __restrict__ qkv, int64_t ld, int S, int H, 
         };
 
         using full_c = std::integral_constant<int, 0>;
+        using fast_c = std::integral_constant<int, 3>;
         const int nfull = S / AK;  // full tiles
         int t = 0;
+        // iterations t..t+3 all have a full next tile and stage tile (t+3)+3 < ntiles with tile (t+3)+3 in
+        // flight: no runtime tests inside
+        for (; t + 5 <= nfull && t + 6 < ntiles; t += NS) {
+            iter(fast_c{}, smem + 0 * KV_SLOT, smem + 1 * KV_SLOT, t);
+            iter(fast_c{}, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, t + 1);
+            iter(fast_c{}, smem + 2 * KV_SLOT, smem + 3 * KV_SLOT, t + 2);
+            iter(fast_c{}, smem + 3 * KV_SLOT, smem + 0 * KV_SLOT, t + 3);
+        }
         for (; t + 5 <= nfull; t += NS) {  // iterations t..t+3 all have a full next tile
             iter(full_c{}, smem + 0 * KV_SLOT, smem + 1 * KV_SLOT, t);
             iter(full_c{}, smem + 1 * KV_SLOT, smem + 2 * KV_SLOT, t + 1);

@@ -393,9 +393,13 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
     wait_tiles<LPT, ST - 2>(nk - 1);
     block_sync_lds();
 
-    for (int t = 0; t < nk; ++t) {
+    // one k-tile; FAST (compile time) when t <= nk - ST: tile t+ST-1 is staged and the retire count
+    // is the steady-state one, so the steady loop carries no runtime tests (round 6: their scalar
+    // compares and branches cost the ping-pong kernel 4 %)
+    auto ktile = [&](auto FAST, int t) __attribute__((always_inline)) {
         const int slot = t % ST;
-        if (t + ST - 1 < nk) stage(t + ST - 1, (t + ST - 1) % ST);
+        if constexpr (decltype(FAST)::value) stage(t + ST - 1, (t + ST - 1) % ST);
+        else if (t + ST - 1 < nk) stage(t + ST - 1, (t + ST - 1) % ST);
         const char* At = smem + slot * SLOT;
         const char* Wt = At + BM * 128;
 
@@ -420,8 +424,47 @@ gemm_bf16_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __
                         acc[i][j] = mfma16x32<ET>(wf[kk][j], af[kk][i], acc[i][j]);
         }
         // retire tile t+1 (tiles t+2 .. t+ST-1 may stay in flight), then all waves pass the barrier
-        wait_tiles<LPT, ST - 2>(nk - 2 - t);
+        if constexpr (decltype(FAST)::value) wait_vm<LPT * (ST - 2)>();
+        else wait_tiles<LPT, ST - 2>(nk - 2 - t);
         block_sync_lds();
+    };
+    // the 64-row tiles (cfgs 7 / 21: K = 96 .. 384, two to six k-tiles) keep the one tested loop: split
+    // they ran 1.8-3 % slower (round 6, tools/r06_i.sh)
+    if constexpr (BM >= 128) {
+        int t = 0;
+        for (; t <= nk - ST; ++t) ktile(std::true_type{}, t);
+        for (; t < nk; ++t) ktile(std::false_type{}, t);
+    } else {
+        for (int t = 0; t < nk; ++t) {
+            const int slot = t % ST;
+            if (t + ST - 1 < nk) stage(t + ST - 1, (t + ST - 1) % ST);
+            const char* At = smem + slot * SLOT;
+            const char* Wt = At + BM * 128;
+
+            v8s af[2][MI], wf[2][NI];
+            {
+                // two 32-deep k-steps: lane (c16, q) reads row 16i + c16, 16-B chunk 4kk + q (the 16
+                // rows of a ds_read_b128 lane group land on 16 distinct bank slots under swz)
+#pragma unroll
+                for (int i = 0; i < MI; ++i) af[0][i] = lds_frag(At, wm * TM + i * 16 + c16, q);
+#pragma unroll
+                for (int j = 0; j < NI; ++j) wf[0][j] = lds_frag(Wt, wn * TN + j * 16 + c16, q);
+#pragma unroll
+                for (int i = 0; i < MI; ++i) af[1][i] = lds_frag(At, wm * TM + i * 16 + c16, 4 + q);
+#pragma unroll
+                for (int j = 0; j < NI; ++j) wf[1][j] = lds_frag(Wt, wn * TN + j * 16 + c16, 4 + q);
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+                    for (int i = 0; i < MI; ++i)
+#pragma unroll
+                        for (int j = 0; j < NI; ++j)
+                            acc[i][j] = mfma16x32<ET>(wf[kk][j], af[kk][i], acc[i][j]);
+            }
+            // retire tile t+1 (tiles t+2 .. t+ST-1 may stay in flight), then all waves pass the barrier
+            wait_tiles<LPT, ST - 2>(nk - 2 - t);
+            block_sync_lds();
+        }
     }
 
     if constexpr (RPRE) {
@@ -1132,19 +1175,26 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
 
     const int nk = K / BKH;  // even, >= 4
     v8s alo[4], ahi[4], wA[NI], wB[NI];
-    auto phase_a = [&](int u, v8s (&fw)[NI]) __attribute__((always_inline)) {
+    // FAST (compile time): a K-half of the steady state, u + 3 < nk -- every staging, retire count and
+    // barrier of the phase is known to be needed, so the phase carries no runtime tests (their scalar
+    // compares and branches sat between the fragment reads and the barrier the other group waits on)
+    auto phase_a = [&](auto FAST, int u, v8s (&fw)[NI]) __attribute__((always_inline)) {
         read_a(u, 0, alo);
         read_w(u, fw);
-        if (u + 2 < nk) stage_w(u + 2);
+        if constexpr (decltype(FAST)::value) stage_w(u + 2);
+        else if (u + 2 < nk) stage_w(u + 2);
         __builtin_amdgcn_sched_barrier(0);
         mma(C0{}, alo, fw);
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
     };
-    auto phase_b = [&](int u, const v8s (&fw)[NI]) __attribute__((always_inline)) {
+    auto phase_b = [&](auto FAST, int u, const v8s (&fw)[NI]) __attribute__((always_inline)) {
         read_a(u, 64, ahi);
-        if (u + 3 < nk) {
+        if constexpr (decltype(FAST)::value) {
+            stage_a(u + 3);
+            wait_vm<6>();
+        } else if (u + 3 < nk) {
             stage_a(u + 3);
             wait_vm<6>();
         } else if (u + 2 < nk) {
@@ -1155,10 +1205,13 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
         __builtin_amdgcn_sched_barrier(0);
         mma(C4{}, ahi, fw);
         // the lagging group skips its last barrier: both groups then pass the same number
-        if (u + 1 < nk || wm == 0) __builtin_amdgcn_s_barrier();
+        if constexpr (decltype(FAST)::value) __builtin_amdgcn_s_barrier();
+        else if (u + 1 < nk || wm == 0) __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
     };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
 
     // prologue: A0 W0 A1 W1 A2 in flight, retire A0 W0, publish; group 1 falls one barrier behind
     stage_a(0);
@@ -1174,11 +1227,18 @@ gemm_pp_kernel(const uint16_t* __restrict__ A, int64_t lda, const uint16_t* __re
     if (wm == 1) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
 
-    for (int u = 0; u < nk; u += 2) {
-        phase_a(u, wA);
-        phase_b(u, wA);
-        phase_a(u + 1, wB);
-        phase_b(u + 1, wB);
+    int u = 0;
+    for (; u + 4 < nk; u += 2) {  // K-halves u, u + 1 with u + 1 + 3 < nk
+        phase_a(T_{}, u, wA);
+        phase_b(T_{}, u, wA);
+        phase_a(T_{}, u + 1, wB);
+        phase_b(T_{}, u + 1, wB);
+    }
+    for (; u < nk; u += 2) {
+        phase_a(F_{}, u, wA);
+        phase_b(F_{}, u, wA);
+        phase_a(F_{}, u + 1, wB);
+        phase_b(F_{}, u + 1, wB);
     }
     store_tile16<EPI, MI, NI, ET>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bq, out, ldo, aux, ldaux, G, gstride,
                                   goff);
@@ -1658,9 +1718,10 @@ conv_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx, ConvGeomG g, const
     wait_tiles<LPT, ST - 2>(nk - 1);
     block_sync_lds();
 
-    for (int t = 0; t < nk; ++t) {
+    auto ktile = [&](auto FAST, int t) {  // FAST: t <= nk - ST, no runtime tests (see gemm_bf16_kernel)
         const int slot = t % ST;
-        if (t + ST - 1 < nk) stage(t + ST - 1, (t + ST - 1) % ST);
+        if constexpr (decltype(FAST)::value) stage(t + ST - 1, (t + ST - 1) % ST);
+        else if (t + ST - 1 < nk) stage(t + ST - 1, (t + ST - 1) % ST);
         const char* At = smem + slot * SLOT;
         const char* Wt = At + BM * 128;
         v8s af[2][MI], wf[2][NI];
@@ -1679,9 +1740,13 @@ conv_gemm_kernel(const uint16_t* __restrict__ X, int64_t ldx, ConvGeomG g, const
 #pragma unroll
                 for (int j = 0; j < NI; ++j) acc[i][j] = mfma16x32<VC_ELEM_BF16>(wf[kk][j], af[kk][i], acc[i][j]);
         // retire tile t + 1; the tiles staged after it (up to ST - 2) may stay in flight
-        wait_tiles<LPT, ST - 2>(nk - 2 - t);
+        if constexpr (decltype(FAST)::value) wait_vm<LPT * (ST - 2)>();
+        else wait_tiles<LPT, ST - 2>(nk - 2 - t);
         block_sync_lds();
-    }
+    };
+    int t = 0;
+    for (; t <= nk - ST; ++t) ktile(std::true_type{}, t);
+    for (; t < nk; ++t) ktile(std::false_type{}, t);
     store_tile16<EPI, MI, NI, VC_ELEM_BF16>(acc, m0 + wm * TM, n0 + wn * TN, c16, q, bq, out, ldo, aux, ldaux, 1, 0,
                                             0);
 }

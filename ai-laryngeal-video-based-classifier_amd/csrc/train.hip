@@ -504,8 +504,9 @@ wgrad_big_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __
             for (int j = 0; j < NI; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     };
     // retire half-tile u + 1 once u + 3 may have been staged (4 pieces per wave per half-tile)
-    auto retire = [&](int u) __attribute__((always_inline)) {
-        if (u + 3 < nk) wg_wait_vm<8>();
+    auto retire = [&](auto FAST, int u) __attribute__((always_inline)) {
+        if constexpr (decltype(FAST)::value) wg_wait_vm<8>();
+        else if (u + 3 < nk) wg_wait_vm<8>();
         else if (u + 2 < nk) wg_wait_vm<4>();
         else wg_wait_vm<0>();
         wg_sync();
@@ -523,17 +524,22 @@ wgrad_big_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __
         read_frags(0, fa0, fb0);
         // one 32-deep k-step per half-tile: its MFMAs run while the next half-tile's fragments
         // are read behind the barrier that publishes it; fragment sets alternate
-        int t = 0;
-        for (; t + 2 < nk; t += 2) {
-            if (t + 3 < nk) stage(t + 3);
+        // FAST (compile time) while t + 4 < nk: every stage and retire is the steady-state one, so
+        // that loop carries no runtime tests
+        auto step2 = [&](auto FAST, int t) __attribute__((always_inline)) {
+            constexpr bool fast = decltype(FAST)::value;
+            if (fast || t + 3 < nk) stage(t + 3);
             mfmas(fa0, fb0);
-            retire(t);
+            retire(FAST, t);
             read_frags(t + 1, fa1, fb1);
-            if (t + 4 < nk) stage(t + 4);
+            if (fast || t + 4 < nk) stage(t + 4);
             mfmas(fa1, fb1);
-            retire(t + 1);
+            retire(FAST, t + 1);
             read_frags(t + 2, fa0, fb0);
-        }
+        };
+        int t = 0;
+        for (; t + 4 < nk; t += 2) step2(std::true_type{}, t);
+        for (; t + 2 < nk; t += 2) step2(std::false_type{}, t);
         mfmas(fa0, fb0);
         if (t + 1 < nk) {
             wg_wait_vm<0>();
@@ -662,19 +668,24 @@ wgrad_pp_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __r
         __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_sched_barrier(0);
     };
-    auto phase_a = [&](int u) __attribute__((always_inline)) {
+    // FAST (compile time) while u + 3 < nk: steady-state staging and retire counts, no runtime tests
+    auto phase_a = [&](auto FAST, int u) __attribute__((always_inline)) {
         read_x(u, 0);
         read_g(u);
-        if (u + 2 < nk) stage_g(u + 2);
+        if constexpr (decltype(FAST)::value) stage_g(u + 2);
+        else if (u + 2 < nk) stage_g(u + 2);
         __builtin_amdgcn_sched_barrier(0);
         mma(0);
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
     };
-    auto phase_b = [&](int u) __attribute__((always_inline)) {
+    auto phase_b = [&](auto FAST, int u) __attribute__((always_inline)) {
         read_x(u, 4);
-        if (u + 3 < nk) {
+        if constexpr (decltype(FAST)::value) {
+            stage_x(u + 3);
+            wg_wait_vm<6>();
+        } else if (u + 3 < nk) {
             stage_x(u + 3);
             wg_wait_vm<6>();
         } else if (u + 2 < nk) {
@@ -685,7 +696,8 @@ wgrad_pp_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __r
         __builtin_amdgcn_sched_barrier(0);
         mma(4);
         // the lagging group skips its last barrier: both groups then pass the same number
-        if (u + 1 < nk || w2 == 0) __builtin_amdgcn_s_barrier();
+        if constexpr (decltype(FAST)::value) __builtin_amdgcn_s_barrier();
+        else if (u + 1 < nk || w2 == 0) __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
     };
@@ -703,9 +715,14 @@ wgrad_pp_kernel(const uint16_t* __restrict__ G, int64_t ldg, const uint16_t* __r
     __builtin_amdgcn_sched_barrier(0);
     if (w2 == 1) __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    for (int u = 0; u < nk; ++u) {
-        phase_a(u);
-        phase_b(u);
+    int u = 0;
+    for (; u + 3 < nk; ++u) {
+        phase_a(std::true_type{}, u);
+        phase_b(std::true_type{}, u);
+    }
+    for (; u < nk; ++u) {
+        phase_a(std::false_type{}, u);
+        phase_b(std::false_type{}, u);
     }
 
     float* o = out + (int64_t)blockIdx.y * split_stride;

@@ -5,7 +5,7 @@
 set -e
 name=$1; src=$2; shift 2
 root=$(cd "$(dirname "$0")/.." && pwd)
-out=$root/ab/attn; mkdir -p "$out"
+out=${AB_OUT:-$root/tools/abso}; mkdir -p "$out"
 inc="-I $root/include -I $root/ai-laryngeal-video-based-classifier_amd/csrc"
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $inc -Wno-unused-result "$@" -c "$src" -o "$out/$name.o" 2>/dev/null
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -c "$root/tools/ab_attn_stub.cpp" -o "$out/stub.o"

@@ -3,7 +3,7 @@ rule 24): python tools/ab_model_cfg.py '{}' '{"o_proj": 7, "fc2": 7}' [--B 8] [-
 times model.forward_logits under each model.gemm_cfg in alternating rounds; logits must match.
 A list value gives one config per stream part ({"fc1": [26, 25]}); the key "_rows" sets model.rows for
 that variant ("pad" / "tight"), "_prio" the per-part HIP stream priorities ([-1, 0]: part 0 high), "_split"
-the clips per part."""
+the clips per part, "_streams" the number of parts."""
 import argparse
 import json
 import sys
@@ -39,6 +39,7 @@ def apply(c):
     m.rows = c.pop("_rows", a.rows or "pad")
     m.stream_priorities = c.pop("_prio", None)
     m.split_sizes = c.pop("_split", None)
+    m.concurrent_streams = c.pop("_streams", a.streams)
     m.gemm_cfg = c
 
 
