@@ -48,6 +48,7 @@ SIGNATURES = {
                      c_i64, c_i64, c_i64, c_int, c_int, c_p], c_int),
     "vc_layernorm_f32_h16": ([c_p, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_int, c_p, c_i64, c_p], c_int),
     "vc_attention_fwd_h16": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_int, c_int, c_p, c_i64, c_p], c_int),
+    "vc_spin": ([c_i64, c_i64, c_p], c_int),
     "vc_cls_init": ([c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p], c_int),
     "vc_cls_head": ([c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_p, c_f, c_p, c_p, c_i64, c_p, c_p], c_int),
     "vc_temporal_attention": ([c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i64, c_f, c_int, c_p, c_i64, c_p], c_int),

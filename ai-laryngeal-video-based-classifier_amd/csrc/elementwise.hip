@@ -411,11 +411,25 @@ __global__ void __launch_bounds__(256) cls_head_kernel(const float* __restrict__
     }
 }
 
+// `blocks` one-wave workgroups, each sleeping `iters` x s_sleep 127 (about 8k clocks each): the
+// hardware-queue probe of vclip_amd.streams.pick_streams -- spins on two streams overlap iff the streams
+// sit on different hardware queues (kernels of streams that share one run one after the other)
+__global__ void __launch_bounds__(64) spin_kernel(int64_t iters) {
+    for (int64_t i = 0; i < iters; ++i) __builtin_amdgcn_s_sleep(127);
+}
+
 }  // namespace vc
 
 using namespace vc;
 
 extern "C" {
+
+int vc_spin(int64_t iters, int64_t blocks, hipStream_t stream) {
+    if (iters < 0 || iters > (int64_t{1} << 20)) return fail(VC_ERR_INVALID_ARG, "vc_spin: iters outside [0, 2^20]");
+    if (blocks < 1 || blocks > (int64_t{1} << 20)) return fail(VC_ERR_INVALID_ARG, "vc_spin: blocks outside [1, 2^20]");
+    spin_kernel<<<(unsigned)blocks, 64, 0, stream>>>(iters);
+    return check_launch("vc_spin");
+}
 
 const char* vc_version(void) { return "vclip 0.1.0 gfx950"; }
 

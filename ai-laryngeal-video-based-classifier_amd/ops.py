@@ -391,6 +391,12 @@ def attention(qkv: torch.Tensor, B: int, S: int, H: int, scale: float, out: torc
     return out
 
 
+def spin(iters: int, device, blocks: int = 1) -> None:
+    """`blocks` one-wave workgroups sleeping `iters` x s_sleep 127 each, on the current stream of `device`
+    (streams.pick_streams)."""
+    _lib.call("vc_spin", int(iters), int(blocks), torch.cuda.current_stream(device).cuda_stream)
+
+
 def cls_init(cls: torch.Tensor, pos: torch.Tensor, x: torch.Tensor, B: int, S: int) -> torch.Tensor:
     _dev(cls, pos, x)
     D = cls.numel()

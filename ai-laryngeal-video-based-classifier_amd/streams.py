@@ -8,8 +8,11 @@ kernels (ViViT-B B = 8: 840 -> 916 clips/s with 2 streams, tools/exp_streams.py,
 from __future__ import annotations
 
 import contextlib
+import time
 
 import torch
+
+from . import ops
 
 # instrumentation switch (bench.py's per-kernel tables): every part of a split forward runs on the
 # CALLER's stream, one after the other -- the headline's launches (same part sizes, kernels and
@@ -42,6 +45,104 @@ def split_bounds(B: int, ns: int, sizes=None) -> list:
     return [sum(sizes[:i]) for i in range(ns + 1)]
 
 
+# Part streams (round 6).  Whether the parts of a split forward overlap depends on the streams they run on:
+#  * streams on ONE hardware queue serialize.  HIP maps streams onto a few queues per process
+#    (GPU_MAX_HW_QUEUES, 4 here) and which of torch's pool streams share one depends on how many streams
+#    the process made before (tools/hwq_probe.py: of six consecutive pool streams, three pairs shared).
+#    pick_streams measures: a one-wave spin (vc_spin) on each of two streams takes one spin's time on
+#    different queues and two on a shared one;
+#  * beyond that, through state no probe here predicted: with every pair on different queues the ViViT-B
+#    B = 8 5 + 3-clip forward ran 850-900 or 960-1000 clips/s from one stream set to the next, ResNet3D-50
+#    990 or 1517, TimeSformer-B 1430 or 1829, each set stable over repeated replays in its process
+#    (tools/exp_vivit_hwq.py, tools/ab_stream_modes.py; priorities did not decide it either, and a probe
+#    of whether one queue's dispatch waits for the other's, tools/hwq_pipe_probe.py, did not predict it).
+#    So GraphReplay times the captured part graphs on several picked stream sets and keeps the fastest.
+# The picked set is cached per (device, priorities).
+_PICKED = {}
+PICK_STATUS = {}  # (device, priorities) -> True when every picked pair measured concurrent
+
+
+def default_priorities(n: int) -> tuple:
+    return (0,) * n
+
+
+def _spin_time(sts, iters, device):
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for st in sts:
+        with torch.cuda.stream(st):
+            ops.spin(iters, device)
+    torch.cuda.synchronize(device)
+    return time.perf_counter() - t0
+
+
+def pick_streams(device, n: int, priorities=None, candidates: int = 12, fresh: bool = False) -> list:
+    """`n` streams of torch's pool, stream i at priority priorities[i] (default_priorities(n) when None), on
+    pairwise different hardware queues, measured; cached unless `fresh` (a new set from the next pool
+    streams, for GraphReplay._tune).  Falls back to unmeasured candidates (PICK_STATUS False) when no such
+    set turns up, and to fresh pool streams while a graph capture is running (no synchronisation then)."""
+    device = torch.device(device)
+    prios = tuple(int(p) for p in (default_priorities(n) if priorities is None else priorities))
+    if len(prios) != n:
+        raise ValueError(f"pick_streams: {len(prios)} priorities for {n} streams")
+    key = (device.index, prios)
+    got = None if fresh else _PICKED.get(key)
+    if got is not None:
+        return got
+    if n <= 1 or torch.cuda.is_current_stream_capturing():
+        return [torch.cuda.Stream(device=device, priority=p) for p in prios]
+    cur = [torch.cuda.current_stream(device)]
+    iters = 16
+    _spin_time(cur, iters, device)  # first launch: kernel load
+    while iters < (1 << 16) and _spin_time(cur, iters, device) < 5e-4:
+        iters *= 2
+    one = min(_spin_time(cur, iters, device) for _ in range(3))
+    picked, ok = [], True
+    for p in prios:
+        cands = [torch.cuda.Stream(device=device, priority=p) for _ in range(candidates)]
+        for c in cands:
+            if all(min(_spin_time([q, c], iters, device) for _ in range(2)) < 1.5 * one for q in picked):
+                picked.append(c)
+                break
+        else:
+            picked.append(cands[0])
+            ok = False
+    PICK_STATUS[key] = ok
+    if not fresh:
+        _PICKED[key] = picked
+    return picked
+
+
+# A/B switch: False captures a split forward as ONE graph holding every part's branch (rounds 2-5)
+PART_GRAPHS = [True]
+# stream sets GraphReplay._tune times the part graphs on (1: the capture's own, no tuning)
+TUNE_CANDIDATES = [6]
+
+# set by GraphReplay while it captures a split forward: fork_parts then captures each part into a graph of
+# its own (stream, graph) instead of running it
+_PART_CAPTURE = [None]
+
+
+def fork_parts(sts, cur, fns) -> None:
+    """fns[i]() on stream sts[i] after everything queued on `cur`; `cur` then waits for every part.
+    Under GraphReplay's capture each part becomes a graph of its own, replayed on its own stream: one
+    graph holding both branches runs them on queues HIP picks at instantiation, which serialized the
+    parts in about half the processes (tools/exp_vivit_hwq.py)."""
+    cap = _PART_CAPTURE[0]
+    for st, fn in zip(sts, fns):
+        st.wait_stream(cur)
+        with torch.cuda.stream(st):
+            if cap is None:
+                fn()
+            else:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=st, capture_error_mode="thread_local"):
+                    fn()
+                cap.append((st, g))
+    for st in sts:
+        cur.wait_stream(st)
+
+
 def run_split(owner, x: torch.Tensor, ns: int, part_fn, num_labels: int, prepare=None) -> torch.Tensor:
     """part_fn(x_part, part_index, out=logits_rows) for each of `ns` contiguous batch parts, part i on
     owner._streams[i]; returns the [B, num_labels] logits (a buffer of `owner`, reused per call).
@@ -55,8 +156,8 @@ def run_split(owner, x: torch.Tensor, ns: int, part_fn, num_labels: int, prepare
         prepare()
     B = x.shape[0]
     ns = max(1, min(int(ns), B))
-    if owner._streams is None or len(owner._streams) < ns or owner._streams[0].device != dev:
-        owner._streams = [torch.cuda.Stream(device=dev) for _ in range(ns)]
+    prios = getattr(owner, "stream_priorities", None)
+    owner._streams = pick_streams(dev, ns, None if prios is None else tuple(prios)[:ns])
     key = (B, str(dev), "split_logits")
     if key not in owner._split_out:
         owner._split_out[key] = torch.zeros(B, num_labels, dtype=torch.float32, device=dev)
@@ -67,14 +168,11 @@ def run_split(owner, x: torch.Tensor, ns: int, part_fn, num_labels: int, prepare
         for i in range(ns):
             part_fn(x[bounds[i]:bounds[i + 1]], i, out=logits[bounds[i]:bounds[i + 1]])
         return logits
-    for i in range(ns):
-        st = owner._streams[i]
-        st.wait_stream(cur)
+    for st in owner._streams[:ns]:
         x.record_stream(st)  # x may be freed by the caller while the side streams still read it
-        with torch.cuda.stream(st):
-            part_fn(x[bounds[i]:bounds[i + 1]], i, out=logits[bounds[i]:bounds[i + 1]])
-    for i in range(ns):
-        cur.wait_stream(owner._streams[i])
+    fork_parts(owner._streams[:ns], cur,
+               [lambda i=i: part_fn(x[bounds[i]:bounds[i + 1]], i, out=logits[bounds[i]:bounds[i + 1]])
+                for i in range(ns)])
     return logits
 
 
@@ -93,12 +191,16 @@ class GraphReplay:
     them is freed under it: torch.cuda.graph empties the allocator's cache when a capture starts, which
     unmaps freed blocks, so a graph whose buffers were merely dropped from a model cache would fault
     on replay after the next capture.  `run` returns the owner's logits buffer (overwritten by the
-    next call), as the eager forward does."""
+    next call), as the eager forward does.
+
+    A split forward (one that forks its batch parts through fork_parts) is captured as one graph per
+    part, each replayed on its part stream (see fork_parts); other forwards as one graph."""
 
     def __init__(self, max_entries: int = 4):
         self.max_entries = max_entries
         self._entries = {}
         self.captures = 0
+        self.tune_log = None
 
     def clear(self):
         self._entries = {}
@@ -114,15 +216,74 @@ class GraphReplay:
             forward(x)  # first launches (kernel attributes), packing and workspaces outside the capture
         cur.wait_stream(side)
         torch.cuda.synchronize(dev)
-        g = torch.cuda.CUDAGraph()
-        # thread_local: HIP calls other threads make meanwhile (e.g. a process group's watchdog)
-        # neither break this capture nor are broken by it.  A refused capture raises (measured:
-        # after one, the next launch on the device fails too, so there is no eager fallback)
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
+        # a split forward (fork_parts) first: each part captured into a graph of its own on its own
+        # stream, everything outside the parts (cached packing) run eagerly -- it queues no kernel on a
+        # repeat call, so the part graphs are the whole forward
+        parts = []
+        _PART_CAPTURE[0] = parts if PART_GRAPHS[0] else None
+        try:
             out = forward(x)
+        finally:
+            _PART_CAPTURE[0] = None
+        torch.cuda.synchronize(dev)
+        if parts:
+            g = self._tune(parts, dev)
+        else:
+            g = torch.cuda.CUDAGraph()
+            # thread_local: HIP calls other threads make meanwhile (e.g. a process group's watchdog)
+            # neither break this capture nor are broken by it.  A refused capture raises (measured:
+            # after one, the next launch on the device fails too, so there is no eager fallback)
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                out = forward(x)
         self.captures += 1
         e = self._entries[key] = (g, out, x, (x,) + tuple(keep()))
         return e
+
+    def _tune(self, parts, device):
+        """The part graphs replayed on TUNE_CANDIDATES stream sets -- the capture's own, then fresh
+        pick_streams sets, alternately all at priority 0 and part 0 at high priority -- three timed
+        replays each; the set with the lowest median is kept ((priorities, ms) per set in tune_log).
+
+        Why measured: whether two stream parts overlap depends on which streams they run on, through
+        state no probe of this round predicted (round 6, tools/exp_vivit_hwq.py / ab_stream_modes.py:
+        ViViT-B B = 8 850-900 vs 960-1000 clips/s, ResNet3D-50 990 vs 1517, TimeSformer-B 1430 vs 1829
+        from one stream set to the next, every set stable over repeated replays in its process)."""
+        n = len(parts)
+        graphs = [pg for _, pg in parts]
+        cands = [[st for st, _ in parts]]
+        pats = [(0,) * n, (-1,) + (0,) * (n - 1)]
+        for t in range(TUNE_CANDIDATES[0] - 1):
+            cands.append(pick_streams(device, n, pats[t % 2], fresh=True))
+        best, best_t, log = None, float("inf"), []
+        for sts in cands:
+            lst = list(zip(sts, graphs))
+            self._replay(lst, device)
+            ts = []
+            for _ in range(3):
+                torch.cuda.synchronize(device)
+                t0 = time.perf_counter()
+                self._replay(lst, device)
+                torch.cuda.synchronize(device)
+                ts.append(time.perf_counter() - t0)
+            med = sorted(ts)[1]
+            log.append((tuple(st.priority for st in sts), round(med * 1e3, 3)))
+            if med < best_t:
+                best, best_t = lst, med
+        self.tune_log = log
+        return best
+
+    @staticmethod
+    def _replay(g, device):
+        if isinstance(g, list):  # part graphs: each on its own stream, forked from and joined to the caller's
+            cur = torch.cuda.current_stream(device)
+            for st, pg in g:
+                st.wait_stream(cur)
+                with torch.cuda.stream(st):
+                    pg.replay()
+            for st, _ in g:
+                cur.wait_stream(st)
+        else:
+            g.replay()
 
     def run(self, key, x: torch.Tensor, forward, keep=lambda: ()):
         e = self._entries.get(key)
@@ -136,9 +297,9 @@ class GraphReplay:
                 else:
                     e[2].copy_(x)
                 g, out, _, _ = e
-                g.replay()
+                self._replay(g, x.device)
                 return out
             e = self._capture(key, x, forward, keep)
         g, out, _, _ = e
-        g.replay()
+        self._replay(g, x.device)
         return out

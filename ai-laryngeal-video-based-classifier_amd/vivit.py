@@ -126,10 +126,9 @@ class VivitForVideoClassification(torch.nn.Module):
         self._ws_used = []
         self._streams = None
         self.concurrent_streams = None  # None / 1: one stream; n > 1: batch split over n HIP streams
-        # HIP stream priority per part (torch.cuda.Stream(priority=...): lower is higher).  None: part 0 (the
-        # largest) high, the others normal -- the eager two-stream B = 8 forward 843.6 -> 968.6 clips/s (and far
-        # steadier: min 8.49 vs median 9.48 ms without); under graph replay it makes no difference (976.1 vs
-        # 975.0).  profiles/r06_stream_prio.txt
+        # HIP stream priority per part (lower is higher; None: all normal) of the eager forward's part
+        # streams (streams.pick_streams: on different hardware queues, measured).  Under graph replay the
+        # part graphs run on the stream set streams.GraphReplay._tune timed fastest; profiles/r06_hwq.txt
         self.stream_priorities = None
         # clips per stream part (A/B hook; must sum to the batch): None = as even as possible
         self.split_sizes = None
@@ -450,12 +449,9 @@ class VivitForVideoClassification(torch.nn.Module):
             self.last_split = [B]
             return self._forward_part(pix, 0)
         dev = pix.device
-        prio = (tuple(self.stream_priorities) if self.stream_priorities is not None
-                else (-1,) + (0,) * (ns - 1))
-        if (self._streams is None or len(self._streams) < ns or self._streams[0].device != dev
-                or getattr(self, "_streams_prio", None) != prio):
-            self._streams = [torch.cuda.Stream(device=dev, priority=prio[i] if prio else 0) for i in range(ns)]
-            self._streams_prio = prio
+        # the parts on different hardware queues (streams.pick_streams)
+        self._streams = streams.pick_streams(dev, ns, None if self.stream_priorities is None
+                                             else tuple(self.stream_priorities)[:ns])
         key = (B, str(dev), "logits")
         if key not in self._ws:
             self._ws[key] = torch.zeros(B, c.num_labels, dtype=torch.float32, device=dev)
@@ -475,13 +471,11 @@ class VivitForVideoClassification(torch.nn.Module):
         # whole parts enqueued one after the other (measured, tools/exp_streams.py: enqueueing the
         # parts layer by layer round robin ran 725 vs 911 clips/s, chaining their attention launches
         # across the streams 721, and starting part i+1 at a fixed op of part i's first layer 887-906)
-        for i, st in enumerate(sts):
-            st.wait_stream(cur)
-            pix.record_stream(st)
-            with torch.cuda.stream(st):
-                self._forward_part(pix[bounds[i]:bounds[i + 1]], i, out=logits[bounds[i]:bounds[i + 1]])
         for st in sts:
-            cur.wait_stream(st)
+            pix.record_stream(st)
+        streams.fork_parts(sts, cur, [lambda i=i: self._forward_part(pix[bounds[i]:bounds[i + 1]], i,
+                                                                      out=logits[bounds[i]:bounds[i + 1]])
+                                      for i in range(ns)])
         return logits
 
     def _forward_part(self, pix: torch.Tensor, part: int, out=None) -> torch.Tensor:

@@ -151,6 +151,13 @@ def _graph_used(model, a) -> bool:
     return bool(a.graph) and getattr(model, "_graphs", None) is not None
 
 
+def _stream_tuning(model):
+    """(priorities, ms per replay) of each stream set the headline's part graphs were timed on at capture
+    (streams.GraphReplay._tune; the fastest is the one replayed), or None (no split graph)"""
+    g = getattr(model, "_graphs", None)
+    return None if g is None or g.tune_log is None else [{"priorities": list(p), "ms": t} for p, t in g.tune_log]
+
+
 def timed_loop(step, steps: int, warmup: int, dist=None, sync=None):
     """W untimed warm-up steps, then exactly `steps` timed steps bracketed by a barrier and
     a device sync on both sides; returns the MAX elapsed seconds over ranks (the job's
@@ -465,6 +472,7 @@ def run_family(a, dist, rank, world, dev):
     # per-kernel table of 3 one-stream steps with HIP events around every launch, whose largest row is
     # the roofline line (the step's dominant kernel)
     dt = timed(a.streams)
+    tune = _stream_tuning(model)
     model.graph_replay = False  # the passes below are event-instrumented or one-off calls
     dt1 = timed(1)
     # the per-kernel table on the headline's own launches: its split, the parts serialised on one stream
@@ -511,7 +519,7 @@ def run_family(a, dist, rank, world, dev):
             "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (uint8 frames RandomState(1+rank) -> the family's processor affine; weights RandomState(0))",
             "config": {"workload": workload, "global_batch": a.batch * world, "parallelism": f"dp{world}",
-                       "streams": a.streams, "hip_graph": _graph_used(model, a)},
+                       "streams": a.streams, "hip_graph": _graph_used(model, a), "stream_sets_timed": tune},
             "logit_max_abs_err": err,
             "logit_err_note": "max |logit - oracle| relative to max(1, max |oracle logit|)" if a.mode == "resnet3d" else None,
             "roofline": roof,
@@ -752,6 +760,7 @@ def main():
     # the headline: the batch split over `--streams` concurrent HIP streams (the clips are independent,
     # every kernel is batch-invariant: logits bit-identical to one stream), nothing instrumented
     dt = timed(a.streams)
+    tune = _stream_tuning(model)
     streams = model.last_streams
     split = list(model.last_split)  # clips per part (vivit.SPLIT_DEFAULT: 5 + 3 at B = 8 on two streams)
     split_desc = " + ".join(str(v) for v in split)
@@ -855,7 +864,8 @@ def main():
             "config": {"workload": "ViViT-B/16x2 forward, 32x224x224 clips, batch 8 per GPU (BASELINE configs[1])",
                        "model": "ViViT-B/16x2 (joint space-time, 12L, d768, 12H, 3137 tokens)",
                        "global_batch": a.batch * world, "seq_len": 3137, "parallelism": f"dp{world}",
-                       "streams": a.streams, "split": split, "hip_graph": _graph_used(model, a)},
+                       "streams": a.streams, "split": split, "hip_graph": _graph_used(model, a),
+                       "stream_sets_timed": tune},
             "logit_max_abs_err": logit_err,
             "roofline": {"bound": "mfma", "kernel": ATTN_KERNEL, "achieved": round(attn_tflops, 1),
                          "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4),

@@ -209,6 +209,11 @@ int vc_attention_fwd_h16(const uint16_t* qkv, int64_t ld, int64_t B, int64_t S, 
 int vc_layernorm_f32(const float* x, int64_t ldx, int64_t M, int64_t D, const float* gamma, const float* beta,
                      float eps, float* y, int64_t ldy, hipStream_t stream);
 
+/* `blocks` one-wave workgroups, each sleeping iters x s_sleep 127, on `stream` (no memory traffic): the
+ * hardware-queue probe of vclip_amd.streams.pick_streams.  No reference counterpart (the reference
+ * runs one CUDA stream). */
+int vc_spin(int64_t iters, int64_t blocks, hipStream_t stream);
+
 /* CLS rows: x[b*S][:] = cls[:] + pos[0][:]   (TF5/.../modeling_vivit.py:131-142). */
 int vc_cls_init(const float* cls, const float* pos, float* x, int64_t ldx, int64_t B, int64_t S, int64_t D,
                 hipStream_t stream);

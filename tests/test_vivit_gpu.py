@@ -160,6 +160,48 @@ def test_vivit_graph_replay_bit_identical(streams):
     assert np.abs(m.forward_logits(pix).cpu().numpy() - g["logits"]).max() < 1e-2
 
 
+def test_pick_streams_on_different_hardware_queues():
+    """streams.pick_streams: the picked streams are cached and sit on different hardware queues: one-wave
+    spins on a picked pair overlap (well under two spins' time), while two on ONE stream take two (the
+    probe's premise)."""
+    from vclip_amd import streams
+    dev = torch.device("cuda", 0)
+    sts = streams.pick_streams(dev, 2)
+    assert streams.pick_streams(dev, 2) is sts
+    assert streams.PICK_STATUS[(0, (0, 0))] is True
+    fresh = streams.pick_streams(dev, 2, (-1, 0), fresh=True)
+    assert [st.priority for st in fresh] == [-1, 0] and streams.pick_streams(dev, 2) is sts
+    cur = [torch.cuda.current_stream(dev)]
+    iters = 64
+    while streams._spin_time(cur, iters, dev) < 1e-3:
+        iters *= 2
+        assert iters <= 1 << 20
+    one = min(streams._spin_time(cur, iters, dev) for _ in range(3))
+    assert min(streams._spin_time(sts, iters, dev) for _ in range(3)) < 1.5 * one
+    assert min(streams._spin_time([sts[0], sts[0]], iters, dev) for _ in range(3)) > 1.7 * one
+
+
+def test_vivit_graph_replay_part_graphs():
+    """A split forward under graph replay is captured as one graph per part (streams.fork_parts), each
+    replayed on its own stream (the fastest of the sets GraphReplay._tune timed); logits equal the
+    eager forward's bit for bit."""
+    from vclip_amd import streams
+    g = np.load(os.path.join(GD, "vivit_tiny.npz"))
+    cfg = json.loads(str(g["config"]))
+    m = _model(cfg)
+    m.concurrent_streams = 2
+    pix = torch.from_numpy(g["pixel_values"]).cuda()
+    want = m.forward_logits(pix).clone()
+    m.graph_replay = True
+    assert torch.equal(m.forward_logits(pix), want)
+    (entry,) = m._graphs._entries.values()
+    parts = entry[0]
+    assert isinstance(parts, list) and len(parts) == 2
+    assert len(m._graphs.tune_log) == streams.TUNE_CANDIDATES[0]  # stream sets timed, the fastest kept
+    for _ in range(3):
+        assert torch.equal(m.forward_logits(pix), want)
+
+
 def test_vivit_graph_replay_survives_workspace_cache_reset():
     """A captured forward keeps the workspaces it addresses alive: after enough other batch sizes /
     stream splits / operand types to reset the model's workspace cache (8 entries) and another

@@ -73,4 +73,6 @@ if mode in ("swin", "fwd", "timesformer") and hasattr(m, "kernel_events"):
     m.kernel_events = None
     torch.cuda.synchronize()
     extra = f", attention {np.mean([e[0].elapsed_time(e[1]) for e in evs]) * 1e3:.1f} us/launch"
-print(f"{path} {mode}: {min(ts):.3f} ms/step (min of 3), {B / min(ts) * 1e3:.1f} clips/s{extra}", flush=True)
+from vclip_amd import streams  # noqa: E402
+print(f"{path} {mode}: {min(ts):.3f} ms/step (min of 3), {B / min(ts) * 1e3:.1f} clips/s{extra}"
+      f"  picked streams concurrent {streams.PICK_STATUS}", flush=True)
