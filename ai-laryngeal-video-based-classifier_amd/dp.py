@@ -36,7 +36,8 @@ class GradAllReduce:
         if device.type != "cuda":
             return None
         if self._side is None:
-            self._side = torch.cuda.Stream(device=device)
+            from . import streams  # the train step's third side stream (vivit_train: wgrad, dQ)
+            self._side = streams.pick_streams(device, 3, against=(torch.cuda.current_stream(device),))[2]
         return self._side
 
     def _on_ready(self, stage, start, end, gflat):

@@ -49,8 +49,7 @@ def split_bounds(B: int, ns: int, sizes=None) -> list:
 #  * streams on ONE hardware queue serialize.  HIP maps streams onto a few queues per process
 #    (GPU_MAX_HW_QUEUES, 4 here) and which of torch's pool streams share one depends on how many streams
 #    the process made before (tools/hwq_probe.py: of six consecutive pool streams, three pairs shared).
-#    pick_streams measures: a one-wave spin (vc_spin) on each of two streams takes one spin's time on
-#    different queues and two on a shared one;
+#    pick_streams measures (two probes, see there);
 #  * beyond that, through state no probe here predicted: with every pair on different queues the ViViT-B
 #    B = 8 5 + 3-clip forward ran 850-900 or 960-1000 clips/s from one stream set to the next, ResNet3D-50
 #    990 or 1517, TimeSformer-B 1430 or 1829, each set stable over repeated replays in its process
@@ -76,20 +75,48 @@ def _spin_time(sts, iters, device):
     return time.perf_counter() - t0
 
 
-def pick_streams(device, n: int, priorities=None, candidates: int = 12, fresh: bool = False) -> list:
-    """`n` streams of torch's pool, stream i at priority priorities[i] (default_priorities(n) when None), on
-    pairwise different hardware queues, measured; cached unless `fresh` (a new set from the next pool
-    streams, for GraphReplay._tune).  Falls back to unmeasured candidates (PICK_STATUS False) when no such
-    set turns up, and to fresh pool streams while a graph capture is running (no synchronisation then)."""
+def _behind(a, b, device, blocks: int, iters: int = 24) -> float:
+    """Completion time of a one-workgroup spin on stream b queued right after a `blocks`-workgroup spin
+    (four rounds of the GPU's wave slots) on stream a, over a's: ~0.3 when b's workgroup is dispatched
+    beside a's, ~0.96 when b waits for a's whole dispatch (best of two; tools/hwq_pipe_probe.py)."""
+    best = 9.0
+    for _ in range(2):
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        with torch.cuda.stream(a):
+            ops.spin(iters, device, blocks)
+        with torch.cuda.stream(b):
+            ops.spin(1, device, 1)
+        b.synchronize()
+        tb = time.perf_counter() - t0
+        a.synchronize()
+        best = min(best, tb / (time.perf_counter() - t0))
+    return best
+
+
+def pick_streams(device, n: int, priorities=None, candidates: int = 12, fresh: bool = False, against=()) -> list:
+    """`n` streams of torch's pool, stream i at priority priorities[i] (default_priorities(n) when None),
+    every pair among them and with each stream of `against` (e.g. the caller's stream, when it runs work
+    beside them) measured to run side by side; cached unless `fresh` (a new set from the next pool
+    streams, for GraphReplay._tune).  Falls back to unmeasured candidates (PICK_STATUS False) when no
+    such set turns up, and to fresh pool streams while a graph capture is running (no synchronisation).
+
+    Two probes: (1) a one-wave spin on each of two streams takes one spin's time when they sit on
+    different hardware queues and two when they share one; (2) a one-workgroup spin queued behind a
+    four-round spin on the other stream finishes after the first round (0.3 of it) unless the two
+    queues are dispatched one kernel at a time (0.96).  The ViViT-B train step ran 183 clips/s with
+    its weight-gradient stream in relation (2) to the main stream and 206 with the two side streams
+    so, 219-222 in every trial with all pairs at 0.3 (tools/exp_train_streams.py, twelve trials)."""
     device = torch.device(device)
     prios = tuple(int(p) for p in (default_priorities(n) if priorities is None else priorities))
     if len(prios) != n:
         raise ValueError(f"pick_streams: {len(prios)} priorities for {n} streams")
-    key = (device.index, prios)
+    against = tuple(against)
+    key = (device.index, prios) + ((tuple(s.cuda_stream for s in against),) if against else ())
     got = None if fresh else _PICKED.get(key)
     if got is not None:
         return got
-    if n <= 1 or torch.cuda.is_current_stream_capturing():
+    if n <= 1 and not against or torch.cuda.is_current_stream_capturing():
         return [torch.cuda.Stream(device=device, priority=p) for p in prios]
     cur = [torch.cuda.current_stream(device)]
     iters = 16
@@ -97,11 +124,18 @@ def pick_streams(device, n: int, priorities=None, candidates: int = 12, fresh: b
     while iters < (1 << 16) and _spin_time(cur, iters, device) < 5e-4:
         iters *= 2
     one = min(_spin_time(cur, iters, device) for _ in range(3))
+    blocks = 4 * 32 * torch.cuda.get_device_properties(device).multi_processor_count
+    _behind(torch.cuda.Stream(device=device), cur[0], device, blocks)
+
+    def fits(c, q):
+        return (min(_spin_time([q, c], iters, device) for _ in range(2)) < 1.5 * one
+                and _behind(q, c, device, blocks) < 0.6 and _behind(c, q, device, blocks) < 0.6)
+
     picked, ok = [], True
     for p in prios:
         cands = [torch.cuda.Stream(device=device, priority=p) for _ in range(candidates)]
         for c in cands:
-            if all(min(_spin_time([q, c], iters, device) for _ in range(2)) < 1.5 * one for q in picked):
+            if all(fits(c, q) for q in list(against) + picked):
                 picked.append(c)
                 break
         else:

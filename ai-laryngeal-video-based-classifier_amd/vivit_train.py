@@ -24,7 +24,7 @@ import math
 
 import torch
 
-from . import ops
+from . import ops, streams
 
 ALIGN = 64
 
@@ -217,7 +217,10 @@ class TrainEngine:
         main = torch.cuda.current_stream(self.device)
         side_on = self.side_wgrad
         if side_on and self.side is None:
-            self.side = torch.cuda.Stream(device=self.device)
+            # the weight-gradient, dQ and gradient all-reduce side streams, measured to run beside each
+            # other and beside the main stream (streams.pick_streams): streams drawn blind ran the step
+            # at 183 / 206 instead of 220 clips/s in 5 of 12 trials (tools/exp_train_streams.py)
+            self.side = streams.pick_streams(self.device, 3, against=(main,))[0]
         ws0 = self.work_side if side_on else self.work
 
         class _WS:  # the split-K scratch of one weight gradient, capped at wgrad_max_splits partials
@@ -284,7 +287,7 @@ class TrainEngine:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
             if self.attn_bwd_2s and self.side_dq is None:
-                self.side_dq = torch.cuda.Stream(device=self.device)
+                self.side_dq = streams.pick_streams(self.device, 3, against=(main,))[1]
             ops.attention_bwd(self.QKV[i], self.O[i], dO, self.LSE[i], self.delta, B, S, H, dQKV,
                               stream2=self.side_dq if self.attn_bwd_2s else None)
             if ev is not None:

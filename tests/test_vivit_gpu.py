@@ -179,6 +179,12 @@ def test_pick_streams_on_different_hardware_queues():
     one = min(streams._spin_time(cur, iters, dev) for _ in range(3))
     assert min(streams._spin_time(sts, iters, dev) for _ in range(3)) < 1.5 * one
     assert min(streams._spin_time([sts[0], sts[0]], iters, dev) for _ in range(3)) > 1.7 * one
+    # against the caller's stream too (the train step's side streams): dispatched side by side with it
+    side = streams.pick_streams(dev, 2, against=cur)
+    blocks = 4 * 32 * torch.cuda.get_device_properties(dev).multi_processor_count
+    for st in side:
+        assert streams._behind(cur[0], st, dev, blocks) < 0.6 and streams._behind(st, cur[0], dev, blocks) < 0.6
+    assert streams._behind(side[0], side[0], dev, blocks) > 0.9  # one stream: behind the whole dispatch
 
 
 def test_vivit_graph_replay_part_graphs():
