@@ -15,8 +15,12 @@ from vclip_amd.weights import make_synthetic_clips  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--trials", type=int, default=8)
+ap.add_argument("--tune", type=int, default=6, help="streams.TUNE_CANDIDATES")
+ap.add_argument("--pats", default="0:0,-1:0", help="streams.TUNE_PRIORITIES for two parts (comma-separated p0:p1)")
 ap.add_argument("--prios", default="default,0:0", help="comma-separated stream priority sets ('default' or p0:p1)")
 a = ap.parse_args()
+streams.TUNE_CANDIDATES[0] = a.tune
+streams.TUNE_PRIORITIES[:] = [(lambda i, n, pr=tuple(int(v) for v in ps.split(":")): pr[i]) for ps in a.pats.split(",")]
 dev = torch.device("cuda", 0)
 pix = torch.from_numpy(make_synthetic_clips(8, 32, 224, seed=1)).to(dev)
 m = create_model(num_frames=32, device=dev)
