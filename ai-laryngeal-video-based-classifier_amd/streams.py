@@ -147,8 +147,8 @@ def pick_streams(device, n: int, priorities=None, candidates: int = 12, fresh: b
         else:
             picked.append(cands[0])
             ok = False
-    PICK_STATUS[key] = ok
-    if not fresh:
+    if not fresh:  # PICK_STATUS / _PICKED describe the cached set only
+        PICK_STATUS[key] = ok
         _PICKED[key] = picked
     return picked
 

@@ -73,7 +73,7 @@ for k in range(a.trials):
     eng = m._engine
     if k % 2:
         eng.side, eng.side_dq = streams.pick_streams(dev, 2, fresh=True)
-        how = f"picked (ok {streams.PICK_STATUS[(0, (0, 0))]})"
+        how = "picked (fresh)"
     elif k == 0:
         how = f"default (the engine's own picks, ok {list(streams.PICK_STATUS.values())})"
     else:
