@@ -35,6 +35,9 @@ ATTN_GFLOP_PER_CLIP_LAYER = 4.0 * 3137 * 3137 * 64 * 12 / 1e9  # QK^T + PV, 30.2
 VIVIT_GFLOP_PER_CLIP = 903.05   # measured with torch.utils.flop_counter on the HF model
 ATTN_GFLOP_PER_CLIP = 362.77
 ATTN_IO_BYTES_PER_CLIP = 3137 * 768 * 2 * 4  # q,k,v read + o written once, bf16
+# attention backward, compulsory per clip and layer: q,k,v, o and dO read, dq,dk,dv written (bf16), the
+# log-sum-exp read and delta = rowsum(dO * o) written and read (f32 per query and head)
+TRAIN_ATTN_IO_BYTES_PER_CLIP = 3137 * 768 * 2 * (3 + 1 + 1 + 3) + 3137 * 12 * 4 * 3
 PEAK_BF16_TFLOPS = 2500.0       # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 # the headline's dominant kernel as rocprofv3 names it (template args: no rebase test build, no
 # lse, bf16 operands) -- the key of its counters in profiles/rNN_*_{traffic,pmc}.json
@@ -658,8 +661,8 @@ def run_train(a, dist, rank, world, dev):
             "roofline": {"bound": "mfma", "kernel": "attention backward (attn_bwd_dkdv + attn_bwd_dq + prep)",
                          "achieved": round(attn_tflops, 1), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(attn_tflops / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
-                         "traffic_source": traffic_src, "avg_launch_ms": round(attn_ms, 4),
-                         "mfma_busy_dkdv": mfma_busy, "valu_per_mfma_dkdv": valu_per_mfma, "pmc_source": pmc_src,
+                         "traffic_source": traffic_src, "algorithmic_bytes": TRAIN_ATTN_IO_BYTES_PER_CLIP * a.batch,
+                         "avg_launch_ms": round(attn_ms, 4), "mfma_busy_dkdv": mfma_busy, "valu_per_mfma_dkdv": valu_per_mfma, "pmc_source": pmc_src,
                          "flop_per_launch": f"{TRAIN_ATTN_GFLOP_PER_CLIP_LAYER:.2f} GF/clip x {a.batch} clips"},
             "step_tflops": round(step_tflops, 1), "step_frac_of_peak": round(step_tflops / PEAK_BF16_TFLOPS, 4),
             "wgrad_roofline": wgrad_line(ktable, instr_ms),
