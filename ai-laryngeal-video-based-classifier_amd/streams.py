@@ -185,6 +185,65 @@ def fork_parts(sts, cur, fns) -> None:
         cur.wait_stream(st)
 
 
+def _rank_sets(cands, run, device):
+    """Time run(streams) on every candidate stream set: three warm-up runs of the first (the clock ramps up
+    over the first launches of a fresh process), then two passes in opposite orders (a drifting clock
+    favours no position) of one untimed and two timed runs per set.  Returns (index of the set with the
+    lowest second-best of its four times, [that time per set])."""
+    for _ in range(3):
+        run(cands[0])
+    ts = [[] for _ in cands]
+    for rnd in range(2):
+        for i in (range(len(cands)) if rnd == 0 else reversed(range(len(cands)))):
+            run(cands[i])
+            for _ in range(2):
+                torch.cuda.synchronize(device)
+                t0 = time.perf_counter()
+                run(cands[i])
+                torch.cuda.synchronize(device)
+                ts[i].append(time.perf_counter() - t0)
+    score = [sorted(t)[1] for t in ts]
+    return min(range(len(cands)), key=lambda i: score[i]), score
+
+
+def _candidate_sets(device, n, first):
+    """`first` and TUNE_CANDIDATES - 1 fresh pick_streams sets, priority patterns TUNE_PRIORITIES in rotation"""
+    pats = [tuple(p(i, n) for i in range(n)) for p in TUNE_PRIORITIES]
+    return [list(first)] + [pick_streams(device, n, pats[t % len(pats)], fresh=True)
+                            for t in range(TUNE_CANDIDATES[0] - 1)]
+
+
+# eager split forwards tune their part streams on the first call per configuration (EAGER_TUNE); _NO_TUNE > 0
+# while GraphReplay runs a forward for its own purposes (its warm-up and part-capture passes)
+EAGER_TUNE = [True]
+_NO_TUNE = [0]
+
+
+def part_streams(owner, key, n: int, run, device, priorities=None) -> list:
+    """The part streams of an eager split forward.  Explicit `priorities` (an A/B hook): pick_streams of
+    those.  Otherwise, on the first call per `key`, the forward itself (`run(streams)` enqueues it on a
+    stream set) is timed on the sets _candidate_sets gives and the fastest is kept for this owner and key
+    (`owner.eager_tune_log`: (priorities, ms) per set); later calls reuse it.  Untuned (the cached
+    pick_streams set) while instrumented (serial parts, an op recorder, kernel events), inside a capture,
+    or under _NO_TUNE.  The eager ViViT-B B = 8 two-stream forward ran 850-885 clips/s instead of
+    930-970 in about one process in five on the cached pick alone (tools/exp_vivit_hwq.py)."""
+    if priorities is not None:
+        return pick_streams(device, n, tuple(priorities)[:n])
+    cache = owner.__dict__.setdefault("_eager_sets", {})
+    got = cache.get(key)
+    if got is not None:
+        return got
+    base = pick_streams(device, n)
+    if (n <= 1 or not EAGER_TUNE[0] or _NO_TUNE[0] or _SERIAL[0] or ops._REC[0] is not None
+            or getattr(owner, "kernel_events", None) is not None or torch.cuda.is_current_stream_capturing()):
+        return base
+    cands = _candidate_sets(device, n, base)
+    k, score = _rank_sets(cands, run, device)
+    owner.eager_tune_log = [(tuple(st.priority for st in sts), round(v * 1e3, 3)) for sts, v in zip(cands, score)]
+    cache[key] = cands[k]
+    return cands[k]
+
+
 def run_split(owner, x: torch.Tensor, ns: int, part_fn, num_labels: int, prepare=None) -> torch.Tensor:
     """part_fn(x_part, part_index, out=logits_rows) for each of `ns` contiguous batch parts, part i on
     owner._streams[i]; returns the [B, num_labels] logits (a buffer of `owner`, reused per call).
@@ -198,8 +257,6 @@ def run_split(owner, x: torch.Tensor, ns: int, part_fn, num_labels: int, prepare
         prepare()
     B = x.shape[0]
     ns = max(1, min(int(ns), B))
-    prios = getattr(owner, "stream_priorities", None)
-    owner._streams = pick_streams(dev, ns, None if prios is None else tuple(prios)[:ns])
     key = (B, str(dev), "split_logits")
     if key not in owner._split_out:
         owner._split_out[key] = torch.zeros(B, num_labels, dtype=torch.float32, device=dev)
@@ -210,11 +267,16 @@ def run_split(owner, x: torch.Tensor, ns: int, part_fn, num_labels: int, prepare
         for i in range(ns):
             part_fn(x[bounds[i]:bounds[i + 1]], i, out=logits[bounds[i]:bounds[i + 1]])
         return logits
-    for st in owner._streams[:ns]:
-        x.record_stream(st)  # x may be freed by the caller while the side streams still read it
-    fork_parts(owner._streams[:ns], cur,
-               [lambda i=i: part_fn(x[bounds[i]:bounds[i + 1]], i, out=logits[bounds[i]:bounds[i + 1]])
-                for i in range(ns)])
+
+    def go(sts):
+        for st in sts:
+            x.record_stream(st)  # x may be freed by the caller while the side streams still read it
+        fork_parts(sts, cur, [lambda i=i: part_fn(x[bounds[i]:bounds[i + 1]], i, out=logits[bounds[i]:bounds[i + 1]])
+                              for i in range(ns)])
+
+    owner._streams = part_streams(owner, (B, ns, str(dev), tuple(bounds)), ns, go, dev,
+                                  getattr(owner, "stream_priorities", None))
+    go(owner._streams)
     return logits
 
 
@@ -254,8 +316,12 @@ class GraphReplay:
         cur = torch.cuda.current_stream(dev)
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(cur)
-        with torch.cuda.stream(side):
-            forward(x)  # first launches (kernel attributes), packing and workspaces outside the capture
+        _NO_TUNE[0] += 1
+        try:
+            with torch.cuda.stream(side):
+                forward(x)  # first launches (kernel attributes), packing and workspaces outside the capture
+        finally:
+            _NO_TUNE[0] -= 1
         cur.wait_stream(side)
         torch.cuda.synchronize(dev)
         # a split forward (fork_parts) first: each part captured into a graph of its own on its own
@@ -263,10 +329,12 @@ class GraphReplay:
         # repeat call, so the part graphs are the whole forward
         parts = []
         _PART_CAPTURE[0] = parts if PART_GRAPHS[0] else None
+        _NO_TUNE[0] += 1
         try:
             out = forward(x)
         finally:
             _PART_CAPTURE[0] = None
+            _NO_TUNE[0] -= 1
         torch.cuda.synchronize(dev)
         if parts:
             g = self._tune(parts, dev)
@@ -293,29 +361,12 @@ class GraphReplay:
         from one stream set to the next, every set stable over repeated replays in its process)."""
         n = len(parts)
         graphs = [pg for _, pg in parts]
-        cands = [[st for st, _ in parts]]
         # (one candidate per assignment of the parts to distinct hardware queues instead, all at priority 0,
         # ran 953-963 clips/s where these sets gave 956-991 on the same box: profiles/r06_hwq.txt)
-        pats = [tuple(p(i, n) for i in range(n)) for p in TUNE_PRIORITIES]
-        for t in range(TUNE_CANDIDATES[0] - 1):
-            cands.append(pick_streams(device, n, pats[t % len(pats)], fresh=True))
-        sets = [list(zip(sts, graphs)) for sts in cands]
-        for _ in range(3):  # the clock ramps up over the first replays of a fresh process
-            self._replay(sets[0], device)
-        ts = [[] for _ in sets]
-        for rnd in range(2):  # two passes in opposite orders: a drifting clock favours no position
-            for i in (range(len(sets)) if rnd == 0 else reversed(range(len(sets)))):
-                self._replay(sets[i], device)
-                for _ in range(2):
-                    torch.cuda.synchronize(device)
-                    t0 = time.perf_counter()
-                    self._replay(sets[i], device)
-                    torch.cuda.synchronize(device)
-                    ts[i].append(time.perf_counter() - t0)
-        score = [sorted(t)[1] for t in ts]  # second best of four
-        k = min(range(len(sets)), key=lambda i: score[i])
+        cands = _candidate_sets(device, n, [st for st, _ in parts])
+        k, score = _rank_sets(cands, lambda sts: self._replay(list(zip(sts, graphs)), device), device)
         self.tune_log = [(tuple(st.priority for st in sts), round(v * 1e3, 3)) for sts, v in zip(cands, score)]
-        return sets[k]
+        return list(zip(cands[k], graphs))
 
     @staticmethod
     def _replay(g, device):

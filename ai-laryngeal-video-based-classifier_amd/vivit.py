@@ -126,9 +126,9 @@ class VivitForVideoClassification(torch.nn.Module):
         self._ws_used = []
         self._streams = None
         self.concurrent_streams = None  # None / 1: one stream; n > 1: batch split over n HIP streams
-        # HIP stream priority per part (lower is higher; None: all normal) of the eager forward's part
-        # streams (streams.pick_streams: on different hardware queues, measured).  Under graph replay the
-        # part graphs run on the stream set streams.GraphReplay._tune timed fastest; profiles/r06_hwq.txt
+        # HIP stream priority per part (lower is higher) of the eager forward's part streams, an A/B hook;
+        # None: the stream set streams.part_streams timed fastest on the first call.  Under graph replay
+        # the part graphs run on the set streams.GraphReplay._tune timed fastest; profiles/r06_hwq.txt
         self.stream_priorities = None
         # clips per stream part (A/B hook; must sum to the batch): None = as even as possible
         self.split_sizes = None
@@ -449,9 +449,6 @@ class VivitForVideoClassification(torch.nn.Module):
             self.last_split = [B]
             return self._forward_part(pix, 0)
         dev = pix.device
-        # the parts on different hardware queues (streams.pick_streams)
-        self._streams = streams.pick_streams(dev, ns, None if self.stream_priorities is None
-                                             else tuple(self.stream_priorities)[:ns])
         key = (B, str(dev), "logits")
         if key not in self._ws:
             self._ws[key] = torch.zeros(B, c.num_labels, dtype=torch.float32, device=dev)
@@ -467,15 +464,21 @@ class VivitForVideoClassification(torch.nn.Module):
             for i in range(ns):
                 self._forward_part(pix[bounds[i]:bounds[i + 1]], i, out=logits[bounds[i]:bounds[i + 1]])
             return logits
-        sts = self._streams[:ns]
         # whole parts enqueued one after the other (measured, tools/exp_streams.py: enqueueing the
         # parts layer by layer round robin ran 725 vs 911 clips/s, chaining their attention launches
         # across the streams 721, and starting part i+1 at a fixed op of part i's first layer 887-906)
-        for st in sts:
-            pix.record_stream(st)
-        streams.fork_parts(sts, cur, [lambda i=i: self._forward_part(pix[bounds[i]:bounds[i + 1]], i,
-                                                                      out=logits[bounds[i]:bounds[i + 1]])
-                                      for i in range(ns)])
+        def go(sts):
+            for st in sts:
+                pix.record_stream(st)
+            streams.fork_parts(sts, cur, [lambda i=i: self._forward_part(pix[bounds[i]:bounds[i + 1]], i,
+                                                                          out=logits[bounds[i]:bounds[i + 1]])
+                                          for i in range(ns)])
+
+        # the parts' streams: on different hardware queues, the fastest of several sets timed on the first
+        # call per configuration (streams.part_streams)
+        self._streams = streams.part_streams(self, (B, ns, str(dev), tuple(bounds), self.compute_dtype), ns, go,
+                                             dev, self.stream_priorities)
+        go(self._streams)
         return logits
 
     def _forward_part(self, pix: torch.Tensor, part: int, out=None) -> torch.Tensor:

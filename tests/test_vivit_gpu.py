@@ -204,6 +204,16 @@ def test_vivit_graph_replay_part_graphs():
     parts = entry[0]
     assert isinstance(parts, list) and len(parts) == 2
     assert len(m._graphs.tune_log) == streams.TUNE_CANDIDATES[0]  # stream sets timed, the fastest kept
+    # the eager split forward tunes its own part streams on its first call (streams.part_streams), and
+    # instrumented (serial) forwards do not
+    m.graph_replay = False
+    m.__dict__.pop("_eager_sets", None)
+    with streams.serial_parts():
+        assert torch.equal(m.forward_logits(pix), want)
+    assert not m.__dict__.get("_eager_sets")
+    assert torch.equal(m.forward_logits(pix), want)
+    assert len(m.eager_tune_log) == streams.TUNE_CANDIDATES[0] and len(m._eager_sets) == 1
+    assert torch.equal(m.forward_logits(pix), want)
     for _ in range(3):
         assert torch.equal(m.forward_logits(pix), want)
 

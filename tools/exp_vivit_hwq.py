@@ -47,6 +47,7 @@ for k in range(a.trials):
         m.stream_priorities = None if ps == "default" else [int(v) for v in ps.split(":")]
         m._streams = None
         streams._PICKED.clear()  # pick again (streams.pick_streams) after the offset
+        m.__dict__.pop("_eager_sets", None)  # and tune the eager forward's sets again (streams.part_streams)
         m._graphs.clear()
         m.graph_replay = False
         te = timeit()
