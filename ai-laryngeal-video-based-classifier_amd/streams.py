@@ -55,7 +55,8 @@ def split_bounds(B: int, ns: int, sizes=None) -> list:
 #    990 or 1517, TimeSformer-B 1430 or 1829, each set stable over repeated replays in its process
 #    (tools/exp_vivit_hwq.py, tools/ab_stream_modes.py; priorities did not decide it either, and a probe
 #    of whether one queue's dispatch waits for the other's, tools/hwq_pipe_probe.py, did not predict it).
-#    So GraphReplay times the captured part graphs on several picked stream sets and keeps the fastest.
+#    So GraphReplay times the captured part graphs, and part_streams the eager forward, on several picked
+#    stream sets and keep the fastest.
 # The picked set is cached per (device, priorities).
 _PICKED = {}
 PICK_STATUS = {}  # (device, priorities) -> True when every picked pair measured concurrent
